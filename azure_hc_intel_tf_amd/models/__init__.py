@@ -1,0 +1,47 @@
+"""Model registry: name -> model (tf_cnn_benchmarks ``models/model_config.py`` role,
+SURVEY.md §2.2). Names follow ``--model=`` of tf_cnn_benchmarks."""
+from __future__ import annotations
+
+from .base import CNNModel
+from .resnet import ResNet
+
+
+def _resnet(depth, version):
+    return lambda **kw: ResNet(depth=depth, version=version, **kw)
+
+
+def _inception3(**kw):
+    from .inception import InceptionV3
+
+    return InceptionV3(**kw)
+
+
+def _trivial(**kw):
+    from .trivial import Trivial
+
+    return Trivial(**kw)
+
+
+_MODELS = {
+    "resnet50": _resnet(50, "v1"),
+    "resnet50_v1.5": _resnet(50, "v1.5"),
+    "resnet101": _resnet(101, "v1"),
+    "resnet101_v1.5": _resnet(101, "v1.5"),
+    "resnet152": _resnet(152, "v1"),
+    "resnet152_v1.5": _resnet(152, "v1.5"),
+    "inception3": _inception3,
+    "trivial": _trivial,
+}
+
+
+def model_names():
+    return sorted(_MODELS)
+
+
+def create_model(name: str, **kw) -> CNNModel:
+    if name not in _MODELS:
+        raise ValueError(f"unknown model {name!r}; available: {', '.join(model_names())}")
+    return _MODELS[name](**kw)
+
+
+__all__ = ["create_model", "model_names", "CNNModel", "ResNet"]

@@ -1,0 +1,74 @@
+"""Model base class: a ParamStore plus explicit forward / backward over NHWC activations."""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from ..nn.layers import act_dtype
+from ..nn.params import ParamStore
+
+
+class CNNModel:
+    """Subclasses build their layers in ``build()`` using ``self.ps`` and implement
+    ``forward(images) -> logits`` and ``backward(dlogits)``.
+
+    ``image_channels`` is what the input tensor carries: on the GPU the 3 RGB channels are
+    zero-padded to 8 so every conv operand is a whole number of 16-byte vectors.
+    """
+
+    name = "model"
+    default_image_size = 224
+    default_batch_size = 64
+    default_lr_per_256 = 0.1  # tf_cnn_benchmarks: lr = 0.1 * global_batch / 256 for ResNets
+
+    def __init__(self, num_classes: int = 1001, image_size: int = None, device="cpu", seed: int = 1234,
+                 image_channels: int = None):
+        self.num_classes = num_classes
+        self.image_size = image_size or self.default_image_size
+        self.device = torch.device(device)
+        if image_channels is None:
+            image_channels = 8 if self.device.type == "cuda" else 3
+        assert image_channels in (3, 8) and (self.device.type != "cuda" or image_channels == 8)
+        self.image_channels = image_channels
+        self.ps = ParamStore(seed=seed)
+        self.layers: List = []
+        self.build()
+        self.ps.finalize(self.device)
+
+    # -- to implement
+    def build(self):
+        raise NotImplementedError
+
+    def forward(self, images: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def backward(self, dlogits: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    # -- helpers
+    @property
+    def act_dtype(self):
+        return act_dtype(self.device)
+
+    def input_shape(self, batch: int):
+        return (batch, self.image_size, self.image_size, self.image_channels)
+
+    def num_params(self) -> int:
+        return self.ps.num_params()
+
+    def flops_per_image(self) -> float:
+        """Forward FLOPs per image (multiply-adds x 2) of the conv / affine layers."""
+        tot = 0
+        for l in self.all_layers():
+            if hasattr(l, "flops"):
+                tot += l.flops(1)
+        return float(tot)
+
+    def all_layers(self):
+        return list(self.layers)
+
+    def clear(self):
+        for l in self.all_layers():
+            if hasattr(l, "clear"):
+                l.clear()

@@ -1,0 +1,105 @@
+"""ResNet v1 / v1.5 (50 / 101 / 152) as trained by tf_cnn_benchmarks ``--model=resnet50``
+(the reference's hard-coded model, /root/reference/benchmark-scripts/
+run-tf-sing-ucx-openmpi.sh:34,66).
+
+Architecture (tf_cnn_benchmarks resnet_model semantics):
+  conv 7x7/2 'SAME_RESNET' (64) + BN + ReLU -> max-pool 3x3/2 'SAME'
+  -> bottleneck stages [3,4,6,3] (50) / [3,4,23,3] (101) / [3,8,36,3] (152),
+     depths 256/512/1024/2048, bottleneck widths 64/128/256/512,
+     v1: stride on the first 1x1 of the first block of stages 2-4,
+     v1.5: stride on the 3x3 instead; projection shortcut (1x1 conv + BN) when the
+     channel count changes
+  -> spatial mean -> affine 2048 -> 1001 classes (ImageNet + background).
+BN: decay 0.9, epsilon 1e-5, scale=True. ResNet-50 v1: 25,559,081 trainable params.
+"""
+from __future__ import annotations
+
+from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool
+from .base import CNNModel
+
+LAYER_COUNTS = {18: None, 50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}
+
+
+class Bottleneck:
+    def __init__(self, ps, name, in_shape, depth, bottleneck, stride, v15: bool):
+        H, W, C = in_shape
+        self.proj = C != depth
+        s1, s2 = (1, stride) if v15 else (stride, 1)
+        if self.proj:
+            self.sc = ConvBN(ps, f"{name}/shortcut", in_shape, depth, 1, 1, stride, stride, "SAME", relu=False)
+        else:
+            assert stride == 1, "identity shortcut with stride is not used by these ResNets"
+            self.sc = None
+        self.c1 = ConvBN(ps, f"{name}/conv1", in_shape, bottleneck, 1, 1, s1, s1, "SAME")
+        self.c2 = ConvBN(ps, f"{name}/conv2", self.c1.out_shape, bottleneck, 3, 3, s2, s2, "SAME_RESNET")
+        self.c3 = ConvBN(ps, f"{name}/conv3", self.c2.out_shape, depth, 1, 1, 1, 1, "SAME", relu=True)
+        self.in_shape = in_shape
+        self.out_shape = self.c3.out_shape
+
+    def layers(self):
+        return [l for l in (self.sc, self.c1, self.c2, self.c3) if l is not None]
+
+    def forward(self, x):
+        sc = self.sc.forward(x) if self.proj else x
+        a = self.c1.forward(x)
+        b = self.c2.forward(a)
+        return self.c3.forward(b, residual=sc)
+
+    def backward(self, dy):
+        db, gres = self.c3.backward(dy, want_gres=True)
+        da, _ = self.c2.backward(db)
+        if self.proj:
+            dx, _ = self.c1.backward(da)
+            self.sc.backward(gres, dx=dx, accumulate=True)
+        else:
+            # identity shortcut: dx = gres + dgrad(c1), accumulated in place by the GEMM epilogue
+            dx, _ = self.c1.backward(da, dx=gres, accumulate=True)
+        return dx
+
+
+class ResNet(CNNModel):
+    default_image_size = 224
+
+    def __init__(self, depth: int = 50, version: str = "v1", **kw):
+        self.depth = depth
+        self.version = version
+        self.name = f"resnet{depth}" + ("_v1.5" if version == "v1.5" else "")
+        super().__init__(**kw)
+
+    def build(self):
+        ps = self.ps
+        S = self.image_size
+        v15 = self.version == "v1.5"
+        self.stem = ConvBN(ps, "conv0", (S, S, self.image_channels), 64, 7, 7, 2, 2, "SAME_RESNET",
+                           relu=True, need_dx=False, logical_cin=3)
+        self.pool = Pool("mpool0", self.stem.out_shape, 3, 3, 2, 2, "SAME", is_max=True)
+        shape = self.pool.out_shape
+        self.blocks = []
+        counts = LAYER_COUNTS[self.depth]
+        for si, (n, depth, bott) in enumerate(zip(counts, (256, 512, 1024, 2048), (64, 128, 256, 512))):
+            for bi in range(n):
+                stride = 2 if (si > 0 and bi == 0) else 1
+                blk = Bottleneck(ps, f"stage{si + 1}/block{bi + 1}", shape, depth, bott, stride, v15)
+                self.blocks.append(blk)
+                shape = blk.out_shape
+        self.gap = GlobalAvgPool("spatial_mean", shape)
+        self.fc = Logits(ps, "logits", shape[2], self.num_classes)
+        self.layers = [self.stem, self.pool] + [l for b in self.blocks for l in b.layers()] + [self.gap, self.fc]
+
+    def forward(self, images):
+        x = self.stem.forward(images)
+        x = self.pool.forward(x)
+        for b in self.blocks:
+            x = b.forward(x)
+        self._last = x
+        feat = self.gap.forward(x)
+        return self.fc.forward(feat)
+
+    def backward(self, dlogits):
+        dfeat = self.fc.backward(dlogits)
+        dx = self.gap.backward(dfeat)
+        for b in reversed(self.blocks):
+            dx = b.backward(dx)
+        dx = self.pool.backward(dx)
+        self.stem.backward(dx)
+        self._last = None

@@ -1,0 +1,282 @@
+"""Layer DSL with explicit forward / backward (the convnet_builder role of tf_cnn_benchmarks,
+SURVEY.md §2.2 "convnet_builder.py": conv(+BN+ReLU), mpool, apool, affine, spatial_mean,
+inception concat).
+
+Layers run on NHWC activations and call the primitive ops of ``ops.functional`` (HIP
+kernels on the GPU, PyTorch on the CPU). Backward is written out by hand instead of using
+autograd so that
+  * BN statistics come fused from the conv epilogue,
+  * the ReLU mask / residual-gradient fan-out is produced by the BN-backward kernel,
+  * the residual add of a bottleneck block becomes the beta-accumulate of the data-grad
+    GEMM epilogue (no separate add kernel),
+  * weight gradients land directly in the flat gradient (allreduce) buffer, and
+  * the whole step (fwd + bwd + optimizer) is a fixed kernel sequence that is captured in
+    a HIP graph.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import List, Optional, Tuple
+
+import torch
+
+from ..ops import functional as Fn
+from ..ops.functional import ConvSpec, same_pads
+from .params import ParamStore
+
+
+def act_dtype(device) -> torch.dtype:
+    """bf16 activations on the GPU; fp32 on the CPU (HCB_CPU_DTYPE=float64 for exact tests)."""
+    if torch.device(device).type == "cuda":
+        return torch.bfloat16
+    return torch.float64 if os.environ.get("HCB_CPU_DTYPE") == "float64" else torch.float32
+
+
+def empty_act(shape, device, zero=False):
+    f = torch.zeros if zero else torch.empty
+    return f(shape, dtype=act_dtype(device), device=device)
+
+
+def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
+    """Padding (pt, pb, pl, pr) for tf_cnn_benchmarks modes 'SAME', 'VALID', 'SAME_RESNET'."""
+    if isinstance(mode, (tuple, list)):
+        return tuple(mode)
+    if mode == "VALID":
+        return (0, 0, 0, 0)
+    if mode == "SAME_RESNET":  # explicit symmetric (k-1)//2 padding then VALID
+        ph = (dh * (kh - 1)) // 2
+        pw = (dw * (kw - 1)) // 2
+        return (ph, dh * (kh - 1) - ph, pw, dw * (kw - 1) - pw)
+    if mode == "SAME":
+        pt, pb = same_pads(H, kh, sh, dh)
+        pl, pr = same_pads(W, kw, sw, dw)
+        return (pt, pb, pl, pr)
+    raise ValueError(mode)
+
+
+class Layer:
+    in_shape: Tuple[int, int, int]
+    out_shape: Tuple[int, int, int]
+
+    def clear(self):
+        pass
+
+
+class ConvBN(Layer):
+    """conv(k x k, stride, padding) -> BatchNorm(train) -> [residual add] -> [ReLU]."""
+
+    def __init__(self, ps: ParamStore, name: str, in_shape, cout: int, kh: int, kw: int, sh: int = 1,
+                 sw: int = 1, mode="SAME", relu: bool = True, bn: bool = True, need_dx: bool = True,
+                 eps: float = 1e-5, decay: float = 0.9, logical_cin: Optional[int] = None,
+                 dilation: int = 1):
+        H, W, cin = in_shape
+        self.name = name
+        self.in_shape = in_shape
+        pt, pb, pl, pr = resolve_pads(mode, H, W, kh, kw, sh, sw, dilation, dilation)
+        self.spec = ConvSpec(cin=logical_cin or cin, cin_pad=cin, cout=cout, kh=kh, kw=kw, sh=sh, sw=sw,
+                             pt=pt, pl=pl, pb=pb, pr=pr, dh=dilation, dw=dilation)
+        P, Q = self.spec.out_hw(H, W)
+        assert P > 0 and Q > 0, f"{name}: empty output"
+        self.out_shape = (P, Q, cout)
+        self.relu = relu
+        self.bn = bn
+        self.need_dx = need_dx
+        self.eps = eps
+        self.decay = decay
+        lc = logical_cin or cin
+        fan_in = kh * kw * lc
+        self.w = ps.add(f"{name}/conv2d/kernel", (cout, kh, kw, cin), True,
+                        ps.variance_scaling(fan_in, lc if lc != cin else -1),
+                        logical_numel=cout * kh * kw * lc)
+        self.pack = ps.add_pack(self.w, cout, kh, kw, cin, self.spec.Kpad, self.spec.Kpad_t, want_tr=need_dx)
+        if bn:
+            self.gamma = ps.add(f"{name}/batchnorm/gamma", (cout,), False, ParamStore.const(1.0))
+            self.beta = ps.add(f"{name}/batchnorm/beta", (cout,), False, ParamStore.const(0.0))
+            self.rmean = ps.add_buffer(f"{name}/batchnorm/moving_mean", (cout,), 0.0)
+            self.rvar = ps.add_buffer(f"{name}/batchnorm/moving_variance", (cout,), 1.0)
+        else:
+            self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0))
+        self._saved = None
+
+    def flops(self, batch: int) -> int:
+        P, Q, C = self.out_shape
+        return 2 * batch * P * Q * C * self.spec.kh * self.spec.kw * self.spec.cin
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x, out=None, residual=None):
+        N = x.shape[0]
+        P, Q, C = self.out_shape
+        dev = x.device
+        if self.bn:
+            z = empty_act((N, P, Q, C), dev)
+            if x.is_cuda:
+                slab, T, cfg = Fn.conv_stats_slab(x.shape, self.spec, dev)
+                Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=slab, cfg=cfg)
+            else:
+                slab, T = None, 0
+                Fn.conv_forward(x, self.spec, None, self.w.data, z)
+            y = out if out is not None else empty_act((N, P, Q, C), dev)
+            saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
+                                  self.decay, self.eps, y, self.relu, residual=residual, stats=slab, stats_T=T)
+            self._saved = (x, z, y, saved, residual is not None)
+            return y
+        y = out if out is not None else empty_act((N, P, Q, C), dev)
+        if x.is_cuda:
+            Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, y, bias=self.bias.data)
+            assert not self.relu and residual is None, "plain conv: no fused activation on this path"
+        else:
+            Fn.conv_forward(x, self.spec, None, self.w.data, y, bias=self.bias.data)
+            if residual is not None:
+                y.add_(residual)
+            if self.relu:
+                y.relu_()
+        self._saved = (x, None, y, None, residual is not None)
+        return y
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False):
+        """Returns (dx or None, gres or None). gres = gradient w.r.t. the residual input."""
+        x, z, y, saved, had_res = self._saved
+        dev = dy.device
+        N = dy.shape[0]
+        P, Q, C = self.out_shape
+        gres = None
+        if self.bn:
+            dz = empty_act((N, P, Q, C), dev)
+            if want_gres:
+                gres = empty_act((N, P, Q, C), dev)
+            relu_mode = (1 if had_res else 2) if self.relu else 0
+            Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
+                           self.beta.grad, dz, gres)
+        else:
+            assert not self.relu
+            dz = dy
+            Fn.colsum(dz.reshape(-1, C) if dz.is_contiguous() else dz, N * P * Q, C, self.bias.grad)
+            if want_gres:
+                gres = dy
+        Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(C, -1) if dz.is_cuda else self.w.grad)
+        if self.need_dx:
+            H, W, Cin = self.in_shape
+            if dx is None:
+                strided_1x1 = (self.spec.sh > 1 or self.spec.sw > 1) and self.spec.kh == 1 and self.spec.kw == 1
+                dx = empty_act((N, H, W, Cin), dev, zero=strided_1x1 and dev.type == "cuda")
+                accumulate = False
+            Fn.conv_dgrad(dz, self.spec, self.pack.tr, self.w.data, dx, accumulate)
+        self._saved = None
+        return dx, gres
+
+    def clear(self):
+        self._saved = None
+
+
+class Pool(Layer):
+    def __init__(self, name, in_shape, kh, kw, sh, sw, mode="VALID", is_max=True, incl_pad=False):
+        H, W, C = in_shape
+        self.name = name
+        self.in_shape = in_shape
+        self.k = (kh, kw)
+        self.s = (sh, sw)
+        self.pads = resolve_pads(mode, H, W, kh, kw, sh, sw)
+        pt, pb, pl, pr = self.pads
+        P = (H + pt + pb - kh) // sh + 1
+        Q = (W + pl + pr - kw) // sw + 1
+        self.out_shape = (P, Q, C)
+        self.is_max = is_max
+        self.incl_pad = incl_pad
+        self._saved = None
+
+    def forward(self, x, out=None):
+        N = x.shape[0]
+        y = out if out is not None else empty_act((N,) + self.out_shape, x.device)
+        Fn.pool_forward(x, y, *self.k, *self.s, self.pads, self.is_max, self.incl_pad)
+        self._saved = (x, y)
+        return y
+
+    def backward(self, dy, dx=None, accumulate=False):
+        x, y = self._saved
+        if dx is None:
+            dx = empty_act(x.shape, dy.device)
+            accumulate = False
+        Fn.pool_backward(dy, x, y, dx, *self.k, *self.s, self.pads, self.is_max, self.incl_pad, accumulate)
+        self._saved = None
+        return dx
+
+    def clear(self):
+        self._saved = None
+
+
+class GlobalAvgPool(Layer):
+    def __init__(self, name, in_shape):
+        self.name = name
+        self.in_shape = in_shape
+        self.out_shape = (1, 1, in_shape[2])
+
+    def forward(self, x):
+        N = x.shape[0]
+        y = torch.empty((N, self.in_shape[2]), dtype=x.dtype, device=x.device)
+        Fn.gap_forward(x, y)
+        return y
+
+    def backward(self, dy):
+        N = dy.shape[0]
+        dx = empty_act((N,) + tuple(self.in_shape), dy.device)
+        Fn.gap_backward(dy, dx)
+        return dx
+
+
+class Logits(Layer):
+    """Final affine layer: logits[B, ncls] (fp32, row stride padded to 8) = x W^T + b."""
+
+    def __init__(self, ps: ParamStore, name, in_features: int, ncls: int, stddev: float = 0.01):
+        self.name = name
+        self.cin = in_features
+        self.ncls = ncls
+        self.ld = (ncls + 7) // 8 * 8
+        self.spec = ConvSpec(cin=in_features, cin_pad=in_features, cout=ncls, kh=1, kw=1)
+        self.w = ps.add(f"{name}/affine/weights", (ncls, 1, 1, in_features), True, ps.trunc_normal(stddev))
+        self.b = ps.add(f"{name}/affine/biases", (ncls,), True, ParamStore.const(0.0))
+        # dgrad operand uses the padded logits width as its reduction length
+        kt = (self.ld + 63) // 64 * 64
+        self.pack = ps.add_pack(self.w, ncls, 1, 1, in_features, self.spec.Kpad, kt, want_tr=True)
+        self._x = None
+
+    def forward(self, x):
+        B = x.shape[0]
+        x4 = x.view(B, 1, 1, self.cin)
+        logits = torch.empty((B, self.ld), dtype=torch.float32, device=x.device)
+        if x.is_cuda:
+            Fn.conv_forward(x4, self.spec, self.pack.pack, None, logits.view(B, 1, 1, self.ld)[..., :self.ld],
+                            bias=self.b.data)
+        else:
+            logits.zero_()
+            logits[:, :self.ncls] = (x @ self.w.data.view(self.ncls, self.cin).t().to(x.dtype)
+                                     + self.b.data.to(x.dtype)).float()
+        self._x = x
+        return logits
+
+    def backward(self, dlogits):
+        """dlogits: [B, ld] (bf16 on GPU, zero in the padding columns)."""
+        x = self._x
+        B = x.shape[0]
+        Fn.colsum(dlogits, B, self.ncls, self.b.grad)
+        if x.is_cuda:
+            hcb = Fn._ext.ops()
+            geom = [B, 1, 1, self.cin, self.cin, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, self.ncls, self.ld]
+            cfg, splits = 2, 1
+            hcb.conv_wgrad(dlogits, x, self.w.grad.view(self.ncls, self.cin), geom, cfg, splits)
+            dx = torch.empty((B, self.cin), dtype=x.dtype, device=x.device)
+            C = self.ld
+            geom = [B, 1, 1, C, C, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, self.cin, C, self.pack.Kpad_t, self.cin,
+                    0, 1, 1, 1, 1, 0, 0]
+            cfgd = Fn.conv_cfg(B, self.cin, C)
+            hcb.conv_igemm(dlogits, self.pack.tr, dx, None, None, None, geom, cfgd)
+        else:
+            g = dlogits[:, :self.ncls]
+            self.w.grad.view(self.ncls, self.cin).add_((g.t() @ x).float())
+            dx = g @ self.w.data.view(self.ncls, self.cin).to(x.dtype)
+        self._x = None
+        return dx
+
+    def flops(self, batch):
+        return 2 * batch * self.cin * self.ncls

@@ -1,0 +1,417 @@
+"""Primitive training ops on NHWC activations with explicit forward / backward halves.
+
+Each op has two implementations selected by the device of its tensors:
+
+* GPU (MI355X): the hand-written gfx950 HIP kernels in ``csrc/kernels`` via
+  ``torch.ops.hcb`` -- bf16 activations, fp32 accumulation / statistics / masters.
+  There is NO PyTorch fallback for GPU tensors: a missing library raises.
+* CPU: a PyTorch reference of the same math (fp32), which is the reference's
+  ``--device=cpu`` path (/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:75;
+  BASELINE config 1) and the oracle the GPU numerics tests compare against.
+
+Activations are ``[N, H, W, C]`` tensors whose channel dim may be a strided slice of a
+wider buffer (``t.stride(2) = ld``): Inception's branch outputs are written straight into
+their channel window of the concat buffer (no concat kernel).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+
+def ld(t: torch.Tensor) -> int:
+    """Pixel stride (elements) of an NHWC activation (supports channel-slice views)."""
+    if t.dim() == 4:
+        assert t.stride(3) == 1, "activation channels must be contiguous"
+        return t.stride(2)
+    assert t.dim() == 2 and t.stride(1) == 1
+    return t.stride(0)
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+# --------------------------------------------------------------------------- conv
+@dataclass
+class ConvSpec:
+    """Geometry of one convolution (NHWC activations, KRSC weights)."""
+
+    cin: int          # logical input channels (stem: 3)
+    cin_pad: int      # channels as stored (multiple of 8; stem 3 -> 8)
+    cout: int
+    kh: int
+    kw: int
+    sh: int = 1
+    sw: int = 1
+    pt: int = 0       # top / left padding (bottom / right implied by the output size)
+    pl: int = 0
+    pb: int = 0
+    pr: int = 0
+    dh: int = 1
+    dw: int = 1
+
+    @property
+    def K(self) -> int:
+        return self.kh * self.kw * self.cin_pad
+
+    @property
+    def Kpad(self) -> int:
+        return _round_up(self.K, 64)
+
+    @property
+    def Kt(self) -> int:  # reduction length of the data-gradient GEMM
+        return self.kh * self.kw * self.cout
+
+    @property
+    def Kpad_t(self) -> int:
+        return _round_up(self.Kt, 64)
+
+    def out_hw(self, H: int, W: int):
+        P = (H + self.pt + self.pb - self.dh * (self.kh - 1) - 1) // self.sh + 1
+        Q = (W + self.pl + self.pr - self.dw * (self.kw - 1) - 1) // self.sw + 1
+        return P, Q
+
+
+def same_pads(size: int, k: int, s: int, d: int = 1):
+    """TensorFlow 'SAME' padding (extra padding at the end)."""
+    out = (size + s - 1) // s
+    eff = d * (k - 1) + 1
+    total = max((out - 1) * s + eff - size, 0)
+    return total // 2, total - total // 2
+
+
+# ----------------------------------------------------------------- tile selection
+_CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128)}
+_WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64)}
+N_CU = 256
+_tuned: dict = {}
+
+
+def conv_cfg(M: int, N: int, K: int) -> int:
+    """Pick a block tile for C[M,N] (+K): enough workgroups to fill 256 CUs, biggest tile first."""
+    key = ("fwd", M, N, K)
+    if key in _tuned:
+        return _tuned[key]
+    cands = [0, 3, 1, 2] if N > 64 else [1, 2]
+    for c in cands:
+        bm, bn = _CONV_TILES[c]
+        if math.ceil(M / bm) * math.ceil(N / bn) >= 2 * N_CU:
+            return c
+    return cands[-1]
+
+
+def wgrad_cfg(Nout: int, K: int, M: int):
+    """(tile cfg, split-K) for dW[Nout, K] reduced over M pixels."""
+    key = ("wgrad", Nout, K, M)
+    if key in _tuned:
+        return _tuned[key]
+    c = 0 if Nout >= 128 and K >= 128 else (1 if K >= 128 else 2)
+    bm, bn = _WGRAD_TILES[c]
+    tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
+    ksteps = math.ceil(M / 64)
+    target = 2 * N_CU
+    splits = max(1, min(ksteps // 4 if ksteps >= 4 else 1, math.ceil(target / tiles)))
+    return c, splits
+
+
+def set_tuned(table: dict) -> None:
+    _tuned.update(table)
+
+
+# ---------------------------------------------------------------- conv forward
+def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None):
+    """out[N,P,Q,cout] = conv(x, W) (+bias). GPU: fp32 acc, bf16 (or fp32) out + BN stat slab."""
+    N, H, W, _ = x.shape
+    P, Q = spec.out_hw(H, W)
+    if x.is_cuda:
+        M = N * P * Q
+        if cfg is None:
+            cfg = conv_cfg(M, spec.cout, spec.K)
+        out_f32 = out.dtype == torch.float32
+        geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
+                spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1, 0,
+                1 if out_f32 else 0]
+        _ext.ops().conv_igemm(x, wpack, out, None, bias, stats, geom, cfg)
+        return out
+    xt = x.permute(0, 3, 1, 2)
+    if spec.pt or spec.pb or spec.pl or spec.pr:
+        xt = F.pad(xt, (spec.pl, spec.pr, spec.pt, spec.pb))
+    wt = w_master.permute(0, 3, 1, 2).to(x.dtype)
+    y = F.conv2d(xt, wt, bias=None if bias is None else bias.to(x.dtype), stride=(spec.sh, spec.sw), dilation=(spec.dh, spec.dw))
+    out.copy_(y.permute(0, 2, 3, 1))
+    return out
+
+
+def conv_stats_slab(x_shape, spec: ConvSpec, device, cfg=None):
+    N, H, W, _ = x_shape
+    P, Q = spec.out_hw(H, W)
+    M = N * P * Q
+    if cfg is None:
+        cfg = conv_cfg(M, spec.cout, spec.K)
+    bm = _CONV_TILES[cfg][0]
+    T = math.ceil(M / bm)
+    return torch.empty(T * 2 * spec.cout, dtype=torch.float32, device=device), T, cfg
+
+
+# ---------------------------------------------------------------- conv data grad
+def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool):
+    """dx[N,H,W,cin] (+)= conv_transpose(dz, W). dx must be zero-filled by the caller when
+    not accumulating and the conv is a strided 1x1 (remap path leaves gaps)."""
+    N, P, Q, _ = dz.shape
+    _, H, W, _ = dx.shape
+    if dz.is_cuda:
+        Cdz = spec.cout if spec.cout % 8 == 0 else _round_up(spec.cout, 8)
+        K = spec.kh * spec.kw * Cdz
+        Kpad = spec.Kpad_t
+        assert K <= Kpad
+        strided = spec.sh > 1 or spec.sw > 1
+        if strided and spec.kh == 1 and spec.kw == 1 and spec.pt == 0 and spec.pl == 0:
+            # 1x1 strided: dense GEMM over dz pixels, scatter rows to (p*sh, q*sw)
+            M = N * P * Q
+            geom = [N, P, Q, Cdz, ld(dz), P, Q, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, spec.cin_pad, K, Kpad,
+                    ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, 0]
+        else:
+            M = N * H * W
+            pt = spec.dh * (spec.kh - 1) - spec.pt
+            pl = spec.dw * (spec.kw - 1) - spec.pl
+            geom = [N, P, Q, Cdz, ld(dz), H, W, spec.kh, spec.kw, 1, 1, pt, pl, spec.dh, spec.dw,
+                    spec.sh, spec.sw, spec.cin_pad, K, Kpad, ld(dx), 0, H, W, 1, 1,
+                    1 if accumulate else 0, 0]
+        cfg = conv_cfg(M, spec.cin_pad, K)
+        _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg)
+        return dx
+    Hp = H + spec.pt + spec.pb
+    Wp = W + spec.pl + spec.pr
+    wt = w_master.permute(0, 3, 1, 2).to(dz.dtype)
+    g = torch.nn.grad.conv2d_input((N, spec.cin_pad, Hp, Wp), wt, dz.permute(0, 3, 1, 2),
+                                   stride=(spec.sh, spec.sw), dilation=(spec.dh, spec.dw))
+    g = g[:, :, spec.pt:spec.pt + H, spec.pl:spec.pl + W].permute(0, 2, 3, 1)
+    if accumulate:
+        dx.add_(g)
+    else:
+        dx.copy_(g)
+    return dx
+
+
+# ---------------------------------------------------------------- conv weight grad
+def conv_wgrad(dz, x, spec: ConvSpec, dw):
+    """dw[cout, kh, kw, cin_pad] (fp32) += sum over pixels of dz (x) im2col(x)."""
+    N, H, W, _ = x.shape
+    _, P, Q, _ = dz.shape
+    if dz.is_cuda:
+        M = N * P * Q
+        cfg, splits = wgrad_cfg(spec.cout, spec.K, M)
+        geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
+                spec.dh, spec.dw, spec.cout, ld(dz)]
+        _ext.ops().conv_wgrad(dz, x, dw, geom, cfg, splits)
+        return dw
+    xt = x.permute(0, 3, 1, 2)
+    if spec.pt or spec.pb or spec.pl or spec.pr:
+        xt = F.pad(xt, (spec.pl, spec.pr, spec.pt, spec.pb))
+    g = torch.nn.grad.conv2d_weight(xt, (spec.cout, spec.cin_pad, spec.kh, spec.kw), dz.permute(0, 3, 1, 2),
+                                    stride=(spec.sh, spec.sw), dilation=(spec.dh, spec.dw))
+    dw.add_(g.permute(0, 2, 3, 1).reshape(dw.shape).to(dw.dtype))
+    return dw
+
+
+# --------------------------------------------------------------------------- BN
+class BNSaved:
+    __slots__ = ("mean", "invstd")
+
+    def __init__(self, mean, invstd):
+        self.mean = mean
+        self.invstd = invstd
+
+
+def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, relu: bool,
+               residual=None, stats=None, stats_T: int = 0):
+    """Training BN: batch stats (from a fused conv slab when given), running-stat update,
+    out = act(gamma*xhat + beta [+ residual])."""
+    N, H, W, C = z.shape
+    M = N * H * W
+    if z.is_cuda:
+        hcb = _ext.ops()
+        if stats is None:
+            stats_T = hcb.bn_partials(M, C)
+            stats = torch.empty(stats_T * 2 * C, dtype=torch.float32, device=z.device)
+            hcb.bn_stats(z, M, C, ld(z), stats)
+        mean = torch.empty(C, dtype=torch.float32, device=z.device)
+        invstd = torch.empty_like(mean)
+        hcb.bn_finalize(stats, stats_T, C, float(M), eps, momentum, mean, invstd, running_mean, running_var)
+        hcb.bn_apply(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0, M, C,
+                     mean, invstd, gamma, beta, 1 if relu else 0)
+        return BNSaved(mean, invstd)
+    zf = z.reshape(M, C) if z.is_contiguous() else z.contiguous().reshape(M, C)
+    mean = zf.mean(0)
+    var = zf.var(0, unbiased=False)
+    invstd = torch.rsqrt(var + eps)
+    with torch.no_grad():
+        if running_mean is not None:
+            unb = var * M / max(M - 1, 1)
+            running_mean.mul_(momentum).add_((1 - momentum) * mean)
+            running_var.mul_(momentum).add_((1 - momentum) * unb)
+    y = (z - mean) * (invstd * gamma) + beta
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = torch.relu(y)
+    out.copy_(y)
+    return BNSaved(mean, invstd)
+
+
+def bn_backward(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, gres=None):
+    """BN(+ReLU) backward. relu_mode: 0 none, 1 mask from stored output y (residual blocks),
+    2 mask recomputed from z. Writes dgamma/dbeta (fp32, overwrite), dz, and optionally the
+    masked upstream gradient gres (the residual branch's gradient)."""
+    N, H, W, C = z.shape
+    M = N * H * W
+    if z.is_cuda:
+        hcb = _ext.ops()
+        T = hcb.bn_partials(M, C)
+        slab = torch.empty(T * 2 * C, dtype=torch.float32, device=z.device)
+        hcb.bn_bwd_reduce(dy, ld(dy), y if relu_mode == 1 else None, ld(y) if relu_mode == 1 else 0, z, ld(z),
+                          M, C, saved.mean, saved.invstd, gamma, beta, relu_mode, slab, gres,
+                          ld(gres) if gres is not None else 0)
+        hcb.bn_bwd_finalize(slab, T, C, dgamma, dbeta)
+        hcb.bn_bwd_apply(dy, ld(dy), y if relu_mode == 1 else None, ld(y) if relu_mode == 1 else 0, z, ld(z),
+                         dz, ld(dz), M, C, saved.mean, saved.invstd, gamma, beta, dgamma, dbeta, relu_mode)
+        return dz
+    xhat = (z - saved.mean) * saved.invstd
+    g = dy
+    if relu_mode == 1:
+        g = dy * (y > 0).to(dy.dtype)
+    elif relu_mode == 2:
+        g = dy * ((xhat * gamma + beta) > 0).to(dy.dtype)
+    gf = g.reshape(-1, C) if g.is_contiguous() else g.contiguous().reshape(-1, C)
+    xf = xhat.reshape(-1, C)
+    db = gf.sum(0)
+    dg = (gf * xf).sum(0)
+    dbeta.copy_(db)
+    dgamma.copy_(dg)
+    dz.copy_(gamma.to(dz.dtype) * saved.invstd * (g - db / M - xhat * dg / M))
+    if gres is not None:
+        gres.copy_(g)
+    return dz
+
+
+# ----------------------------------------------------------------------- pooling
+def pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad):
+    N, H, W, C = x.shape
+    _, P, Q, _ = out.shape
+    return [N, H, W, C, ld(x), P, Q, ld(out), kh, kw, sh, sw, pt, pl, 1 if is_max else 0, 1 if incl_pad else 0]
+
+
+def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False):
+    pt, pb, pl, pr = pads
+    if x.is_cuda:
+        _ext.ops().pool_fwd(x, out, pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad))
+        return out
+    xt = x.permute(0, 3, 1, 2)
+    if is_max:
+        xt = F.pad(xt, (pl, pr, pt, pb), value=-float("inf"))
+        y = F.max_pool2d(xt, (kh, kw), (sh, sw))
+    else:
+        if incl_pad:
+            y = F.avg_pool2d(F.pad(xt, (pl, pr, pt, pb)), (kh, kw), (sh, sw))
+        else:
+            ones = torch.ones_like(xt[:, :1])
+            s = F.avg_pool2d(F.pad(xt, (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+            c = F.avg_pool2d(F.pad(ones, (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+            y = s / c
+    out.copy_(y.permute(0, 2, 3, 1))
+    return out
+
+
+def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, accumulate=False):
+    pt, pb, pl, pr = pads
+    if x.is_cuda:
+        _ext.ops().pool_bwd(dy, x, y, dx, pool_geom(x, dy, kh, kw, sh, sw, pt, pl, is_max, incl_pad), accumulate)
+        return dx
+    with torch.enable_grad():
+        xr = x.detach().clone().requires_grad_(True)
+        yy = torch.empty_like(y)
+        xt = xr.permute(0, 3, 1, 2)
+        if is_max:
+            t = F.max_pool2d(F.pad(xt, (pl, pr, pt, pb), value=-float("inf")), (kh, kw), (sh, sw))
+        elif incl_pad:
+            t = F.avg_pool2d(F.pad(xt, (pl, pr, pt, pb)), (kh, kw), (sh, sw))
+        else:
+            ones = torch.ones_like(xt[:, :1])
+            s = F.avg_pool2d(F.pad(xt, (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+            c = F.avg_pool2d(F.pad(ones, (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+            t = s / c
+        del yy
+        (g,) = torch.autograd.grad(t, xr, dy.permute(0, 3, 1, 2))
+    if accumulate:
+        dx.add_(g)
+    else:
+        dx.copy_(g)
+    return dx
+
+
+def gap_forward(x, out):
+    N, H, W, C = x.shape
+    if x.is_cuda:
+        assert x.is_contiguous()
+        _ext.ops().gap_fwd(x, out, N, H * W, C)
+        return out
+    out.copy_(x.mean(dim=(1, 2)))
+    return out
+
+
+def gap_backward(dy, dx):
+    N, H, W, C = dx.shape
+    if dy.is_cuda:
+        _ext.ops().gap_bwd(dy, dx, N, H * W, C)
+        return dx
+    dx.copy_((dy / (H * W)).view(N, 1, 1, C).expand(N, H, W, C))
+    return dx
+
+
+# ------------------------------------------------------------------------- loss
+def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale):
+    """Per-row cross entropy (into row_loss) and dlogits = (softmax - onehot) * scale."""
+    B = labels.numel()
+    if logits.is_cuda:
+        _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale)
+        return
+    lg = logits[:, :ncls].float()
+    lse = torch.logsumexp(lg, dim=1)
+    row_loss.copy_(lse - lg.gather(1, labels.view(-1, 1)).view(-1))
+    p = torch.softmax(lg, dim=1)
+    p[torch.arange(B), labels] -= 1.0
+    dlogits.zero_()
+    dlogits[:, :ncls].copy_(p * scale)
+
+
+def colsum(g, M, N, out):
+    if g.is_cuda:
+        _ext.ops().colsum(g, ld(g), M, N, out)
+        return out
+    out.copy_(g[:M, :N].float().sum(0))
+    return out
+
+
+# -------------------------------------------------------------------- optimizer
+def sgd_momentum(w, mom, g, n_decay, hyper, l2=None, nesterov=False):
+    """TF ApplyMomentum on the flat parameter buffer: hyper = [lr, momentum, wd, grad_scale]."""
+    if w.is_cuda:
+        _ext.ops().sgd_momentum(w, mom, g, n_decay, hyper, l2, nesterov)
+        return
+    lr, mu, wd, gs = [float(v) for v in hyper.tolist()]
+    gg = g * gs
+    if n_decay > 0:
+        if l2 is not None:
+            l2 += (w[:n_decay] * w[:n_decay]).sum()
+        gg[:n_decay] += wd * w[:n_decay]
+    mom.mul_(mu).add_(gg)
+    if nesterov:
+        w.sub_(lr * (gg + mu * mom))
+    else:
+        w.sub_(lr * mom)

@@ -1,0 +1,84 @@
+"""Gradient reducers over the flat gradient buffer.
+
+The flat gradient buffer IS the fusion buffer (see nn/params.py): buckets are contiguous
+slices of it, so there is no memcpy-in/out (Horovod's MEMCPY_IN_FUSION_BUFFER /
+MEMCPY_OUT_FUSION_BUFFER phases disappear). Bucket size follows
+``HOROVOD_FUSION_THRESHOLD`` (the reference sets 128 MiB,
+/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:105).
+
+* ``TorchDistReducer``: torch.distributed all_reduce per bucket (RCCL when the process group
+  backend is "nccl" on ROCm, gloo on CPU). Optional bf16/fp16 compression
+  (Horovod ``Compression.fp16``): pack kernel (scale + cast) -> allreduce -> unpack kernel.
+* The C++ RCCL bucket engine with a side HIP stream lives in ``parallel/native.py``.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_FUSION_BYTES = 128 * 1024 * 1024
+
+
+def fusion_threshold_bytes() -> int:
+    v = os.environ.get("HOROVOD_FUSION_THRESHOLD")
+    if v is None or v == "":
+        return DEFAULT_FUSION_BYTES
+    return max(int(v), 4096)
+
+
+def make_buckets(numel: int, bucket_elems: int, align: int = 64) -> List[Tuple[int, int]]:
+    """Split [0, numel) into contiguous (offset, length) buckets, issued from the END of the
+    buffer first (the classifier / last stage's gradients are produced first in backward)."""
+    bucket_elems = max(align, bucket_elems // align * align)
+    out = []
+    end = numel
+    while end > 0:
+        start = max(0, end - bucket_elems)
+        out.append((start, end - start))
+        end = start
+    return out
+
+
+class TorchDistReducer:
+    graph_safe = False
+
+    def __init__(self, group=None, compression: Optional[str] = None, bucket_bytes: Optional[int] = None,
+                 average: bool = False):
+        self.group = group
+        self.compression = compression  # None | "fp16" | "bf16"
+        self.bucket_bytes = bucket_bytes or fusion_threshold_bytes()
+        self.average = average  # the trainer folds 1/N into the optimizer by default
+        self._buckets = None
+        self._comm_buf = None
+
+    def allreduce_(self, flat: torch.Tensor) -> torch.Tensor:
+        world = dist.get_world_size(self.group)
+        if world == 1:
+            return flat
+        esz = 2 if self.compression else 4
+        if self._buckets is None:
+            self._buckets = make_buckets(flat.numel(), self.bucket_bytes // esz)
+        if self.compression:
+            dt = torch.float16 if self.compression == "fp16" else torch.bfloat16
+            if self._comm_buf is None or self._comm_buf.numel() != flat.numel():
+                self._comm_buf = torch.empty(flat.numel(), dtype=dt, device=flat.device)
+        for off, n in self._buckets:
+            view = flat[off:off + n]
+            if self.compression:
+                cb = self._comm_buf[off:off + n]
+                cb.copy_(view)
+                dist.all_reduce(cb, group=self.group)
+                view.copy_(cb)
+            else:
+                dist.all_reduce(view, group=self.group)
+        if self.average:
+            flat.mul_(1.0 / world)
+        return flat
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        if dist.get_world_size(self.group) > 1:
+            dist.broadcast(t, src=root, group=self.group)
+        return t

@@ -1,0 +1,184 @@
+"""One synchronous data-parallel training step, HIP-graph captured.
+
+The step is the reference's tf_cnn_benchmarks ``train_op`` with
+``--variable_update=horovod --optimizer=momentum`` (/root/reference/benchmark-scripts/
+run-tf-sing-ucx-openmpi.sh:62-81):
+
+    zero grads -> fp32 masters -> bf16 GEMM operands (1 launch)
+    -> forward (conv/BN/ReLU/pool/affine) -> softmax cross-entropy (+dlogits)
+    -> backward (weight grads written straight into the flat gradient buffer)
+    -> gradient allreduce (average over workers)
+    -> fused momentum update (+L2 weight decay, + L2 term of total_loss) in ONE launch.
+
+On the GPU the whole sequence (≈500-1000 kernels for ResNet-50) is captured once in a HIP
+graph (torch.cuda.CUDAGraph == hipGraph on ROCm) and replayed every step, so Python and
+launch overhead vanish. With more than one worker the gradient allreduce runs between two
+graphs, (a) fwd+bwd and (b) optimizer, on the communication engine (see
+``parallel/``), so collectives never need to be captured.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Optional
+
+import torch
+
+from .ops import functional as Fn
+from .ops import _ext
+
+
+def resnet_lr_schedule(global_batch: int, num_examples_per_epoch: int = 1281167, base_lr: float = 0.128,
+                       warmup_epochs: float = 5.0):
+    """tf_cnn_benchmarks ResnetModel.get_learning_rate: linear warmup, then piecewise decay
+    at epochs 30/60/80/90; base lr scaled by batch/256."""
+    rescaled = base_lr * global_batch / 256.0
+    per_epoch = num_examples_per_epoch / float(global_batch)
+    bounds = [int(per_epoch * e) for e in (30, 60, 80, 90)]
+    vals = [rescaled * v for v in (1, 0.1, 0.01, 0.001, 0.0001)]
+    warm = int(per_epoch * warmup_epochs)
+
+    def lr(step: int) -> float:
+        if step < warm:
+            return rescaled * step / max(warm, 1)
+        for b, v in zip(bounds, vals):
+            if step < b:
+                return v
+        return vals[-1]
+
+    return lr
+
+
+def constant_lr(v: float):
+    return lambda step: v
+
+
+class Trainer:
+    def __init__(self, model, batch_size: int, lr_fn: Callable[[int], float], momentum: float = 0.9,
+                 weight_decay: float = 4e-5, reducer=None, world_size: int = 1, use_graph: bool = True,
+                 nesterov: bool = False, graph_warmup: int = 2, forward_only: bool = False):
+        self.model = model
+        self.ps = model.ps
+        self.B = batch_size
+        self.dev = model.device
+        self.lr_fn = lr_fn
+        self.momentum = momentum
+        self.wd = weight_decay
+        self.reducer = reducer
+        self.world = world_size
+        self.nesterov = nesterov
+        self.forward_only = forward_only
+        self.use_graph = use_graph and self.dev.type == "cuda"
+        self.graph_warmup = graph_warmup
+        ld = model.fc.ld if hasattr(model, "fc") else (model.num_classes + 7) // 8 * 8
+        self.ld = ld
+        self.hyper = torch.tensor([0.0, momentum, weight_decay, 1.0 / world_size], dtype=torch.float32,
+                                  device=self.dev)
+        self.row_loss = torch.zeros(batch_size, dtype=torch.float32, device=self.dev)
+        self.dlogits = torch.zeros((batch_size, ld), dtype=model.act_dtype, device=self.dev)
+        self.l2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        self.steps_done = 0
+        self._g_fb = None
+        self._g_opt = None
+        self._g_all = None
+        self._static = None
+
+    # ---------------------------------------------------------------- pieces
+    def _forward_backward(self, images, labels):
+        ps = self.ps
+        if not self.forward_only:
+            ps.zero_grad()
+        ps.repack()
+        logits = self.model.forward(images)
+        Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B)
+        if self.forward_only:
+            self.model.clear()
+            return
+        self.model.backward(self.dlogits)
+
+    def _optimizer(self):
+        if self.forward_only:
+            self.loss.copy_(self.row_loss.mean().view(1))
+            return
+        self.l2.zero_()
+        Fn.sgd_momentum(self.ps.master, self.ps.momentum, self.ps.grad, self.ps.n_decay, self.hyper, self.l2,
+                        self.nesterov)
+        self.loss.copy_((self.row_loss.mean() + 0.5 * self.wd * self.l2).view(1))
+
+    def _reduce(self):
+        if self.reducer is not None and self.world > 1 and not self.forward_only:
+            self.reducer.allreduce_(self.ps.grad)
+
+    def _eager_step(self, images, labels):
+        self._forward_backward(images, labels)
+        self._reduce()
+        self._optimizer()
+
+    # ---------------------------------------------------------------- graphs
+    def _capture(self, images, labels):
+        torch.cuda.synchronize()
+        single = self.reducer is None or self.world <= 1 or getattr(self.reducer, "graph_safe", False)
+        pool = torch.cuda.graph_pool_handle()
+        if single:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self._forward_backward(images, labels)
+                if self.reducer is not None and self.world > 1:
+                    self._reduce()
+                self._optimizer()
+            self._g_all = g
+        else:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, pool=pool):
+                self._forward_backward(images, labels)
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=pool):
+                self._optimizer()
+            self._g_fb, self._g_opt = g1, g2
+        self._static = (images, labels)
+        torch.cuda.synchronize()
+
+    def step(self, images, labels):
+        """One training step; returns the device tensor holding total_loss of this step."""
+        self.hyper[0:1].fill_(float(self.lr_fn(self.steps_done)))
+        if not self.use_graph:
+            self._eager_step(images, labels)
+        else:
+            if self._static is not None and (images is not self._static[0] or labels is not self._static[1]):
+                raise ValueError("graph-captured trainer needs the same (static) input buffers every step")
+            if self._g_all is None and self._g_fb is None:
+                if self.steps_done < self.graph_warmup:
+                    self._eager_step(images, labels)
+                    self.steps_done += 1
+                    return self.loss
+                self._capture(images, labels)
+            if self._g_all is not None:
+                self._g_all.replay()
+            else:
+                self._g_fb.replay()
+                self._reduce()
+                self._g_opt.replay()
+        self.steps_done += 1
+        return self.loss
+
+
+def synthetic_batch(model, batch_size: int, seed: int = 0):
+    """tf_cnn_benchmarks synthetic ImageNet: truncated-normal images (mean 127, sd 60) and
+    uniform labels in [0, num_classes-1), created once and reused every step."""
+    shape = model.input_shape(batch_size)
+    dev = model.device
+    if dev.type == "cuda":
+        img = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+        lab = torch.empty(batch_size, dtype=torch.int64, device=dev)
+        hcb = _ext.ops()
+        hcb.synth_images(img, 3, shape[3], 127.0, 60.0, seed + 1)
+        hcb.synth_labels(lab, model.num_classes - 1, seed + 2)
+        return img, lab
+    g = torch.Generator().manual_seed(seed)
+    img = torch.empty(shape, dtype=torch.float32)
+    img.normal_(0, 1, generator=g)
+    img.clamp_(-2, 2).mul_(60.0).add_(127.0)
+    if shape[3] > 3:
+        img[..., 3:] = 0
+    lab = torch.randint(0, model.num_classes - 1, (batch_size,), generator=g, dtype=torch.int64)
+    return img.to(dev), lab.to(dev)

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 synchronous data-parallel training throughput,
+images/sec for the whole node, bs=64 per GPU, synthetic ImageNet, random-init weights
+(BASELINE.json metric; the reference's tf_cnn_benchmarks run of
+/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-113).
+
+    python bench.py --gpus N --steps K --warmup W          (N=1)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One process per MI355X; gradients averaged with RCCL over xGMI. W untimed warmup steps
+(the first ones also capture the HIP graph), then EXACTLY K timed steps bracketed by
+barrier + device sync; the max time over ranks is used; rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch_size", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--compression", default=None, choices=[None, "fp16", "bf16"])
+    ap.add_argument("--engine", default="torch", choices=["native", "torch"])
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        print("bench.py needs a GPU", file=sys.stderr)
+        sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.trainer import Trainer, resnet_lr_schedule, synthetic_batch
+    from azure_hc_intel_tf_amd.ops import _ext
+
+    _ext.load()
+    reducer = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        from azure_hc_intel_tf_amd.parallel import make_reducer
+
+        reducer = make_reducer(args.engine, compression=args.compression)
+
+    model = create_model(args.model, device=dev)
+    B = args.batch_size
+    if reducer is not None:
+        reducer.broadcast_(model.ps.master, 0)
+        reducer.broadcast_(model.ps.buf, 0)
+    images, labels = synthetic_batch(model, B, seed=rank)
+    trainer = Trainer(model, B, resnet_lr_schedule(B * world), reducer=reducer, world_size=world,
+                      use_graph=not args.no_graph)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    warmup = max(args.warmup, 0)
+    for _ in range(warmup):
+        trainer.step(images, labels)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step(images, labels)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = float(trainer.loss.item())
+    ips = world * B * args.steps / elapsed
+    if rank == 0:
+        res = {
+            "metric": "images/sec (whole node) ResNet-50 bs=64/worker at 1/2/4/8 MI355X"
+            if args.model == "resnet50" else f"images/sec (whole node) {args.model} bs={B}/worker",
+            "value": round(ips, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (ips / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (truncated-normal ImageNet 224x224, random-init weights)",
+            "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
+                       "image_size": model.image_size, "parallelism": f"dp{world}",
+                       "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": not args.no_graph,
+                       "engine": args.engine if world > 1 else None, "compression": args.compression,
+                       "final_loss": round(loss, 4)},
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,479 @@
+// torch.library registrations (namespace `hcb`) for the hand-written gfx950 kernels.
+//
+// Every op is a thin, allocation-free launcher: Python pre-allocates outputs with the
+// caching allocator (so the whole training step can be captured in a HIP graph) and
+// passes geometry as an int list; the launcher validates shapes / byte ranges on the
+// host BEFORE anything reaches the GPU (an out-of-range gather must never be launched)
+// and enqueues on the current HIP stream.
+#include <torch/library.h>
+#include <ATen/core/Tensor.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/util/Exception.h>
+
+#include "kernels/kernels.h"
+
+using at::Tensor;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "hcb: ", name, " must be a GPU tensor");
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "hcb: ", name, " must be bfloat16");
+}
+void check_f32(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "hcb: ", name, " must be float32");
+}
+// bytes addressable from t.data_ptr() to the end of its storage
+int64_t avail_bytes(const Tensor& t) {
+  return (int64_t)t.storage().nbytes() - t.storage_offset() * (int64_t)t.element_size();
+}
+void check_range(const Tensor& t, int64_t need_bytes, const char* name) {
+  TORCH_CHECK(need_bytes <= avail_bytes(t), "hcb: ", name, " needs ", need_bytes,
+              " bytes but only ", avail_bytes(t), " are addressable");
+}
+void check_align16(const void* p, const char* name) {
+  TORCH_CHECK(((uintptr_t)p & 15) == 0, "hcb: ", name, " must be 16-byte aligned");
+}
+
+// geom = [N,H,W,C,ldx, P,Q,R,S, sh,sw,ph,pw,dh,dw,idh,idw, Nout,K,Kpad,ldy,
+//         remap,OH,OW,osh,osw, beta,out_f32]
+void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
+                const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
+                at::IntArrayRef g, int64_t cfg) {
+  TORCH_CHECK(g.size() == 28, "hcb.conv_igemm: geom must have 28 entries");
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_cuda(y, "y");
+  hcb::ConvParams p{};
+  p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];
+  p.P = g[5]; p.Q = g[6]; p.R = g[7]; p.S = g[8];
+  p.stride_h = g[9]; p.stride_w = g[10]; p.pad_h = g[11]; p.pad_w = g[12];
+  p.dil_h = g[13]; p.dil_w = g[14]; p.idil_h = g[15]; p.idil_w = g[16];
+  p.Nout = g[17]; p.K = g[18]; p.Kpad = g[19]; p.ldy = g[20];
+  p.remap = g[21]; p.OH = g[22]; p.OW = g[23]; p.osh = g[24]; p.osw = g[25];
+  p.beta = g[26]; p.out_f32 = g[27];
+  p.M = p.N * p.P * p.Q;
+  TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0 && p.ldx >= p.C, "hcb.conv_igemm: C, ldx must be multiples of 8");
+  TORCH_CHECK(p.Kpad % 64 == 0 && p.Kpad >= p.K && p.K == p.R * p.S * p.C,
+              "hcb.conv_igemm: Kpad must be a multiple of 64 >= K = R*S*C");
+  TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm: bad ldy");
+  TORCH_CHECK(p.idil_h >= 1 && p.idil_w >= 1 && p.dil_h >= 1 && p.dil_w >= 1, "hcb.conv_igemm: bad dilation");
+  TORCH_CHECK(p.M > 0 && p.Nout > 0, "hcb.conv_igemm: empty problem");
+  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * 2 + (int64_t)p.C * 2;
+  int64_t wb = (int64_t)p.Nout * p.Kpad * 2;
+  TORCH_CHECK(xb < (1ll << 31) && wb < (1ll << 31), "hcb.conv_igemm: operand exceeds 2 GiB buffer range");
+  check_range(x, xb, "x");
+  check_range(w, wb, "w");
+  int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
+  if (p.remap)
+    TORCH_CHECK((p.P - 1) * p.osh < p.OH && (p.Q - 1) * p.osw < p.OW, "hcb.conv_igemm: remap out of range");
+  int64_t esz = p.out_f32 ? 4 : 2;
+  TORCH_CHECK(y.scalar_type() == (p.out_f32 ? at::kFloat : at::kBFloat16), "hcb.conv_igemm: y dtype");
+  check_range(y, rows * p.ldy * esz - (p.ldy - ((p.Nout + 7) / 8) * 8) * esz, "y");
+  check_align16(x.data_ptr(), "x");
+  check_align16(w.data_ptr(), "w");
+  check_align16(y.data_ptr(), "y");
+  p.x = x.data_ptr();
+  p.w = w.data_ptr();
+  p.y = y.data_ptr();
+  p.yres = nullptr;
+  if (p.beta) {
+    TORCH_CHECK(yres.has_value(), "hcb.conv_igemm: beta needs yres");
+    check_range(*yres, rows * p.ldy * esz - (p.ldy - ((p.Nout + 7) / 8) * 8) * esz, "yres");
+    check_align16(yres->data_ptr(), "yres");
+    p.yres = yres->data_ptr();
+  }
+  p.bias = nullptr;
+  if (bias.has_value()) {
+    check_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() >= p.Nout, "hcb.conv_igemm: bias too small");
+    p.bias = bias->data_ptr<float>();
+  }
+  p.stats = nullptr;
+  if (stats.has_value()) {
+    check_f32(*stats, "stats");
+    int tiles_m = (p.M + hcb::conv_tile_m(cfg) - 1) / hcb::conv_tile_m(cfg);
+    TORCH_CHECK(stats->numel() >= (int64_t)tiles_m * 2 * p.Nout, "hcb.conv_igemm: stats slab too small");
+    p.stats = stats->data_ptr<float>();
+  }
+  p.x_bytes = (uint32_t)xb;
+  p.w_bytes = (uint32_t)wb;
+  hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
+}
+
+int64_t conv_tiles_m(int64_t M, int64_t cfg) {
+  int t = hcb::conv_tile_m((int)cfg);
+  return (M + t - 1) / t;
+}
+
+// geom = [N,H,W,C,ldx, P,Q,R,S, sh,sw,ph,pw,dh,dw, Nout,ldy]
+void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArrayRef g, int64_t cfg,
+                int64_t splits) {
+  TORCH_CHECK(g.size() == 17, "hcb.conv_wgrad: geom must have 17 entries");
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_f32(dw, "dw");
+  hcb::WgradParams p{};
+  p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];
+  p.P = g[5]; p.Q = g[6]; p.R = g[7]; p.S = g[8];
+  p.stride_h = g[9]; p.stride_w = g[10]; p.pad_h = g[11]; p.pad_w = g[12];
+  p.dil_h = g[13]; p.dil_w = g[14];
+  p.Nout = g[15]; p.ldy = g[16];
+  p.K = p.R * p.S * p.C;
+  p.M = p.N * p.P * p.Q;
+  TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0, "hcb.conv_wgrad: C, ldx multiples of 8");
+  TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= p.Nout, "hcb.conv_wgrad: bad ldy");
+  TORCH_CHECK(splits >= 1, "hcb.conv_wgrad: splits >= 1");
+  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * 2 + (int64_t)p.C * 2;
+  int64_t yb = ((int64_t)p.M - 1) * p.ldy * 2 + (int64_t)((p.Nout + 7) / 8) * 16;
+  TORCH_CHECK(xb < (1ll << 31) && yb < (1ll << 31), "hcb.conv_wgrad: operand exceeds 2 GiB");
+  check_range(x, xb, "x");
+  check_range(dy, yb, "dy");
+  check_range(dw, (int64_t)p.Nout * p.K * 4, "dw");
+  check_align16(x.data_ptr(), "x");
+  check_align16(dy.data_ptr(), "dy");
+  int nkt = (p.M + 63) / 64;
+  int per = (nkt + (int)splits - 1) / (int)splits;
+  p.ksteps_per_split = per;
+  int eff_splits = (nkt + per - 1) / per;
+  p.fd_pq = hcb::make_fastdiv((uint32_t)(p.P * p.Q));
+  p.fd_q = hcb::make_fastdiv((uint32_t)p.Q);
+  p.fd_c = hcb::make_fastdiv((uint32_t)p.C);
+  p.fd_s = hcb::make_fastdiv((uint32_t)p.S);
+  p.dy = dy.data_ptr();
+  p.x = x.data_ptr();
+  p.dw = dw.data_ptr<float>();
+  p.dy_bytes = (uint32_t)yb;
+  p.x_bytes = (uint32_t)xb;
+  hcb::launch_conv_wgrad(p, (int)cfg, eff_splits, cur_stream());
+}
+
+void bn_stats(const Tensor& x, int64_t M, int64_t C, int64_t ldx, const Tensor& slab) {
+  check_bf16(x, "x");
+  check_f32(slab, "slab");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0, "hcb.bn_stats: C % 8 == 0, C <= 2048");
+  check_range(x, M * ldx * 2, "x");
+  int T = hcb::bn_num_partials((int)M, (int)C);
+  TORCH_CHECK(slab.numel() >= (int64_t)T * 2 * C, "hcb.bn_stats: slab too small");
+  hcb::launch_bn_stats(x.data_ptr(), (int)M, (int)C, (int)ldx, slab.data_ptr<float>(), T, cur_stream());
+}
+
+int64_t bn_partials(int64_t M, int64_t C) { return hcb::bn_num_partials((int)M, (int)C); }
+
+void bn_finalize(const Tensor& slab, int64_t T, int64_t C, double count, double eps, double momentum,
+                 const Tensor& mean, const Tensor& invstd, const c10::optional<Tensor>& rm,
+                 const c10::optional<Tensor>& rv) {
+  check_f32(slab, "slab");
+  check_f32(mean, "mean");
+  check_f32(invstd, "invstd");
+  TORCH_CHECK(slab.numel() >= T * 2 * C && mean.numel() >= C && invstd.numel() >= C, "hcb.bn_finalize: sizes");
+  float* rmp = nullptr;
+  float* rvp = nullptr;
+  if (rm.has_value() && rv.has_value()) {
+    check_f32(*rm, "running_mean");
+    check_f32(*rv, "running_var");
+    rmp = rm->data_ptr<float>();
+    rvp = rv->data_ptr<float>();
+  }
+  hcb::launch_bn_finalize(slab.data_ptr<float>(), (int)T, (int)C, count, (float)eps, (float)momentum,
+                          mean.data_ptr<float>(), invstd.data_ptr<float>(), rmp, rvp, cur_stream());
+}
+
+void bn_apply(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, const c10::optional<Tensor>& res,
+              int64_t ldr, int64_t M, int64_t C, const Tensor& mean, const Tensor& invstd,
+              const Tensor& gamma, const Tensor& beta, int64_t relu) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldy % 8 == 0, "hcb.bn_apply: C/ld");
+  check_range(x, M * ldx * 2, "x");
+  check_range(y, ((M - 1) * ldy + C) * 2, "y");
+  const void* rp = nullptr;
+  if (res.has_value()) {
+    check_bf16(*res, "res");
+    TORCH_CHECK(ldr % 8 == 0, "hcb.bn_apply: ldr");
+    check_range(*res, ((M - 1) * ldr + C) * 2, "res");
+    rp = res->data_ptr();
+  }
+  hcb::launch_bn_apply(x.data_ptr(), (int)ldx, y.data_ptr(), (int)ldy, rp, (int)ldr, (int)M, (int)C,
+                       mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                       beta.data_ptr<float>(), (int)relu, cur_stream());
+}
+
+void bn_bwd_reduce(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
+                   const Tensor& x, int64_t ldx, int64_t M, int64_t C, const Tensor& mean,
+                   const Tensor& invstd, const Tensor& gamma, const Tensor& beta, int64_t relu,
+                   const Tensor& slab, const c10::optional<Tensor>& gout, int64_t ldg) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_f32(slab, "slab");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "hcb.bn_bwd_reduce: C");
+  check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
+  check_range(x, ((M - 1) * ldx + C) * 2, "x");
+  const void* yp = nullptr;
+  if (relu == 1) {
+    TORCH_CHECK(y.has_value(), "hcb.bn_bwd_reduce: relu=1 needs y");
+    check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    yp = y->data_ptr();
+  }
+  void* gp = nullptr;
+  if (gout.has_value()) {
+    check_bf16(*gout, "gout");
+    check_range(*gout, ((M - 1) * ldg + C) * 2, "gout");
+    gp = gout->data_ptr();
+  }
+  int T = hcb::bn_num_partials((int)M, (int)C);
+  TORCH_CHECK(slab.numel() >= (int64_t)T * 2 * C, "hcb.bn_bwd_reduce: slab too small");
+  hcb::launch_bn_bwd_reduce2(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, (int)M,
+                             (int)C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                             gamma.data_ptr<float>(), beta.data_ptr<float>(), (int)relu,
+                             slab.data_ptr<float>(), T, gp, (int)ldg, cur_stream());
+}
+
+void bn_bwd_finalize(const Tensor& slab, int64_t T, int64_t C, const Tensor& dgamma, const Tensor& dbeta) {
+  check_f32(slab, "slab");
+  check_f32(dgamma, "dgamma");
+  check_f32(dbeta, "dbeta");
+  hcb::launch_bn_bwd_finalize(slab.data_ptr<float>(), (int)T, (int)C, dgamma.data_ptr<float>(),
+                              dbeta.data_ptr<float>(), cur_stream());
+}
+
+void bn_bwd_apply(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
+                  const Tensor& x, int64_t ldx, const Tensor& dx, int64_t lddx, int64_t M, int64_t C,
+                  const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
+                  const Tensor& dgamma, const Tensor& dbeta, int64_t relu) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_bf16(dx, "dx");
+  check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
+  check_range(x, ((M - 1) * ldx + C) * 2, "x");
+  check_range(dx, ((M - 1) * lddx + C) * 2, "dx");
+  const void* yp = nullptr;
+  if (relu == 1) {
+    TORCH_CHECK(y.has_value(), "hcb.bn_bwd_apply: relu=1 needs y");
+    check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    yp = y->data_ptr();
+  }
+  hcb::launch_bn_bwd_apply2(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx,
+                            dx.data_ptr(), (int)lddx, (int)M, (int)C, mean.data_ptr<float>(),
+                            invstd.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                            dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu, cur_stream());
+}
+
+// geom = [N,H,W,C,ldx,P,Q,ldy,kh,kw,sh,sw,ph,pw,is_max,incl_pad]
+void pool_fwd(const Tensor& x, const Tensor& y, at::IntArrayRef g) {
+  TORCH_CHECK(g.size() == 16, "hcb.pool_fwd: geom");
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_fwd: C/ld % 8");
+  check_range(x, g[0] * g[1] * g[2] * g[4] * 2, "x");
+  check_range(y, g[0] * g[5] * g[6] * g[7] * 2, "y");
+  hcb::launch_pool_fwd(x.data_ptr(), y.data_ptr(), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8],
+                       g[9], g[10], g[11], g[12], g[13], g[14], g[15], cur_stream());
+}
+
+void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& dx, at::IntArrayRef g,
+              bool accumulate) {
+  TORCH_CHECK(g.size() == 16, "hcb.pool_bwd: geom");
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  check_bf16(dx, "dx");
+  check_range(x, g[0] * g[1] * g[2] * g[4] * 2, "x");
+  check_range(dx, g[0] * g[1] * g[2] * g[4] * 2, "dx");
+  check_range(y, g[0] * g[5] * g[6] * g[7] * 2, "y");
+  check_range(dy, g[0] * g[5] * g[6] * g[7] * 2, "dy");
+  hcb::launch_pool_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), dx.data_ptr(), g[0], g[1], g[2], g[3],
+                       g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], g[15],
+                       accumulate ? 1 : 0, cur_stream());
+}
+
+void gap_fwd(const Tensor& x, const Tensor& y, int64_t N, int64_t HW, int64_t C) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(C % 8 == 0, "hcb.gap_fwd: C % 8");
+  check_range(x, N * HW * C * 2, "x");
+  check_range(y, N * C * 2, "y");
+  hcb::launch_gap_fwd(x.data_ptr(), y.data_ptr(), (int)N, (int)HW, (int)C, cur_stream());
+}
+
+void gap_bwd(const Tensor& dy, const Tensor& dx, int64_t N, int64_t HW, int64_t C) {
+  check_bf16(dy, "dy");
+  check_bf16(dx, "dx");
+  check_range(dy, N * C * 2, "dy");
+  check_range(dx, N * HW * C * 2, "dx");
+  hcb::launch_gap_bwd(dy.data_ptr(), dx.data_ptr(), (int)N, (int)HW, (int)C, cur_stream());
+}
+
+void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_t ncls,
+                  const Tensor& row_loss, const Tensor& dlogits, int64_t lddl, double scale) {
+  check_f32(logits, "logits");
+  check_cuda(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "hcb.softmax_xent: labels int64");
+  check_bf16(dlogits, "dlogits");
+  int64_t B = labels.numel();
+  check_range(logits, B * ld * 4, "logits");
+  check_range(dlogits, B * lddl * 2, "dlogits");
+  TORCH_CHECK(row_loss.numel() >= B, "hcb.softmax_xent: row_loss");
+  hcb::launch_softmax_xent(logits.data_ptr<float>(), (int)ld, labels.data_ptr<int64_t>(), (int)B, (int)ncls,
+                           row_loss.data_ptr<float>(), dlogits.data_ptr(), (int)lddl, (float)scale,
+                           cur_stream());
+}
+
+void colsum(const Tensor& g, int64_t ld, int64_t M, int64_t N, const Tensor& out) {
+  check_cuda(g, "g");
+  check_f32(out, "out");
+  bool f32 = g.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || g.scalar_type() == at::kBFloat16, "hcb.colsum: dtype");
+  check_range(g, ((M - 1) * ld + N) * (f32 ? 4 : 2), "g");
+  hcb::launch_colsum2(g.data_ptr(), (int)ld, (int)M, (int)N, f32 ? 1 : 0, out.data_ptr<float>(), cur_stream());
+}
+
+void sgd_momentum(const Tensor& w, const Tensor& mom, const Tensor& g, int64_t n_decay, const Tensor& hyper,
+                  const c10::optional<Tensor>& l2, bool nesterov) {
+  check_f32(w, "w");
+  check_f32(mom, "mom");
+  check_f32(g, "g");
+  check_f32(hyper, "hyper");
+  TORCH_CHECK(w.is_contiguous() && mom.is_contiguous() && g.is_contiguous(), "hcb.sgd_momentum: contiguous");
+  TORCH_CHECK(w.numel() == mom.numel() && w.numel() == g.numel(), "hcb.sgd_momentum: sizes");
+  check_align16(w.data_ptr(), "w");
+  check_align16(mom.data_ptr(), "mom");
+  check_align16(g.data_ptr(), "g");
+  hcb::launch_sgd_momentum(w.data_ptr<float>(), mom.data_ptr<float>(), g.data_ptr<float>(), w.numel(),
+                           n_decay, hyper.data_ptr<float>(), l2.has_value() ? l2->data_ptr<float>() : nullptr,
+                           nesterov ? 1 : 0, cur_stream());
+}
+
+void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, int64_t max_work) {
+  check_f32(master, "master");
+  check_bf16(pack, "pack");
+  check_cuda(table, "table");
+  TORCH_CHECK(table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 9, "hcb.weight_pack: table [n][9] int64");
+  TORCH_CHECK(table.is_contiguous(), "hcb.weight_pack: table contiguous");
+  hcb::launch_weight_pack(master.data_ptr<float>(), (uint16_t*)pack.data_ptr(),
+                          reinterpret_cast<const hcb::WPackEntry*>(table.data_ptr<int64_t>()),
+                          (int)table.size(0), max_work, cur_stream());
+}
+
+void cast_f32_bf16(const Tensor& x, const Tensor& y) {
+  check_f32(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "hcb.cast: shape");
+  hcb::launch_cast_f32_bf16(x.data_ptr<float>(), (uint16_t*)y.data_ptr(), x.numel(), cur_stream());
+}
+
+void add_bf16(const Tensor& a, const Tensor& b, const Tensor& y) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  check_bf16(y, "y");
+  TORCH_CHECK(a.numel() == b.numel() && a.numel() == y.numel() && a.numel() % 8 == 0, "hcb.add_bf16: sizes");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && y.is_contiguous(), "hcb.add_bf16: contiguous");
+  hcb::launch_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream());
+}
+
+void scale_f32(const Tensor& x, double s) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "hcb.scale_f32: contiguous");
+  hcb::launch_scale_f32(x.data_ptr<float>(), x.numel(), (float)s, cur_stream());
+}
+
+void l2norm_sq(const Tensor& x, const Tensor& out) {
+  check_f32(x, "x");
+  check_f32(out, "out");
+  hcb::launch_l2norm_sq(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), cur_stream());
+}
+
+void synth_images(const Tensor& out, int64_t C, int64_t Cpad, double mean, double std, int64_t seed) {
+  check_bf16(out, "out");
+  TORCH_CHECK(out.numel() % Cpad == 0, "hcb.synth_images: numel % Cpad");
+  hcb::launch_synth_images(out.data_ptr(), out.numel() / Cpad, (int)C, (int)Cpad, (float)mean, (float)std,
+                           (uint64_t)seed, cur_stream());
+}
+
+void synth_labels(const Tensor& out, int64_t ncls, int64_t seed) {
+  check_cuda(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kLong, "hcb.synth_labels: int64");
+  hcb::launch_synth_labels(out.data_ptr<int64_t>(), (int)out.numel(), (int)ncls, (uint64_t)seed, cur_stream());
+}
+
+void bucket_pack(const Tensor& src, const Tensor& dst, double scale) {
+  check_f32(src, "src");
+  check_cuda(dst, "dst");
+  bool bf = dst.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || dst.scalar_type() == at::kFloat, "hcb.bucket_pack: dst dtype");
+  TORCH_CHECK(src.numel() == dst.numel(), "hcb.bucket_pack: sizes");
+  hcb::launch_bucket_pack(src.data_ptr<float>(), dst.data_ptr(), src.numel(), (float)scale, bf ? 1 : 0, cur_stream());
+}
+
+void bucket_unpack(const Tensor& src, const Tensor& dst, double scale) {
+  check_cuda(src, "src");
+  check_f32(dst, "dst");
+  bool bf = src.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(src.numel() == dst.numel(), "hcb.bucket_unpack: sizes");
+  hcb::launch_bucket_unpack(src.data_ptr(), dst.data_ptr<float>(), src.numel(), (float)scale, bf ? 1 : 0,
+                            cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(hcb, m) {
+  m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg) -> ()");
+  m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
+  m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
+  m.def("bn_stats(Tensor x, int M, int C, int ldx, Tensor(a!) slab) -> ()");
+  m.def("bn_partials(int M, int C) -> int", bn_partials);
+  m.def("bn_finalize(Tensor slab, int T, int C, float count, float eps, float momentum, Tensor(a!) mean, Tensor(b!) invstd, Tensor(c!)? running_mean, Tensor(d!)? running_var) -> ()");
+  m.def("bn_apply(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu) -> ()");
+  m.def("bn_bwd_reduce(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) slab, Tensor(b!)? gout, int ldg) -> ()");
+  m.def("bn_bwd_finalize(Tensor slab, int T, int C, Tensor(a!) dgamma, Tensor(b!) dbeta) -> ()");
+  m.def("bn_bwd_apply(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor dgamma, Tensor dbeta, int relu) -> ()");
+  m.def("pool_fwd(Tensor x, Tensor(a!) y, int[] geom) -> ()");
+  m.def("pool_bwd(Tensor dy, Tensor x, Tensor y, Tensor(a!) dx, int[] geom, bool accumulate) -> ()");
+  m.def("gap_fwd(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
+  m.def("gap_bwd(Tensor dy, Tensor(a!) dx, int N, int HW, int C) -> ()");
+  m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale) -> ()");
+  m.def("colsum(Tensor g, int ld, int M, int N, Tensor(a!) out) -> ()");
+  m.def("sgd_momentum(Tensor(a!) w, Tensor(b!) mom, Tensor g, int n_decay, Tensor hyper, Tensor(c!)? l2, bool nesterov) -> ()");
+  m.def("weight_pack(Tensor master, Tensor(a!) pack, Tensor table, int max_work) -> ()");
+  m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()");
+  m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
+  m.def("scale_f32(Tensor(a!) x, float s) -> ()");
+  m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
+  m.def("synth_images(Tensor(a!) out, int C, int Cpad, float mean, float std, int seed) -> ()");
+  m.def("synth_labels(Tensor(a!) out, int ncls, int seed) -> ()");
+  m.def("bucket_pack(Tensor src, Tensor(a!) dst, float scale) -> ()");
+  m.def("bucket_unpack(Tensor src, Tensor(a!) dst, float scale) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
+  m.impl("conv_igemm", conv_igemm);
+  m.impl("conv_wgrad", conv_wgrad);
+  m.impl("bn_stats", bn_stats);
+  m.impl("bn_finalize", bn_finalize);
+  m.impl("bn_apply", bn_apply);
+  m.impl("bn_bwd_reduce", bn_bwd_reduce);
+  m.impl("bn_bwd_finalize", bn_bwd_finalize);
+  m.impl("bn_bwd_apply", bn_bwd_apply);
+  m.impl("pool_fwd", pool_fwd);
+  m.impl("pool_bwd", pool_bwd);
+  m.impl("gap_fwd", gap_fwd);
+  m.impl("gap_bwd", gap_bwd);
+  m.impl("softmax_xent", softmax_xent);
+  m.impl("colsum", colsum);
+  m.impl("sgd_momentum", sgd_momentum);
+  m.impl("weight_pack", weight_pack);
+  m.impl("cast_f32_bf16", cast_f32_bf16);
+  m.impl("add_bf16", add_bf16);
+  m.impl("scale_f32", scale_f32);
+  m.impl("l2norm_sq", l2norm_sq);
+  m.impl("synth_images", synth_images);
+  m.impl("synth_labels", synth_labels);
+  m.impl("bucket_pack", bucket_pack);
+  m.impl("bucket_unpack", bucket_unpack);
+}

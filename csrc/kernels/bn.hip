@@ -1,0 +1,291 @@
+// Training-mode batch normalisation for NHWC bf16 activations on gfx950
+// (the MKL-DNN FusedBatchNorm fwd/bwd role; tf_cnn_benchmarks ResNet
+// config decay=0.9, eps=1e-5, scale=True).
+//
+// Layout: x is [M = N*H*W][C] with C contiguous. Every thread owns one 16-byte vector of
+// 8 channels, keeps that channel vector's scale/shift (or partial sums) in registers and
+// walks rows, so every global access is a 16-byte coalesced load/store and the per
+// channel parameters are read once per thread (guide: always vectorize bf16).
+//
+// Statistics are reduced in two levels: per-block partial sums in an fp32 slab
+// [T][2][C] (the conv epilogue writes the same slab format, so stats can be fused into
+// the producing GEMM), then a finalize kernel that sums the slab in fp64 — no float
+// atomics, bitwise reproducible.
+#include "common.h"
+#include "kernels.h"
+
+namespace hcb {
+
+// thread -> (channel vector, row lane) mapping shared by all kernels below
+struct RowMap {
+  int cv, r0, rstep, active;
+};
+__device__ __forceinline__ RowMap rowmap(int C) {
+  RowMap m;
+  int CV = C >> 3;
+  int rows = 256 / CV;
+  m.cv = threadIdx.x % CV;
+  m.r0 = threadIdx.x / CV;
+  m.rstep = rows;
+  m.active = m.r0 < rows;
+  return m;
+}
+
+// reduce per-thread partial (s1, s2) over threads sharing a channel vector, write slab row
+__device__ __forceinline__ void slab_write(float* lds, const float* s1, const float* s2, int C,
+                                           const RowMap& rm, float* slab_row) {
+  int CV = C >> 3;
+  int rows = 256 / CV;
+  // lds: [rows][C] for s1 then s2
+  if (rm.active) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      lds[rm.r0 * C + rm.cv * 8 + e] = s1[e];
+      lds[rows * C + rm.r0 * C + rm.cv * 8 + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rows; ++r) {
+      a += lds[r * C + c];
+      b += lds[rows * C + r * C + c];
+    }
+    slab_row[c] = a;
+    slab_row[C + c] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restrict__ x, int M, int C,
+                                                       int ldx, float* slab) {
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  RowMap rm = rowmap(C);
+  float s1[8] = {0}, s2[8] = {0};
+  if (rm.active) {
+    for (int m = blockIdx.x * rm.rstep + rm.r0; m < M; m += gridDim.x * rm.rstep) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(x + (size_t)m * ldx + rm.cv * 8);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += f[e];
+        s2[e] += f[e] * f[e];
+      }
+    }
+  }
+  slab_write(lds_f, s1, s2, C, rm, slab + (size_t)blockIdx.x * 2 * C);
+}
+
+__global__ void bn_finalize_kernel(const float* slab, int T, int C, double count, float eps,
+                                   float momentum, float* mean, float* invstd, float* run_mean,
+                                   float* run_var) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int t = 0; t < T; ++t) {
+    a += (double)slab[(size_t)t * 2 * C + c];
+    b += (double)slab[(size_t)t * 2 * C + C + c];
+  }
+  double mu = a / count;
+  double var = b / count - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean != nullptr) {
+    double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+    run_mean[c] = (float)(momentum * run_mean[c] + (1.0 - momentum) * mu);
+    run_var[c] = (float)(momentum * run_var[c] + (1.0 - momentum) * unbiased);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, int ldx,
+                                                       uint16_t* __restrict__ y, int ldy,
+                                                       const uint16_t* __restrict__ res, int ldr,
+                                                       int M, int C, const float* mean,
+                                                       const float* invstd, const float* gamma,
+                                                       const float* beta, int relu) {
+  RowMap rm = rowmap(C);
+  if (!rm.active) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    int c = rm.cv * 8 + e;
+    float s = gamma[c] * invstd[c];
+    sc[e] = s;
+    sh[e] = beta[c] - mean[c] * s;
+  }
+  for (int m = blockIdx.x * rm.rstep + rm.r0; m < M; m += gridDim.x * rm.rstep) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + (size_t)m * ldx + rm.cv * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = f[e] * sc[e] + sh[e];
+    if (res != nullptr) {
+      float r[8];
+      unpack8(*reinterpret_cast<const u32x4*>(res + (size_t)m * ldr + rm.cv * 8), r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += r[e];
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+    }
+    *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + rm.cv * 8) = pack8(f);
+  }
+}
+
+// relu: 0 = none, 1 = mask from stored output y (y > 0), 2 = mask recomputed from x
+// (gamma*xhat + beta > 0; valid when the block had no residual add)
+__device__ __forceinline__ void bwd_load(const uint16_t* dy, int lddy, const uint16_t* y, int ldyv,
+                                         const uint16_t* x, int ldx, int m, int cv, int relu,
+                                         const float* mu, const float* is, const float* sc,
+                                         const float* sh, float* g, float* xh) {
+  float d[8], xv[8];
+  unpack8(*reinterpret_cast<const u32x4*>(dy + (size_t)m * lddy + cv * 8), d);
+  unpack8(*reinterpret_cast<const u32x4*>(x + (size_t)m * ldx + cv * 8), xv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xh[e] = (xv[e] - mu[e]) * is[e];
+  if (relu == 1) {
+    float yv[8];
+    unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)m * ldyv + cv * 8), yv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? d[e] : 0.f;
+  } else if (relu == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (xv[e] * sc[e] + sh[e]) > 0.f ? d[e] : 0.f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = d[e];
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
+    const uint16_t* __restrict__ x, int ldx, int M, int C, const float* mean, const float* invstd,
+    const float* gamma, const float* beta, int relu, float* slab, uint16_t* gout, int ldg) {
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  RowMap rm = rowmap(C);
+  float s1[8] = {0}, s2[8] = {0};
+  if (rm.active) {
+    float mu[8], is[8], sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int c = rm.cv * 8 + e;
+      mu[e] = mean[c];
+      is[e] = invstd[c];
+      sc[e] = gamma != nullptr ? gamma[c] * is[e] : 0.f;
+      sh[e] = beta != nullptr ? beta[c] - mu[e] * sc[e] : 0.f;
+    }
+    for (int m = blockIdx.x * rm.rstep + rm.r0; m < M; m += gridDim.x * rm.rstep) {
+      float g[8], xh[8];
+      bwd_load(dy, lddy, y, ldyv, x, ldx, m, rm.cv, relu, mu, is, sc, sh, g, xh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += g[e];
+        s2[e] += g[e] * xh[e];
+      }
+      if (gout != nullptr) *reinterpret_cast<u32x4*>(gout + (size_t)m * ldg + rm.cv * 8) = pack8(g);
+    }
+  }
+  slab_write(lds_f, s1, s2, C, rm, slab + (size_t)blockIdx.x * 2 * C);
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* slab, int T, int C, float* dgamma,
+                                       float* dbeta) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int t = 0; t < T; ++t) {
+    a += (double)slab[(size_t)t * 2 * C + c];
+    b += (double)slab[(size_t)t * 2 * C + C + c];
+  }
+  dbeta[c] = (float)a;
+  dgamma[c] = (float)b;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
+    const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ dx, int lddx, int M, int C,
+    const float* mean, const float* invstd, const float* gamma, const float* beta,
+    const float* dgamma, const float* dbeta, int relu) {
+  RowMap rm = rowmap(C);
+  if (!rm.active) return;
+  float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    int c = rm.cv * 8 + e;
+    mu[e] = mean[c];
+    is[e] = invstd[c];
+    sc[e] = gamma[c] * is[e];
+    sh[e] = beta[c] - mu[e] * sc[e];
+    k1[e] = dbeta[c] * invM;
+    k2[e] = dgamma[c] * invM;
+  }
+  for (int m = blockIdx.x * rm.rstep + rm.r0; m < M; m += gridDim.x * rm.rstep) {
+    float g[8], xh[8], o[8];
+    bwd_load(dy, lddy, y, ldyv, x, ldx, m, rm.cv, relu, mu, is, sc, sh, g, xh);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
+    *reinterpret_cast<u32x4*>(dx + (size_t)m * lddx + rm.cv * 8) = pack8(o);
+  }
+}
+
+static int bn_grid(int M, int C) {
+  int rows = 256 / (C / 8);
+  int need = (M + rows - 1) / rows;
+  // ~4 blocks per CU over 256 CUs; each block loops over its rows
+  int g = need < 1024 ? need : 1024;
+  return g < 1 ? 1 : g;
+}
+
+int bn_num_partials(int M, int C) { return bn_grid(M, C); }
+
+void launch_bn_stats(const void* x, int M, int C, int ldx, float* slab, int T, hipStream_t st) {
+  int rows = 256 / (C / 8);
+  size_t lds = (size_t)2 * rows * C * 4;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(T), dim3(256), lds, st, (const uint16_t*)x, M, C, ldx,
+                     slab);
+}
+
+void launch_bn_finalize(const float* slab, int T, int C, double count, float eps, float momentum,
+                        float* mean, float* invstd, float* run_mean, float* run_var,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, slab, T, C,
+                     count, eps, momentum, mean, invstd, run_mean, run_var);
+}
+
+void launch_bn_apply(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M,
+                     int C, const float* mean, const float* invstd, const float* gamma,
+                     const float* beta, int relu, hipStream_t st) {
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_grid(M, C)), dim3(256), 0, st, (const uint16_t*)x,
+                     ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, mean, invstd, gamma,
+                     beta, relu);
+}
+
+void launch_bn_bwd_reduce2(const void* dy, int lddy, const void* y, int ldyv, const void* x,
+                           int ldx, int M, int C, const float* mean, const float* invstd,
+                           const float* gamma, const float* beta, int relu, float* slab, int T,
+                           void* gout, int ldg, hipStream_t st) {
+  int rows = 256 / (C / 8);
+  size_t lds = (size_t)2 * rows * C * 4;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(T), dim3(256), lds, st, (const uint16_t*)dy, lddy,
+                     (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, mean, invstd, gamma,
+                     beta, relu, slab, (uint16_t*)gout, ldg);
+}
+
+void launch_bn_bwd_finalize(const float* slab, int T, int C, float* dgamma, float* dbeta,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, slab, T, C,
+                     dgamma, dbeta);
+}
+
+void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx,
+                          void* dx, int lddx, int M, int C, const float* mean, const float* invstd,
+                          const float* gamma, const float* beta, const float* dgamma,
+                          const float* dbeta, int relu, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(M, C)), dim3(256), 0, st,
+                     (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx,
+                     (uint16_t*)dx, lddx, M, C, mean, invstd, gamma, beta, dgamma, dbeta, relu);
+}
+
+}  // namespace hcb

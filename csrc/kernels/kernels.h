@@ -1,0 +1,143 @@
+// Host-visible launch interface of the HIP kernels (no torch headers here so the
+// .hip translation units compile in seconds).
+#pragma once
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#else
+#include <hip/hip_runtime_api.h>
+#endif
+#include <stdint.h>
+
+namespace hcb {
+
+// Unsigned division by a runtime-invariant divisor: q = (umulhi(n, m) + n) >> s,
+// exact for n < 2^31 (round-up magic number method).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+#if defined(__HIPCC__)
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+#endif
+
+// ---------------------------------------------------------------- implicit GEMM conv
+struct ConvParams {
+  const void* x;   // NHWC bf16 input, pixel stride ldx elements
+  const void* w;   // [Nout][Kpad] bf16
+  void* y;         // output rows, stride ldy (bf16 or fp32)
+  const void* yres;  // beta-accumulate source (same layout as y)
+  const float* bias;  // [Nout] or null
+  float* stats;       // [tiles_m][2][Nout] or null
+  int N, H, W, C, ldx;
+  int P, Q, R, S;
+  int stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, idil_h, idil_w;
+  int Nout, K, Kpad, ldy;
+  int M;
+  int remap, OH, OW, osh, osw;
+  int beta, out_f32;
+  uint32_t x_bytes, w_bytes;
+};
+void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
+int conv_tile_m(int cfg);
+int conv_tile_n(int cfg);
+
+// weight-gradient implicit GEMM: dW[Nout][K] += sum_m dY[m][Nout] * im2col(X)[m][K]
+struct WgradParams {
+  const void* dy;  // [M][ldy] bf16
+  const void* x;   // NHWC bf16, pixel stride ldx
+  float* dw;       // [Nout][K] fp32 (atomically accumulated)
+  int N, H, W, C, ldx;
+  int P, Q, R, S;
+  int stride_h, stride_w, pad_h, pad_w, dil_h, dil_w;
+  int Nout, K, M, ldy;
+  int ksteps_per_split;
+  FastDiv fd_pq, fd_q, fd_c, fd_s;
+  uint32_t dy_bytes, x_bytes;
+};
+void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st);
+int wgrad_tile_m(int cfg);
+int wgrad_tile_n(int cfg);
+
+// ---------------------------------------------------------------- batch norm
+// stats slab [T][2][C] -> mean, invstd (fp32) and running stats update
+void launch_bn_finalize(const float* slab, int T, int C, double count, float eps, float momentum,
+                        float* mean, float* invstd, float* run_mean, float* run_var,
+                        hipStream_t st);
+// stats directly from an activation tensor [M][C] (when not fused into the producer)
+void launch_bn_stats(const void* x, int M, int C, int ldx, float* slab, int T, hipStream_t st);
+// y = act(gamma*(x-mean)*invstd + beta [+ res])
+void launch_bn_apply(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M,
+                     int C, const float* mean, const float* invstd, const float* gamma,
+                     const float* beta, int relu, hipStream_t st);
+int bn_num_partials(int M, int C);
+// backward reduce: g = dy*mask (relu: 0 none, 1 mask y>0, 2 mask recomputed from x);
+// per-block partial sums of g and g*xhat -> slab; optionally writes g to gout
+void launch_bn_bwd_reduce2(const void* dy, int lddy, const void* y, int ldyv, const void* x,
+                           int ldx, int M, int C, const float* mean, const float* invstd,
+                           const float* gamma, const float* beta, int relu, float* slab, int T,
+                           void* gout, int ldg, hipStream_t st);
+// dgamma/dbeta from slab
+void launch_bn_bwd_finalize(const float* slab, int T, int C, float* dgamma, float* dbeta,
+                            hipStream_t st);
+// dx = gamma*invstd*(g - dbeta/M - xhat*dgamma/M)
+void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, const void* x,
+                          int ldx, void* dx, int lddx, int M, int C, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta,
+                          const float* dgamma, const float* dbeta, int relu, hipStream_t st);
+
+// ---------------------------------------------------------------- pooling
+void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,
+                     int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
+                     int count_include_pad, hipStream_t st);
+void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int N, int H, int W,
+                     int C, int ldx, int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph,
+                     int pw, int is_max, int count_include_pad, int accum, hipStream_t st);
+void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
+void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
+
+// ---------------------------------------------------------------- loss / fc helpers
+void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
+                         float* row_loss, void* dlogits, int lddl, float scale, hipStream_t st);
+void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st);
+
+// ---------------------------------------------------------------- optimizer / weights
+// hyper (device fp32): [lr, momentum, weight_decay, grad_scale] so a captured graph
+// picks up a new learning rate every replay
+void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
+                         const float* hyper, float* l2_out, int nesterov, hipStream_t st);
+struct WPackEntry {  // all int64 so the table is a plain int64 tensor [n][9]
+  int64_t src_off;   // fp32 master offset (elements)
+  int64_t pack_off;  // bf16 packed [Nout][Kpad] offset (elements), -1 = skip
+  int64_t tr_off;    // bf16 transposed-flipped [C][Kpad_t] offset, -1 = skip
+  int64_t Nout, R, S, C, Kpad, Kpad_t;
+};
+void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
+                        int n_entries, int64_t max_work, hipStream_t st);
+void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
+void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
+void launch_add_bf16(const void* a, const void* b, void* y, int64_t n, hipStream_t st);
+void launch_scale_f32(float* x, int64_t n, float s, hipStream_t st);
+void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st);
+
+// ---------------------------------------------------------------- data
+void launch_synth_images(void* out, int64_t n_pix, int C, int Cpad, float mean, float std,
+                         uint64_t seed, hipStream_t st);
+void launch_synth_labels(int64_t* out, int n, int ncls, uint64_t seed, hipStream_t st);
+
+// ---------------------------------------------------------------- gradient buckets
+void launch_bucket_pack(const float* src, void* dst, int64_t n, float scale, int to_bf16,
+                        hipStream_t st);
+void launch_bucket_unpack(const void* src, float* dst, int64_t n, float scale, int from_bf16,
+                          hipStream_t st);
+
+}  // namespace hcb

@@ -1,0 +1,317 @@
+// Loss, optimizer, weight-preparation, data and gradient-bucket kernels (gfx950).
+//
+//   * softmax_xent: tf.losses.sparse_softmax_cross_entropy + its gradient in one pass
+//     (one 256-thread block per row, wave64 shuffles + LDS for the row max / sum).
+//   * sgd_momentum: TF ApplyMomentum over ALL parameters in ONE launch (flat fp32
+//     master/momentum/grad buffers; L2 weight decay folded in as wd*w for the decayed
+//     prefix, Horovod averaging / loss-scale folded in as grad_scale, and the L2 term of
+//     the reported total_loss reduced on the fly) — SURVEY.md §2.6 "ApplyMomentum",
+//     "L2 weight decay"; tf_cnn_benchmarks flags --optimizer=momentum
+//     (/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:73).
+//   * weight_pack: one multi-tensor launch producing the bf16 GEMM operands of every
+//     conv from the fp32 masters: [Cout][Kpad] for fwd and the flipped/transposed
+//     [Cin][Kpad_t] for the data gradient.
+//   * synth: tf_cnn_benchmarks synthetic ImageNet (truncated normal, mean 127, sd 60,
+//     generated once on device) + uniform labels.
+//   * bucket pack/unpack: Horovod fusion-buffer memcpy-in/out role with scale and
+//     optional bf16 compression.
+#include "common.h"
+#include "kernels.h"
+
+namespace hcb {
+
+// ------------------------------------------------------------------ softmax xent
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits, int ld,
+                                                           const int64_t* __restrict__ labels,
+                                                           int ncls, float* row_loss,
+                                                           uint16_t* dl, int lddl, float scale) {
+  __shared__ float red[8];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* lr = logits + (size_t)row * ld;
+  float mx = -INFINITY;
+  for (int c = tid; c < ncls; c += 256) mx = fmaxf(mx, lr[c]);
+  mx = wave_max(mx);
+  if (lane == 0) red[wid] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int c = tid; c < ncls; c += 256) s += __expf(lr[c] - mx);
+  s = wave_sum(s);
+  if (lane == 0) red[4 + wid] = s;
+  __syncthreads();
+  s = red[4] + red[5] + red[6] + red[7];
+  const float lse = mx + __logf(s);
+  const int lab = (int)labels[row];
+  if (tid == 0) row_loss[row] = lse - lr[lab];
+  const float inv = 1.f / s;
+  for (int c = tid; c < lddl; c += 256) {
+    float g = 0.f;
+    if (c < ncls) g = (__expf(lr[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * scale;
+    dl[(size_t)row * lddl + c] = f2bf(g);
+  }
+}
+
+// column sums: out[n] = sum_m g[m][n] (bf16 or fp32 input), fp32 out
+__global__ __launch_bounds__(256) void colsum_kernel(const void* g, int ld, int M, int N, int is_f32,
+                                                     float* out) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int m = 0; m < M; ++m) {
+    if (is_f32)
+      s += reinterpret_cast<const float*>(g)[(size_t)m * ld + n];
+    else
+      s += bf2f(reinterpret_cast<const uint16_t*>(g)[(size_t)m * ld + n]);
+  }
+  out[n] = s;
+}
+
+// ------------------------------------------------------------------ optimizer
+__global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w,
+                                                           float* __restrict__ mom,
+                                                           const float* __restrict__ g, int64_t n,
+                                                           int64_t n_decay,
+                                                           const float* __restrict__ hyper,
+                                                           float* l2_out, int nesterov) {
+  __shared__ float red[4];
+  const float lr = hyper[0], mu = hyper[1], wd = hyper[2], gscale = hyper[3];
+  float l2 = 0.f;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 wv = reinterpret_cast<f32x4*>(w)[i];
+    f32x4 mv = reinterpret_cast<f32x4*>(mom)[i];
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      int64_t j = i * 4 + e;
+      float gg = gv[e] * gscale;
+      if (j < n_decay) {
+        gg += wd * wv[e];
+        l2 += wv[e] * wv[e];
+      }
+      float m = mu * mv[e] + gg;
+      mv[e] = m;
+      wv[e] -= nesterov ? lr * (gg + mu * m) : lr * m;
+    }
+    reinterpret_cast<f32x4*>(w)[i] = wv;
+    reinterpret_cast<f32x4*>(mom)[i] = mv;
+  }
+  // scalar tail
+  for (int64_t j = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    float gg = g[j] * gscale;
+    if (j < n_decay) {
+      gg += wd * w[j];
+      l2 += w[j] * w[j];
+    }
+    float m = mu * mom[j] + gg;
+    mom[j] = m;
+    w[j] -= nesterov ? lr * (gg + mu * m) : lr * m;
+  }
+  if (l2_out != nullptr) {
+    l2 = wave_sum(l2);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l2;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(l2_out, red[0] + red[1] + red[2] + red[3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ x, int64_t n,
+                                                     float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += x[i] * x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+// ------------------------------------------------------------------ weights
+__global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ master,
+                                                          uint16_t* __restrict__ pack,
+                                                          const WPackEntry* __restrict__ ents) {
+  const WPackEntry e = ents[blockIdx.y];
+  const int K = (int)(e.R * e.S * e.C);
+  const int Kt = (int)(e.R * e.S * e.Nout);
+  const float* src = master + e.src_off;
+  const int64_t n1 = e.pack_off >= 0 ? (int64_t)e.Nout * e.Kpad : 0;
+  const int64_t n2 = e.tr_off >= 0 ? (int64_t)e.C * e.Kpad_t : 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n1 + n2;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n1) {
+      int j = (int)(i / e.Kpad), k = (int)(i % e.Kpad);
+      float v = k < K ? src[(int64_t)j * K + k] : 0.f;
+      pack[e.pack_off + i] = f2bf(v);
+    } else {
+      int64_t t = i - n1;
+      int c = (int)(t / e.Kpad_t), k = (int)(t % e.Kpad_t);
+      float v = 0.f;
+      if (k < Kt) {
+        int tap = k / e.Nout, kk = k % e.Nout;
+        int rr = tap / e.S, ss = tap % e.S;
+        int r = e.R - 1 - rr, s = e.S - 1 - ss;
+        v = src[(((int64_t)kk * e.R + r) * e.S + s) * e.C + c];
+      }
+      pack[e.tr_off + t] = f2bf(v);
+    }
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* x, uint16_t* y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+__global__ void cast_bf16_f32_kernel(const uint16_t* x, float* y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = bf2f(x[i]);
+}
+__global__ void add_bf16_kernel(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float fa[8], fb[8];
+    unpack8(reinterpret_cast<const u32x4*>(a)[i], fa);
+    unpack8(reinterpret_cast<const u32x4*>(b)[i], fb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) fa[e] += fb[e];
+    reinterpret_cast<u32x4*>(y)[i] = pack8(fa);
+  }
+}
+__global__ void scale_f32_kernel(float* x, int64_t n, float s) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] *= s;
+}
+
+// ------------------------------------------------------------------ synthetic data
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+__device__ __forceinline__ float u01(uint64_t key) {
+  return ((mix32(key) >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+__global__ void synth_images_kernel(uint16_t* out, int64_t n_pix, int C, int Cpad, float mean,
+                                    float std, uint64_t seed) {
+  const int64_t total = n_pix * Cpad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % Cpad);
+    float v = 0.f;
+    if (c < C) {
+      // truncated normal: resample until |z| <= 2 (tf.truncated_normal)
+      float z = 0.f;
+      for (uint64_t a = 0; a < 64; ++a) {
+        uint64_t key = seed * 0x9E3779B97F4A7C15ULL + (uint64_t)i * 128 + 2 * a;
+        float u1 = u01(key), u2 = u01(key + 1);
+        z = sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853f * u2);
+        if (fabsf(z) <= 2.f) break;
+        z = 0.f;
+      }
+      v = mean + std * z;
+    }
+    out[i] = f2bf(v);
+  }
+}
+
+__global__ void synth_labels_kernel(int64_t* out, int n, int ncls, uint64_t seed) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int64_t)(mix32(seed * 0x2545F4914F6CDD1DULL + i) % (uint32_t)ncls);
+}
+
+// ------------------------------------------------------------------ gradient buckets
+__global__ void bucket_pack_kernel(const float* src, void* dst, int64_t n, float scale, int to_bf16) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v = src[i] * scale;
+    if (to_bf16)
+      reinterpret_cast<uint16_t*>(dst)[i] = f2bf(v);
+    else
+      reinterpret_cast<float*>(dst)[i] = v;
+  }
+}
+__global__ void bucket_unpack_kernel(const void* src, float* dst, int64_t n, float scale,
+                                     int from_bf16) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v = from_bf16 ? bf2f(reinterpret_cast<const uint16_t*>(src)[i])
+                        : reinterpret_cast<const float*>(src)[i];
+    dst[i] = v * scale;
+  }
+}
+
+static int grid_for(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
+                         float* row_loss, void* dlogits, int lddl, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls,
+                     row_loss, (uint16_t*)dlogits, lddl, scale);
+}
+void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256), dim3(256), 0, st, g, ld, M, N, is_f32,
+                     out);
+}
+void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
+                         const float* hyper, float* l2_out, int nesterov, hipStream_t st) {
+  hipLaunchKernelGGL(sgd_momentum_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, w, mom, g,
+                     n, n_decay, hyper, l2_out, nesterov);
+}
+void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(l2norm_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, out);
+}
+void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
+                        int n_entries, int64_t max_work, hipStream_t st) {
+  int gx = grid_for(max_work);
+  if (gx > 256) gx = 256;
+  hipLaunchKernelGGL(weight_pack_kernel, dim3(gx, n_entries), dim3(256), 0, st, master, pack,
+                     entries_dev);
+}
+void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);
+}
+void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);
+}
+void launch_add_bf16(const void* a, const void* b, void* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)a,
+                     (const uint16_t*)b, (uint16_t*)y, n / 8);
+}
+void launch_scale_f32(float* x, int64_t n, float s, hipStream_t st) {
+  hipLaunchKernelGGL(scale_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, s);
+}
+void launch_synth_images(void* out, int64_t n_pix, int C, int Cpad, float mean, float std,
+                         uint64_t seed, hipStream_t st) {
+  hipLaunchKernelGGL(synth_images_kernel, dim3(grid_for(n_pix * Cpad)), dim3(256), 0, st,
+                     (uint16_t*)out, n_pix, C, Cpad, mean, std, seed);
+}
+void launch_synth_labels(int64_t* out, int n, int ncls, uint64_t seed, hipStream_t st) {
+  hipLaunchKernelGGL(synth_labels_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out, n, ncls,
+                     seed);
+}
+void launch_bucket_pack(const float* src, void* dst, int64_t n, float scale, int to_bf16,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(bucket_pack_kernel, dim3(grid_for(n)), dim3(256), 0, st, src, dst, n, scale,
+                     to_bf16);
+}
+void launch_bucket_unpack(const void* src, float* dst, int64_t n, float scale, int from_bf16,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(bucket_unpack_kernel, dim3(grid_for(n)), dim3(256), 0, st, src, dst, n, scale,
+                     from_bf16);
+}
+
+}  // namespace hcb

@@ -1,0 +1,224 @@
+// Pooling kernels, NHWC bf16 (MKL-DNN max/avg pool role):
+//   * generic k x k max / average pool with TF-style (possibly asymmetric) padding:
+//     ResNet's 3x3/2 'SAME' max pool, Inception's 3x3/1 avg-pool branches and 3x3/2
+//     max-pool reductions, 8x8 avg pool heads.
+//   * backward as a GATHER over the (at most ceil(k/s)^2) windows covering an input
+//     pixel, so no atomics; the max pool recomputes the first-max position of each
+//     window (TF semantics: gradient goes to the first maximal element).
+//   * global average pool (spatial mean) fwd/bwd.
+// Each thread handles one pixel x 8 channels (16-byte vectors).
+#include "common.h"
+#include "kernels.h"
+
+namespace hcb {
+
+__global__ __launch_bounds__(256) void pool_fwd_kernel(const uint16_t* __restrict__ x,
+                                                       uint16_t* __restrict__ y, int N, int H,
+                                                       int W, int C, int ldx, int P, int Q,
+                                                       int ldy, int kh, int kw, int sh, int sw,
+                                                       int ph, int pw, int is_max, int incl_pad) {
+  const int CV = C >> 3;
+  const long total = (long)N * P * Q * CV;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    int cv = (int)(idx % CV);
+    long pix = idx / CV;
+    int q = (int)(pix % Q);
+    long t = pix / Q;
+    int p = (int)(t % P);
+    int n = (int)(t / P);
+    int h0 = p * sh - ph, w0 = q * sw - pw;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = is_max ? -INFINITY : 0.f;
+    int cnt = 0;
+    for (int r = 0; r < kh; ++r) {
+      int h = h0 + r;
+      if (h < 0 || h >= H) continue;
+      for (int s = 0; s < kw; ++s) {
+        int w = w0 + s;
+        if (w < 0 || w >= W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + ((size_t)(n * H + h) * W + w) * ldx + cv * 8), f);
+        ++cnt;
+        if (is_max) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] = fmaxf(acc[e], f[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += f[e];
+        }
+      }
+    }
+    if (!is_max) {
+      float div = incl_pad ? (float)(kh * kw) : (float)(cnt > 0 ? cnt : 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] /= div;
+    }
+    *reinterpret_cast<u32x4*>(y + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8) = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void pool_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+    const uint16_t* __restrict__ y, uint16_t* __restrict__ dx, int N, int H, int W, int C, int ldx,
+    int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
+    int incl_pad, int accum) {
+  const int CV = C >> 3;
+  const long total = (long)N * H * W * CV;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    int cv = (int)(idx % CV);
+    long pix = idx / CV;
+    int w = (int)(pix % W);
+    long t = pix / W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    float xv[8], g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = 0.f;
+    if (is_max)
+      unpack8(*reinterpret_cast<const u32x4*>(x + ((size_t)(n * H + h) * W + w) * ldx + cv * 8), xv);
+    // windows p with p*sh - ph <= h <= p*sh - ph + kh - 1
+    int p_lo = (h + ph - kh + sh) / sh;  // ceil((h+ph-kh+1)/sh) for non-negative numerators
+    if (h + ph - kh + 1 <= 0) p_lo = 0;
+    int p_hi = (h + ph) / sh;
+    if (p_hi > P - 1) p_hi = P - 1;
+    int q_lo = (w + pw - kw + sw) / sw;
+    if (w + pw - kw + 1 <= 0) q_lo = 0;
+    int q_hi = (w + pw) / sw;
+    if (q_hi > Q - 1) q_hi = Q - 1;
+    for (int p = p_lo; p <= p_hi; ++p) {
+      for (int q = q_lo; q <= q_hi; ++q) {
+        float d[8];
+        unpack8(*reinterpret_cast<const u32x4*>(dy + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8), d);
+        int h0 = p * sh - ph, w0 = q * sw - pw;
+        if (is_max) {
+          float yv[8];
+          unpack8(*reinterpret_cast<const u32x4*>(y + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8), yv);
+          // first position (row-major within the window) holding the max, per channel
+          int mine = (h - h0) * kw + (w - w0);
+          int first[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) first[e] = 1 << 30;
+          for (int r = 0; r < kh; ++r) {
+            int hh = h0 + r;
+            if (hh < 0 || hh >= H) continue;
+            for (int s = 0; s < kw; ++s) {
+              int ww = w0 + s;
+              if (ww < 0 || ww >= W) continue;
+              int pos = r * kw + s;
+              if (pos > mine) break;
+              float f[8];
+              unpack8(*reinterpret_cast<const u32x4*>(x + ((size_t)(n * H + hh) * W + ww) * ldx + cv * 8), f);
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if (f[e] == yv[e] && pos < first[e]) first[e] = pos;
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (first[e] == mine) g[e] += d[e];
+        } else {
+          int cnt;
+          if (incl_pad) {
+            cnt = kh * kw;
+          } else {
+            int hs = h0 < 0 ? 0 : h0, he = h0 + kh > H ? H : h0 + kh;
+            int ws = w0 < 0 ? 0 : w0, we = w0 + kw > W ? W : w0 + kw;
+            cnt = (he - hs) * (we - ws);
+          }
+          float inv = 1.f / (float)cnt;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] += d[e] * inv;
+        }
+      }
+    }
+    uint16_t* dp = dx + ((size_t)(n * H + h) * W + w) * ldx + cv * 8;
+    if (accum) {
+      float o[8];
+      unpack8(*reinterpret_cast<const u32x4*>(dp), o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] += o[e];
+    }
+    *reinterpret_cast<u32x4*>(dp) = pack8(g);
+  }
+}
+
+// global average pool [N][HW][C] -> [N][C]
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const uint16_t* __restrict__ x,
+                                                      uint16_t* __restrict__ y, int N, int HW,
+                                                      int C) {
+  const int CV = C >> 3;
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * CV) return;
+  int n = idx / CV, cv = idx % CV;
+  float acc[8] = {0};
+  for (int i = 0; i < HW; ++i) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + ((size_t)n * HW + i) * C + cv * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += f[e];
+  }
+  float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] *= inv;
+  *reinterpret_cast<u32x4*>(y + (size_t)n * C + cv * 8) = pack8(acc);
+}
+
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                      uint16_t* __restrict__ dx, int N, int HW,
+                                                      int C) {
+  const int CV = C >> 3;
+  const long total = (long)N * HW * CV;
+  float inv = 1.f / (float)HW;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    int cv = (int)(idx % CV);
+    long pix = idx / CV;
+    int n = (int)(pix / HW);
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dy + (size_t)n * C + cv * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= inv;
+    *reinterpret_cast<u32x4*>(dx + (size_t)pix * C + cv * 8) = pack8(f);
+  }
+}
+
+static int ew_grid(long total) {
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,
+                     int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
+                     int count_include_pad, hipStream_t st) {
+  long total = (long)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)x,
+                     (uint16_t*)y, N, H, W, C, ldx, P, Q, ldy, kh, kw, sh, sw, ph, pw, is_max,
+                     count_include_pad);
+}
+
+void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int N, int H, int W,
+                     int C, int ldx, int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph,
+                     int pw, int is_max, int count_include_pad, int accum, hipStream_t st) {
+  long total = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
+                     (const uint16_t*)x, (const uint16_t*)y, (uint16_t*)dx, N, H, W, C, ldx, P, Q,
+                     ldy, kh, kw, sh, sw, ph, pw, is_max, count_include_pad, accum);
+}
+
+void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
+  int total = N * (C / 8);
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, st,
+                     (const uint16_t*)x, (uint16_t*)y, N, HW, C);
+}
+
+void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
+  long total = (long)N * HW * (C / 8);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
+                     (uint16_t*)dx, N, HW, C);
+}
+
+}  // namespace hcb

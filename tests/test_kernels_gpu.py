@@ -1,0 +1,278 @@
+"""Numerics of every hand-written gfx950 kernel against the fp32 PyTorch reference path of
+the same op (the CPU implementation in ops/functional.py). Runs on an MI355X via gpurun."""
+import math
+
+import pytest
+import torch
+
+from azure_hc_intel_tf_amd.nn.params import ParamStore
+from azure_hc_intel_tf_amd.ops import _ext
+from azure_hc_intel_tf_amd.ops import functional as Fn
+from azure_hc_intel_tf_amd.ops.functional import ConvSpec
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def rel_err(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def make_conv(cin, cout, kh, kw, sh=1, sw=1, pads=(0, 0, 0, 0), seed=0, cin_pad=None, need_tr=True):
+    cin_pad = cin_pad or cin
+    pt, pb, pl, pr = pads
+    spec = ConvSpec(cin=cin, cin_pad=cin_pad, cout=cout, kh=kh, kw=kw, sh=sh, sw=sw, pt=pt, pl=pl, pb=pb, pr=pr)
+    ps = ParamStore(seed=seed)
+    p = ps.add("w", (cout, kh, kw, cin_pad), True, ps.variance_scaling(kh * kw * cin, cin if cin != cin_pad else -1))
+    pk = ps.add_pack(p, cout, kh, kw, cin_pad, spec.Kpad, spec.Kpad_t, want_tr=need_tr)
+    ps.finalize(DEV)
+    ps.repack()
+    return spec, p, pk
+
+
+CONV_CASES = [
+    # cin, cout, kh, kw, stride, pads, H  (ResNet-50 shapes at small batch + Inception-style)
+    (64, 256, 1, 1, 1, (0, 0, 0, 0), 14),
+    (256, 64, 1, 1, 1, (0, 0, 0, 0), 14),
+    (64, 64, 3, 3, 1, (1, 1, 1, 1), 14),
+    (256, 512, 1, 1, 2, (0, 0, 0, 0), 14),
+    (128, 128, 3, 3, 2, (1, 1, 1, 1), 14),
+    (8, 64, 7, 7, 2, (3, 3, 3, 3), 32),      # stem (3 channels padded to 8)
+    (80, 192, 3, 3, 1, (0, 0, 0, 0), 11),     # Inception: generic-C path, VALID
+    (128, 192, 1, 7, 1, (0, 0, 3, 3), 9),     # asymmetric 1x7
+    (160, 160, 7, 1, 1, (3, 3, 0, 0), 9),     # 7x1
+    (48, 64, 5, 5, 1, (2, 2, 2, 2), 9),       # 5x5
+    (32, 48, 3, 3, 2, (0, 0, 0, 0), 15),      # 3x3/2 VALID
+    (2048, 1001 + 7, 1, 1, 1, (0, 0, 0, 0), 1),  # FC-like, Nout not a multiple of the tile
+]
+
+
+def cpu_ref_conv(x, spec, w):
+    out = torch.empty((x.shape[0],) + spec.out_hw(x.shape[1], x.shape[2]) + (spec.cout,))
+    return Fn.conv_forward(x.float().cpu(), spec, None, w.float().cpu(), out)
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}{c[3]}s{c[4]}")
+def test_conv_fwd_and_stats(case):
+    cin, cout, kh, kw, s, pads, H = case
+    torch.manual_seed(0)
+    cpad = cin if cin % 8 == 0 else 8
+    spec, p, pk = make_conv(cin, cout, kh, kw, s, s, pads, cin_pad=cpad)
+    N = 3
+    x = bf(torch.randn(N, H, H, cpad, device=DEV))
+    P, Q = spec.out_hw(H, H)
+    y = torch.empty(N, P, Q, cout, dtype=torch.bfloat16, device=DEV)
+    slab, T, cfg = Fn.conv_stats_slab(x.shape, spec, DEV)
+    Fn.conv_forward(x, spec, pk.pack, p.data, y, stats=slab, cfg=cfg)
+    ref = cpu_ref_conv(x, spec, bf(p.data))
+    assert rel_err(y, ref) < 1e-2
+    s1 = slab.view(T, 2, cout).sum(0)[0].cpu()
+    assert rel_err(s1, ref.reshape(-1, cout).sum(0)) < 2e-2
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_conv_fwd_all_tile_configs(cfg):
+    torch.manual_seed(1)
+    spec, p, pk = make_conv(128, 192, 3, 3, 1, 1, (1, 1, 1, 1))
+    x = bf(torch.randn(2, 13, 13, 128, device=DEV))
+    y = torch.empty(2, 13, 13, 192, dtype=torch.bfloat16, device=DEV)
+    Fn.conv_forward(x, spec, pk.pack, p.data, y, cfg=cfg)
+    assert rel_err(y, cpu_ref_conv(x, spec, bf(p.data))) < 1e-2
+
+
+def test_conv_fwd_channel_slice_views():
+    """input is a channel window of a wider buffer and output lands in a concat window"""
+    torch.manual_seed(2)
+    spec, p, pk = make_conv(64, 96, 3, 3, 1, 1, (1, 1, 1, 1))
+    big = bf(torch.randn(2, 9, 9, 192, device=DEV))
+    x = big[..., 64:128]
+    outbuf = torch.zeros(2, 9, 9, 256, dtype=torch.bfloat16, device=DEV)
+    y = outbuf[..., 32:128]
+    Fn.conv_forward(x, spec, pk.pack, p.data, y)
+    ref = cpu_ref_conv(x.contiguous(), spec, bf(p.data))
+    assert rel_err(y, ref) < 1e-2
+    assert outbuf[..., :32].abs().max().item() == 0 and outbuf[..., 128:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("case", CONV_CASES[:-1], ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}{c[3]}s{c[4]}")
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_conv_dgrad(case, accumulate):
+    cin, cout, kh, kw, s, pads, H = case
+    if cin % 8:
+        pytest.skip("stem has no data gradient")
+    torch.manual_seed(3)
+    spec, p, pk = make_conv(cin, cout, kh, kw, s, s, pads)
+    N = 2
+    P, Q = spec.out_hw(H, H)
+    dz = bf(torch.randn(N, P, Q, cout, device=DEV))
+    base = bf(torch.randn(N, H, H, cin, device=DEV))
+    strided_1x1 = s > 1 and kh == 1 and kw == 1
+    dx = base.clone() if accumulate else (torch.zeros_like(base) if strided_1x1 else torch.empty_like(base))
+    Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate)
+    ref = torch.empty(N, H, H, cin)
+    Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), ref, False)
+    if accumulate:
+        ref = ref + base.float().cpu()
+    assert rel_err(dx, ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}{c[3]}s{c[4]}")
+def test_conv_wgrad(case):
+    cin, cout, kh, kw, s, pads, H = case
+    torch.manual_seed(4)
+    cpad = cin if cin % 8 == 0 else 8
+    spec, p, pk = make_conv(cin, cout, kh, kw, s, s, pads, cin_pad=cpad)
+    N = 4
+    P, Q = spec.out_hw(H, H)
+    x = bf(torch.randn(N, H, H, cpad, device=DEV))
+    dz = bf(torch.randn(N, P, Q, cout, device=DEV))
+    dw = torch.zeros(cout, kh, kw, cpad, dtype=torch.float32, device=DEV)
+    Fn.conv_wgrad(dz, x, spec, dw.view(cout, -1))
+    ref = torch.zeros(cout, kh, kw, cpad)
+    Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
+    assert rel_err(dw, ref) < 1e-2
+
+
+def test_conv_wgrad_split_k_large_reduction():
+    torch.manual_seed(5)
+    spec, p, pk = make_conv(64, 64, 3, 3, 1, 1, (1, 1, 1, 1))
+    x = bf(torch.randn(8, 56, 56, 64, device=DEV))
+    dz = bf(torch.randn(8, 56, 56, 64, device=DEV))
+    dw = torch.zeros(64, 3 * 3 * 64, dtype=torch.float32, device=DEV)
+    Fn.conv_wgrad(dz, x, spec, dw)
+    ref = torch.zeros(64, 3, 3, 64)
+    Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
+    assert rel_err(dw, ref) < 1e-2
+
+
+@pytest.mark.parametrize("C", [64, 256, 80, 2048])
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
+def test_bn_fwd_bwd(C, relu, residual):
+    torch.manual_seed(6)
+    N, H = 4, 7
+    z = bf(torch.randn(N, H, H, C, device=DEV) * 3 + 1)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    res = bf(torch.randn(N, H, H, C, device=DEV)) if residual else None
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    y = torch.empty_like(z)
+    saved = Fn.bn_forward(z, gamma, beta, rm, rv, 0.9, 1e-5, y, relu, residual=res)
+    zc, gc, bc = z.float().cpu(), gamma.cpu(), beta.cpu()
+    rmc, rvc = torch.zeros(C), torch.ones(C)
+    yc = torch.empty(N, H, H, C)
+    sc = Fn.bn_forward(zc, gc, bc, rmc, rvc, 0.9, 1e-5, yc, relu, residual=None if res is None else res.float().cpu())
+    assert rel_err(y, yc) < 1e-2
+    assert rel_err(saved.mean, sc.mean) < 1e-4 and rel_err(saved.invstd, sc.invstd) < 1e-4
+    assert rel_err(rm, rmc) < 1e-4 and rel_err(rv, rvc) < 1e-4
+    dy = bf(torch.randn(N, H, H, C, device=DEV))
+    mode = (1 if residual else 2) if relu else 0
+    dz = torch.empty_like(z)
+    gres = torch.empty_like(z)
+    dg = torch.empty(C, device=DEV)
+    db = torch.empty(C, device=DEV)
+    Fn.bn_backward(dy, y, z, saved, gamma, beta, mode, dg, db, dz, gres)
+    dzc, gresc, dgc, dbc = torch.empty(N, H, H, C), torch.empty(N, H, H, C), torch.empty(C), torch.empty(C)
+    Fn.bn_backward(dy.float().cpu(), y.float().cpu(), zc, sc, gc, bc, mode, dgc, dbc, dzc, gresc)
+    assert rel_err(db, dbc) < 1e-2 and rel_err(dg, dgc) < 1e-2
+    assert rel_err(dz, dzc) < 2e-2
+    assert rel_err(gres, gresc) < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["max3s2same", "avg3s1same", "max3s2valid", "avg8valid"])
+def test_pool_fwd_bwd(kind):
+    from azure_hc_intel_tf_amd.nn.layers import Pool
+
+    torch.manual_seed(7)
+    N, H, C = 2, 17, 64
+    if kind == "max3s2same":
+        layer = Pool("p", (H, H, C), 3, 3, 2, 2, "SAME", is_max=True)
+    elif kind == "avg3s1same":
+        layer = Pool("p", (H, H, C), 3, 3, 1, 1, "SAME", is_max=False)
+    elif kind == "max3s2valid":
+        layer = Pool("p", (H, H, C), 3, 3, 2, 2, "VALID", is_max=True)
+    else:
+        H = 8
+        layer = Pool("p", (H, H, C), 8, 8, 1, 1, "VALID", is_max=False)
+    x = bf(torch.randn(N, H, H, C, device=DEV))
+    y = layer.forward(x)
+    yc = layer.forward(x.float().cpu())
+    assert rel_err(y, yc) < 1e-2
+    dy = bf(torch.randn_like(y.float()))
+    layer._saved = (x, y)
+    dx = layer.backward(dy)
+    layer._saved = (x.float().cpu(), y.float().cpu())
+    dxc = layer.backward(dy.float().cpu())
+    assert rel_err(dx, dxc) < 1e-2
+
+
+def test_gap_and_softmax_and_colsum():
+    torch.manual_seed(8)
+    x = bf(torch.randn(4, 7, 7, 2048, device=DEV))
+    y = torch.empty(4, 2048, dtype=torch.bfloat16, device=DEV)
+    Fn.gap_forward(x, y)
+    assert rel_err(y, x.float().cpu().mean(dim=(1, 2))) < 1e-2
+    dx = torch.empty_like(x)
+    Fn.gap_backward(y, dx)
+    assert rel_err(dx, (y.float().cpu() / 49).view(4, 1, 1, 2048).expand(4, 7, 7, 2048)) < 1e-2
+    B, ncls, ldl = 8, 1001, 1008
+    logits = torch.randn(B, ldl, device=DEV) * 3
+    labels = torch.randint(0, ncls, (B,), device=DEV)
+    rl = torch.empty(B, device=DEV)
+    dl = torch.empty(B, ldl, dtype=torch.bfloat16, device=DEV)
+    Fn.softmax_xent(logits, labels, ncls, rl, dl, 1.0 / B)
+    rlc, dlc = torch.empty(B), torch.empty(B, ldl)
+    Fn.softmax_xent(logits.cpu(), labels.cpu(), ncls, rlc, dlc, 1.0 / B)
+    assert rel_err(rl, rlc) < 1e-4
+    assert rel_err(dl, dlc) < 1e-2
+    assert dl[:, ncls:].abs().max().item() == 0
+    cs = torch.empty(ncls, device=DEV)
+    Fn.colsum(dl, B, ncls, cs)
+    assert rel_err(cs, dl.float().cpu()[:, :ncls].sum(0)) < 1e-3
+
+
+def test_sgd_momentum_flat():
+    torch.manual_seed(9)
+    n, nd = 100_003, 60_000
+    w = torch.randn(n, device=DEV)
+    m = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    hyper = torch.tensor([0.1, 0.9, 4e-5, 0.5], device=DEV)
+    l2 = torch.zeros(1, device=DEV)
+    wc, mc, gc, l2c = w.cpu(), m.cpu(), g.cpu(), torch.zeros(1)
+    Fn.sgd_momentum(w, m, g, nd, hyper, l2)
+    Fn.sgd_momentum(wc, mc, gc, nd, hyper.cpu(), l2c)
+    assert rel_err(w, wc) < 1e-6 and rel_err(m, mc) < 1e-6
+    assert abs(l2.item() - l2c.item()) / l2c.item() < 1e-4
+
+
+def test_weight_pack_transposed_flip():
+    torch.manual_seed(10)
+    spec, p, pk = make_conv(16, 24, 3, 3, 1, 1, (1, 1, 1, 1))
+    w = p.data.cpu()
+    packed = pk.pack.view(24, spec.Kpad).float().cpu()
+    assert torch.allclose(packed[:, :spec.K], bf(w).float().reshape(24, -1))
+    assert packed[:, spec.K:].abs().max() == 0
+    tr = pk.tr.view(16, spec.Kpad_t).float().cpu()
+    # tr[c][(r'*S+s')*Cout + k] = W[k][R-1-r'][S-1-s'][c]
+    ref = bf(w).float().flip(1).flip(2).permute(3, 1, 2, 0).reshape(16, -1)
+    assert torch.allclose(tr[:, :spec.Kt], ref)
+
+
+def test_synthetic_data_stats():
+    img = torch.empty(16, 64, 64, 8, dtype=torch.bfloat16, device=DEV)
+    _ext.ops().synth_images(img, 3, 8, 127.0, 60.0, 7)
+    f = img.float()[..., :3]
+    assert abs(f.mean().item() - 127.0) < 2.0
+    assert 45 < f.std().item() < 60  # truncated at 2 sigma: sd ~ 0.88 * 60
+    assert f.min().item() >= 127 - 121 and f.max().item() <= 127 + 121
+    assert img[..., 3:].abs().max().item() == 0
+    lab = torch.empty(4096, dtype=torch.int64, device=DEV)
+    _ext.ops().synth_labels(lab, 1000, 3)
+    assert lab.min().item() >= 0 and lab.max().item() < 1000 and lab.unique().numel() > 900
