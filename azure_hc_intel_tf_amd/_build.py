@@ -88,6 +88,7 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
     if _newer(KERNELS_SO, objs):
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", KERNELS_SO, *objs,
+              "-Wl,-soname,_hcb_kernels.so",
               "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip",
               "-Wl,-rpath," + tlib], verbose)
     return KERNELS_SO
@@ -111,12 +112,14 @@ def build_comm(verbose: bool = False, jobs: int = 8) -> str:
     if jobs_list:
         with _cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
-    if _newer(COMM_SO, objs):
+    if _newer(COMM_SO, objs + [KERNELS_SO]):
         # link RCCL from torch's lib dir: the process already has torch's librccl loaded,
-        # so both resolve to ONE RCCL instance.
-        _run(["g++", "-shared", "-fPIC", "-o", COMM_SO, *objs, "-L" + tlib, "-lc10", "-lc10_hip",
-              "-ltorch_cpu", "-ltorch_hip", "-lrccl", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64",
-              "-Wl,-rpath," + tlib], verbose)
+        # so both resolve to ONE RCCL instance. The bucket pack/unpack kernels come from
+        # _hcb_kernels.so (found next to this library through $ORIGIN).
+        _run(["g++", "-shared", "-fPIC", "-o", COMM_SO, *objs, "-L" + PKG_DIR, "-l:_hcb_kernels.so",
+              "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-lrccl",
+              "-L" + os.path.join(ROCM, "lib"), "-lamdhip64",
+              "-Wl,-rpath,$ORIGIN", "-Wl,-rpath," + tlib], verbose)
     return COMM_SO
 
 

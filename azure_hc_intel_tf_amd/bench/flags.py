@@ -1,0 +1,153 @@
+"""tf_cnn_benchmarks-compatible flag surface.
+
+Accepts every flag the reference passes (/root/reference/benchmark-scripts/
+run-tf-sing-ucx-openmpi.sh:62-81 and run-tf-sing-libfabric-intelmpi.sh:63-82)
+in absl style (``--flag=value``, ``--flag value``, ``--flag`` / ``--noflag`` for booleans,
+``TRUE/False/1/0`` values) plus the tf_cnn_benchmarks flags the BASELINE configs need.
+TensorFlow-runtime-only flags (``--mkl``, ``--kmp_*``, ``--local_parameter_device``,
+``--xla`` ...) are accepted; on the GPU they are no-ops and are reported as such.
+"""
+from __future__ import annotations
+
+import argparse
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional
+
+_TRUE = {"true", "1", "yes", "y", "t", "on"}
+_FALSE = {"false", "0", "no", "n", "f", "off"}
+
+
+def parse_bool(v) -> bool:
+    if isinstance(v, bool):
+        return v
+    s = str(v).strip().lower()
+    if s in _TRUE:
+        return True
+    if s in _FALSE:
+        return False
+    raise argparse.ArgumentTypeError(f"not a boolean: {v!r}")
+
+
+@dataclass
+class Flag:
+    name: str
+    default: Any
+    type: Any
+    help: str
+    noop_on_gpu: bool = False
+    choices: Optional[List[Any]] = None
+
+
+FLAGS: List[Flag] = [
+    # --- the reference's flag set (run-tf-sing-ucx-openmpi.sh:62-81)
+    Flag("batch_size", 0, int, "per-device (per-worker) batch size; 0 = model default"),
+    Flag("num_warmup_batches", None, int, "untimed warmup steps (default: model/device dependent)"),
+    Flag("num_batches", 100, int, "timed steps"),
+    Flag("model", "trivial", str, "model name (resnet50, resnet50_v1.5, resnet101, resnet152, inception3, trivial)"),
+    Flag("num_intra_threads", 0, int, "host intra-op threads (CPU path: torch.set_num_threads)"),
+    Flag("num_inter_threads", 0, int, "host inter-op threads (CPU path)"),
+    Flag("kmp_blocktime", 0, int, "KMP_BLOCKTIME for the CPU path", noop_on_gpu=True),
+    Flag("kmp_affinity", "granularity=fine,verbose,compact,1,0", str, "KMP_AFFINITY for the CPU path",
+         noop_on_gpu=True),
+    Flag("kmp_settings", 1, int, "KMP_SETTINGS", noop_on_gpu=True),
+    Flag("display_every", 10, int, "log cadence (steps)"),
+    Flag("data_format", "NCHW", str, "logical layout (kernels run NHWC internally)", choices=["NCHW", "NHWC"]),
+    Flag("optimizer", "sgd", str, "sgd | momentum", choices=["sgd", "momentum"]),
+    Flag("forward_only", False, parse_bool, "inference-only benchmark"),
+    Flag("device", "gpu", str, "gpu (MI355X) or cpu", choices=["gpu", "cpu"]),
+    Flag("mkl", False, parse_bool, "TF-MKL switch", noop_on_gpu=True),
+    Flag("variable_update", "horovod", str, "horovod (RCCL data parallel) | replicated (single process)",
+         choices=["horovod", "replicated", "parameter_server", "distributed_replicated", "independent"]),
+    Flag("horovod_device", "", str, "where gradients are reduced: gpu (RCCL, default) | cpu (gloo)"),
+    Flag("local_parameter_device", "gpu", str, "accepted for compatibility", noop_on_gpu=True),
+    Flag("data_dir", None, str, "real-data directory; absent = synthetic ImageNet"),
+    Flag("data_name", None, str, "dataset name (imagenet)"),
+    # --- tf_cnn_benchmarks flags used by the BASELINE configs / common runs
+    Flag("num_gpus", 1, int, "GPUs per process (horovod: 1)"),
+    Flag("use_fp16", False, parse_bool, "fp16 compute (bf16 is the default GPU compute type)"),
+    Flag("fp16_loss_scale", 128.0, float, "static loss scale for --use_fp16"),
+    Flag("init_learning_rate", None, float, "constant learning rate (overrides the model schedule)"),
+    Flag("momentum", 0.9, float, "momentum for --optimizer=momentum"),
+    Flag("weight_decay", 0.00004, float, "L2 weight decay (coupled, tf_cnn_benchmarks semantics)"),
+    Flag("num_epochs", None, float, "alternative to --num_batches"),
+    Flag("train_dir", None, str, "checkpoint directory"),
+    Flag("save_model_steps", None, int, "checkpoint every N steps"),
+    Flag("save_model_secs", 0, int, "checkpoint every N seconds"),
+    Flag("trace_file", "", str, "Chrome trace of one profiled step (torch.profiler / roctracer)"),
+    Flag("benchmark_log_dir", None, str, "directory for the machine-readable JSON summary"),
+    Flag("tf_random_seed", 1234, int, "random seed"),
+    Flag("print_training_accuracy", False, parse_bool, "log top-1/top-5 of the training batch"),
+    Flag("summary_verbosity", 0, int, "accepted"),
+    Flag("xla", False, parse_bool, "accepted", noop_on_gpu=True),
+    Flag("xla_compile", False, parse_bool, "accepted", noop_on_gpu=True),
+    Flag("allow_growth", None, parse_bool, "accepted", noop_on_gpu=True),
+    Flag("gradient_repacking", 0, int, "accepted", noop_on_gpu=True),
+    Flag("all_reduce_spec", None, str, "accepted", noop_on_gpu=True),
+    Flag("label_smoothing", 0.0, float, "label smoothing (0 only)"),
+    Flag("image_size", 0, int, "override the model's input resolution (0 = model default)"),
+    # --- MI355X engine knobs
+    Flag("use_hip_graph", True, parse_bool, "capture the training step in a HIP graph"),
+    Flag("comm_engine", "torch", str, "gradient allreduce engine: native (C++ RCCL) | torch",
+         choices=["native", "torch"]),
+    Flag("gradient_compression", "none", str, "none | fp16 | bf16 (Horovod Compression)",
+         choices=["none", "fp16", "bf16"]),
+    Flag("json_summary", None, str, "write the run summary JSON to this path"),
+    Flag("fault_rank", -1, int, "fault injection: rank that aborts (testing)"),
+    Flag("fault_step", -1, int, "fault injection: step at which --fault_rank aborts"),
+]
+
+_BY_NAME = {f.name: f for f in FLAGS}
+
+
+class Params(dict):
+    __getattr__ = dict.get
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def _normalise(argv: List[str]) -> List[str]:
+    out = []
+    for a in argv:
+        if a.startswith("--no") and "=" not in a:
+            name = a[4:]
+            if name in _BY_NAME and _BY_NAME[name].type is parse_bool:
+                out.append(f"--{name}=false")
+                continue
+        if a.startswith("--") and "=" not in a:
+            name = a[2:]
+            if name in _BY_NAME and _BY_NAME[name].type is parse_bool:
+                out.append(f"--{name}=true")
+                continue
+        out.append(a)
+    return out
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="tf_cnn_benchmarks.py",
+                                 description="MI355X-native tf_cnn_benchmarks-compatible CNN training benchmark")
+    for f in FLAGS:
+        kw = dict(default=f.default, help=f.help)
+        kw["type"] = f.type
+        if f.choices:
+            kw["choices"] = f.choices
+        ap.add_argument(f"--{f.name}", **kw)
+    return ap
+
+
+def parse_flags(argv: Optional[List[str]] = None, allow_unknown: bool = True) -> Params:
+    import sys
+
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = build_parser()
+    ns, unknown = ap.parse_known_args(_normalise(argv))
+    p = Params(vars(ns))
+    p["_unknown"] = unknown
+    if unknown and not allow_unknown:
+        ap.error(f"unrecognized flags: {unknown}")
+    return p
+
+
+def noop_flags_set(p: Params) -> Dict[str, Any]:
+    """TF-only flags explicitly given a non-default value (reported as no-ops on the GPU)."""
+    return {f.name: p[f.name] for f in FLAGS if f.noop_on_gpu and p.get(f.name) != f.default}

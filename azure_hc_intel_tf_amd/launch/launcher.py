@@ -1,0 +1,154 @@
+"""Per-GPU process launcher (the mpirun / mpiexec.hydra role of the reference,
+/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:99-113,
+run-tf-sing-libfabric-intelmpi.sh:94-105; SURVEY.md §2.3 last row, §2.5).
+
+* one worker process per MI355X (``--nproc_per_node``), ranks ``node_rank*nproc + local``;
+* rendezvous env for torch.distributed / RCCL: RANK, LOCAL_RANK, WORLD_SIZE,
+  LOCAL_WORLD_SIZE, GROUP_RANK, MASTER_ADDR, MASTER_PORT (+ HSA_ENABLE_IPC_MODE_LEGACY=0,
+  which the host driver needs for dmabuf IPC);
+* CPU pinning: each worker gets a contiguous, equal share of the node's cores (the
+  ``--map-by ppr:W:socket,pe=C`` role), applied in the child before exec;
+* fabric selection: ``ib`` = RCCL peer-to-peer over xGMI (default transports), ``sock`` =
+  RCCL's socket transport only (P2P / SHM / IB disabled), the reference's A/B fabric arm;
+* failure propagation: if any worker exits non-zero, the others are terminated and the
+  launcher exits with that worker's code (MPI_Abort semantics).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import Dict, List, Optional
+
+
+def fabric_env(fabric: str) -> Dict[str, str]:
+    if fabric in ("ib", "xgmi", "", None):
+        return {}
+    if fabric in ("sock", "socket", "tcp"):
+        return {"NCCL_P2P_DISABLE": "1", "NCCL_SHM_DISABLE": "1", "NCCL_IB_DISABLE": "1",
+                "NCCL_SOCKET_IFNAME": os.environ.get("NCCL_SOCKET_IFNAME", "lo")}
+    raise ValueError(f"unknown fabric {fabric!r} (expected ib or sock)")
+
+
+def cpu_shares(n_workers: int, cpus: Optional[List[int]] = None) -> List[List[int]]:
+    cpus = sorted(cpus if cpus is not None else os.sched_getaffinity(0))
+    if n_workers <= 0:
+        return []
+    per = max(len(cpus) // n_workers, 1)
+    return [cpus[i * per:(i + 1) * per] or cpus for i in range(n_workers)]
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker_env(base: Dict[str, str], rank: int, local_rank: int, world: int, nproc: int, node_rank: int,
+               master_addr: str, master_port: int, fabric: str, omp_threads: Optional[int]) -> Dict[str, str]:
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": str(node_rank), "NODE_RANK": str(node_rank),
+                "MASTER_ADDR": master_addr, "MASTER_PORT": str(master_port),
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    env.update(fabric_env(fabric))
+    if omp_threads:
+        env["OMP_NUM_THREADS"] = str(omp_threads)
+    return env
+
+
+def launch(cmd: List[str], nproc_per_node: int, nnodes: int = 1, node_rank: int = 0,
+           master_addr: str = "127.0.0.1", master_port: Optional[int] = None, fabric: str = "ib",
+           pin_cpus: bool = True, omp_threads: Optional[int] = None, env: Optional[Dict[str, str]] = None,
+           poll_s: float = 0.2) -> int:
+    world = nproc_per_node * nnodes
+    port = master_port or int(os.environ.get("MASTER_PORT", 0)) or free_port()
+    base = dict(os.environ if env is None else env)
+    shares = cpu_shares(nproc_per_node) if pin_cpus else [None] * nproc_per_node
+    procs = []
+    for lr in range(nproc_per_node):
+        rank = node_rank * nproc_per_node + lr
+        e = worker_env(base, rank, lr, world, nproc_per_node, node_rank, master_addr, port, fabric, omp_threads)
+        share = shares[lr]
+
+        def pre(share=share):
+            os.setsid()
+            if share:
+                try:
+                    os.sched_setaffinity(0, share)
+                except OSError:
+                    pass
+
+        procs.append(subprocess.Popen(cmd, env=e, preexec_fn=pre))
+    rc = 0
+    try:
+        while True:
+            alive = 0
+            for p in procs:
+                r = p.poll()
+                if r is None:
+                    alive += 1
+                elif r != 0 and rc == 0:
+                    rc = r
+            if rc != 0:
+                _terminate(procs)
+                break
+            if alive == 0:
+                break
+            time.sleep(poll_s)
+    except KeyboardInterrupt:
+        _terminate(procs)
+        rc = 130
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+    return rc
+
+
+def _terminate(procs):
+    for p in procs:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+    deadline = time.time() + 10
+    for p in procs:
+        while p.poll() is None and time.time() < deadline:
+            time.sleep(0.1)
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="one process per MI355X launcher")
+    ap.add_argument("--nproc_per_node", "--nproc-per-node", type=int, default=1)
+    ap.add_argument("--nnodes", type=int, default=1)
+    ap.add_argument("--node_rank", type=int, default=0)
+    ap.add_argument("--master_addr", default="127.0.0.1")
+    ap.add_argument("--master_port", type=int, default=0)
+    ap.add_argument("--fabric", default="ib")
+    ap.add_argument("--no_pin", action="store_true")
+    ap.add_argument("--omp_threads", type=int, default=None)
+    ap.add_argument("cmd", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
+    if not cmd:
+        ap.error("missing worker command")
+    return launch(cmd, a.nproc_per_node, a.nnodes, a.node_rank, a.master_addr, a.master_port or None, a.fabric,
+                  pin_cpus=not a.no_pin, omp_threads=a.omp_threads)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -189,16 +189,20 @@ class Pool(Layer):
     def forward(self, x, out=None):
         N = x.shape[0]
         y = out if out is not None else empty_act((N,) + self.out_shape, x.device)
-        Fn.pool_forward(x, y, *self.k, *self.s, self.pads, self.is_max, self.incl_pad)
-        self._saved = (x, y)
+        amax = None
+        if self.is_max and x.is_cuda:
+            amax = torch.empty((N,) + self.out_shape, dtype=torch.uint8, device=x.device)
+        Fn.pool_forward(x, y, *self.k, *self.s, self.pads, self.is_max, self.incl_pad, argmax=amax)
+        self._saved = (x, y, amax)
         return y
 
     def backward(self, dy, dx=None, accumulate=False):
-        x, y = self._saved
+        x, y, amax = self._saved
         if dx is None:
             dx = empty_act(x.shape, dy.device)
             accumulate = False
-        Fn.pool_backward(dy, x, y, dx, *self.k, *self.s, self.pads, self.is_max, self.incl_pad, accumulate)
+        Fn.pool_backward(dy, x, y, dx, *self.k, *self.s, self.pads, self.is_max, self.incl_pad, accumulate,
+                         argmax=amax)
         self._saved = None
         return dx
 

@@ -307,10 +307,12 @@ def pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad):
     return [N, H, W, C, ld(x), P, Q, ld(out), kh, kw, sh, sw, pt, pl, 1 if is_max else 0, 1 if incl_pad else 0]
 
 
-def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False):
+def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False, argmax=None):
+    """argmax (GPU, max pool): uint8 [N,P,Q,C] window position of the first maximum, which
+    makes the backward a cheap gather."""
     pt, pb, pl, pr = pads
     if x.is_cuda:
-        _ext.ops().pool_fwd(x, out, pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad))
+        _ext.ops().pool_fwd(x, out, argmax, pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad))
         return out
     xt = x.permute(0, 3, 1, 2)
     if is_max:
@@ -328,10 +330,11 @@ def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False):
     return out
 
 
-def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, accumulate=False):
+def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, accumulate=False, argmax=None):
     pt, pb, pl, pr = pads
     if x.is_cuda:
-        _ext.ops().pool_bwd(dy, x, y, dx, pool_geom(x, dy, kh, kw, sh, sw, pt, pl, is_max, incl_pad), accumulate)
+        _ext.ops().pool_bwd(dy, x, y, argmax, dx, pool_geom(x, dy, kh, kw, sh, sw, pt, pl, is_max, incl_pad),
+                            accumulate)
         return dx
     with torch.enable_grad():
         xr = x.detach().clone().requires_grad_(True)

@@ -1,0 +1,147 @@
+"""Python face of the native C++ RCCL engine (``csrc/comm/comm.cpp`` -> ``_hcb_comm.so``).
+
+``NativeReducer`` owns one RCCL communicator (created from an ncclUniqueId exchanged through
+the torch.distributed TCP store -- no MPI) and reduces the flat gradient buffer bucket by
+bucket on a dedicated high-priority comm stream forked from / joined to the compute stream.
+Bucket size: ``HOROVOD_FUSION_THRESHOLD``. Optional bf16 compression (pack kernel -> bf16
+allreduce -> unpack kernel, all on the comm stream). ``HOROVOD_TIMELINE`` writes a Chrome
+trace of the bucket reductions; the watchdog honours ``HOROVOD_STALL_CHECK_TIME_SECONDS`` and
+``HCB_STALL_ABORT_SECONDS``.
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import threading
+
+import torch
+import torch.distributed as dist
+
+from .reducer import fusion_threshold_bytes, make_buckets
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMM_SO = os.path.join(_PKG, "_hcb_comm.so")
+_loaded = False
+_lock = threading.Lock()
+_counter = itertools.count()
+
+
+def load():
+    global _loaded
+    if _loaded:
+        return torch.ops.hcb_comm
+    with _lock:
+        if not _loaded:
+            from ..ops import _ext
+
+            _ext.load()  # the comm library links against the kernel library
+            if not os.path.exists(COMM_SO):
+                from .. import _build
+
+                _build.build_comm()
+            torch.ops.load_library(COMM_SO)
+            _loaded = True
+    return torch.ops.hcb_comm
+
+
+def rccl_version() -> int:
+    return int(load().version())
+
+
+def _exchange_uid(rank: int, world: int, tag: str) -> torch.Tensor:
+    cc = load()
+    if world == 1:
+        return cc.unique_id()
+    store = dist.distributed_c10d._get_default_store()
+    key = f"hcb_comm_uid/{tag}"
+    if rank == 0:
+        uid = cc.unique_id()
+        store.set(key, bytes(uid.numpy().tobytes()))
+        return uid
+    raw = store.get(key)
+    return torch.frombuffer(bytearray(raw), dtype=torch.uint8).clone()
+
+
+class Communicator:
+    """One RCCL communicator over all ranks of the default process group (or a 1-rank one)."""
+
+    def __init__(self, device=None):
+        cc = load()
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        tag = str(next(_counter))
+        uid = _exchange_uid(self.rank, self.world, tag)
+        self.h = cc.create(uid, self.rank, self.world, self.device)
+        self._cc = cc
+
+    def allreduce_(self, t, average=False):
+        self._cc.allreduce_(self.h, t, average)
+        return t
+
+    def broadcast_(self, t, root=0):
+        self._cc.broadcast_(self.h, t, root)
+        return t
+
+    def allgather_(self, inp, out):
+        self._cc.allgather_(self.h, inp, out)
+        return out
+
+    def reduce_scatter_(self, inp, out, average=False):
+        self._cc.reduce_scatter_(self.h, inp, out, average)
+        return out
+
+    def bucket_allreduce_(self, flat, buckets, compress=0, scale=1.0, average=False):
+        self._cc.bucket_allreduce_(self.h, flat, buckets, compress, scale, average)
+        return flat
+
+    def barrier(self):
+        self._cc.barrier(self.h)
+
+    def close(self):
+        if getattr(self, "h", None) is not None:
+            self._cc.destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class NativeReducer:
+    """Flat-buffer gradient allreduce on the C++ RCCL engine."""
+
+    def __init__(self, compression=None, bucket_bytes=None, average=False):
+        if compression not in (None, "none", "bf16", "fp16"):
+            raise ValueError(compression)
+        # fp16 wire format maps to bf16 on MI355X: same 2 bytes, fp32 exponent range
+        self.compress = 0 if compression in (None, "none") else 1
+        self.bucket_bytes = bucket_bytes or fusion_threshold_bytes()
+        self.average = average
+        self.comm = Communicator()
+        self.graph_safe = os.environ.get("HCB_GRAPH_COMM", "0") == "1"
+        self._buckets = None
+
+    def _bucket_table(self, numel):
+        if self._buckets is None or self._numel != numel:
+            esz = 2 if self.compress else 4
+            b = make_buckets(numel, max(self.bucket_bytes // esz, 64))
+            self._buckets = torch.tensor(b, dtype=torch.int64)
+            self._numel = numel
+        return self._buckets
+
+    def allreduce_(self, flat):
+        if self.comm.world == 1 and not self.compress:
+            return flat
+        self.comm.bucket_allreduce_(flat, self._bucket_table(flat.numel()), self.compress, 1.0, self.average)
+        return flat
+
+    def broadcast_(self, t, root=0):
+        if self.comm.world > 1:
+            self.comm.broadcast_(t, root)
+        return t
+
+    def close(self):
+        self.comm.close()

@@ -266,19 +266,25 @@ void bn_bwd_apply(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y
 }
 
 // geom = [N,H,W,C,ldx,P,Q,ldy,kh,kw,sh,sw,ph,pw,is_max,incl_pad]
-void pool_fwd(const Tensor& x, const Tensor& y, at::IntArrayRef g) {
+void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx, at::IntArrayRef g) {
   TORCH_CHECK(g.size() == 16, "hcb.pool_fwd: geom");
   check_bf16(x, "x");
   check_bf16(y, "y");
   TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_fwd: C/ld % 8");
   check_range(x, g[0] * g[1] * g[2] * g[4] * 2, "x");
   check_range(y, g[0] * g[5] * g[6] * g[7] * 2, "y");
+  void* ip = nullptr;
+  if (idx.has_value()) {
+    TORCH_CHECK(idx->scalar_type() == at::kByte && idx->is_contiguous() && idx->numel() >= g[0] * g[5] * g[6] * g[3],
+                "hcb.pool_fwd: idx must be contiguous uint8 [N,P,Q,C]");
+    ip = idx->data_ptr();
+  }
   hcb::launch_pool_fwd(x.data_ptr(), y.data_ptr(), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8],
-                       g[9], g[10], g[11], g[12], g[13], g[14], g[15], cur_stream());
+                       g[9], g[10], g[11], g[12], g[13], g[14], g[15], ip, cur_stream());
 }
 
-void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& dx, at::IntArrayRef g,
-              bool accumulate) {
+void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx,
+              const Tensor& dx, at::IntArrayRef g, bool accumulate) {
   TORCH_CHECK(g.size() == 16, "hcb.pool_bwd: geom");
   check_bf16(dy, "dy");
   check_bf16(x, "x");
@@ -290,7 +296,7 @@ void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& 
   check_range(dy, g[0] * g[5] * g[6] * g[7] * 2, "dy");
   hcb::launch_pool_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), dx.data_ptr(), g[0], g[1], g[2], g[3],
                        g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], g[15],
-                       accumulate ? 1 : 0, cur_stream());
+                       accumulate ? 1 : 0, idx.has_value() ? idx->data_ptr() : nullptr, cur_stream());
 }
 
 void gap_fwd(const Tensor& x, const Tensor& y, int64_t N, int64_t HW, int64_t C) {
@@ -433,8 +439,8 @@ TORCH_LIBRARY(hcb, m) {
   m.def("bn_bwd_reduce(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) slab, Tensor(b!)? gout, int ldg) -> ()");
   m.def("bn_bwd_finalize(Tensor slab, int T, int C, Tensor(a!) dgamma, Tensor(b!) dbeta) -> ()");
   m.def("bn_bwd_apply(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor dgamma, Tensor dbeta, int relu) -> ()");
-  m.def("pool_fwd(Tensor x, Tensor(a!) y, int[] geom) -> ()");
-  m.def("pool_bwd(Tensor dy, Tensor x, Tensor y, Tensor(a!) dx, int[] geom, bool accumulate) -> ()");
+  m.def("pool_fwd(Tensor x, Tensor(a!) y, Tensor(b!)? idx, int[] geom) -> ()");
+  m.def("pool_bwd(Tensor dy, Tensor x, Tensor y, Tensor? idx, Tensor(a!) dx, int[] geom, bool accumulate) -> ()");
   m.def("gap_fwd(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx, int N, int HW, int C) -> ()");
   m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale) -> ()");

@@ -1,0 +1,455 @@
+// Native data-parallel communication runtime for MI355X: RCCL communicator + bucketed
+// gradient allreduce engine on a side HIP stream + Chrome-trace timeline + stall watchdog.
+//
+// This is the MI355X replacement for the Horovod C++ core the reference drives
+// (background thread, tensor-fusion buffer, MPI_Allreduce, HOROVOD_TIMELINE, stall
+// inspector; SURVEY.md §2.2 "Horovod core", §2.3, §5; reference knobs at
+// /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:105-106). Design:
+//   * no negotiation: every rank runs the same static bucket schedule over ONE flat
+//     gradient buffer (the fusion buffer IS the gradient storage), so a "cycle" is just
+//     a sequence of ncclAllReduce calls;
+//   * the communicator is created from an ncclUniqueId exchanged through the
+//     torch.distributed TCP store (no MPI);
+//   * collectives run on a dedicated comm stream forked from / joined back to the
+//     caller's stream with HIP events (capturable into a HIP graph);
+//   * optional bf16/fp16 compression: pack kernel (scale+cast) -> allreduce -> unpack,
+//     all on the comm stream;
+//   * timeline: per-bucket PACK / ALLREDUCE / UNPACK intervals measured with HIP events
+//     and written as Chrome trace JSON (HOROVOD_TIMELINE);
+//   * watchdog thread: warns when a launched reduction has not completed within
+//     HOROVOD_STALL_CHECK_TIME_SECONDS, polls ncclCommGetAsyncError, optionally aborts
+//     the communicator (HCB_STALL_ABORT_SECONDS) so a dead rank cannot hang the job.
+#include <torch/library.h>
+#include <ATen/core/Tensor.h>
+#include <ATen/ops/empty.h>
+#include <ATen/ops/zeros.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/util/Exception.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kernels/kernels.h"
+
+using at::Tensor;
+
+#define HCB_HIP(x)                                                                    \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    TORCH_CHECK(e_ == hipSuccess, "hcb_comm: ", #x, " failed: ", hipGetErrorString(e_)); \
+  } while (0)
+#define HCB_NCCL(x)                                                                     \
+  do {                                                                                  \
+    ncclResult_t r_ = (x);                                                              \
+    TORCH_CHECK(r_ == ncclSuccess, "hcb_comm: ", #x, " failed: ", ncclGetErrorString(r_)); \
+  } while (0)
+
+namespace {
+
+double env_double(const char* name, double dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return std::atof(v);
+}
+
+ncclDataType_t nccl_type(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    default: TORCH_CHECK(false, "hcb_comm: unsupported dtype ", t.scalar_type());
+  }
+}
+
+struct TimelineRec {
+  std::string name;
+  int bucket;
+  int64_t bytes;
+  hipEvent_t b, e;
+};
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1, device = 0;
+  hipStream_t stream = nullptr;  // comm stream
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr, base_ev = nullptr;
+  // compression scratch (grown on demand, owned by the engine)
+  void* cbuf = nullptr;
+  size_t cbuf_bytes = 0;
+  // timeline
+  std::string timeline_path;
+  std::vector<TimelineRec> pending;  // recorded, not yet written
+  std::vector<hipEvent_t> free_events;
+  std::ofstream tl;
+  bool tl_first = true;
+  int64_t cycle = 0;
+  // watchdog
+  std::thread wd;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<bool> stop{false};
+  hipEvent_t watch_ev = nullptr;  // last join event to watch
+  std::chrono::steady_clock::time_point watch_since;
+  bool watching = false;
+  int64_t watch_cycle = 0;
+  double stall_warn_s = 60.0, stall_abort_s = 0.0;
+  std::atomic<bool> aborted{false};
+
+  hipEvent_t get_event() {
+    if (!free_events.empty()) {
+      hipEvent_t e = free_events.back();
+      free_events.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HCB_HIP(hipEventCreate(&e));
+    return e;
+  }
+};
+
+std::mutex g_mu;
+std::map<int64_t, std::unique_ptr<Comm>> g_comms;
+int64_t g_next = 1;
+
+Comm* get(int64_t h) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_comms.find(h);
+  TORCH_CHECK(it != g_comms.end(), "hcb_comm: invalid communicator handle ", h);
+  return it->second.get();
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
+  return st == hipStreamCaptureStatusActive;
+}
+
+void watchdog_loop(Comm* c) {
+  bool warned = false;
+  while (!c->stop.load()) {
+    std::unique_lock<std::mutex> lk(c->mu);
+    c->cv.wait_for(lk, std::chrono::milliseconds(500));
+    if (c->stop.load()) break;
+    if (c->comm) {
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+        std::fprintf(stderr, "[hcb watchdog] rank %d: RCCL async error: %s -- aborting communicator\n", c->rank,
+                     ncclGetErrorString(ae));
+        c->aborted = true;
+        ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        std::fflush(stderr);
+        std::_Exit(18);
+      }
+    }
+    if (!c->watching || !c->watch_ev) {
+      warned = false;
+      continue;
+    }
+    hipError_t q = hipEventQuery(c->watch_ev);
+    if (q == hipSuccess) {
+      c->watching = false;
+      warned = false;
+      continue;
+    }
+    double waited =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - c->watch_since).count();
+    if (!warned && waited > c->stall_warn_s) {
+      std::fprintf(stderr,
+                   "[hcb watchdog] rank %d: gradient allreduce of cycle %lld has not completed after %.0f s; "
+                   "one or more ranks may have stalled (HOROVOD_STALL_CHECK_TIME_SECONDS=%.0f)\n",
+                   c->rank, (long long)c->watch_cycle, waited, c->stall_warn_s);
+      std::fflush(stderr);
+      warned = true;
+    }
+    if (c->stall_abort_s > 0 && waited > c->stall_abort_s && c->comm) {
+      std::fprintf(stderr, "[hcb watchdog] rank %d: stalled for %.0f s > HCB_STALL_ABORT_SECONDS; aborting\n", c->rank,
+                   waited);
+      std::fflush(stderr);
+      c->aborted = true;
+      ncclCommAbort(c->comm);
+      c->comm = nullptr;
+      std::_Exit(19);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- ops
+Tensor unique_id() {
+  ncclUniqueId id;
+  HCB_NCCL(ncclGetUniqueId(&id));
+  Tensor t = at::empty({(int64_t)sizeof(id)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &id, sizeof(id));
+  return t;
+}
+
+int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
+  TORCH_CHECK(uid.numel() == (int64_t)sizeof(ncclUniqueId) && uid.scalar_type() == at::kByte && !uid.is_cuda(),
+              "hcb_comm.create: uid must be a CPU uint8 tensor of ", sizeof(ncclUniqueId), " bytes");
+  auto c = std::make_unique<Comm>();
+  c->rank = (int)rank;
+  c->world = (int)world;
+  c->device = (int)device;
+  HCB_HIP(hipSetDevice(c->device));
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data_ptr(), sizeof(id));
+  HCB_NCCL(ncclCommInitRank(&c->comm, c->world, id, c->rank));
+  int prio_lo = 0, prio_hi = 0;
+  HCB_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  // communication at high priority so its few kernels are not queued behind compute
+  HCB_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi));
+  HCB_HIP(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+  HCB_HIP(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+  HCB_HIP(hipEventCreate(&c->base_ev));
+  HCB_HIP(hipEventRecord(c->base_ev, c->stream));
+  if (const char* tl = std::getenv("HOROVOD_TIMELINE")) {
+    if (*tl) {
+      std::string p(tl);
+      if (c->world > 1) p += "." + std::to_string(c->rank);
+      c->timeline_path = p;
+      c->tl.open(p);
+      c->tl << "[\n";
+    }
+  }
+  c->stall_warn_s = env_double("HOROVOD_STALL_CHECK_TIME_SECONDS", 60.0);
+  c->stall_abort_s = env_double("HCB_STALL_ABORT_SECONDS", 0.0);
+  Comm* raw = c.get();
+  raw->wd = std::thread(watchdog_loop, raw);
+  std::lock_guard<std::mutex> lk(g_mu);
+  int64_t h = g_next++;
+  g_comms[h] = std::move(c);
+  return h;
+}
+
+void flush_timeline(Comm* c, bool block) {
+  if (!c->tl.is_open()) {
+    for (auto& r : c->pending) {
+      c->free_events.push_back(r.b);
+      c->free_events.push_back(r.e);
+    }
+    c->pending.clear();
+    return;
+  }
+  std::vector<TimelineRec> keep;
+  for (auto& r : c->pending) {
+    if (!block && hipEventQuery(r.e) != hipSuccess) {
+      keep.push_back(r);
+      continue;
+    }
+    hipEventSynchronize(r.e);
+    float t0 = 0.f, t1 = 0.f;
+    hipEventElapsedTime(&t0, c->base_ev, r.b);
+    hipEventElapsedTime(&t1, c->base_ev, r.e);
+    if (!c->tl_first) c->tl << ",\n";
+    c->tl_first = false;
+    c->tl << "{\"name\":\"" << r.name << "\",\"ph\":\"X\",\"pid\":" << c->rank << ",\"tid\":" << r.bucket
+          << ",\"ts\":" << (double)t0 * 1000.0 << ",\"dur\":" << (double)(t1 - t0) * 1000.0
+          << ",\"args\":{\"bytes\":" << r.bytes << ",\"bucket\":" << r.bucket << "}}";
+    c->free_events.push_back(r.b);
+    c->free_events.push_back(r.e);
+  }
+  c->pending.swap(keep);
+  c->tl.flush();
+}
+
+void destroy(int64_t h) {
+  std::unique_ptr<Comm> c;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_comms.find(h);
+    if (it == g_comms.end()) return;
+    c = std::move(it->second);
+    g_comms.erase(it);
+  }
+  c->stop = true;
+  c->cv.notify_all();
+  if (c->wd.joinable()) c->wd.join();
+  hipStreamSynchronize(c->stream);
+  flush_timeline(c.get(), true);
+  if (c->tl.is_open()) {
+    c->tl << "\n]\n";
+    c->tl.close();
+  }
+  if (c->comm) ncclCommDestroy(c->comm);
+  for (auto e : c->free_events) hipEventDestroy(e);
+  hipEventDestroy(c->fork_ev);
+  hipEventDestroy(c->join_ev);
+  hipEventDestroy(c->base_ev);
+  if (c->cbuf) hipFree(c->cbuf);
+  hipStreamDestroy(c->stream);
+}
+
+// fork the comm stream off the caller's stream
+hipStream_t fork(Comm* c) {
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  HCB_HIP(hipEventRecord(c->fork_ev, cur));
+  HCB_HIP(hipStreamWaitEvent(c->stream, c->fork_ev, 0));
+  return cur;
+}
+void join(Comm* c, hipStream_t cur) {
+  HCB_HIP(hipEventRecord(c->join_ev, c->stream));
+  HCB_HIP(hipStreamWaitEvent(cur, c->join_ev, 0));
+}
+
+void allreduce_(int64_t h, const Tensor& t, bool average) {
+  Comm* c = get(h);
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "hcb_comm.allreduce_: contiguous GPU tensor");
+  TORCH_CHECK(c->comm, "hcb_comm: communicator aborted");
+  hipStream_t cur = fork(c);
+  HCB_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), average ? ncclAvg : ncclSum,
+                         c->comm, c->stream));
+  join(c, cur);
+}
+
+void broadcast_(int64_t h, const Tensor& t, int64_t root) {
+  Comm* c = get(h);
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "hcb_comm.broadcast_: contiguous GPU tensor");
+  hipStream_t cur = fork(c);
+  HCB_NCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), (int)root, c->comm, c->stream));
+  join(c, cur);
+}
+
+void allgather_(int64_t h, const Tensor& in, const Tensor& out) {
+  Comm* c = get(h);
+  TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.is_contiguous() && out.is_contiguous(), "hcb_comm.allgather_");
+  TORCH_CHECK(out.numel() == in.numel() * c->world && in.scalar_type() == out.scalar_type(), "hcb_comm.allgather_: sizes");
+  hipStream_t cur = fork(c);
+  HCB_NCCL(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_type(in), c->comm, c->stream));
+  join(c, cur);
+}
+
+void reduce_scatter_(int64_t h, const Tensor& in, const Tensor& out, bool average) {
+  Comm* c = get(h);
+  TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.is_contiguous() && out.is_contiguous(), "hcb_comm.reduce_scatter_");
+  TORCH_CHECK(in.numel() == out.numel() * c->world && in.scalar_type() == out.scalar_type(), "hcb_comm.reduce_scatter_: sizes");
+  hipStream_t cur = fork(c);
+  HCB_NCCL(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_type(in), average ? ncclAvg : ncclSum,
+                             c->comm, c->stream));
+  join(c, cur);
+}
+
+// Bucketed allreduce of the flat fp32 gradient buffer.
+// buckets: int64 CPU tensor [nb][2] of (offset, length) in elements, issued in order.
+// compress: 0 none, 1 bf16, 2 fp16 (fp16 goes through an fp32->fp16 cast kernel pair)
+// scale: multiplied in during pack (e.g. 1/world for averaging when compressing).
+void bucket_allreduce_(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale,
+                       bool average) {
+  Comm* c = get(h);
+  TORCH_CHECK(c->comm, "hcb_comm: communicator aborted");
+  TORCH_CHECK(flat.is_cuda() && flat.is_contiguous() && flat.scalar_type() == at::kFloat,
+              "hcb_comm.bucket_allreduce_: flat fp32 GPU buffer");
+  TORCH_CHECK(!buckets.is_cuda() && buckets.scalar_type() == at::kLong && buckets.dim() == 2 && buckets.size(1) == 2,
+              "hcb_comm.bucket_allreduce_: buckets int64 [n][2] on CPU");
+  TORCH_CHECK(compress == 0 || compress == 1, "hcb_comm.bucket_allreduce_: compress must be 0 (none) or 1 (bf16)");
+  const int64_t* bk = buckets.data_ptr<int64_t>();
+  const int64_t nb = buckets.size(0);
+  const int64_t n = flat.numel();
+  for (int64_t i = 0; i < nb; ++i)
+    TORCH_CHECK(bk[2 * i] >= 0 && bk[2 * i + 1] > 0 && bk[2 * i] + bk[2 * i + 1] <= n, "hcb_comm: bucket out of range");
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  const bool cap = capturing(cur);
+  if (!cap) flush_timeline(c, false);
+  if (compress && c->cbuf_bytes < (size_t)n * 2) {
+    TORCH_CHECK(!cap, "hcb_comm: first compressed reduction must run outside graph capture");
+    HCB_HIP(hipStreamSynchronize(c->stream));
+    if (c->cbuf) HCB_HIP(hipFree(c->cbuf));
+    HCB_HIP(hipMalloc(&c->cbuf, (size_t)n * 2));
+    c->cbuf_bytes = (size_t)n * 2;
+  }
+  HCB_HIP(hipEventRecord(c->fork_ev, cur));
+  HCB_HIP(hipStreamWaitEvent(c->stream, c->fork_ev, 0));
+  const bool tl = c->tl.is_open() && !cap;
+  float* fp = flat.data_ptr<float>();
+  for (int64_t i = 0; i < nb; ++i) {
+    int64_t off = bk[2 * i], len = bk[2 * i + 1];
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (tl) {
+      e0 = c->get_event();
+      HCB_HIP(hipEventRecord(e0, c->stream));
+    }
+    if (compress) {
+      uint16_t* cb = reinterpret_cast<uint16_t*>(c->cbuf) + off;
+      hcb::launch_bucket_pack(fp + off, cb, len, (float)scale, 1, c->stream);
+      HCB_NCCL(ncclAllReduce(cb, cb, len, ncclBfloat16, average ? ncclAvg : ncclSum, c->comm, c->stream));
+      hcb::launch_bucket_unpack(cb, fp + off, len, 1.0f, 1, c->stream);
+    } else {
+      HCB_NCCL(ncclAllReduce(fp + off, fp + off, len, ncclFloat32, average ? ncclAvg : ncclSum, c->comm, c->stream));
+    }
+    if (tl) {
+      e1 = c->get_event();
+      HCB_HIP(hipEventRecord(e1, c->stream));
+      c->pending.push_back({compress ? "PACK_ALLREDUCE_UNPACK" : "ALLREDUCE", (int)i, len * (compress ? 2 : 4), e0, e1});
+    }
+  }
+  HCB_HIP(hipEventRecord(c->join_ev, c->stream));
+  HCB_HIP(hipStreamWaitEvent(cur, c->join_ev, 0));
+  if (!cap) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->watch_ev = c->join_ev;
+    c->watch_since = std::chrono::steady_clock::now();
+    c->watching = true;
+    c->watch_cycle = c->cycle;
+  }
+  c->cycle++;
+}
+
+void barrier(int64_t h) {
+  Comm* c = get(h);
+  Tensor t = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, c->device));
+  allreduce_(h, t, false);
+  HCB_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStream().stream()));
+}
+
+int64_t comm_rank(int64_t h) { return get(h)->rank; }
+int64_t comm_size(int64_t h) { return get(h)->world; }
+
+void abort_comm(int64_t h) {
+  Comm* c = get(h);
+  if (c->comm) {
+    ncclCommAbort(c->comm);
+    c->comm = nullptr;
+  }
+}
+
+std::string version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return std::to_string(v);
+}
+
+}  // namespace
+
+TORCH_LIBRARY(hcb_comm, m) {
+  m.def("unique_id() -> Tensor", unique_id);
+  m.def("create(Tensor uid, int rank, int world, int device) -> int", create);
+  m.def("destroy(int h) -> ()", destroy);
+  m.def("allreduce_(int h, Tensor(a!) t, bool average) -> ()", allreduce_);
+  m.def("broadcast_(int h, Tensor(a!) t, int root) -> ()", broadcast_);
+  m.def("allgather_(int h, Tensor input, Tensor(a!) output) -> ()", allgather_);
+  m.def("reduce_scatter_(int h, Tensor input, Tensor(a!) output, bool average) -> ()", reduce_scatter_);
+  m.def("bucket_allreduce_(int h, Tensor(a!) flat, Tensor buckets, int compress, float scale, bool average) -> ()",
+        bucket_allreduce_);
+  m.def("barrier(int h) -> ()", barrier);
+  m.def("rank(int h) -> int", comm_rank);
+  m.def("size(int h) -> int", comm_size);
+  m.def("abort(int h) -> ()", abort_comm);
+  m.def("version() -> str", version);
+}

@@ -76,16 +76,57 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restric
   slab_write(lds_f, s1, s2, C, rm, slab + (size_t)blockIdx.x * 2 * C);
 }
 
-__global__ void bn_finalize_kernel(const float* slab, int T, int C, double count, float eps,
-                                   float momentum, float* mean, float* invstd, float* run_mean,
-                                   float* run_var) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Parallel slab reduction: a block owns 64 channels (one per lane, so every load is a
+// 256-byte coalesced row segment); its 8 waves stride over the T partial rows with 4
+// independent loads in flight each, accumulate in fp64, then combine through LDS.
+constexpr int FIN_WAVES = 8;
+__device__ __forceinline__ void slab_reduce64(const float* slab, int T, int C, double* a_out,
+                                              double* b_out, double* lds) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   double a = 0.0, b = 0.0;
-  for (int t = 0; t < T; ++t) {
-    a += (double)slab[(size_t)t * 2 * C + c];
-    b += (double)slab[(size_t)t * 2 * C + C + c];
+  if (c < C) {
+    int t = wid;
+    for (; t + 3 * FIN_WAVES < T; t += 4 * FIN_WAVES) {
+      float x0 = slab[(size_t)t * 2 * C + c], y0 = slab[(size_t)t * 2 * C + C + c];
+      float x1 = slab[(size_t)(t + FIN_WAVES) * 2 * C + c], y1 = slab[(size_t)(t + FIN_WAVES) * 2 * C + C + c];
+      float x2 = slab[(size_t)(t + 2 * FIN_WAVES) * 2 * C + c],
+            y2 = slab[(size_t)(t + 2 * FIN_WAVES) * 2 * C + C + c];
+      float x3 = slab[(size_t)(t + 3 * FIN_WAVES) * 2 * C + c],
+            y3 = slab[(size_t)(t + 3 * FIN_WAVES) * 2 * C + C + c];
+      a += ((double)x0 + (double)x1) + ((double)x2 + (double)x3);
+      b += ((double)y0 + (double)y1) + ((double)y2 + (double)y3);
+    }
+    for (; t < T; t += FIN_WAVES) {
+      a += (double)slab[(size_t)t * 2 * C + c];
+      b += (double)slab[(size_t)t * 2 * C + C + c];
+    }
   }
+  lds[wid * 64 + lane] = a;
+  lds[FIN_WAVES * 64 + wid * 64 + lane] = b;
+  __syncthreads();
+  if (wid == 0) {
+    a = 0.0;
+    b = 0.0;
+#pragma unroll
+    for (int w = 0; w < FIN_WAVES; ++w) {
+      a += lds[w * 64 + lane];
+      b += lds[FIN_WAVES * 64 + w * 64 + lane];
+    }
+  }
+  *a_out = a;
+  *b_out = b;
+}
+
+__global__ __launch_bounds__(512) void bn_finalize_kernel(const float* slab, int T, int C, double count,
+                                                          float eps, float momentum, float* mean,
+                                                          float* invstd, float* run_mean,
+                                                          float* run_var) {
+  __shared__ double lds[2 * FIN_WAVES * 64];
+  double a, b;
+  slab_reduce64(slab, T, C, &a, &b, lds);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
   double mu = a / count;
   double var = b / count - mu * mu;
   if (var < 0.0) var = 0.0;
@@ -189,15 +230,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   slab_write(lds_f, s1, s2, C, rm, slab + (size_t)blockIdx.x * 2 * C);
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* slab, int T, int C, float* dgamma,
-                                       float* dbeta) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int t = 0; t < T; ++t) {
-    a += (double)slab[(size_t)t * 2 * C + c];
-    b += (double)slab[(size_t)t * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(512) void bn_bwd_finalize_kernel(const float* slab, int T, int C,
+                                                              float* dgamma, float* dbeta) {
+  __shared__ double lds[2 * FIN_WAVES * 64];
+  double a, b;
+  slab_reduce64(slab, T, C, &a, &b, lds);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
   dbeta[c] = (float)a;
   dgamma[c] = (float)b;
 }
@@ -250,7 +289,7 @@ void launch_bn_stats(const void* x, int M, int C, int ldx, float* slab, int T, h
 void launch_bn_finalize(const float* slab, int T, int C, double count, float eps, float momentum,
                         float* mean, float* invstd, float* run_mean, float* run_var,
                         hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, slab, T, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, st, slab, T, C,
                      count, eps, momentum, mean, invstd, run_mean, run_var);
 }
 
@@ -275,7 +314,7 @@ void launch_bn_bwd_reduce2(const void* dy, int lddy, const void* y, int ldyv, co
 
 void launch_bn_bwd_finalize(const float* slab, int T, int C, float* dgamma, float* dbeta,
                             hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, slab, T, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, st, slab, T, C,
                      dgamma, dbeta);
 }
 

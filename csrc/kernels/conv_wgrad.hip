@@ -19,7 +19,13 @@
 
 namespace hcb {
 
-__device__ __forceinline__ int wg_swz(int row) { return (row & 3) | ((row >> 1) & 4); }
+// 32-byte-slot XOR swizzle for an LDS row of NSLOT slots (NSLOT = tile cols / 16): the 8 rows
+// read by one 32-lane half of a ds_read_b64_tr_b16 land on distinct bank groups.
+template <int NSLOT>
+__device__ __forceinline__ int wg_swz(int row) {
+  if constexpr (NSLOT >= 8) return (row & 3) | ((row >> 1) & 4);
+  else return ((row >> 1) & 1) | ((row >> 2) & 2);
+}
 
 template <int WM, int WN, int TM, int TN, bool CBIG>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
@@ -111,25 +117,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       int row = a_r0 + A_RSTEP * v;
-      int slot = (a_cv >> 1) ^ wg_swz(row);
+      int slot = (a_cv >> 1) ^ wg_swz<BM / 16>(row);
       *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + row * BM * 2 + slot * 32 + (a_cv & 1) * 16) = ra[v];
     }
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       int row = b_r0 + B_RSTEP * v;
-      int slot = (b_cv >> 1) ^ wg_swz(row);
+      int slot = (b_cv >> 1) ^ wg_swz<BN / 16>(row);
       *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + row * BN * 2 + slot * 32 + (b_cv & 1) * 16) = rb[v];
     }
   };
 
   const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
-  auto tr_read = [&](const char* base, int rowbytes, int row, int col) -> short4v {
-    // lane supplies row (row + q4), columns col + 4*p4 (col multiple of 16)
-    int rr = row + q4;
-    int cb = (col + 4 * p4) * 2;
-    int slot = (cb >> 5) ^ wg_swz(rr);
-    const char* a = base + rr * rowbytes + slot * 32 + (cb & 31);
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(a));
+  // lane supplies row (row + q4), columns col + 4*p4 (col a multiple of 16); rows are NSLOT*32 B
+  auto tr_read_a = [&](const char* base, int row, int col) -> short4v {
+    int rr = row + q4, cb = (col + 4 * p4) * 2;
+    int slot = (cb >> 5) ^ wg_swz<BM / 16>(rr);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BM * 2 + slot * 32 + (cb & 31)));
+  };
+  auto tr_read_b = [&](const char* base, int row, int col) -> short4v {
+    int rr = row + q4, cb = (col + 4 * p4) * 2;
+    int slot = (cb >> 5) ^ wg_swz<BN / 16>(rr);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BN * 2 + slot * 32 + (cb & 31)));
   };
 
   gload(kt_begin);
@@ -146,16 +155,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         int col = wm * TM + i * 16;
-        short4v lo = tr_read(Ab, BM * 2, ks * 32 + 8 * g, col);
-        short4v hi = tr_read(Ab, BM * 2, ks * 32 + 8 * g + 4, col);
+        short4v lo = tr_read_a(Ab, ks * 32 + 8 * g, col);
+        short4v hi = tr_read_a(Ab, ks * 32 + 8 * g + 4, col);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[i] = __builtin_bit_cast(bf16x8, t);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         int col = wn * TN + j * 16;
-        short4v lo = tr_read(Bb, BN * 2, ks * 32 + 8 * g, col);
-        short4v hi = tr_read(Bb, BN * 2, ks * 32 + 8 * g + 4, col);
+        short4v lo = tr_read_b(Bb, ks * 32 + 8 * g, col);
+        short4v hi = tr_read_b(Bb, ks * 32 + 8 * g + 4, col);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[j] = __builtin_bit_cast(bf16x8, t);
       }

@@ -98,10 +98,11 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
 // ---------------------------------------------------------------- pooling
 void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,
                      int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
-                     int count_include_pad, hipStream_t st);
+                     int count_include_pad, void* idx, hipStream_t st);
 void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int N, int H, int W,
                      int C, int ldx, int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph,
-                     int pw, int is_max, int count_include_pad, int accum, hipStream_t st);
+                     int pw, int is_max, int count_include_pad, int accum, const void* idx,
+                     hipStream_t st);
 void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
 void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
 

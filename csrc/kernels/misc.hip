@@ -136,26 +136,28 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
                                                           uint16_t* __restrict__ pack,
                                                           const WPackEntry* __restrict__ ents) {
   const WPackEntry e = ents[blockIdx.y];
-  const int K = (int)(e.R * e.S * e.C);
-  const int Kt = (int)(e.R * e.S * e.Nout);
+  const int R = (int)e.R, S = (int)e.S, C = (int)e.C, Nout = (int)e.Nout;
+  const int Kpad = (int)e.Kpad, Kpad_t = (int)e.Kpad_t;
+  const int K = R * S * C;
+  const int Kt = R * S * Nout;
   const float* src = master + e.src_off;
-  const int64_t n1 = e.pack_off >= 0 ? (int64_t)e.Nout * e.Kpad : 0;
-  const int64_t n2 = e.tr_off >= 0 ? (int64_t)e.C * e.Kpad_t : 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n1 + n2;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int n1 = e.pack_off >= 0 ? Nout * Kpad : 0;
+  const int n2 = e.tr_off >= 0 ? C * Kpad_t : 0;
+  // 32-bit index math (every conv weight is < 2^31 elements); packed part is a straight
+  // row-padded copy, the transposed part reads the master through L2 (weights are small)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1 + n2; i += gridDim.x * blockDim.x) {
     if (i < n1) {
-      int j = (int)(i / e.Kpad), k = (int)(i % e.Kpad);
-      float v = k < K ? src[(int64_t)j * K + k] : 0.f;
+      int j = i / Kpad, k = i - j * Kpad;
+      float v = k < K ? src[j * K + k] : 0.f;
       pack[e.pack_off + i] = f2bf(v);
     } else {
-      int64_t t = i - n1;
-      int c = (int)(t / e.Kpad_t), k = (int)(t % e.Kpad_t);
+      int t = i - n1;
+      int c = t / Kpad_t, k = t - c * Kpad_t;
       float v = 0.f;
       if (k < Kt) {
-        int tap = k / e.Nout, kk = k % e.Nout;
-        int rr = tap / e.S, ss = tap % e.S;
-        int r = e.R - 1 - rr, s = e.S - 1 - ss;
-        v = src[(((int64_t)kk * e.R + r) * e.S + s) * e.C + c];
+        int tap = k / Nout, kk = k - tap * Nout;
+        int rr = tap / S, ss = tap - rr * S;
+        v = src[((kk * R + (R - 1 - rr)) * S + (S - 1 - ss)) * C + c];
       }
       pack[e.tr_off + t] = f2bf(v);
     }
@@ -277,7 +279,7 @@ void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st) {
 void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
                         int n_entries, int64_t max_work, hipStream_t st) {
   int gx = grid_for(max_work);
-  if (gx > 256) gx = 256;
+  if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(weight_pack_kernel, dim3(gx, n_entries), dim3(256), 0, st, master, pack,
                      entries_dev);
 }

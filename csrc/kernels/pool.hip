@@ -16,7 +16,8 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const uint16_t* __restric
                                                        uint16_t* __restrict__ y, int N, int H,
                                                        int W, int C, int ldx, int P, int Q,
                                                        int ldy, int kh, int kw, int sh, int sw,
-                                                       int ph, int pw, int is_max, int incl_pad) {
+                                                       int ph, int pw, int is_max, int incl_pad,
+                                                       uint8_t* __restrict__ amax) {
   const int CV = C >> 3;
   const long total = (long)N * P * Q * CV;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -29,8 +30,12 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const uint16_t* __restric
     int n = (int)(t / P);
     int h0 = p * sh - ph, w0 = q * sw - pw;
     float acc[8];
+    int arg[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = is_max ? -INFINITY : 0.f;
+    for (int e = 0; e < 8; ++e) {
+      acc[e] = is_max ? -INFINITY : 0.f;
+      arg[e] = 255;
+    }
     int cnt = 0;
     for (int r = 0; r < kh; ++r) {
       int h = h0 + r;
@@ -42,8 +47,13 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const uint16_t* __restric
         unpack8(*reinterpret_cast<const u32x4*>(x + ((size_t)(n * H + h) * W + w) * ldx + cv * 8), f);
         ++cnt;
         if (is_max) {
+          const int pos = r * kw + s;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[e] = fmaxf(acc[e], f[e]);
+          for (int e = 0; e < 8; ++e)
+            if (f[e] > acc[e]) {  // strict: the FIRST maximal element keeps the gradient
+              acc[e] = f[e];
+              arg[e] = pos;
+            }
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[e] += f[e];
@@ -56,6 +66,12 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const uint16_t* __restric
       for (int e = 0; e < 8; ++e) acc[e] /= div;
     }
     *reinterpret_cast<u32x4*>(y + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8) = pack8(acc);
+    if (is_max && amax != nullptr) {
+      u32x2 a;
+      a[0] = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+      a[1] = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+      *reinterpret_cast<u32x2*>(amax + ((size_t)(n * P + p) * Q + q) * C + cv * 8) = a;
+    }
   }
 }
 
@@ -63,7 +79,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ y, uint16_t* __restrict__ dx, int N, int H, int W, int C, int ldx,
     int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
-    int incl_pad, int accum) {
+    int incl_pad, int accum, const uint8_t* __restrict__ amax) {
   const int CV = C >> 3;
   const long total = (long)N * H * W * CV;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -93,7 +109,13 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(
         float d[8];
         unpack8(*reinterpret_cast<const u32x4*>(dy + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8), d);
         int h0 = p * sh - ph, w0 = q * sw - pw;
-        if (is_max) {
+        if (is_max && amax != nullptr) {
+          const int mine = (h - h0) * kw + (w - w0);
+          u32x2 a = *reinterpret_cast<const u32x2*>(amax + ((size_t)(n * P + p) * Q + q) * C + cv * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if ((int)((a[e >> 2] >> (8 * (e & 3))) & 0xff) == mine) g[e] += d[e];
+        } else if (is_max) {
           float yv[8];
           unpack8(*reinterpret_cast<const u32x4*>(y + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8), yv);
           // first position (row-major within the window) holding the max, per channel
@@ -193,20 +215,22 @@ static int ew_grid(long total) {
 
 void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,
                      int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
-                     int count_include_pad, hipStream_t st) {
+                     int count_include_pad, void* idx, hipStream_t st) {
   long total = (long)N * P * Q * (C / 8);
   hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)x,
                      (uint16_t*)y, N, H, W, C, ldx, P, Q, ldy, kh, kw, sh, sw, ph, pw, is_max,
-                     count_include_pad);
+                     count_include_pad, (uint8_t*)idx);
 }
 
 void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int N, int H, int W,
                      int C, int ldx, int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph,
-                     int pw, int is_max, int count_include_pad, int accum, hipStream_t st) {
+                     int pw, int is_max, int count_include_pad, int accum, const void* idx,
+                     hipStream_t st) {
   long total = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(pool_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
                      (const uint16_t*)x, (const uint16_t*)y, (uint16_t*)dx, N, H, W, C, ldx, P, Q,
-                     ldy, kh, kw, sh, sw, ph, pw, is_max, count_include_pad, accum);
+                     ldy, kh, kw, sh, sw, ph, pw, is_max, count_include_pad, accum,
+                     (const uint8_t*)idx);
 }
 
 void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {

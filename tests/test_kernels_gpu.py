@@ -148,7 +148,7 @@ def test_conv_wgrad_split_k_large_reduction():
     Fn.conv_wgrad(dz, x, spec, dw)
     ref = torch.zeros(64, 3, 3, 64)
     Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
-    assert rel_err(dw, ref) < 1e-2
+    assert rel_err(dw, ref.view(64, -1)) < 1e-2
 
 
 @pytest.mark.parametrize("C", [64, 256, 80, 2048])
@@ -201,15 +201,17 @@ def test_pool_fwd_bwd(kind):
         H = 8
         layer = Pool("p", (H, H, C), 8, 8, 1, 1, "VALID", is_max=False)
     x = bf(torch.randn(N, H, H, C, device=DEV))
-    y = layer.forward(x)
     yc = layer.forward(x.float().cpu())
-    assert rel_err(y, yc) < 1e-2
-    dy = bf(torch.randn_like(y.float()))
-    layer._saved = (x, y)
-    dx = layer.backward(dy)
-    layer._saved = (x.float().cpu(), y.float().cpu())
+    dy = bf(torch.randn(yc.shape, device=DEV))
     dxc = layer.backward(dy.float().cpu())
+    y = layer.forward(x)
+    assert rel_err(y, yc) < 1e-2
+    dx = layer.backward(dy)
     assert rel_err(dx, dxc) < 1e-2
+    if layer.is_max:  # the recompute path (no argmax buffer) must agree with the argmax path
+        dx2 = torch.empty_like(dx)
+        Fn.pool_backward(dy, x, y, dx2, *layer.k, *layer.s, layer.pads, True, False, False, argmax=None)
+        assert torch.equal(dx, dx2)
 
 
 def test_gap_and_softmax_and_colsum():
