@@ -1,0 +1,144 @@
+"""Per-shape kernel configuration autotuning for the implicit-GEMM convolutions (the
+``cudnn.benchmark`` / MIOpen find-db role, done for our own kernels).
+
+For every distinct GEMM problem of a model (forward conv, data-grad conv, weight-grad conv)
+each candidate block-tile configuration (and split-K factor for weight gradients) is timed
+with HIP events on scratch buffers of the real shapes, and the fastest is recorded. The
+table is cached in JSON (``tuned/<arch>.json``, shipped in-tree so a multi-GPU run does not
+re-tune) and consulted by ``functional.conv_cfg`` / ``functional.wgrad_cfg``.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from typing import Dict, List, Tuple
+
+import torch
+
+from . import _ext
+from . import functional as Fn
+
+_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned")
+DEFAULT_CACHE = os.path.join(_DIR, "mi355x.json")
+
+
+def _key_str(k) -> str:
+    return "|".join(str(v) for v in k)
+
+
+def _key_parse(s: str):
+    parts = s.split("|")
+    return (parts[0],) + tuple(int(p) for p in parts[1:])
+
+
+def load_cache(path: str = DEFAULT_CACHE) -> int:
+    if not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        d = json.load(f)
+    table = {}
+    for k, v in d.get("entries", {}).items():
+        table[_key_parse(k)] = tuple(v) if isinstance(v, list) else v
+    Fn.set_tuned(table)
+    return len(table)
+
+
+def save_cache(path: str = DEFAULT_CACHE) -> None:
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    old = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f).get("entries", {})
+    for k, v in Fn._tuned.items():
+        old[_key_str(k)] = list(v) if isinstance(v, tuple) else v
+    with open(path, "w") as f:
+        json.dump({"arch": "gfx950", "entries": old}, f, indent=0, sort_keys=True)
+
+
+def _time(fn, reps=3) -> float:
+    fn()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _bf(shape, dev):
+    return torch.randn(shape, device=dev).to(torch.bfloat16)
+
+
+def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
+    """Tune fwd / dgrad / wgrad problems of one ConvBN layer (skips already-tuned keys)."""
+    hcb = _ext.ops()
+    spec = layer.spec
+    H, W, Cin = layer.in_shape
+    P, Q, Cout = layer.out_shape
+    N = batch
+    out = []
+    x = _bf((N, H, W, Cin), dev)
+    dz = _bf((N, P, Q, Cout), dev)
+    # forward
+    M = N * P * Q
+    k = Fn.fwd_key(M, Cout, spec.K)
+    if k not in Fn._tuned:
+        y = torch.empty((N, P, Q, Cout), dtype=torch.bfloat16, device=dev)
+        best = None
+        for cfg in Fn.fwd_candidates(Cout):
+            bm = Fn._CONV_TILES[cfg][0]
+            slab = torch.empty(math.ceil(M / bm) * 2 * Cout, dtype=torch.float32, device=dev)
+            t = _time(lambda: Fn.conv_forward(x, spec, layer.pack.pack, None, y, stats=slab, cfg=cfg))
+            if best is None or t < best[0]:
+                best = (t, cfg)
+        Fn._tuned[k] = best[1]
+        out.append((k, best))
+    # data gradient
+    if layer.need_dx:
+        dx = torch.zeros((N, H, W, Cin), dtype=torch.bfloat16, device=dev)
+        geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
+        k = Fn.fwd_key(geo[0], Cin, geo[1])
+        if k not in Fn._tuned:
+            best = None
+            for cfg in Fn.fwd_candidates(Cin):
+                t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=cfg))
+                if best is None or t < best[0]:
+                    best = (t, cfg)
+            Fn._tuned[k] = best[1]
+            out.append((k, best))
+    # weight gradient
+    k = Fn.wgrad_key(Cout, spec.K, M)
+    if k not in Fn._tuned:
+        dw = torch.zeros((Cout, spec.K), dtype=torch.float32, device=dev)
+        best = None
+        for cfg, splits in Fn.wgrad_candidates(Cout, spec.K, M):
+            t = _time(lambda: Fn.conv_wgrad(dz, x, spec, dw, cfg=(cfg, splits)))
+            if best is None or t < best[0]:
+                best = (t, (cfg, splits))
+        Fn._tuned[k] = best[1]
+        out.append((k, best))
+    if verbose:
+        for kk, (t, c) in out:
+            print(f"  tuned {kk}: cfg={c} {t * 1000:.1f} us")
+    return out
+
+
+def tune_model(model, batch: int, verbose=False, cache: str = DEFAULT_CACHE, save=True) -> int:
+    from ..nn.layers import ConvBN
+
+    dev = model.device
+    model.ps.repack()
+    n = 0
+    for l in model.all_layers():
+        if isinstance(l, ConvBN) and l.bn:
+            n += len(tune_conv_layer(l, batch, dev, verbose))
+    torch.cuda.synchronize()
+    if save and n and cache:
+        try:
+            save_cache(cache)
+        except OSError:
+            pass
+    return n

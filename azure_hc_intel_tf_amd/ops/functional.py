@@ -93,12 +93,39 @@ N_CU = 256
 _tuned: dict = {}
 
 
+def fwd_key(M: int, N: int, K: int):
+    return ("fwd", M, N, K)
+
+
+def wgrad_key(Nout: int, K: int, M: int):
+    return ("wgrad", Nout, K, M)
+
+
+def fwd_candidates(N: int):
+    return [0, 3, 1, 2] if N > 64 else [1, 2]
+
+
+def wgrad_candidates(Nout: int, K: int, M: int):
+    ksteps = math.ceil(M / 64)
+    out = []
+    for c, (bm, bn) in _WGRAD_TILES.items():
+        tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
+        for s in (1, 2, 4, 8, 16, 32, 64, 128):
+            if s > 1 and ksteps // s < 2:
+                break
+            if tiles * s > 8 * N_CU:
+                break
+            out.append((c, s))
+    return out
+
+
 def conv_cfg(M: int, N: int, K: int) -> int:
-    """Pick a block tile for C[M,N] (+K): enough workgroups to fill 256 CUs, biggest tile first."""
-    key = ("fwd", M, N, K)
+    """Block tile for C[M,N] (+K): the autotuned choice if known, else the biggest tile that
+    still gives >= 2 workgroups per CU."""
+    key = fwd_key(M, N, K)
     if key in _tuned:
         return _tuned[key]
-    cands = [0, 3, 1, 2] if N > 64 else [1, 2]
+    cands = fwd_candidates(N)
     for c in cands:
         bm, bn = _CONV_TILES[c]
         if math.ceil(M / bm) * math.ceil(N / bn) >= 2 * N_CU:
@@ -108,9 +135,9 @@ def conv_cfg(M: int, N: int, K: int) -> int:
 
 def wgrad_cfg(Nout: int, K: int, M: int):
     """(tile cfg, split-K) for dW[Nout, K] reduced over M pixels."""
-    key = ("wgrad", Nout, K, M)
+    key = wgrad_key(Nout, K, M)
     if key in _tuned:
-        return _tuned[key]
+        return tuple(_tuned[key])
     c = 0 if Nout >= 128 and K >= 128 else (1 if K >= 128 else 2)
     bm, bn = _WGRAD_TILES[c]
     tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
@@ -118,6 +145,15 @@ def wgrad_cfg(Nout: int, K: int, M: int):
     target = 2 * N_CU
     splits = max(1, min(ksteps // 4 if ksteps >= 4 else 1, math.ceil(target / tiles)))
     return c, splits
+
+
+def dgrad_problem(spec, N, H, W, P, Q):
+    """(M, K) of the data-gradient GEMM of a conv."""
+    Cdz = spec.cout if spec.cout % 8 == 0 else _round_up(spec.cout, 8)
+    K = spec.kh * spec.kw * Cdz
+    if (spec.sh > 1 or spec.sw > 1) and spec.kh == 1 and spec.kw == 1 and spec.pt == 0 and spec.pl == 0:
+        return N * P * Q, K
+    return N * H * W, K
 
 
 def set_tuned(table: dict) -> None:
@@ -160,7 +196,7 @@ def conv_stats_slab(x_shape, spec: ConvSpec, device, cfg=None):
 
 
 # ---------------------------------------------------------------- conv data grad
-def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool):
+def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None):
     """dx[N,H,W,cin] (+)= conv_transpose(dz, W). dx must be zero-filled by the caller when
     not accumulating and the conv is a strided 1x1 (remap path leaves gaps)."""
     N, P, Q, _ = dz.shape
@@ -183,7 +219,8 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool):
             geom = [N, P, Q, Cdz, ld(dz), H, W, spec.kh, spec.kw, 1, 1, pt, pl, spec.dh, spec.dw,
                     spec.sh, spec.sw, spec.cin_pad, K, Kpad, ld(dx), 0, H, W, 1, 1,
                     1 if accumulate else 0, 0]
-        cfg = conv_cfg(M, spec.cin_pad, K)
+        if cfg is None:
+            cfg = conv_cfg(M, spec.cin_pad, K)
         _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg)
         return dx
     Hp = H + spec.pt + spec.pb
@@ -200,13 +237,13 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool):
 
 
 # ---------------------------------------------------------------- conv weight grad
-def conv_wgrad(dz, x, spec: ConvSpec, dw):
+def conv_wgrad(dz, x, spec: ConvSpec, dw, cfg=None):
     """dw[cout, kh, kw, cin_pad] (fp32) += sum over pixels of dz (x) im2col(x)."""
     N, H, W, _ = x.shape
     _, P, Q, _ = dz.shape
     if dz.is_cuda:
         M = N * P * Q
-        cfg, splits = wgrad_cfg(spec.cout, spec.K, M)
+        cfg, splits = cfg if cfg is not None else wgrad_cfg(spec.cout, spec.K, M)
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
                 spec.dh, spec.dw, spec.cout, ld(dz)]
         _ext.ops().conv_wgrad(dz, x, dw, geom, cfg, splits)

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch_size", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--no_tune", action="store_true", help="skip per-shape kernel autotuning")
     ap.add_argument("--compression", default=None, choices=[None, "fp16", "bf16"])
     ap.add_argument("--engine", default="torch", choices=["native", "torch"])
     args = ap.parse_args()
@@ -63,6 +64,13 @@ def main():
 
     model = create_model(args.model, device=dev)
     B = args.batch_size
+    from azure_hc_intel_tf_amd.ops import autotune
+
+    autotune.load_cache()
+    if not args.no_tune:
+        n = autotune.tune_model(model, B, save=(rank == 0))
+        if n and rank == 0:
+            print(f"[bench] autotuned {n} conv problems", file=sys.stderr)
     if reducer is not None:
         reducer.broadcast_(model.ps.master, 0)
         reducer.broadcast_(model.ps.buf, 0)

@@ -171,6 +171,32 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   // ---- epilogue: accumulators -> LDS (fp32, padded rows) -> coalesced stores
   constexpr int LDC = BN + 4;
   float* Cs = reinterpret_cast<float*>(smem);
+  float* red = Cs + BM * LDC;  // [WM][2][BN] per-wave column partial sums
+  if (p.stats != nullptr) {
+    // per-column partial BN statistics straight from the accumulators (rows beyond M are
+    // exact zeros): sum the wave's 4 row-quads in registers, then across the 4 lane groups
+    // that share a column with two xor-shuffles.
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[i][j][e];
+          s1 += v;
+          s2 += v * v;
+        }
+      s1 += __shfl_xor(s1, 16, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (fq == 0) {
+        red[(wm * 2) * BN + wn * TN + j * 16 + frow] = s1;
+        red[(wm * 2 + 1) * BN + wn * TN + j * 16 + frow] = s2;
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -184,13 +210,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   __syncthreads();
 
   if (p.stats != nullptr) {
-    // per-column partial BN statistics of this M tile (rows beyond M are exact zeros)
     for (int col = tid; col < BN; col += 256) {
       float s1 = 0.f, s2 = 0.f;
-      for (int r = 0; r < BM; ++r) {
-        float v = Cs[r * LDC + col];
-        s1 += v;
-        s2 += v * v;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s1 += red[(w * 2) * BN + col];
+        s2 += red[(w * 2 + 1) * BN + col];
       }
       int gc = n0 + col;
       if (gc < p.Nout) {
@@ -252,7 +277,7 @@ static void launch_cfg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
   size_t lds_main = (size_t)2 * (BM + BN) * 8 * 16;
-  size_t lds_epi = (size_t)BM * (BN + 4) * 4;
+  size_t lds_epi = (size_t)BM * (BN + 4) * 4 + (size_t)WM * 2 * BN * 4;
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;

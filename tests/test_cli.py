@@ -1,0 +1,113 @@
+"""CLI / flag / launcher-math parity with the reference runners (no GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from azure_hc_intel_tf_amd.bench.benchmark_cnn import get_perf_timing_str
+from azure_hc_intel_tf_amd.bench.flags import noop_flags_set, parse_flags
+from azure_hc_intel_tf_amd.launch.launcher import cpu_shares, fabric_env, worker_env
+from azure_hc_intel_tf_amd.launch.run_tf_sing import tf_args, worker_math
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+REFERENCE_FLAGS = [  # /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81
+    "--batch_size=64", "--num_warmup_batches=50", "--num_batches=100", "--model=resnet50",
+    "--num_intra_threads=11", "--num_inter_threads=2", "--kmp_blocktime=1",
+    "--kmp_affinity=granularity=fine,noverbose,compact,1,0", "--display_every=10", "--data_format=NCHW",
+    "--optimizer=momentum", "--forward_only=False", "--device=cpu", "--mkl=TRUE", "--variable_update=horovod",
+    "--horovod_device=cpu", "--local_parameter_device=cpu", "--data_dir=/mnt/shared/imagenet-data/tfrecords-20",
+    "--data_name=imagenet",
+]
+
+
+def test_reference_flag_set_parses():
+    p = parse_flags(REFERENCE_FLAGS)
+    assert p.batch_size == 64 and p.num_warmup_batches == 50 and p.num_batches == 100
+    assert p.model == "resnet50" and p.optimizer == "momentum" and p.mkl is True and p.forward_only is False
+    assert p.variable_update == "horovod" and p.horovod_device == "cpu" and p.data_format == "NCHW"
+    assert not p._unknown
+    assert "mkl" in noop_flags_set(p) and "kmp_blocktime" in noop_flags_set(p)
+
+
+def test_bool_flag_forms():
+    assert parse_flags(["--use_fp16"]).use_fp16 is True
+    assert parse_flags(["--nouse_hip_graph"]).use_hip_graph is False
+    assert parse_flags(["--forward_only=1"]).forward_only is True
+    p = parse_flags(["--some_future_tf_flag=3"])
+    assert p._unknown == ["--some_future_tf_flag=3"]
+
+
+@pytest.mark.parametrize("wps,sockets,cps,gpus,exp_wpn,exp_total", [
+    (0, 2, 22, 8, 1, 4),      # reference quirk fixed: WPS=0 -> 1 worker per node
+    (1, 2, 22, 8, 2, 8),
+    (4, 2, 22, 8, 8, 16),
+    (8, 2, 22, 8, 8, 16),     # capped at one worker per GPU
+])
+def test_worker_math_gpu(wps, sockets, cps, gpus, exp_wpn, exp_total):
+    p = worker_math(2 if exp_total > exp_wpn else 4, wps, sockets, cps, "gpu", gpus)
+    assert p.workers_per_node == exp_wpn
+
+
+def test_worker_math_cpu_matches_reference():
+    # run-tf-sing-ucx-openmpi.sh:40-50 on a 2-socket 22-core node (HC44rs)
+    p = worker_math(4, 1, 2, 22, "cpu")
+    assert (p.workers_per_node, p.cores_per_worker, p.intra_t, p.inter_t, p.total_workers) == (2, 22, 11, 2, 8)
+    p = worker_math(2, 2, 2, 22, "cpu")
+    assert (p.workers_per_node, p.cores_per_worker, p.intra_t, p.total_workers) == (4, 11, 5, 8)
+    p = worker_math(1, 0, 2, 22, "cpu")
+    assert (p.workers_per_node, p.cores_per_worker, p.intra_t) == (1, 44, 22)
+
+
+def test_tf_args_are_reference_flags(monkeypatch):
+    monkeypatch.delenv("EXTRA_ARGS", raising=False)
+    p = worker_math(1, 1, 2, 22, "cpu", batch_size=64)
+    args = tf_args(p, env={})
+    parsed = parse_flags(args)
+    assert parsed.model == "resnet50" and parsed.num_warmup_batches == 50 and parsed.num_batches == 100
+    assert parsed.num_intra_threads == 11 and parsed.variable_update == "horovod"
+
+
+def test_fabric_env_and_worker_env():
+    assert fabric_env("ib") == {}
+    e = fabric_env("sock")
+    assert e["NCCL_P2P_DISABLE"] == "1" and e["NCCL_SHM_DISABLE"] == "1"
+    w = worker_env({}, 5, 1, 8, 4, 1, "10.0.0.1", 1234, "ib", 11)
+    assert w["RANK"] == "5" and w["LOCAL_RANK"] == "1" and w["WORLD_SIZE"] == "8" and w["GROUP_RANK"] == "1"
+    assert w["OMP_NUM_THREADS"] == "11" and w["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    shares = cpu_shares(4, list(range(16)))
+    assert shares == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9, 10, 11], [12, 13, 14, 15]]
+
+
+def test_perf_timing_string_format():
+    s = get_perf_timing_str(64, [0.1, 0.1, 0.1])
+    assert s == "images/sec: 640.0 +/- 0.0 (jitter = 0.0)"
+
+
+def test_run_script_dry_run():
+    env = dict(os.environ, DRY_RUN="1", DEVICE="cpu")
+    out = subprocess.run([os.path.join(ROOT, "benchmark-scripts", "run-tf-sing-ucx-openmpi.sh"), "2", "1", "64",
+                          "sock"], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "TOTAL_WORKERS" in out.stdout and "tf_cnn_benchmarks.py" in out.stdout
+    bad = subprocess.run([os.path.join(ROOT, "benchmark-scripts", "run-tf-sing-libfabric-intelmpi.sh"), "1"],
+                         env=env, capture_output=True, text=True, timeout=60)
+    assert bad.returncode != 0 and "usage" in bad.stderr
+
+
+def test_cpu_benchmark_end_to_end(tmp_path):
+    js = tmp_path / "s.json"
+    cmd = [sys.executable, os.path.join(ROOT, "tf_cnn_benchmarks.py"), "--device=cpu", "--model=resnet50",
+           "--batch_size=2", "--image_size=32", "--num_batches=3", "--num_warmup_batches=1", "--display_every=1",
+           "--optimizer=momentum", f"--json_summary={js}", f"--train_dir={tmp_path / 'ckpt'}"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "Step\tImg/sec\ttotal_loss" in out.stdout and "total images/sec:" in out.stdout
+    s = json.loads(js.read_text())
+    assert s["workers"] == 1 and s["num_batches"] == 3 and s["total_images_per_sec"] > 0
+    assert (tmp_path / "ckpt" / "model.ckpt-4.pt").exists()
+    # resume continues from the saved step
+    out2 = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert out2.returncode == 0 and "Restored checkpoint at step 4" in out2.stdout

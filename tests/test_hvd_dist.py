@@ -1,0 +1,121 @@
+"""Horovod-compatible API and gradient reducers on CPU with gloo, world_size 2 and 4."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    try:
+        from azure_hc_intel_tf_amd.parallel import hvd
+
+        hvd.init(backend="gloo")
+        fn(hvd)
+        hvd.shutdown()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+def run(world, fn):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    errs = [r for r in res if r[1] != "ok"]
+    assert not errs, errs
+
+
+def _collectives(hvd):
+    r, n = hvd.rank(), hvd.size()
+    t = torch.full((5,), float(r + 1))
+    assert torch.allclose(hvd.allreduce(t), torch.full((5,), (n + 1) / 2))
+    assert torch.allclose(hvd.allreduce(t, average=False), torch.full((5,), n * (n + 1) / 2))
+    from azure_hc_intel_tf_amd.parallel.compression import Compression
+
+    c = hvd.allreduce(t, compression=Compression.fp16)
+    assert c.dtype == torch.float32 and torch.allclose(c, torch.full((5,), (n + 1) / 2))
+    g = hvd.allgather(torch.full((r + 1, 2), float(r)))
+    assert g.shape == (n * (n + 1) // 2, 2)
+    b = hvd.broadcast(torch.full((3,), float(r)), root_rank=n - 1)
+    assert torch.all(b == n - 1)
+    assert hvd.broadcast_object({"r": r}, 0) == {"r": 0}
+    assert hvd.local_rank() == r and hvd.local_size() == n and hvd.cross_size() == 1
+    ts = [torch.full((7,), float(r)), torch.full((3, 3), 2.0 * r)]
+    hvd.grouped_allreduce_(ts)
+    assert torch.allclose(ts[0], torch.full((7,), (n - 1) / 2))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_hvd_collectives(world):
+    run(world, _collectives)
+
+
+def _dist_optimizer(hvd):
+    torch.manual_seed(hvd.rank())
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    hvd.broadcast_parameters(model.state_dict(), root_rank=0)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters())
+    hvd.broadcast_optimizer_state(opt, root_rank=0)
+    x = torch.randn(4, 8)
+    for _ in range(3):
+        opt.zero_grad()
+        model(x).pow(2).mean().backward()
+        opt.step()
+    # every rank must hold identical weights after averaged updates
+    w = torch.cat([p.detach().flatten() for p in model.parameters()])
+    allw = hvd.allgather(w.view(1, -1))
+    assert torch.allclose(allw[0], allw[-1], atol=1e-6)
+
+
+def test_distributed_optimizer_keeps_replicas_in_sync():
+    run(2, _dist_optimizer)
+
+
+def _engine_training(hvd):
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.parallel import make_reducer
+    from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+    m = create_model("resnet50", image_size=32, device="cpu", seed=100 + hvd.rank())
+    hvd.broadcast_global_variables(m, 0)
+    red = make_reducer("torch", bucket_bytes=1 << 20)
+    img, lab = synthetic_batch(m, 2, seed=hvd.rank())
+    img = (img - 127) / 60
+    t = Trainer(m, 2, constant_lr(0.01), reducer=red, world_size=hvd.size())
+    for _ in range(2):
+        t.step(img, lab)
+    allw = hvd.allgather(m.ps.master.view(1, -1))
+    assert torch.allclose(allw[0], allw[1])
+
+
+def test_flat_buffer_reducer_training_in_sync():
+    run(2, _engine_training)
+
+
+def test_make_buckets_cover_buffer_in_reverse():
+    from azure_hc_intel_tf_amd.parallel import make_buckets
+
+    b = make_buckets(1000, 256)
+    assert b[0] == (744, 256) and sum(n for _, n in b) == 1000 and b[-1][0] == 0
