@@ -55,6 +55,22 @@ def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
     raise ValueError(mode)
 
 
+class _FixedParam:
+    """A non-trainable per-channel constant with a scratch gradient sink (BN scale=False)."""
+
+    def __init__(self, value_buf, sink_buf):
+        self._v = value_buf
+        self._g = sink_buf
+
+    @property
+    def data(self):
+        return self._v.data
+
+    @property
+    def grad(self):
+        return self._g.data
+
+
 class Layer:
     in_shape: Tuple[int, int, int]
     out_shape: Tuple[int, int, int]
@@ -69,7 +85,7 @@ class ConvBN(Layer):
     def __init__(self, ps: ParamStore, name: str, in_shape, cout: int, kh: int, kw: int, sh: int = 1,
                  sw: int = 1, mode="SAME", relu: bool = True, bn: bool = True, need_dx: bool = True,
                  eps: float = 1e-5, decay: float = 0.9, logical_cin: Optional[int] = None,
-                 dilation: int = 1):
+                 dilation: int = 1, scale: bool = True):
         H, W, cin = in_shape
         self.name = name
         self.in_shape = in_shape
@@ -91,7 +107,11 @@ class ConvBN(Layer):
                         logical_numel=cout * kh * kw * lc)
         self.pack = ps.add_pack(self.w, cout, kh, kw, cin, self.spec.Kpad, self.spec.Kpad_t, want_tr=need_dx)
         if bn:
-            self.gamma = ps.add(f"{name}/batchnorm/gamma", (cout,), False, ParamStore.const(1.0))
+            if scale:
+                self.gamma = ps.add(f"{name}/batchnorm/gamma", (cout,), False, ParamStore.const(1.0))
+            else:  # tf batch_norm(scale=False): gamma fixed at 1, not a variable
+                self.gamma = _FixedParam(ps.add_buffer(f"{name}/batchnorm/gamma_fixed", (cout,), 1.0),
+                                         ps.add_buffer(f"{name}/batchnorm/gamma_grad_sink", (cout,), 0.0))
             self.beta = ps.add(f"{name}/batchnorm/beta", (cout,), False, ParamStore.const(0.0))
             self.rmean = ps.add_buffer(f"{name}/batchnorm/moving_mean", (cout,), 0.0)
             self.rvar = ps.add_buffer(f"{name}/batchnorm/moving_variance", (cout,), 1.0)
@@ -121,17 +141,11 @@ class ConvBN(Layer):
                                   self.decay, self.eps, y, self.relu, residual=residual, stats=slab, stats_T=T)
             self._saved = (x, z, y, saved, residual is not None)
             return y
+        assert residual is None, "conv without BN: no residual input"
         y = out if out is not None else empty_act((N, P, Q, C), dev)
-        if x.is_cuda:
-            Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, y, bias=self.bias.data)
-            assert not self.relu and residual is None, "plain conv: no fused activation on this path"
-        else:
-            Fn.conv_forward(x, self.spec, None, self.w.data, y, bias=self.bias.data)
-            if residual is not None:
-                y.add_(residual)
-            if self.relu:
-                y.relu_()
-        self._saved = (x, None, y, None, residual is not None)
+        Fn.conv_forward(x, self.spec, self.pack.pack if x.is_cuda else None, self.w.data, y, bias=self.bias.data,
+                        relu=self.relu)
+        self._saved = (x, None, y, None, False)
         return y
 
     # ------------------------------------------------------------------ backward
@@ -150,11 +164,13 @@ class ConvBN(Layer):
             Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
                            self.beta.grad, dz, gres)
         else:
-            assert not self.relu
-            dz = dy
-            Fn.colsum(dz.reshape(-1, C) if dz.is_contiguous() else dz, N * P * Q, C, self.bias.grad)
+            if self.relu:
+                dz = Fn.relu_backward(dy, y, empty_act((N, P, Q, C), dev))
+            else:
+                dz = dy if dy.is_contiguous() else dy.contiguous()
+            Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
-                gres = dy
+                gres = dz
         Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(C, -1) if dz.is_cuda else self.w.grad)
         if self.need_dx:
             H, W, Cin = self.in_shape

@@ -87,7 +87,9 @@ def same_pads(size: int, k: int, s: int, d: int = 1):
 
 
 # ----------------------------------------------------------------- tile selection
-_CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128)}
+# cfg -> block tile; 0-3 register-staged main loop, 4-7 LDS-DMA ring (same tiles)
+_CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
+               4: (128, 128), 5: (128, 64), 6: (64, 64), 7: (64, 128)}
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64)}
 N_CU = 256
 _tuned: dict = {}
@@ -102,7 +104,7 @@ def wgrad_key(Nout: int, K: int, M: int):
 
 
 def fwd_candidates(N: int):
-    return [0, 3, 1, 2] if N > 64 else [1, 2]
+    return [0, 3, 1, 2, 4, 7, 5, 6] if N > 64 else [1, 2, 5, 6]
 
 
 def wgrad_candidates(Nout: int, K: int, M: int):
@@ -125,7 +127,7 @@ def conv_cfg(M: int, N: int, K: int) -> int:
     key = fwd_key(M, N, K)
     if key in _tuned:
         return _tuned[key]
-    cands = fwd_candidates(N)
+    cands = [c for c in fwd_candidates(N) if c < 4]
     for c in cands:
         bm, bn = _CONV_TILES[c]
         if math.ceil(M / bm) * math.ceil(N / bn) >= 2 * N_CU:
@@ -161,8 +163,8 @@ def set_tuned(table: dict) -> None:
 
 
 # ---------------------------------------------------------------- conv forward
-def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None):
-    """out[N,P,Q,cout] = conv(x, W) (+bias). GPU: fp32 acc, bf16 (or fp32) out + BN stat slab."""
+def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None, relu=False):
+    """out[N,P,Q,cout] = conv(x, W) (+bias) [ReLU]. GPU: fp32 acc, bf16 (or fp32) out + BN stat slab."""
     N, H, W, _ = x.shape
     P, Q = spec.out_hw(H, W)
     if x.is_cuda:
@@ -172,7 +174,7 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
         out_f32 = out.dtype == torch.float32
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
                 spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1, 0,
-                1 if out_f32 else 0]
+                1 if out_f32 else 0, 1 if relu else 0]
         _ext.ops().conv_igemm(x, wpack, out, None, bias, stats, geom, cfg)
         return out
     xt = x.permute(0, 3, 1, 2)
@@ -180,8 +182,18 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
         xt = F.pad(xt, (spec.pl, spec.pr, spec.pt, spec.pb))
     wt = w_master.permute(0, 3, 1, 2).to(x.dtype)
     y = F.conv2d(xt, wt, bias=None if bias is None else bias.to(x.dtype), stride=(spec.sh, spec.sw), dilation=(spec.dh, spec.dw))
+    if relu:
+        y = torch.relu(y)
     out.copy_(y.permute(0, 2, 3, 1))
     return out
+
+
+def relu_backward(dy, y, dz):
+    if dy.is_cuda:
+        _ext.ops().relu_bwd(dy, y, dz)
+        return dz
+    dz.copy_(dy * (y > 0).to(dy.dtype))
+    return dz
 
 
 def conv_stats_slab(x_shape, spec: ConvSpec, device, cfg=None):

@@ -7,6 +7,7 @@
 // and enqueues on the current HIP stream.
 #include <torch/library.h>
 #include <ATen/core/Tensor.h>
+#include <ATen/ops/empty.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/util/Exception.h>
 
@@ -46,7 +47,7 @@ void check_align16(const void* p, const char* name) {
 void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                 const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
                 at::IntArrayRef g, int64_t cfg) {
-  TORCH_CHECK(g.size() == 28, "hcb.conv_igemm: geom must have 28 entries");
+  TORCH_CHECK(g.size() == 28 || g.size() == 29, "hcb.conv_igemm: geom must have 28 (+relu) entries");
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_cuda(y, "y");
@@ -58,6 +59,7 @@ void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::op
   p.Nout = g[17]; p.K = g[18]; p.Kpad = g[19]; p.ldy = g[20];
   p.remap = g[21]; p.OH = g[22]; p.OW = g[23]; p.osh = g[24]; p.osw = g[25];
   p.beta = g[26]; p.out_f32 = g[27];
+  p.relu = g.size() > 28 ? (int)g[28] : 0;
   p.M = p.N * p.P * p.Q;
   TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0 && p.ldx >= p.C, "hcb.conv_igemm: C, ldx must be multiples of 8");
   TORCH_CHECK(p.Kpad % 64 == 0 && p.Kpad >= p.K && p.K == p.R * p.S * p.C,
@@ -181,8 +183,12 @@ void bn_finalize(const Tensor& slab, int64_t T, int64_t C, double count, double 
     rmp = rm->data_ptr<float>();
     rvp = rv->data_ptr<float>();
   }
-  hcb::launch_bn_finalize(slab.data_ptr<float>(), (int)T, (int)C, count, (float)eps, (float)momentum,
-                          mean.data_ptr<float>(), invstd.data_ptr<float>(), rmp, rvp, cur_stream());
+  TORCH_CHECK(C <= 64 * 64, "hcb.bn_finalize: C too large");
+  Tensor part = at::empty({(int64_t)hcb::bn_finalize_splits((int)T) * 2 * C},
+                          at::TensorOptions().dtype(at::kDouble).device(slab.device()));
+  hcb::launch_bn_finalize_split(slab.data_ptr<float>(), (int)T, (int)C, part.data_ptr<double>(), 1, count,
+                                (float)eps, (float)momentum, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                rmp, rvp, nullptr, nullptr, cur_stream());
 }
 
 void bn_apply(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, const c10::optional<Tensor>& res,
@@ -239,8 +245,12 @@ void bn_bwd_finalize(const Tensor& slab, int64_t T, int64_t C, const Tensor& dga
   check_f32(slab, "slab");
   check_f32(dgamma, "dgamma");
   check_f32(dbeta, "dbeta");
-  hcb::launch_bn_bwd_finalize(slab.data_ptr<float>(), (int)T, (int)C, dgamma.data_ptr<float>(),
-                              dbeta.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(C <= 64 * 64 && slab.numel() >= T * 2 * C, "hcb.bn_bwd_finalize: sizes");
+  Tensor part = at::empty({(int64_t)hcb::bn_finalize_splits((int)T) * 2 * C},
+                          at::TensorOptions().dtype(at::kDouble).device(slab.device()));
+  hcb::launch_bn_finalize_split(slab.data_ptr<float>(), (int)T, (int)C, part.data_ptr<double>(), 0, 0.0, 0.f,
+                                0.f, nullptr, nullptr, nullptr, nullptr, dgamma.data_ptr<float>(),
+                                dbeta.data_ptr<float>(), cur_stream());
 }
 
 void bn_bwd_apply(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
@@ -383,6 +393,15 @@ void add_bf16(const Tensor& a, const Tensor& b, const Tensor& y) {
   hcb::launch_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream());
 }
 
+void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
+  check_bf16(dy, "dy");
+  check_bf16(y, "y");
+  check_bf16(dz, "dz");
+  TORCH_CHECK(dy.numel() == y.numel() && dy.numel() == dz.numel() && dy.numel() % 8 == 0, "hcb.relu_bwd: sizes");
+  TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dz.is_contiguous(), "hcb.relu_bwd: contiguous");
+  hcb::launch_relu_bwd(dy.data_ptr(), y.data_ptr(), dz.data_ptr(), dy.numel(), cur_stream());
+}
+
 void scale_f32(const Tensor& x, double s) {
   check_f32(x, "x");
   TORCH_CHECK(x.is_contiguous(), "hcb.scale_f32: contiguous");
@@ -450,6 +469,7 @@ TORCH_LIBRARY(hcb, m) {
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()");
   m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");
+  m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
   m.def("synth_images(Tensor(a!) out, int C, int Cpad, float mean, float std, int seed) -> ()");
   m.def("synth_labels(Tensor(a!) out, int ncls, int seed) -> ()");
@@ -477,6 +497,7 @@ TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("cast_f32_bf16", cast_f32_bf16);
   m.impl("add_bf16", add_bf16);
   m.impl("scale_f32", scale_f32);
+  m.impl("relu_bwd", relu_bwd);
   m.impl("l2norm_sq", l2norm_sq);
   m.impl("synth_images", synth_images);
   m.impl("synth_labels", synth_labels);

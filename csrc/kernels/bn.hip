@@ -279,6 +279,112 @@ static int bn_grid(int M, int C) {
 
 int bn_num_partials(int M, int C) { return bn_grid(M, C); }
 
+// ---------------------------------------------------------------------------------------
+// One-launch two-level finalize. Grid (C/64 channel groups) x (S row splits): each block
+// reduces T/S slab rows for 64 channels (fp64) into part[S][2][C]; the LAST block of a
+// channel group (agent-scope release -> ticket atomic -> acquire, the placement-independent
+// hand-off of the CDNA guide, Guideline 16) sums the S partials and writes the outputs, then
+// re-arms its counter. Counters start zeroed at module load and are left zeroed by every
+// launch, so graph replays need no memset.
+__device__ unsigned g_fin_counters[64];
+
+template <bool FWD>
+__global__ __launch_bounds__(512) void bn_finalize_split_kernel(
+    const float* __restrict__ slab, int T, int C, int rows_per, double* part, double count, float eps,
+    float momentum, float* mean, float* invstd, float* run_mean, float* run_var, float* dgamma,
+    float* dbeta) {
+  __shared__ double lds[2 * FIN_WAVES * 64];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int S = gridDim.y;
+  const int t0 = blockIdx.y * rows_per;
+  const int t1 = min(T, t0 + rows_per);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int t = t0 + wid; t < t1; t += FIN_WAVES) {
+      a += (double)slab[(size_t)t * 2 * C + c];
+      b += (double)slab[(size_t)t * 2 * C + C + c];
+    }
+  }
+  lds[wid * 64 + lane] = a;
+  lds[FIN_WAVES * 64 + wid * 64 + lane] = b;
+  __syncthreads();
+  if (wid == 0 && c < C) {
+    a = 0.0;
+    b = 0.0;
+#pragma unroll
+    for (int w = 0; w < FIN_WAVES; ++w) {
+      a += lds[w * 64 + lane];
+      b += lds[FIN_WAVES * 64 + w * 64 + lane];
+    }
+    part[(size_t)blockIdx.y * 2 * C + c] = a;
+    part[(size_t)blockIdx.y * 2 * C + C + c] = b;
+  }
+  // publish: every storing wave drains, barrier, one release + ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned tk = __hip_atomic_fetch_add(&g_fin_counters[blockIdx.x], 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    last = (tk == (unsigned)(S - 1));
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  if (c < C) {
+    a = 0.0;
+    b = 0.0;
+    for (int s = 0; s < S; ++s) {
+      a += part[(size_t)s * 2 * C + c];
+      b += part[(size_t)s * 2 * C + C + c];
+    }
+    if constexpr (FWD) {
+      double mu = a / count;
+      double var = b / count - mu * mu;
+      if (var < 0.0) var = 0.0;
+      mean[c] = (float)mu;
+      invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+      if (run_mean != nullptr) {
+        double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+        run_mean[c] = (float)(momentum * run_mean[c] + (1.0 - momentum) * mu);
+        run_var[c] = (float)(momentum * run_var[c] + (1.0 - momentum) * unbiased);
+      }
+    } else {
+      dbeta[c] = (float)a;
+      dgamma[c] = (float)b;
+    }
+  }
+  if (lane == 0) __hip_atomic_store(&g_fin_counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int bn_finalize_splits(int T) {
+  int s = (T + 63) / 64;
+  return s < 1 ? 1 : (s > 32 ? 32 : s);
+}
+
+void launch_bn_finalize_split(const float* slab, int T, int C, double* part, int fwd, double count, float eps,
+                              float momentum, float* mean, float* invstd, float* run_mean, float* run_var,
+                              float* dgamma, float* dbeta, hipStream_t st) {
+  int S = bn_finalize_splits(T);
+  int rows_per = (T + S - 1) / S;
+  S = (T + rows_per - 1) / rows_per;
+  dim3 grid((C + 63) / 64, S);
+  if (fwd)
+    hipLaunchKernelGGL(bn_finalize_split_kernel<true>, grid, dim3(64 * FIN_WAVES), 0, st, slab, T, C, rows_per,
+                       part, count, eps, momentum, mean, invstd, run_mean, run_var, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL(bn_finalize_split_kernel<false>, grid, dim3(64 * FIN_WAVES), 0, st, slab, T, C, rows_per,
+                       part, 0.0, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr, dgamma, dbeta);
+}
+
 void launch_bn_stats(const void* x, int M, int C, int ldx, float* slab, int T, hipStream_t st) {
   int rows = 256 / (C / 8);
   size_t lds = (size_t)2 * rows * C * 4;

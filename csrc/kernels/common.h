@@ -55,6 +55,14 @@ __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t o
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
+// LDS-DMA: 16 bytes per lane from the buffer straight into LDS at (wave-uniform) lds + lane*16.
+// Kept in a __device__ helper so the host compilation pass never sees the LDS address-space
+// cast (a kernel template body containing it loses its host launch stub).
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (HCB_LDS void*)lds, 16, off, 0, 0, 0);
+}
+__device__ __forceinline__ int wave_id_uniform() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

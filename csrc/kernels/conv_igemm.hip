@@ -14,23 +14,111 @@
 // Design (MI355X-first, not a translation):
 //   * 256 threads = 4 waves of 64, wave tile TMxTN built from 16x16x32 bf16 MFMAs
 //     (fp32 accumulate), block tile BM x BN x BK=64.
-//   * im2col is never materialised: each thread gathers 16-byte channel vectors of
-//     the input with raw buffer loads; halo / padding / tail rows use an out-of-range
-//     offset, which the buffer unit turns into zeros (no branches around loads).
-//   * register-staged double-buffered LDS (issue the next tile's global loads before
-//     the MFMAs, write them to the other LDS buffer after), one barrier per k-step.
-//   * LDS rows are 128 B (BK=64 bf16); 16-byte chunks are XOR-swizzled with
-//     (row>>1)&7 so the ds_read_b128 fragment reads are bank-conflict free.
-//   * XCD-aware block remap so neighbouring tiles (sharing the im2col panel) sit on
-//     one XCD's L2.
-//   * epilogue staged through LDS as fp32: fully coalesced 16-byte bf16 stores,
-//     optional beta-accumulate, bias, fp32 output and fused per-channel BatchNorm
-//     statistics (sum / sum of squares per M-tile, reduced later in fp64).
+//   * im2col is never materialised: each lane gathers 16-byte channel vectors of the input
+//     with raw buffer loads; halo / padding / tail rows use an out-of-range offset, which
+//     the buffer unit turns into zeros (no branches around loads).
+//   * two main loops, picked per layer by the autotuner:
+//       - "reg":  register-staged double-buffered LDS, one barrier per k-step;
+//       - "glds": LDS-DMA (buffer_load ... lds) straight into an NST-deep ring of LDS
+//         stages, counted s_waitcnt vmcnt + raw s_barrier so NST-2 stages stay in flight
+//         across barriers (the latency lever at ~1-2 workgroups per CU). The LDS image is
+//         lane-linear; the XOR swizzle is applied to the per-lane SOURCE chunk and to the
+//         fragment reads (same involution), per the gfx950 glds rules.
+//   * LDS rows are 128 B (BK=64 bf16); 16-byte chunks are XOR-swizzled with (row>>1)&7 so
+//     the ds_read_b128 fragment reads are bank-conflict free.
+//   * XCD-aware block remap so neighbouring tiles (sharing the im2col panel) sit on one
+//     XCD's L2.
+//   * epilogue (igemm_epilogue.h): fused per-channel BatchNorm statistics from the
+//     accumulators, LDS-staged fully coalesced 16-byte stores, beta-accumulate, bias,
+//     fp32 output, strided-output remap.
 #include "common.h"
+#include "igemm_epilogue.h"
 #include "kernels.h"
 
 namespace hcb {
 
+// ---- per-thread implicit-im2col address generation, shared by both main loops
+template <int AV, bool CBIG, bool LHSDIL>
+struct ALoader {
+  int pix[AV], h0[AV], w0[AV];
+
+  __device__ __forceinline__ void init(const ConvParams& p, int m0, int tid) {
+    const int PQ = p.P * p.Q;
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      int m = m0 + (tid >> 3) + 32 * v;
+      if (m < p.M) {
+        int n = m / PQ, r = m - n * PQ;
+        int pp = r / p.Q, qq = r - pp * p.Q;
+        pix[v] = n * p.H * p.W;
+        h0[v] = pp * p.stride_h - p.pad_h;
+        w0[v] = qq * p.stride_w - p.pad_w;
+      } else {
+        pix[v] = -1;
+        h0[v] = 0;
+        w0[v] = 0;
+      }
+    }
+  }
+  // byte offset of the 16-byte vector (row v, k-chunk `chunk`) of k-step kt
+  __device__ __forceinline__ void offsets(const ConvParams& p, int kt, int chunk, uint32_t (&off)[AV]) const {
+    const int k0 = kt * 64;
+    int tap, c;
+    if constexpr (CBIG) {
+      tap = k0 / p.C;
+      c = k0 - tap * p.C + chunk * 8;
+    } else {
+      int k = k0 + chunk * 8;
+      tap = k / p.C;
+      c = k - tap * p.C;
+    }
+    const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+    const bool tap_ok = tap < p.R * p.S;
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      int h = h0[v] + r * p.dil_h;
+      int w = w0[v] + s * p.dil_w;
+      bool ok = tap_ok && pix[v] >= 0 && h >= 0 && w >= 0;
+      if constexpr (LHSDIL) {
+        ok = ok && (h % p.idil_h == 0) && (w % p.idil_w == 0);
+        h /= p.idil_h;
+        w /= p.idil_w;
+      }
+      ok = ok && h < p.H && w < p.W;
+      off[v] = ok ? (uint32_t)((pix[v] + h * p.W + w) * p.ldx + c) * 2u : HCB_OOB;
+    }
+  }
+};
+
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb, f32x4 (&acc)[TM / 16][TN / 16],
+                                               int wm, int wn, int lane) {
+  constexpr int MI = TM / 16, NI = TN / 16;
+  const int frow = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    bf16x8 af[MI], bfr[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      int row = wm * TM + i * 16 + frow;
+      int ch = ks * 4 + fq;
+      af[i] = __builtin_bit_cast(bf16x8, Ab[row * 8 + (ch ^ ((row >> 1) & 7))]);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      int row = wn * TN + j * 16 + frow;
+      int ch = ks * 4 + fq;
+      bfr[j] = __builtin_bit_cast(bf16x8, Bb[row * 8 + (ch ^ ((row >> 1) & 7))]);
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// ============================================================== register-staged main loop
 template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
@@ -51,25 +139,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
-
-  // ---- per-thread A row decode (fixed for the whole K loop)
-  int a_pix[AV], a_h0[AV], a_w0[AV];
-  const int PQ = p.P * p.Q;
-#pragma unroll
-  for (int v = 0; v < AV; ++v) {
-    int m = m0 + (tid >> 3) + 32 * v;
-    if (m < p.M) {
-      int n = m / PQ, r = m - n * PQ;
-      int pp = r / p.Q, qq = r - pp * p.Q;
-      a_pix[v] = n * p.H * p.W;
-      a_h0[v] = pp * p.stride_h - p.pad_h;
-      a_w0[v] = qq * p.stride_w - p.pad_w;
-    } else {
-      a_pix[v] = -1;
-      a_h0[v] = 0;
-      a_w0[v] = 0;
-    }
-  }
+  ALoader<AV, CBIG, LHSDIL> al;
+  al.init(p, m0, tid);
   uint32_t b_off[BV];
 #pragma unroll
   for (int v = 0; v < BV; ++v) {
@@ -84,39 +155,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int RS = p.R * p.S;
   auto gload = [&](int kt) {
-    const int k0 = kt * BK;
-    int tap, c;
-    if constexpr (CBIG) {
-      tap = k0 / p.C;
-      c = k0 - tap * p.C + chunk * 8;
-    } else {
-      int k = k0 + chunk * 8;
-      tap = k / p.C;
-      c = k - tap * p.C;
-    }
-    const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
-    const bool tap_ok = tap < RS;
+    uint32_t off[AV];
+    al.offsets(p, kt, chunk, off);
 #pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      int h = a_h0[v] + r * p.dil_h;
-      int w = a_w0[v] + s * p.dil_w;
-      bool ok = tap_ok && a_pix[v] >= 0 && h >= 0 && w >= 0;
-      if constexpr (LHSDIL) {
-        ok = ok && (h % p.idil_h == 0) && (w % p.idil_w == 0);
-        h /= p.idil_h;
-        w /= p.idil_w;
-      }
-      ok = ok && h < p.H && w < p.W;
-      uint32_t off = ok ? (uint32_t)((a_pix[v] + h * p.W + w) * p.ldx + c) * 2u : HCB_OOB;
-      ra[v] = buf_load16(xr, off);
-    }
+    for (int v = 0; v < AV; ++v) ra[v] = buf_load16(xr, off[v]);
 #pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      uint32_t off = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)k0 * 2u;
-      rb[v] = buf_load16(wr, off);
-    }
+    for (int v = 0; v < BV; ++v)
+      rb[v] = buf_load16(wr, b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
   };
   auto lstore = [&](int buf) {
 #pragma unroll
@@ -135,162 +181,117 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   gload(0);
   lstore(0);
   __syncthreads();
-  const int frow = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const u32x4* Ab = As + cur * BM * 8;
-    const u32x4* Bb = Bs + cur * BN * 8;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[MI], bfr[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        int row = wm * TM + i * 16 + frow;
-        int ch = ks * 4 + fq;
-        u32x4 t = Ab[row * 8 + (ch ^ ((row >> 1) & 7))];
-        af[i] = __builtin_bit_cast(bf16x8, t);
-      }
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        int row = wn * TN + j * 16 + frow;
-        int ch = ks * 4 + fq;
-        u32x4 t = Bb[row * 8 + (ch ^ ((row >> 1) & 7))];
-        bfr[j] = __builtin_bit_cast(bf16x8, t);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+    mfma_tile_step<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
+  igemm_epilogue<WM, WN, TM, TN>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
+}
 
-  // ---- epilogue: accumulators -> LDS (fp32, padded rows) -> coalesced stores
-  constexpr int LDC = BN + 4;
-  float* Cs = reinterpret_cast<float*>(smem);
-  float* red = Cs + BM * LDC;  // [WM][2][BN] per-wave column partial sums
-  if (p.stats != nullptr) {
-    // per-column partial BN statistics straight from the accumulators (rows beyond M are
-    // exact zeros): sum the wave's 4 row-quads in registers, then across the 4 lane groups
-    // that share a column with two xor-shuffles.
+// ============================================================== LDS-DMA multi-stage main loop
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL>
+__global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
+  constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int AV = BM / 32, BV = BN / 32;
+  constexpr int LOADS = AV + BV;  // LDS-DMA instructions per thread per stage
+  constexpr int STAGE = (BM + BN) * 128;
+  static_assert(WM * WN == 4 && NST >= 2 && NST <= 4, "config");
+  static_assert(LOADS * (NST - 2) <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = wave_id_uniform();
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_n = (p.Nout + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  // lane-linear LDS image: lane -> (row = (tid>>3)+32v, position tid&7); the lane fetches the
+  // GLOBAL chunk that the swizzled read expects at that position (involution).
+  const int chunk = (tid & 7) ^ ((tid >> 4) & 7);
+
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
+  ALoader<AV, CBIG, LHSDIL> al;
+  al.init(p, m0, tid);
+  uint32_t b_off[BV];
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[i][j][e];
-          s1 += v;
-          s2 += v * v;
-        }
-      s1 += __shfl_xor(s1, 16, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (fq == 0) {
-        red[(wm * 2) * BN + wn * TN + j * 16 + frow] = s1;
-        red[(wm * 2 + 1) * BN + wn * TN + j * 16 + frow] = s2;
-      }
-    }
+  for (int v = 0; v < BV; ++v) {
+    int j = n0 + (tid >> 3) + 32 * v;
+    b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
   }
+  f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int row = wm * TM + i * 16 + fq * 4 + e;
-        int col = wn * TN + j * 16 + frow;
-        Cs[row * LDC + col] = acc[i][j][e];
-      }
-  __syncthreads();
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (p.stats != nullptr) {
-    for (int col = tid; col < BN; col += 256) {
-      float s1 = 0.f, s2 = 0.f;
+  auto issue = [&](int stage, int kt) {
+    uint32_t off[AV];
+    al.offsets(p, kt, chunk, off);
+    char* sbase = smem + stage * STAGE;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        s1 += red[(w * 2) * BN + col];
-        s2 += red[(w * 2 + 1) * BN + col];
-      }
-      int gc = n0 + col;
-      if (gc < p.Nout) {
-        p.stats[(size_t)tm * 2 * p.Nout + gc] = s1;
-        p.stats[(size_t)tm * 2 * p.Nout + p.Nout + gc] = s2;
-      }
-    }
-  }
+    for (int v = 0; v < AV; ++v) glds16(xr, sbase + (wid * 8 + 32 * v) * 128, off[v]);
+#pragma unroll
+    for (int v = 0; v < BV; ++v)
+      glds16(wr, sbase + BM * 128 + (wid * 8 + 32 * v) * 128,
+             b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
+  };
 
-  constexpr int SEGS = BN / 8;
-  for (int sidx = tid; sidx < BM * SEGS; sidx += 256) {
-    int row = sidx / SEGS, cs = sidx - row * SEGS;
-    int m = m0 + row;
-    int col = n0 + cs * 8;
-    if (m >= p.M || col >= p.Nout) continue;
-    size_t orow = (size_t)m;
-    if (p.remap) {
-      int n = m / PQ, r = m - n * PQ;
-      int pp = r / p.Q, qq = r - pp * p.Q;
-      orow = ((size_t)n * p.OH + (size_t)pp * p.osh) * p.OW + (size_t)qq * p.osw;
-    }
-    float v[8];
-    const f32x4* src = reinterpret_cast<const f32x4*>(Cs + row * LDC + cs * 8);
-    f32x4 v0 = src[0], v1 = src[1];
+  const int nk = p.Kpad / BK;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = v0[e];
-      v[4 + e] = v1[e];
-    }
-    if (p.bias != nullptr) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += (col + e < p.Nout) ? p.bias[col + e] : 0.f;
-    }
-    if (p.out_f32) {
-      float* yo = reinterpret_cast<float*>(p.y) + orow * p.ldy + col;
-      if (p.beta) {
-        const float* yi = reinterpret_cast<const float*>(p.yres) + orow * p.ldy + col;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += yi[e];
-      }
-      reinterpret_cast<f32x4*>(yo)[0] = f32x4{v[0], v[1], v[2], v[3]};
-      reinterpret_cast<f32x4*>(yo)[1] = f32x4{v[4], v[5], v[6], v[7]};
-    } else {
-      uint16_t* yo = reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col;
-      if (p.beta) {
-        const uint16_t* yi = reinterpret_cast<const uint16_t*>(p.yres) + orow * p.ldy + col;
-        float o[8];
-        unpack8(*reinterpret_cast<const u32x4*>(yi), o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += o[e];
-      }
-      *reinterpret_cast<u32x4*>(yo) = pack8(v);
-    }
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed for this thread once at most min(NST-2, nk-1-kt) later stages
+    // are still outstanding; the barrier then publishes every thread's DMA.
+    const int ahead = min(NST - 2, nk - 1 - kt);
+    if (ahead >= 2)
+      wait_vmcnt<2 * LOADS>();
+    else if (ahead == 1)
+      wait_vmcnt<LOADS>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, kt + NST - 1);
+    const char* sb = smem + (kt % NST) * STAGE;
+    mfma_tile_step<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + BM * 128),
+                                   acc, wm, wn, lane);
   }
+  __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
+  igemm_epilogue<WM, WN, TM, TN>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
 }
 
+// ============================================================== launch
 template <int WM, int WN, int TM, int TN>
-static void launch_cfg(const ConvParams& p, hipStream_t st) {
+static void launch_reg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
   size_t lds_main = (size_t)2 * (BM + BN) * 8 * 16;
-  size_t lds_epi = (size_t)BM * (BN + 4) * 4 + (size_t)WM * 2 * BN * 4;
+  size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
     (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, true, false>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, true, true>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, false, false>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, false, true>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
   if (cbig && !lhs)
@@ -303,32 +304,60 @@ static void launch_cfg(const ConvParams& p, hipStream_t st) {
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true>), dim3(tiles), dim3(256), lds, st, p);
 }
 
-int conv_tile_m(int cfg) {
-  switch (cfg) {
-    case 0: return 128;
-    case 1: return 128;
-    case 2: return 64;
-    case 3: return 64;
-    default: return 128;
+template <int WM, int WN, int TM, int TN, int NST>
+static void launch_glds(const ConvParams& p, hipStream_t st) {
+  constexpr int BM = WM * TM, BN = WN * TN;
+  int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
+  size_t lds_main = (size_t)NST * (BM + BN) * 128;
+  size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
+  size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+  bool cbig = (p.C % 64) == 0;
+  bool lhs = p.idil_h > 1 || p.idil_w > 1;
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
   }
+  if (cbig && !lhs)
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false>), dim3(tiles), dim3(256), lds, st, p);
+  else if (cbig && lhs)
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true>), dim3(tiles), dim3(256), lds, st, p);
+  else if (!cbig && !lhs)
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false>), dim3(tiles), dim3(256), lds, st,
+                       p);
+  else
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true>), dim3(tiles), dim3(256), lds, st, p);
+}
+
+// cfg: 0..3 register-staged {128x128, 128x64, 64x64, 64x128}; 4..7 the same tiles on the
+// LDS-DMA ring (NST 3, 3, 4, 3)
+int conv_tile_m(int cfg) {
+  static const int t[8] = {128, 128, 64, 64, 128, 128, 64, 64};
+  return (cfg >= 0 && cfg < 8) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
-  switch (cfg) {
-    case 0: return 128;
-    case 1: return 64;
-    case 2: return 64;
-    case 3: return 128;
-    default: return 128;
-  }
+  static const int t[8] = {128, 64, 64, 128, 128, 64, 64, 128};
+  return (cfg >= 0 && cfg < 8) ? t[cfg] : 128;
 }
 
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
   switch (cfg) {
-    case 0: launch_cfg<2, 2, 64, 64>(p, st); break;   // 128 x 128
-    case 1: launch_cfg<4, 1, 32, 64>(p, st); break;   // 128 x 64
-    case 2: launch_cfg<2, 2, 32, 32>(p, st); break;   // 64 x 64
-    case 3: launch_cfg<1, 4, 64, 32>(p, st); break;   // 64 x 128
-    default: launch_cfg<2, 2, 64, 64>(p, st); break;
+    case 0: launch_reg<2, 2, 64, 64>(p, st); break;    // 128 x 128
+    case 1: launch_reg<4, 1, 32, 64>(p, st); break;    // 128 x 64
+    case 2: launch_reg<2, 2, 32, 32>(p, st); break;    // 64 x 64
+    case 3: launch_reg<1, 4, 64, 32>(p, st); break;    // 64 x 128
+    case 4: launch_glds<2, 2, 64, 64, 3>(p, st); break;
+    case 5: launch_glds<4, 1, 32, 64, 3>(p, st); break;
+    case 6: launch_glds<2, 2, 32, 32, 4>(p, st); break;
+    case 7: launch_glds<1, 4, 64, 32, 3>(p, st); break;
+    default: launch_reg<2, 2, 64, 64>(p, st); break;
   }
 }
 

@@ -45,6 +45,7 @@ struct ConvParams {
   int M;
   int remap, OH, OW, osh, osw;
   int beta, out_f32;
+  int relu;  // fused ReLU in the epilogue (affine layers without BN)
   uint32_t x_bytes, w_bytes;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
@@ -80,6 +81,11 @@ void launch_bn_apply(const void* x, int ldx, void* y, int ldy, const void* res, 
                      int C, const float* mean, const float* invstd, const float* gamma,
                      const float* beta, int relu, hipStream_t st);
 int bn_num_partials(int M, int C);
+// one-launch finalize (split rows + last-block combine); part: fp64 scratch [32][2][C]
+int bn_finalize_splits(int T);
+void launch_bn_finalize_split(const float* slab, int T, int C, double* part, int fwd, double count, float eps,
+                              float momentum, float* mean, float* invstd, float* run_mean, float* run_var,
+                              float* dgamma, float* dbeta, hipStream_t st);
 // backward reduce: g = dy*mask (relu: 0 none, 1 mask y>0, 2 mask recomputed from x);
 // per-block partial sums of g and g*xhat -> slab; optionally writes g to gout
 void launch_bn_bwd_reduce2(const void* dy, int lddy, const void* y, int ldyv, const void* x,
@@ -128,6 +134,7 @@ void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st
 void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 void launch_add_bf16(const void* a, const void* b, void* y, int64_t n, hipStream_t st);
 void launch_scale_f32(float* x, int64_t n, float s, hipStream_t st);
+void launch_relu_bwd(const void* dy, const void* y, void* dz, int64_t n, hipStream_t st);
 void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st);
 
 // ---------------------------------------------------------------- data

@@ -185,6 +185,19 @@ __global__ void add_bf16_kernel(const uint16_t* a, const uint16_t* b, uint16_t* 
     reinterpret_cast<u32x4*>(y)[i] = pack8(fa);
   }
 }
+// dz = dy * (y > 0), bf16, 8 elements per thread
+__global__ void relu_bwd_kernel(const uint16_t* dy, const uint16_t* y, uint16_t* dz, int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float d[8], v[8];
+    unpack8(reinterpret_cast<const u32x4*>(dy)[i], d);
+    unpack8(reinterpret_cast<const u32x4*>(y)[i], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = v[e] > 0.f ? d[e] : 0.f;
+    reinterpret_cast<u32x4*>(dz)[i] = pack8(d);
+  }
+}
+
 __global__ void scale_f32_kernel(float* x, int64_t n, float s) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -292,6 +305,10 @@ void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st
 void launch_add_bf16(const void* a, const void* b, void* y, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(add_bf16_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)a,
                      (const uint16_t*)b, (uint16_t*)y, n / 8);
+}
+void launch_relu_bwd(const void* dy, const void* y, void* dz, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)dy,
+                     (const uint16_t*)y, (uint16_t*)dz, n / 8);
 }
 void launch_scale_f32(float* x, int64_t n, float s, hipStream_t st) {
   hipLaunchKernelGGL(scale_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, s);

@@ -55,3 +55,42 @@ def reference_grads(model, images, labels, ref_fn):
     loss = F.cross_entropy(logits, labels)
     loss.backward()
     return loss.detach(), {k: v.grad for k, v in params.items()}, logits.detach()
+
+
+def _gamma(layer, params):
+    name = getattr(layer.gamma, "name", None)
+    return params[name] if name in params else layer.gamma.data.to(next(iter(params.values())).dtype)
+
+
+def convbn_ref2(layer, x, params, residual=None):
+    """convbn_ref that also handles BN(scale=False) layers (fixed gamma)."""
+    z = conv_ref(layer, x, params)
+    z = F.batch_norm(z, None, None, _gamma(layer, params), params[layer.beta.name], training=True, eps=layer.eps)
+    if residual is not None:
+        z = z + residual
+    if layer.relu:
+        z = torch.relu(z)
+    return z
+
+
+def _layer_ref(layer, x, params):
+    from azure_hc_intel_tf_amd.nn.layers import ConvBN
+
+    if isinstance(layer, ConvBN):
+        return convbn_ref2(layer, x, params)
+    return pool_ref(layer, x)
+
+
+def inception_ref(model, images_nhwc, params):
+    x = images_nhwc.permute(0, 3, 1, 2)
+    for l in model.stem:
+        x = _layer_ref(l, x, params)
+    for m in model.modules:
+        outs = {}
+        for n in m.nodes:
+            inp = x if n.src is None else outs[id(n.src)]
+            outs[id(n)] = _layer_ref(n.layer, inp, params)
+        x = torch.cat([outs[id(t)] for t in m.terminals], dim=1)
+    feat = x.mean(dim=(2, 3))
+    w = params[model.fc.w.name].view(model.fc.ncls, -1)
+    return feat @ w.t() + params[model.fc.b.name]

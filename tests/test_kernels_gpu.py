@@ -76,7 +76,32 @@ def test_conv_fwd_and_stats(case):
     assert rel_err(s1, ref.reshape(-1, cout).sum(0)) < 2e-2
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("case", CONV_CASES[:-1], ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}{c[3]}s{c[4]}")
+def test_conv_lds_dma_kernels_all_geometries(case):
+    """The LDS-DMA ring kernels (cfg 4-7) on every geometry, forward and data-gradient."""
+    cin, cout, kh, kw, s, pads, H = case
+    torch.manual_seed(12)
+    cpad = cin if cin % 8 == 0 else 8
+    spec, p, pk = make_conv(cin, cout, kh, kw, s, s, pads, cin_pad=cpad)
+    N = 2
+    P, Q = spec.out_hw(H, H)
+    x = bf(torch.randn(N, H, H, cpad, device=DEV))
+    ref = cpu_ref_conv(x, spec, bf(p.data))
+    dz = bf(torch.randn(N, P, Q, cout, device=DEV))
+    dref = torch.empty(N, H, H, cpad)
+    Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), dref, False)
+    for cfg in (4, 5, 6, 7):
+        y = torch.empty(N, P, Q, cout, dtype=torch.bfloat16, device=DEV)
+        slab = torch.empty(math.ceil(N * P * Q / Fn._CONV_TILES[cfg][0]) * 2 * cout, device=DEV)
+        Fn.conv_forward(x, spec, pk.pack, p.data, y, stats=slab, cfg=cfg)
+        assert rel_err(y, ref) < 1e-2, cfg
+        if cin % 8 == 0:
+            dx = torch.zeros(N, H, H, cpad, dtype=torch.bfloat16, device=DEV)
+            Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, False, cfg=cfg)
+            assert rel_err(dx, dref) < 1e-2, cfg
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_conv_fwd_all_tile_configs(cfg):
     torch.manual_seed(1)
     spec, p, pk = make_conv(128, 192, 3, 3, 1, 1, (1, 1, 1, 1))
