@@ -55,6 +55,9 @@ def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
     raise ValueError(mode)
 
 
+STAT_R = 8  # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
+
+
 class _FixedParam:
     """A non-trainable per-channel constant with a scratch gradient sink (BN scale=False)."""
 
@@ -115,6 +118,11 @@ class ConvBN(Layer):
             self.beta = ps.add(f"{name}/batchnorm/beta", (cout,), False, ParamStore.const(0.0))
             self.rmean = ps.add_buffer(f"{name}/batchnorm/moving_mean", (cout,), 0.0)
             self.rvar = ps.add_buffer(f"{name}/batchnorm/moving_variance", (cout,), 1.0)
+            # GPU: statistic accumulators (R replicas of [2][C]) and saved batch moments
+            self.acc_f = ps.add_stat(f"{name}/bn_acc_fwd", (STAT_R, 2, cout))
+            self.acc_b = ps.add_stat(f"{name}/bn_acc_bwd", (STAT_R, 2, cout))
+            self.sv_mean = ps.add_stat(f"{name}/bn_mean", (cout,))
+            self.sv_invstd = ps.add_stat(f"{name}/bn_invstd", (cout,))
         else:
             self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0))
         self._saved = None
@@ -130,15 +138,18 @@ class ConvBN(Layer):
         dev = x.device
         if self.bn:
             z = empty_act((N, P, Q, C), dev)
-            if x.is_cuda:
-                slab, T, cfg = Fn.conv_stats_slab(x.shape, self.spec, dev)
-                Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=slab, cfg=cfg)
-            else:
-                slab, T = None, 0
-                Fn.conv_forward(x, self.spec, None, self.w.data, z)
             y = out if out is not None else empty_act((N, P, Q, C), dev)
-            saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
-                                  self.decay, self.eps, y, self.relu, residual=residual, stats=slab, stats_T=T)
+            if x.is_cuda:
+                # conv epilogue accumulates the batch statistics; the apply kernel finalizes them
+                Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data,
+                                stats_R=STAT_R)
+                saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
+                                          self.decay, self.eps, y, self.relu, self.acc_f.data, STAT_R,
+                                          self.sv_mean.data, self.sv_invstd.data, residual=residual)
+            else:
+                Fn.conv_forward(x, self.spec, None, self.w.data, z)
+                saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
+                                      self.decay, self.eps, y, self.relu, residual=residual)
             self._saved = (x, z, y, saved, residual is not None)
             return y
         assert residual is None, "conv without BN: no residual input"
@@ -161,8 +172,12 @@ class ConvBN(Layer):
             if want_gres:
                 gres = empty_act((N, P, Q, C), dev)
             relu_mode = (1 if had_res else 2) if self.relu else 0
-            Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
-                           self.beta.grad, dz, gres)
+            if dy.is_cuda:
+                Fn.bn_backward_acc(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
+                                   self.beta.grad, dz, self.acc_b.data, STAT_R, gres)
+            else:
+                Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
+                               self.beta.grad, dz, gres)
         else:
             if self.relu:
                 dz = Fn.relu_backward(dy, y, empty_act((N, P, Q, C), dev))

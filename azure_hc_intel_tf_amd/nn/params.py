@@ -81,6 +81,7 @@ class ParamStore:
     def __init__(self, seed: int = 1234):
         self.params: List[ParamRef] = []
         self.buffers: List[BufferRef] = []
+        self.stats: List[BufferRef] = []
         self.packs: List[PackRef] = []
         self.gen = torch.Generator().manual_seed(seed)
         self.finalized = False
@@ -95,6 +96,13 @@ class ParamStore:
     def add_buffer(self, name, shape, fill: float) -> BufferRef:
         b = BufferRef(name, tuple(shape), fill)
         self.buffers.append(b)
+        return b
+
+    def add_stat(self, name, shape) -> BufferRef:
+        """Per-step scratch (BN statistic accumulators, saved mean/invstd): one flat fp32
+        buffer, zeroed once per step together with the gradients."""
+        b = BufferRef(name, tuple(shape), 0.0)
+        self.stats.append(b)
         return b
 
     def add_pack(self, p: ParamRef, Nout, R, S, C, Kpad, Kpad_t, want_tr=True) -> PackRef:
@@ -168,6 +176,13 @@ class ParamStore:
         self.buf = bcpu.to(device)
         for b in self.buffers:
             b.data = self.buf[b.offset:b.offset + b.numel].view(b.shape)
+        soff = 0
+        for b in self.stats:
+            b.offset = soff
+            soff += _align(b.numel)
+        self.statbuf = torch.zeros(max(soff, ALIGN), dtype=torch.float32, device=device)
+        for b in self.stats:
+            b.data = self.statbuf[b.offset:b.offset + b.numel].view(b.shape)
         # bf16 GEMM operands (GPU only)
         poff = 0
         rows = []
@@ -207,6 +222,9 @@ class ParamStore:
 
     def zero_grad(self):
         self.grad.zero_()
+
+    def zero_stats(self):
+        self.statbuf.zero_()
 
     def num_params(self) -> int:
         return sum(p.logical_numel for p in self.params)

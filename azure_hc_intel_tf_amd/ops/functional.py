@@ -163,8 +163,10 @@ def set_tuned(table: dict) -> None:
 
 
 # ---------------------------------------------------------------- conv forward
-def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None, relu=False):
-    """out[N,P,Q,cout] = conv(x, W) (+bias) [ReLU]. GPU: fp32 acc, bf16 (or fp32) out + BN stat slab."""
+def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None, relu=False,
+                 stats_R: int = 0):
+    """out[N,P,Q,cout] = conv(x, W) (+bias) [ReLU]. GPU: fp32 acc, bf16 (or fp32) out + fused BN
+    statistics: per-tile slab (stats_R=0) or fp32 atomics into stats_R replicas of [2][cout]."""
     N, H, W, _ = x.shape
     P, Q = spec.out_hw(H, W)
     if x.is_cuda:
@@ -174,7 +176,7 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
         out_f32 = out.dtype == torch.float32
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
                 spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1, 0,
-                1 if out_f32 else 0, 1 if relu else 0]
+                1 if out_f32 else 0, 1 if relu else 0, int(stats_R)]
         _ext.ops().conv_igemm(x, wpack, out, None, bias, stats, geom, cfg)
         return out
     xt = x.permute(0, 3, 1, 2)
@@ -312,6 +314,34 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
         y = torch.relu(y)
     out.copy_(y)
     return BNSaved(mean, invstd)
+
+
+def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out, relu: bool, acc, R: int,
+                   saved_mean, saved_invstd, residual=None):
+    """GPU BN forward whose batch statistics were accumulated by the producing conv's epilogue
+    into ``acc`` (R replicas of [2][C]); mean/invstd are derived inside the apply kernel (no
+    finalize launch) and written to saved_mean / saved_invstd for the backward."""
+    N, H, W, C = z.shape
+    M = N * H * W
+    _ext.ops().bn_apply_acc(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0, M, C,
+                            acc, R, eps, momentum, gamma, beta, 1 if relu else 0, saved_mean, saved_invstd,
+                            running_mean, running_var)
+    return BNSaved(saved_mean, saved_invstd)
+
+
+def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, acc, R: int,
+                    gres=None):
+    """GPU BN(+ReLU) backward with the dgamma/dbeta reduction accumulated in ``acc`` replicas
+    (zeroed per step) and consumed directly by the apply kernel."""
+    N, H, W, C = z.shape
+    M = N * H * W
+    hcb = _ext.ops()
+    ym = y if relu_mode == 1 else None
+    hcb.bn_bwd_reduce_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), M, C, saved.mean, saved.invstd,
+                          gamma, beta, relu_mode, acc, R, gres, ld(gres) if gres is not None else 0)
+    hcb.bn_bwd_apply_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), dz, ld(dz), M, C, saved.mean,
+                         saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode)
+    return dz
 
 
 def bn_backward(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, gres=None):

@@ -88,6 +88,7 @@ class Trainer:
         ps = self.ps
         if not self.forward_only:
             ps.zero_grad()
+        ps.zero_stats()
         ps.repack()
         logits = self.model.forward(images)
         Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B)

@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--no_tune", action="store_true", help="skip per-shape kernel autotuning")
     ap.add_argument("--compression", default=None, choices=[None, "fp16", "bf16"])
-    ap.add_argument("--engine", default="torch", choices=["native", "torch"])
+    ap.add_argument("--engine", default="native", choices=["native", "torch"])
     args = ap.parse_args()
 
     import torch
@@ -60,7 +60,25 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
         from azure_hc_intel_tf_amd.parallel import make_reducer
 
-        reducer = make_reducer(args.engine, compression=args.compression)
+        if args.engine == "native":
+            try:
+                reducer = make_reducer("native", compression=args.compression)
+                # self-test of the C++ RCCL engine against the known sum before trusting it
+                t = torch.full((4096,), float(rank + 1), device=dev)
+                reducer.comm.allreduce_(t)
+                torch.cuda.synchronize()
+                ok = torch.tensor([1 if torch.allclose(t, torch.full_like(t, world * (world + 1) / 2)) else 0],
+                                  device=dev)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok.item()) != 1:
+                    raise RuntimeError("self-test mismatch")
+            except Exception as e:  # pragma: no cover - exercised only on multi-GPU nodes
+                print(f"[bench] native RCCL engine unavailable ({e}); falling back to torch.distributed",
+                      file=sys.stderr)
+                args.engine = "torch"
+                reducer = make_reducer("torch", compression=args.compression)
+        else:
+            reducer = make_reducer("torch", compression=args.compression)
 
     model = create_model(args.model, device=dev)
     B = args.batch_size

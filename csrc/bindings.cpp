@@ -47,7 +47,7 @@ void check_align16(const void* p, const char* name) {
 void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                 const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
                 at::IntArrayRef g, int64_t cfg) {
-  TORCH_CHECK(g.size() == 28 || g.size() == 29, "hcb.conv_igemm: geom must have 28 (+relu) entries");
+  TORCH_CHECK(g.size() >= 28 && g.size() <= 30, "hcb.conv_igemm: geom must have 28 (+relu, +stats_R) entries");
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_cuda(y, "y");
@@ -60,6 +60,7 @@ void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::op
   p.remap = g[21]; p.OH = g[22]; p.OW = g[23]; p.osh = g[24]; p.osw = g[25];
   p.beta = g[26]; p.out_f32 = g[27];
   p.relu = g.size() > 28 ? (int)g[28] : 0;
+  p.stats_R = g.size() > 29 ? (int)g[29] : 0;
   p.M = p.N * p.P * p.Q;
   TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0 && p.ldx >= p.C, "hcb.conv_igemm: C, ldx must be multiples of 8");
   TORCH_CHECK(p.Kpad % 64 == 0 && p.Kpad >= p.K && p.K == p.R * p.S * p.C,
@@ -101,7 +102,8 @@ void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::op
   if (stats.has_value()) {
     check_f32(*stats, "stats");
     int tiles_m = (p.M + hcb::conv_tile_m(cfg) - 1) / hcb::conv_tile_m(cfg);
-    TORCH_CHECK(stats->numel() >= (int64_t)tiles_m * 2 * p.Nout, "hcb.conv_igemm: stats slab too small");
+    int64_t rows = p.stats_R > 0 ? p.stats_R : tiles_m;
+    TORCH_CHECK(stats->numel() >= rows * 2 * p.Nout, "hcb.conv_igemm: stats buffer too small");
     p.stats = stats->data_ptr<float>();
   }
   p.x_bytes = (uint32_t)xb;
@@ -393,6 +395,84 @@ void add_bf16(const Tensor& a, const Tensor& b, const Tensor& y) {
   hcb::launch_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream());
 }
 
+// ---- finalize-free BN (statistics in R replicas of [2][C], fp32 atomics)
+void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, const c10::optional<Tensor>& res,
+                  int64_t ldr, int64_t M, int64_t C, const Tensor& acc, int64_t R, double eps, double momentum,
+                  const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& saved_mean,
+                  const Tensor& saved_invstd, const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  check_f32(acc, "acc");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldy % 8 == 0 && R >= 1, "hcb.bn_apply_acc: C/ld/R");
+  TORCH_CHECK(acc.numel() >= R * 2 * C && saved_mean.numel() >= C && saved_invstd.numel() >= C, "hcb.bn_apply_acc: sizes");
+  check_range(x, ((M - 1) * ldx + C) * 2, "x");
+  check_range(y, ((M - 1) * ldy + C) * 2, "y");
+  const void* rp = nullptr;
+  if (res.has_value()) {
+    check_bf16(*res, "res");
+    TORCH_CHECK(ldr % 8 == 0, "hcb.bn_apply_acc: ldr");
+    check_range(*res, ((M - 1) * ldr + C) * 2, "res");
+    rp = res->data_ptr();
+  }
+  hcb::launch_bn_apply_acc(x.data_ptr(), (int)ldx, y.data_ptr(), (int)ldy, rp, (int)ldr, (int)M, (int)C,
+                           acc.data_ptr<float>(), (int)R, (float)eps, (float)momentum, gamma.data_ptr<float>(),
+                           beta.data_ptr<float>(), (int)relu, saved_mean.data_ptr<float>(),
+                           saved_invstd.data_ptr<float>(), rm.has_value() ? rm->data_ptr<float>() : nullptr,
+                           rv.has_value() ? rv->data_ptr<float>() : nullptr, cur_stream());
+}
+
+void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
+                       const Tensor& x, int64_t ldx, int64_t M, int64_t C, const Tensor& mean, const Tensor& invstd,
+                       const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& acc, int64_t R,
+                       const c10::optional<Tensor>& gout, int64_t ldg) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_f32(acc, "acc");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_reduce_acc: C/R");
+  check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
+  check_range(x, ((M - 1) * ldx + C) * 2, "x");
+  const void* yp = nullptr;
+  if (relu == 1) {
+    TORCH_CHECK(y.has_value(), "hcb.bn_bwd_reduce_acc: relu=1 needs y");
+    check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    yp = y->data_ptr();
+  }
+  void* gp = nullptr;
+  if (gout.has_value()) {
+    check_bf16(*gout, "gout");
+    check_range(*gout, ((M - 1) * ldg + C) * 2, "gout");
+    gp = gout->data_ptr();
+  }
+  hcb::launch_bn_bwd_reduce_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, (int)M, (int)C,
+                                mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                                beta.data_ptr<float>(), (int)relu, acc.data_ptr<float>(), (int)R, gp, (int)ldg,
+                                cur_stream());
+}
+
+void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
+                      const Tensor& x, int64_t ldx, const Tensor& dx, int64_t lddx, int64_t M, int64_t C,
+                      const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
+                      const Tensor& acc, int64_t R, const Tensor& dgamma, const Tensor& dbeta, int64_t relu) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_bf16(dx, "dx");
+  check_f32(acc, "acc");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_apply_acc: C/R");
+  check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
+  check_range(x, ((M - 1) * ldx + C) * 2, "x");
+  check_range(dx, ((M - 1) * lddx + C) * 2, "dx");
+  const void* yp = nullptr;
+  if (relu == 1) {
+    TORCH_CHECK(y.has_value(), "hcb.bn_bwd_apply_acc: relu=1 needs y");
+    check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    yp = y->data_ptr();
+  }
+  hcb::launch_bn_bwd_apply_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, dx.data_ptr(),
+                               (int)lddx, (int)M, (int)C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                               gamma.data_ptr<float>(), beta.data_ptr<float>(), acc.data_ptr<float>(), (int)R,
+                               dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu, cur_stream());
+}
+
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
   check_bf16(dy, "dy");
   check_bf16(y, "y");
@@ -470,6 +550,9 @@ TORCH_LIBRARY(hcb, m) {
   m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");
   m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
+  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var) -> ()");
+  m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg) -> ()");
+  m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
   m.def("synth_images(Tensor(a!) out, int C, int Cpad, float mean, float std, int seed) -> ()");
   m.def("synth_labels(Tensor(a!) out, int ncls, int seed) -> ()");
@@ -498,6 +581,9 @@ TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("add_bf16", add_bf16);
   m.impl("scale_f32", scale_f32);
   m.impl("relu_bwd", relu_bwd);
+  m.impl("bn_apply_acc", bn_apply_acc);
+  m.impl("bn_bwd_reduce_acc", bn_bwd_reduce_acc);
+  m.impl("bn_bwd_apply_acc", bn_bwd_apply_acc);
   m.impl("l2norm_sq", l2norm_sq);
   m.impl("synth_images", synth_images);
   m.impl("synth_labels", synth_labels);

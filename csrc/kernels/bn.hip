@@ -16,6 +16,14 @@
 
 namespace hcb {
 
+constexpr int BN_U = 4;  // rows in flight per thread in the streaming kernels
+
+// buffer-resource byte range covering rows [0, M) of a [M][ld] bf16 tensor (clamped to 2 GiB)
+__device__ __forceinline__ uint32_t rsrc_bytes(int M, int ld) {
+  size_t b = (size_t)M * (size_t)ld * 2u;
+  return b > 0x7fffffffu ? 0x7fffffffu : (uint32_t)b;
+}
+
 // thread -> (channel vector, row lane) mapping shared by all kernels below
 struct RowMap {
   int cv, r0, rstep, active;
@@ -155,39 +163,64 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     sc[e] = s;
     sh[e] = beta[c] - mean[c] * s;
   }
-  for (int m = blockIdx.x * rm.rstep + rm.r0; m < M; m += gridDim.x * rm.rstep) {
-    float f[8];
-    unpack8(*reinterpret_cast<const u32x4*>(x + (size_t)m * ldx + rm.cv * 8), f);
+  // BN_U rows in flight per thread: every load of the group is issued before any use
+  // (buffer loads, out-of-range rows return zeros -> no branches around loads)
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx));
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx));
+  const int stride = gridDim.x * rm.rstep;
+  for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+    u32x4 xv[BN_U], rv[BN_U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = f[e] * sc[e] + sh[e];
-    if (res != nullptr) {
-      float r[8];
-      unpack8(*reinterpret_cast<const u32x4*>(res + (size_t)m * ldr + rm.cv * 8), r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] += r[e];
+    for (int u = 0; u < BN_U; ++u) {
+      int m = m0 + u * stride;
+      xv[u] = buf_load16(xr, m < M ? (uint32_t)((size_t)m * ldx + rm.cv * 8) * 2u : HCB_OOB);
+      if (res != nullptr) rv[u] = buf_load16(rr, m < M ? (uint32_t)((size_t)m * ldr + rm.cv * 8) * 2u : HCB_OOB);
     }
-    if (relu) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+    for (int u = 0; u < BN_U; ++u) {
+      int m = m0 + u * stride;
+      float f[8];
+      unpack8(xv[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] * sc[e] + sh[e];
+      if (res != nullptr) {
+        float r[8];
+        unpack8(rv[u], r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += r[e];
+      }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+      }
+      if (m < M) *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + rm.cv * 8) = pack8(f);
     }
-    *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + rm.cv * 8) = pack8(f);
   }
 }
 
 // relu: 0 = none, 1 = mask from stored output y (y > 0), 2 = mask recomputed from x
 // (gamma*xhat + beta > 0; valid when the block had no residual add)
-__device__ __forceinline__ void bwd_load(const uint16_t* dy, int lddy, const uint16_t* y, int ldyv,
-                                         const uint16_t* x, int ldx, int m, int cv, int relu,
-                                         const float* mu, const float* is, const float* sc,
-                                         const float* sh, float* g, float* xh) {
+struct BwdSrc {
+  __amdgpu_buffer_rsrc_t dyr, xr, yr;
+  int lddy, ldx, ldyv, cv;
+  __device__ __forceinline__ void load(int m, int M, int relu, u32x4& d, u32x4& x, u32x4& y) const {
+    const bool ok = m < M;
+    d = buf_load16(dyr, ok ? (uint32_t)((size_t)m * lddy + cv * 8) * 2u : HCB_OOB);
+    x = buf_load16(xr, ok ? (uint32_t)((size_t)m * ldx + cv * 8) * 2u : HCB_OOB);
+    if (relu == 1) y = buf_load16(yr, ok ? (uint32_t)((size_t)m * ldyv + cv * 8) * 2u : HCB_OOB);
+  }
+};
+__device__ __forceinline__ void bwd_math(const u32x4& dv, const u32x4& xvv, const u32x4& yvv, int relu,
+                                         const float* mu, const float* is, const float* sc, const float* sh,
+                                         float* g, float* xh) {
   float d[8], xv[8];
-  unpack8(*reinterpret_cast<const u32x4*>(dy + (size_t)m * lddy + cv * 8), d);
-  unpack8(*reinterpret_cast<const u32x4*>(x + (size_t)m * ldx + cv * 8), xv);
+  unpack8(dv, d);
+  unpack8(xvv, xv);
 #pragma unroll
   for (int e = 0; e < 8; ++e) xh[e] = (xv[e] - mu[e]) * is[e];
   if (relu == 1) {
     float yv[8];
-    unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)m * ldyv + cv * 8), yv);
+    unpack8(yvv, yv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? d[e] : 0.f;
   } else if (relu == 2) {
@@ -216,15 +249,25 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       sc[e] = gamma != nullptr ? gamma[c] * is[e] : 0.f;
       sh[e] = beta != nullptr ? beta[c] - mu[e] * sc[e] : 0.f;
     }
-    for (int m = blockIdx.x * rm.rstep + rm.r0; m < M; m += gridDim.x * rm.rstep) {
-      float g[8], xh[8];
-      bwd_load(dy, lddy, y, ldyv, x, ldx, m, rm.cv, relu, mu, is, sc, sh, g, xh);
+    BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
+               make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, rm.cv};
+    const int stride = gridDim.x * rm.rstep;
+    for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+      u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] += g[e];
-        s2[e] += g[e] * xh[e];
+      for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const int m = m0 + u * stride;
+        float g[8], xh[8];
+        bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {  // rows beyond M load zeros: g = 0 contributes nothing
+          s1[e] += g[e];
+          s2[e] += g[e] * xh[e];
+        }
+        if (gout != nullptr && m < M) *reinterpret_cast<u32x4*>(gout + (size_t)m * ldg + rm.cv * 8) = pack8(g);
       }
-      if (gout != nullptr) *reinterpret_cast<u32x4*>(gout + (size_t)m * ldg + rm.cv * 8) = pack8(g);
     }
   }
   slab_write(lds_f, s1, s2, C, rm, slab + (size_t)blockIdx.x * 2 * C);
@@ -260,12 +303,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     k1[e] = dbeta[c] * invM;
     k2[e] = dgamma[c] * invM;
   }
-  for (int m = blockIdx.x * rm.rstep + rm.r0; m < M; m += gridDim.x * rm.rstep) {
-    float g[8], xh[8], o[8];
-    bwd_load(dy, lddy, y, ldyv, x, ldx, m, rm.cv, relu, mu, is, sc, sh, g, xh);
+  BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
+             make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, rm.cv};
+  const int stride = gridDim.x * rm.rstep;
+  for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+    u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
-    *reinterpret_cast<u32x4*>(dx + (size_t)m * lddx + rm.cv * 8) = pack8(o);
+    for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int m = m0 + u * stride;
+      float g[8], xh[8], o[8];
+      bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
+      if (m < M) *reinterpret_cast<u32x4*>(dx + (size_t)m * lddx + rm.cv * 8) = pack8(o);
+    }
   }
 }
 
@@ -431,6 +484,227 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(M, C)), dim3(256), 0, st,
                      (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx,
                      (uint16_t*)dx, lddx, M, C, mean, invstd, gamma, beta, dgamma, dbeta, relu);
+}
+
+}  // namespace hcb
+
+// =======================================================================================
+// Finalize-free BN: statistics are accumulated with fp32 atomics into R replicas of a
+// [2][C] accumulator (producer tile t adds into replica t % R, spreading the contention);
+// the consumer kernel reduces the R replicas once per block into LDS and derives
+// mean/invstd (or dgamma/dbeta) itself. This removes the separate finalize launch per BN
+// layer (two per layer per step). Accumulators are zeroed once per step by one memset.
+// =======================================================================================
+namespace hcb {
+
+// block-cooperative: sums[c] = sum_r acc[r][0][c], sums[C + c] = sum_r acc[r][1][c]
+__device__ __forceinline__ void reduce_replicas(const float* acc, int R, int C, float* sums) {
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) {
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s += acc[(size_t)r * 2 * C + i];
+    sums[i] = s;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void bn_apply_acc_kernel(
+    const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ y, int ldy, const uint16_t* __restrict__ res,
+    int ldr, int M, int C, const float* __restrict__ acc, int R, float eps, float momentum,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
+    float* saved_invstd, float* run_mean, float* run_var) {
+  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][C]
+  reduce_replicas(acc, R, C, sums);
+  const float inv_n = 1.f / (float)M;
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float mu = sums[c] * inv_n;
+      float var = fmaxf(sums[C + c] * inv_n - mu * mu, 0.f);
+      saved_mean[c] = mu;
+      saved_invstd[c] = rsqrtf(var + eps);
+      if (run_mean != nullptr) {
+        float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * mu;
+        run_var[c] = momentum * run_var[c] + (1.f - momentum) * unb;
+      }
+    }
+  }
+  RowMap rm = rowmap(C);
+  if (!rm.active) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    int c = rm.cv * 8 + e;
+    float mu = sums[c] * inv_n;
+    float var = fmaxf(sums[C + c] * inv_n - mu * mu, 0.f);
+    float s = gamma[c] * rsqrtf(var + eps);
+    sc[e] = s;
+    sh[e] = beta[c] - mu * s;
+  }
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx));
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx));
+  const int stride = gridDim.x * rm.rstep;
+  for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+    u32x4 xv[BN_U], rv[BN_U];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      int m = m0 + u * stride;
+      xv[u] = buf_load16(xr, m < M ? (uint32_t)((size_t)m * ldx + rm.cv * 8) * 2u : HCB_OOB);
+      if (res != nullptr) rv[u] = buf_load16(rr, m < M ? (uint32_t)((size_t)m * ldr + rm.cv * 8) * 2u : HCB_OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      int m = m0 + u * stride;
+      float f[8];
+      unpack8(xv[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] * sc[e] + sh[e];
+      if (res != nullptr) {
+        float r[8];
+        unpack8(rv[u], r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += r[e];
+      }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+      }
+      if (m < M) *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + rm.cv * 8) = pack8(f);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
+    const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
+    const uint16_t* __restrict__ x, int ldx, int M, int C, const float* mean, const float* invstd,
+    const float* gamma, const float* beta, int relu, float* acc, int R, uint16_t* gout, int ldg) {
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  RowMap rm = rowmap(C);
+  float s1[8] = {0}, s2[8] = {0};
+  if (rm.active) {
+    float mu[8], is[8], sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int c = rm.cv * 8 + e;
+      mu[e] = mean[c];
+      is[e] = invstd[c];
+      sc[e] = gamma[c] * is[e];
+      sh[e] = beta[c] - mu[e] * sc[e];
+    }
+    BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
+               make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, rm.cv};
+    const int stride = gridDim.x * rm.rstep;
+    for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+      u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const int m = m0 + u * stride;
+        float g[8], xh[8];
+        bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += g[e];
+          s2[e] += g[e] * xh[e];
+        }
+        if (gout != nullptr && m < M) *reinterpret_cast<u32x4*>(gout + (size_t)m * ldg + rm.cv * 8) = pack8(g);
+      }
+    }
+  }
+  // block partial -> LDS row -> atomics into replica blockIdx % R
+  const int CV = C >> 3, rows = 256 / CV;
+  if (rm.active) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      lds_f[rm.r0 * C + rm.cv * 8 + e] = s1[e];
+      lds_f[rows * C + rm.r0 * C + rm.cv * 8 + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  float* dst = acc + (size_t)(blockIdx.x % R) * 2 * C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rows; ++r) {
+      a += lds_f[r * C + c];
+      b += lds_f[rows * C + r * C + c];
+    }
+    atomicAdd(dst + c, a);
+    atomicAdd(dst + C + c, b);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
+    const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
+    const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ dx, int lddx, int M, int C,
+    const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
+    int R, float* dgamma, float* dbeta, int relu) {
+  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][C]: dbeta, dgamma
+  reduce_replicas(acc, R, C, sums);
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      dbeta[c] = sums[c];
+      dgamma[c] = sums[C + c];
+    }
+  }
+  RowMap rm = rowmap(C);
+  if (!rm.active) return;
+  float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    int c = rm.cv * 8 + e;
+    mu[e] = mean[c];
+    is[e] = invstd[c];
+    sc[e] = gamma[c] * is[e];
+    sh[e] = beta[c] - mu[e] * sc[e];
+    k1[e] = sums[c] * invM;
+    k2[e] = sums[C + c] * invM;
+  }
+  BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
+             make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, rm.cv};
+  const int stride = gridDim.x * rm.rstep;
+  for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+    u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int m = m0 + u * stride;
+      float g[8], xh[8], o[8];
+      bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
+      if (m < M) *reinterpret_cast<u32x4*>(dx + (size_t)m * lddx + rm.cv * 8) = pack8(o);
+    }
+  }
+}
+
+void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
+                         const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
+                         int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(bn_apply_acc_kernel, dim3(bn_grid(M, C)), dim3(256), (size_t)2 * C * 4, st,
+                     (const uint16_t*)x, ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, acc, R, eps,
+                     momentum, gamma, beta, relu, saved_mean, saved_invstd, run_mean, run_var);
+}
+
+void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
+                              int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
+                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st) {
+  int rows = 256 / (C / 8);
+  size_t lds = (size_t)2 * rows * C * 4;
+  hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel, dim3(bn_grid(M, C)), dim3(256), lds, st, (const uint16_t*)dy, lddy,
+                     (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, mean, invstd, gamma, beta, relu, acc,
+                     R, (uint16_t*)gout, ldg);
+}
+
+void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
+                             int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
+                             const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_apply_acc_kernel, dim3(bn_grid(M, C)), dim3(256), (size_t)2 * C * 4, st,
+                     (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, (uint16_t*)dx,
+                     lddx, M, C, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu);
 }
 
 }  // namespace hcb

@@ -68,8 +68,14 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       }
       int gc = n0 + col;
       if (gc < p.Nout) {
-        p.stats[(size_t)tm * 2 * p.Nout + gc] = s1;
-        p.stats[(size_t)tm * 2 * p.Nout + p.Nout + gc] = s2;
+        if (p.stats_R > 0) {  // atomics into replica tm % R of a [R][2][Nout] accumulator
+          float* dst = p.stats + (size_t)(tm % p.stats_R) * 2 * p.Nout;
+          atomicAdd(dst + gc, s1);
+          atomicAdd(dst + p.Nout + gc, s2);
+        } else {
+          p.stats[(size_t)tm * 2 * p.Nout + gc] = s1;
+          p.stats[(size_t)tm * 2 * p.Nout + p.Nout + gc] = s2;
+        }
       }
     }
   }

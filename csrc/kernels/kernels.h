@@ -45,7 +45,8 @@ struct ConvParams {
   int M;
   int remap, OH, OW, osh, osw;
   int beta, out_f32;
-  int relu;  // fused ReLU in the epilogue (affine layers without BN)
+  int relu;     // fused ReLU in the epilogue (affine layers without BN)
+  int stats_R;  // 0: per-tile slab [tiles][2][Nout]; R>0: atomics into [R][2][Nout] replicas
   uint32_t x_bytes, w_bytes;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
@@ -100,6 +101,19 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
                           int ldx, void* dx, int lddx, int M, int C, const float* mean,
                           const float* invstd, const float* gamma, const float* beta,
                           const float* dgamma, const float* dbeta, int relu, hipStream_t st);
+
+// finalize-free variants: statistics accumulated in R replicas of [2][C] (fp32 atomics)
+void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
+                         const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
+                         int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
+                         hipStream_t st);
+void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
+                              int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
+                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st);
+void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
+                             int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
+                             const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
+                             hipStream_t st);
 
 // ---------------------------------------------------------------- pooling
 void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,

@@ -303,3 +303,46 @@ def test_synthetic_data_stats():
     lab = torch.empty(4096, dtype=torch.int64, device=DEV)
     _ext.ops().synth_labels(lab, 1000, 3)
     assert lab.min().item() >= 0 and lab.max().item() < 1000 and lab.unique().numel() > 900
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048])
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
+def test_bn_finalize_free_path(C, relu, residual):
+    """conv-epilogue atomics -> bn_apply_acc (stats finalized in-kernel) and the bwd reduce /
+    apply pair with replica accumulators, vs the fp32 CPU reference."""
+    torch.manual_seed(13)
+    spec, p, pk = make_conv(64, C, 3, 3, 1, 1, (1, 1, 1, 1))
+    N, H = 4, 9
+    x = bf(torch.randn(N, H, H, 64, device=DEV))
+    z = torch.empty(N, H, H, C, dtype=torch.bfloat16, device=DEV)
+    R = 8
+    acc_f = torch.zeros(R * 2 * C, device=DEV)
+    Fn.conv_forward(x, spec, pk.pack, p.data, z, stats=acc_f, stats_R=R, cfg=2)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    res = bf(torch.randn(N, H, H, C, device=DEV)) if residual else None
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mean, invstd = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    y = torch.empty_like(z)
+    saved = Fn.bn_forward_acc(z, gamma, beta, rm, rv, 0.9, 1e-5, y, relu, acc_f, R, mean, invstd, residual=res)
+    zc = z.float().cpu()
+    yc = torch.empty(N, H, H, C)
+    rmc, rvc = torch.zeros(C), torch.ones(C)
+    sc = Fn.bn_forward(zc, gamma.cpu(), beta.cpu(), rmc, rvc, 0.9, 1e-5, yc, relu,
+                       residual=None if res is None else res.float().cpu())
+    assert rel_err(y, yc) < 1e-2
+    # the kernel's statistics come from the fp32 accumulators, the reference's from the
+    # bf16-rounded z: the mean differs by O(bf16 eps * std / sqrt(n)), so measure it in stds
+    mean_err = ((saved.mean.cpu() - sc.mean).abs() * sc.invstd).max().item()
+    assert mean_err < 2e-3 and rel_err(saved.invstd, sc.invstd) < 1e-3
+    assert ((rm.cpu() - rmc).abs() * sc.invstd).max().item() < 2e-3 and rel_err(rv, rvc) < 1e-3
+    dy = bf(torch.randn(N, H, H, C, device=DEV))
+    mode = (1 if residual else 2) if relu else 0
+    dz, gres = torch.empty_like(z), torch.empty_like(z)
+    dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    acc_b = torch.zeros(R * 2 * C, device=DEV)
+    Fn.bn_backward_acc(dy, y, z, saved, gamma, beta, mode, dg, db, dz, acc_b, R, gres)
+    dzc, gresc, dgc, dbc = torch.empty(N, H, H, C), torch.empty(N, H, H, C), torch.empty(C), torch.empty(C)
+    Fn.bn_backward(dy.float().cpu(), y.float().cpu(), zc, sc, gamma.cpu(), beta.cpu(), mode, dgc, dbc, dzc, gresc)
+    assert rel_err(db, dbc) < 2e-2 and rel_err(dg, dgc) < 2e-2
+    assert rel_err(dz, dzc) < 3e-2 and rel_err(gres, gresc) < 1e-2
