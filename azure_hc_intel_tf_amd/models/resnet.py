@@ -45,15 +45,20 @@ class Bottleneck:
         b = self.c2.forward(a)
         return self.c3.forward(b, residual=sc)
 
-    def backward(self, dy):
-        db, gres = self.c3.backward(dy, want_gres=True)
-        da, _ = self.c2.backward(db)
+    def backward(self, dy, prev_bn=None):
+        """``prev_bn``: the ConvBN producing this block's input (the previous block's conv3), whose
+        BN backward is fused into the last data-grad GEMM that completes dx."""
+        db, gres = self.c3.backward(dy, want_gres=True, dx_bn=self.c2)
+        da, _ = self.c2.backward(db, dx_bn=self.c1)
         if self.proj:
-            dx, _ = self.c1.backward(da)
-            self.sc.backward(gres, dx=dx, accumulate=True)
+            # shortcut first: the fused GEMM must be the one that visits every dx pixel (v1.5's
+            # strided 1x1 shortcut only writes the strided ones; v1's two strided 1x1s cover the
+            # same pixels and leave the rest zero)
+            dx, _ = self.sc.backward(gres)
+            self.c1.backward(da, dx=dx, accumulate=True, dx_bn=prev_bn)
         else:
             # identity shortcut: dx = gres + dgrad(c1), accumulated in place by the GEMM epilogue
-            dx, _ = self.c1.backward(da, dx=gres, accumulate=True)
+            dx, _ = self.c1.backward(da, dx=gres, accumulate=True, dx_bn=prev_bn)
         return dx
 
 
@@ -98,8 +103,8 @@ class ResNet(CNNModel):
     def backward(self, dlogits):
         dfeat = self.fc.backward(dlogits)
         dx = self.gap.backward(dfeat)
-        for b in reversed(self.blocks):
-            dx = b.backward(dx)
+        for i in range(len(self.blocks) - 1, -1, -1):
+            dx = self.blocks[i].backward(dx, self.blocks[i - 1].c3 if i > 0 else None)
         dx = self.pool.backward(dx)
         self.stem.backward(dx)
         self._last = None

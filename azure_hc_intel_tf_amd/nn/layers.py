@@ -56,6 +56,8 @@ def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
 
 
 STAT_R = 8  # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
+# fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
+FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
 
 
 class _FixedParam:
@@ -126,6 +128,7 @@ class ConvBN(Layer):
         else:
             self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0))
         self._saved = None
+        self._pre_reduced = False
 
     def flops(self, batch: int) -> int:
         P, Q, C = self.out_shape
@@ -160,14 +163,37 @@ class ConvBN(Layer):
         return y
 
     # ------------------------------------------------------------------ backward
-    def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False):
-        """Returns (dx or None, gres or None). gres = gradient w.r.t. the residual input."""
+    def bwd_fuse_request(self) -> Optional[Fn.BNBwdFuse]:
+        """BN-backward reduction of this layer, to be fused into the GEMM producing its dy."""
+        if not (self.bn and FUSE_BN_BWD) or self._saved is None:
+            return None
+        x, z, y, saved, had_res = self._saved
+        mode = (1 if had_res else 2) if self.relu else 0
+        self._pre_reduced = True
+        return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, self.acc_b.data, STAT_R)
+
+    def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False, dx_bn=None):
+        """Returns (dx or None, gres or None). gres = gradient w.r.t. the residual input.
+        ``dx_bn``: the ConvBN layer whose BN consumes dx; its backward reduction (and ReLU
+        gating) is fused into this layer's data-grad GEMM."""
         x, z, y, saved, had_res = self._saved
         dev = dy.device
         N = dy.shape[0]
         P, Q, C = self.out_shape
         gres = None
-        if self.bn:
+        if self.bn and self._pre_reduced:
+            # dy is already g = dy * mask and (GPU) acc_b holds sum(g), sum(g*xhat)
+            self._pre_reduced = False
+            dz = empty_act((N, P, Q, C), dev)
+            if dy.is_cuda:
+                Fn.bn_backward_acc(dy, None, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
+                                   self.beta.grad, dz, self.acc_b.data, STAT_R, None, pre_reduced=True)
+            else:
+                Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
+                               self.beta.grad, dz, None)
+            if want_gres:
+                gres = dy
+        elif self.bn:
             dz = empty_act((N, P, Q, C), dev)
             if want_gres:
                 gres = empty_act((N, P, Q, C), dev)
@@ -193,12 +219,14 @@ class ConvBN(Layer):
                 strided_1x1 = (self.spec.sh > 1 or self.spec.sw > 1) and self.spec.kh == 1 and self.spec.kw == 1
                 dx = empty_act((N, H, W, Cin), dev, zero=strided_1x1 and dev.type == "cuda")
                 accumulate = False
-            Fn.conv_dgrad(dz, self.spec, self.pack.tr, self.w.data, dx, accumulate)
+            bnb = dx_bn.bwd_fuse_request() if dx_bn is not None else None
+            Fn.conv_dgrad(dz, self.spec, self.pack.tr, self.w.data, dx, accumulate, bnb=bnb)
         self._saved = None
         return dx, gres
 
     def clear(self):
         self._saved = None
+        self._pre_reduced = False
 
 
 class Pool(Layer):

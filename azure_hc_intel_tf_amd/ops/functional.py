@@ -210,9 +210,30 @@ def conv_stats_slab(x_shape, spec: ConvSpec, device, cfg=None):
 
 
 # ---------------------------------------------------------------- conv data grad
-def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None):
+class BNBwdFuse:
+    """Request to fold a BN layer's backward reduction into the data-grad GEMM that produces
+    that layer's dy (ConvParams::bnb_* in csrc/kernels/kernels.h). The GEMM output becomes
+    g = dy * relu_mask; on the GPU sum(g) and sum(g * xhat) are added to ``acc`` replicas, so
+    the BN backward only runs its apply pass (``bn_backward_acc(..., pre_reduced=True)``)."""
+
+    def __init__(self, z, y, saved: "BNSaved", gamma, beta, mode: int, acc, R: int):
+        self.z, self.y, self.saved, self.gamma, self.beta = z, y, saved, gamma, beta
+        self.mode, self.acc, self.R = mode, acc, R
+
+    def gate_cpu(self, g):
+        """CPU semantics of the fused epilogue's gating (the reductions stay in bn_backward)."""
+        if self.mode == 1:
+            g.mul_((self.y > 0).to(g.dtype))
+        elif self.mode == 2:
+            xhat = (self.z - self.saved.mean) * self.saved.invstd
+            g.mul_(((xhat * self.gamma + self.beta) > 0).to(g.dtype))
+        return g
+
+
+def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None, bnb: "BNBwdFuse" = None):
     """dx[N,H,W,cin] (+)= conv_transpose(dz, W). dx must be zero-filled by the caller when
-    not accumulating and the conv is a strided 1x1 (remap path leaves gaps)."""
+    not accumulating and the conv is a strided 1x1 (remap path leaves gaps). With ``bnb`` the
+    result is gated by the consuming BN layer's ReLU mask and its backward sums are fused."""
     N, P, Q, _ = dz.shape
     _, H, W, _ = dx.shape
     if dz.is_cuda:
@@ -235,7 +256,12 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
                     1 if accumulate else 0, 0]
         if cfg is None:
             cfg = conv_cfg(M, spec.cin_pad, K)
-        _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg)
+        if bnb is not None:
+            _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
+                                      bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
+                                      bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
+        else:
+            _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg)
         return dx
     Hp = H + spec.pt + spec.pb
     Wp = W + spec.pl + spec.pr
@@ -247,6 +273,8 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
         dx.add_(g)
     else:
         dx.copy_(g)
+    if bnb is not None:
+        bnb.gate_cpu(dx)
     return dx
 
 
@@ -330,12 +358,19 @@ def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out
 
 
 def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, acc, R: int,
-                    gres=None):
+                    gres=None, pre_reduced: bool = False):
     """GPU BN(+ReLU) backward with the dgamma/dbeta reduction accumulated in ``acc`` replicas
-    (zeroed per step) and consumed directly by the apply kernel."""
+    (zeroed per step) and consumed directly by the apply kernel. ``pre_reduced``: dy is already
+    the gated g and ``acc`` already holds its sums (a BNBwdFuse data-grad epilogue produced it),
+    so only the apply pass runs."""
     N, H, W, C = z.shape
     M = N * H * W
     hcb = _ext.ops()
+    if pre_reduced:
+        assert gres is None, "pre-reduced dy is itself the residual gradient"
+        hcb.bn_bwd_apply_acc(dy, ld(dy), None, 0, z, ld(z), dz, ld(dz), M, C, saved.mean, saved.invstd, gamma,
+                             beta, acc, R, dgamma, dbeta, 0)
+        return dz
     ym = y if relu_mode == 1 else None
     hcb.bn_bwd_reduce_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), M, C, saved.mean, saved.invstd,
                           gamma, beta, relu_mode, acc, R, gres, ld(gres) if gres is not None else 0)

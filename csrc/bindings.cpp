@@ -44,9 +44,9 @@ void check_align16(const void* p, const char* name) {
 
 // geom = [N,H,W,C,ldx, P,Q,R,S, sh,sw,ph,pw,dh,dw,idh,idw, Nout,K,Kpad,ldy,
 //         remap,OH,OW,osh,osw, beta,out_f32]
-void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
-                const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
-                at::IntArrayRef g, int64_t cfg) {
+hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
+                            const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
+                            at::IntArrayRef g, int64_t cfg) {
   TORCH_CHECK(g.size() >= 28 && g.size() <= 30, "hcb.conv_igemm: geom must have 28 (+relu, +stats_R) entries");
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -108,6 +108,55 @@ void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::op
   }
   p.x_bytes = (uint32_t)xb;
   p.w_bytes = (uint32_t)wb;
+  return p;
+}
+
+void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
+                const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
+                at::IntArrayRef g, int64_t cfg) {
+  hcb::ConvParams p = conv_params(x, w, y, yres, bias, stats, g, cfg);
+  hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
+}
+
+// data-grad conv whose output is the dy of a BN layer: the epilogue gates it with the
+// layer's ReLU mask (mode 1: y > 0, 2: recomputed from z, 0: none), stores g and adds
+// sum(g), sum(g*xhat) per channel into acc [R][2][Nout] (see ConvParams::bnb_*)
+void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
+                    at::IntArrayRef g, int64_t cfg, const Tensor& z, const c10::optional<Tensor>& yact,
+                    int64_t ld, const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
+                    const Tensor& acc, int64_t R, int64_t mode) {
+  hcb::ConvParams p = conv_params(x, w, y, yres, c10::nullopt, c10::nullopt, g, cfg);
+  TORCH_CHECK(!p.out_f32 && !p.relu && p.bias == nullptr, "hcb.conv_igemm_bnb: bf16 output without bias/relu");
+  TORCH_CHECK(mode >= 0 && mode <= 2 && R >= 1, "hcb.conv_igemm_bnb: bad mode / R");
+  TORCH_CHECK(ld % 8 == 0 && ld >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm_bnb: bad ld");
+  int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
+  int64_t need = (rows - 1) * ld * 2 + ((p.Nout + 7) / 8) * 8 * 2;
+  check_bf16(z, "z");
+  check_range(z, need, "z");
+  check_align16(z.data_ptr(), "z");
+  p.bnb_y = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(yact.has_value(), "hcb.conv_igemm_bnb: mode 1 needs y");
+    check_bf16(*yact, "y");
+    check_range(*yact, need, "y");
+    check_align16(yact->data_ptr(), "y");
+    p.bnb_y = yact->data_ptr();
+  }
+  for (const Tensor* t : {&mean, &invstd, &gamma, &beta}) {
+    check_f32(*t, "bn param");
+    TORCH_CHECK(t->numel() >= p.Nout, "hcb.conv_igemm_bnb: per-channel tensor too small");
+  }
+  check_f32(acc, "acc");
+  TORCH_CHECK(acc.numel() >= R * 2 * p.Nout, "hcb.conv_igemm_bnb: acc too small");
+  p.bnb_z = z.data_ptr();
+  p.bnb_ld = (int)ld;
+  p.bnb_mean = mean.data_ptr<float>();
+  p.bnb_invstd = invstd.data_ptr<float>();
+  p.bnb_gamma = gamma.data_ptr<float>();
+  p.bnb_beta = beta.data_ptr<float>();
+  p.bnb_acc = acc.data_ptr<float>();
+  p.bnb_mode = (int)mode;
+  p.bnb_R = (int)R;
   hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
 }
 
@@ -529,6 +578,7 @@ void bucket_unpack(const Tensor& src, const Tensor& dst, double scale) {
 
 TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg) -> ()");
+  m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
   m.def("bn_stats(Tensor x, int M, int C, int ldx, Tensor(a!) slab) -> ()");
@@ -562,6 +612,7 @@ TORCH_LIBRARY(hcb, m) {
 
 TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("conv_igemm", conv_igemm);
+  m.impl("conv_igemm_bnb", conv_igemm_bnb);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("bn_stats", bn_stats);
   m.impl("bn_finalize", bn_finalize);

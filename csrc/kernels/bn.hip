@@ -488,20 +488,50 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
 
 }  // namespace hcb
 
+
 // =======================================================================================
 // Finalize-free BN: statistics are accumulated with fp32 atomics into R replicas of a
 // [2][C] accumulator (producer tile t adds into replica t % R, spreading the contention);
-// the consumer kernel reduces the R replicas once per block into LDS and derives
-// mean/invstd (or dgamma/dbeta) itself. This removes the separate finalize launch per BN
-// layer (two per layer per step). Accumulators are zeroed once per step by one memset.
+// the consumer kernel reduces the replicas itself and derives mean/invstd (or dgamma/dbeta),
+// which removes the separate finalize launch per BN layer (two per layer per step).
+// Accumulators are zeroed once per step by one memset.
+//
+// Blocks tile (row split) x (channel group of CB = 8*CVB channels): a block reduces only
+// its group's R*2*CB replica floats (4 KiB for CB = 64) instead of all C channels, and a
+// row segment of a group is CB*2 = 128 contiguous bytes, so loads stay line-sized.
 // =======================================================================================
 namespace hcb {
 
-// block-cooperative: sums[c] = sum_r acc[r][0][c], sums[C + c] = sum_r acc[r][1][c]
-__device__ __forceinline__ void reduce_replicas(const float* acc, int R, int C, float* sums) {
-  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) {
+// channel vectors (of 8) per group: 8 when possible, else the whole (small) C, else the
+// largest divisor <= 32
+static int bn_group_vecs(int CV) {
+  if (CV % 8 == 0) return 8;
+  if (CV <= 32) return CV;
+  for (int d = 32; d > 1; --d)
+    if (CV % d == 0) return d;
+  return 1;
+}
+
+struct GroupMap {
+  int cv, r0, rows, c0, CB;
+};
+__device__ __forceinline__ GroupMap groupmap(int CVB) {
+  GroupMap g;
+  g.CB = CVB * 8;
+  g.c0 = blockIdx.y * g.CB;
+  g.rows = 256 / CVB;
+  g.r0 = threadIdx.x / CVB;
+  g.cv = blockIdx.y * CVB + (threadIdx.x % CVB);
+  return g;
+}
+
+// block-cooperative: sums[i] = sum_r acc[r][0][c0+i], sums[CB+i] = sum_r acc[r][1][c0+i]
+__device__ __forceinline__ void reduce_group_replicas(const float* acc, int R, int C, int c0, int CB,
+                                                      float* sums) {
+  for (int i = threadIdx.x; i < 2 * CB; i += blockDim.x) {
+    const int off = i < CB ? c0 + i : C + c0 + (i - CB);
     float s = 0.f;
-    for (int r = 0; r < R; ++r) s += acc[(size_t)r * 2 * C + i];
+    for (int r = 0; r < R; ++r) s += acc[(size_t)r * 2 * C + off];
     sums[i] = s;
   }
   __syncthreads();
@@ -509,16 +539,18 @@ __device__ __forceinline__ void reduce_replicas(const float* acc, int R, int C, 
 
 __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ y, int ldy, const uint16_t* __restrict__ res,
-    int ldr, int M, int C, const float* __restrict__ acc, int R, float eps, float momentum,
+    int ldr, int M, int C, int CVB, const float* __restrict__ acc, int R, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
     float* saved_invstd, float* run_mean, float* run_var) {
-  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][C]
-  reduce_replicas(acc, R, C, sums);
+  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
+  const GroupMap gm = groupmap(CVB);
+  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
   const float inv_n = 1.f / (float)M;
   if (blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      float mu = sums[c] * inv_n;
-      float var = fmaxf(sums[C + c] * inv_n - mu * mu, 0.f);
+    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
+      const int c = gm.c0 + i;
+      float mu = sums[i] * inv_n;
+      float var = fmaxf(sums[gm.CB + i] * inv_n - mu * mu, 0.f);
       saved_mean[c] = mu;
       saved_invstd[c] = rsqrtf(var + eps);
       if (run_mean != nullptr) {
@@ -528,28 +560,27 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
       }
     }
   }
-  RowMap rm = rowmap(C);
-  if (!rm.active) return;
+  if (gm.r0 >= gm.rows) return;
   float sc[8], sh[8];
+  const int cl = (threadIdx.x % CVB) * 8;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    int c = rm.cv * 8 + e;
-    float mu = sums[c] * inv_n;
-    float var = fmaxf(sums[C + c] * inv_n - mu * mu, 0.f);
-    float s = gamma[c] * rsqrtf(var + eps);
+    float mu = sums[cl + e] * inv_n;
+    float var = fmaxf(sums[gm.CB + cl + e] * inv_n - mu * mu, 0.f);
+    float s = gamma[gm.c0 + cl + e] * rsqrtf(var + eps);
     sc[e] = s;
-    sh[e] = beta[c] - mu * s;
+    sh[e] = beta[gm.c0 + cl + e] - mu * s;
   }
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx));
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx));
-  const int stride = gridDim.x * rm.rstep;
-  for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+  const int stride = gridDim.x * gm.rows;
+  for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
     u32x4 xv[BN_U], rv[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       int m = m0 + u * stride;
-      xv[u] = buf_load16(xr, m < M ? (uint32_t)((size_t)m * ldx + rm.cv * 8) * 2u : HCB_OOB);
-      if (res != nullptr) rv[u] = buf_load16(rr, m < M ? (uint32_t)((size_t)m * ldr + rm.cv * 8) * 2u : HCB_OOB);
+      xv[u] = buf_load16(xr, m < M ? (uint32_t)((size_t)m * ldx + gm.cv * 8) * 2u : HCB_OOB);
+      if (res != nullptr) rv[u] = buf_load16(rr, m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * 2u : HCB_OOB);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -568,32 +599,33 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
       }
-      if (m < M) *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + rm.cv * 8) = pack8(f);
+      if (m < M) *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + gm.cv * 8) = pack8(f);
     }
   }
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
     const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
-    const uint16_t* __restrict__ x, int ldx, int M, int C, const float* mean, const float* invstd,
+    const uint16_t* __restrict__ x, int ldx, int M, int C, int CVB, const float* mean, const float* invstd,
     const float* gamma, const float* beta, int relu, float* acc, int R, uint16_t* gout, int ldg) {
-  extern __shared__ __attribute__((aligned(16))) float lds_f[];
-  RowMap rm = rowmap(C);
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];  // [2][rows][CB]
+  const GroupMap gm = groupmap(CVB);
+  const bool active = gm.r0 < gm.rows;
   float s1[8] = {0}, s2[8] = {0};
-  if (rm.active) {
+  if (active) {
     float mu[8], is[8], sc[8], sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      int c = rm.cv * 8 + e;
+      int c = gm.cv * 8 + e;
       mu[e] = mean[c];
       is[e] = invstd[c];
       sc[e] = gamma[c] * is[e];
       sh[e] = beta[c] - mu[e] * sc[e];
     }
     BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
-               make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, rm.cv};
-    const int stride = gridDim.x * rm.rstep;
-    for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+               make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, gm.cv};
+    const int stride = gridDim.x * gm.rows;
+    for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
       u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
@@ -603,67 +635,68 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
         float g[8], xh[8];
         bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < 8; ++e) {  // rows beyond M load zeros: g = 0 contributes nothing
           s1[e] += g[e];
           s2[e] += g[e] * xh[e];
         }
-        if (gout != nullptr && m < M) *reinterpret_cast<u32x4*>(gout + (size_t)m * ldg + rm.cv * 8) = pack8(g);
+        if (gout != nullptr && m < M) *reinterpret_cast<u32x4*>(gout + (size_t)m * ldg + gm.cv * 8) = pack8(g);
       }
     }
   }
-  // block partial -> LDS row -> atomics into replica blockIdx % R
-  const int CV = C >> 3, rows = 256 / CV;
-  if (rm.active) {
+  // block partial -> LDS rows -> column sums -> atomics into replica blockIdx.x % R
+  const int cl = (threadIdx.x % CVB) * 8;
+  if (active) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      lds_f[rm.r0 * C + rm.cv * 8 + e] = s1[e];
-      lds_f[rows * C + rm.r0 * C + rm.cv * 8 + e] = s2[e];
+      lds_f[gm.r0 * gm.CB + cl + e] = s1[e];
+      lds_f[gm.rows * gm.CB + gm.r0 * gm.CB + cl + e] = s2[e];
     }
   }
   __syncthreads();
   float* dst = acc + (size_t)(blockIdx.x % R) * 2 * C;
-  for (int c = threadIdx.x; c < C; c += 256) {
+  for (int i = threadIdx.x; i < gm.CB; i += 256) {
     float a = 0.f, b = 0.f;
-    for (int r = 0; r < rows; ++r) {
-      a += lds_f[r * C + c];
-      b += lds_f[rows * C + r * C + c];
+    for (int r = 0; r < gm.rows; ++r) {
+      a += lds_f[r * gm.CB + i];
+      b += lds_f[gm.rows * gm.CB + r * gm.CB + i];
     }
-    atomicAdd(dst + c, a);
-    atomicAdd(dst + C + c, b);
+    atomicAdd(dst + gm.c0 + i, a);
+    atomicAdd(dst + C + gm.c0 + i, b);
   }
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
-    const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ dx, int lddx, int M, int C,
+    const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ dx, int lddx, int M, int C, int CVB,
     const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
     int R, float* dgamma, float* dbeta, int relu) {
-  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][C]: dbeta, dgamma
-  reduce_replicas(acc, R, C, sums);
+  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]: dbeta, dgamma
+  const GroupMap gm = groupmap(CVB);
+  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
   if (blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      dbeta[c] = sums[c];
-      dgamma[c] = sums[C + c];
+    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
+      dbeta[gm.c0 + i] = sums[i];
+      dgamma[gm.c0 + i] = sums[gm.CB + i];
     }
   }
-  RowMap rm = rowmap(C);
-  if (!rm.active) return;
+  if (gm.r0 >= gm.rows) return;
   float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
   const float invM = 1.f / (float)M;
+  const int cl = (threadIdx.x % CVB) * 8;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    int c = rm.cv * 8 + e;
+    int c = gm.cv * 8 + e;
     mu[e] = mean[c];
     is[e] = invstd[c];
     sc[e] = gamma[c] * is[e];
     sh[e] = beta[c] - mu[e] * sc[e];
-    k1[e] = sums[c] * invM;
-    k2[e] = sums[C + c] * invM;
+    k1[e] = sums[cl + e] * invM;
+    k2[e] = sums[gm.CB + cl + e] * invM;
   }
   BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
-             make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, rm.cv};
-  const int stride = gridDim.x * rm.rstep;
-  for (int m0 = blockIdx.x * rm.rstep + rm.r0; m0 < M; m0 += BN_U * stride) {
+             make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, gm.cv};
+  const int stride = gridDim.x * gm.rows;
+  for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
     u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
@@ -674,37 +707,57 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
       bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
-      if (m < M) *reinterpret_cast<u32x4*>(dx + (size_t)m * lddx + rm.cv * 8) = pack8(o);
+      if (m < M) *reinterpret_cast<u32x4*>(dx + (size_t)m * lddx + gm.cv * 8) = pack8(o);
     }
   }
+}
+
+// (row splits) x (channel groups); ~2048 blocks in total, each thread >= 1 row
+static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
+  const int CV = C / 8;
+  const int cvb = bn_group_vecs(CV);
+  const int groups = CV / cvb;
+  const int rows = 256 / cvb;
+  int need = (M + rows - 1) / rows;
+  int target = 2048 / groups;
+  if (target < 1) target = 1;
+  int s = need < target ? need : target;
+  if (s < 1) s = 1;
+  *cvb_out = cvb;
+  return dim3(s, groups);
 }
 
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
                          hipStream_t st) {
-  hipLaunchKernelGGL(bn_apply_acc_kernel, dim3(bn_grid(M, C)), dim3(256), (size_t)2 * C * 4, st,
-                     (const uint16_t*)x, ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, acc, R, eps,
-                     momentum, gamma, beta, relu, saved_mean, saved_invstd, run_mean, run_var);
+  int cvb;
+  dim3 grid = bn_grid_groups(M, C, &cvb);
+  hipLaunchKernelGGL(bn_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x, ldx,
+                     (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta,
+                     relu, saved_mean, saved_invstd, run_mean, run_var);
 }
 
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
                               int relu, float* acc, int R, void* gout, int ldg, hipStream_t st) {
-  int rows = 256 / (C / 8);
-  size_t lds = (size_t)2 * rows * C * 4;
-  hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel, dim3(bn_grid(M, C)), dim3(256), lds, st, (const uint16_t*)dy, lddy,
-                     (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, mean, invstd, gamma, beta, relu, acc,
-                     R, (uint16_t*)gout, ldg);
+  int cvb;
+  dim3 grid = bn_grid_groups(M, C, &cvb);
+  size_t lds = (size_t)2 * (256 / cvb) * cvb * 8 * 4;
+  hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
+                     (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu,
+                     acc, R, (uint16_t*)gout, ldg);
 }
 
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
                              hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_apply_acc_kernel, dim3(bn_grid(M, C)), dim3(256), (size_t)2 * C * 4, st,
-                     (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, (uint16_t*)dx,
-                     lddx, M, C, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu);
+  int cvb;
+  dim3 grid = bn_grid_groups(M, C, &cvb);
+  hipLaunchKernelGGL(bn_bwd_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)dy,
+                     lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, (uint16_t*)dx, lddx, M, C, cvb, mean,
+                     invstd, gamma, beta, acc, R, dgamma, dbeta, relu);
 }
 
 }  // namespace hcb

@@ -119,7 +119,7 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
 }
 
 // ============================================================== register-staged main loop
-template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL>
+template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
-  igemm_epilogue<WM, WN, TM, TN>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
+  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
 }
 
 // ============================================================== LDS-DMA multi-stage main loop
@@ -197,7 +197,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL>
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB>
 __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
@@ -269,11 +269,18 @@ __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
                                    acc, wm, wn, lane);
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
-  igemm_epilogue<WM, WN, TM, TN>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
+  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
 }
 
 // ============================================================== launch
-template <int WM, int WN, int TM, int TN>
+// One instantiation per (im2col path, lhs-dilation, fused BN-backward epilogue); the BNB
+// variants are separate kernels so the plain ones keep their register budget.
+template <typename K>
+static void set_lds_once(K kern) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+template <int WM, int WN, int TM, int TN, bool BNB>
 static void launch_reg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
@@ -284,27 +291,23 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, true, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, false, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<WM, WN, TM, TN, false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, false, BNB>);
+    set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, true, BNB>);
+    set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, false, BNB>);
+    set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, false>), dim3(tiles), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, false, BNB>), dim3(tiles), dim3(256), lds, st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, true>), dim3(tiles), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, true, BNB>), dim3(tiles), dim3(256), lds, st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, false>), dim3(tiles), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, false, BNB>), dim3(tiles), dim3(256), lds, st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true>), dim3(tiles), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>), dim3(tiles), dim3(256), lds, st, p);
 }
 
-template <int WM, int WN, int TM, int TN, int NST>
+template <int WM, int WN, int TM, int TN, int NST, bool BNB>
 static void launch_glds(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
@@ -315,25 +318,24 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false>), dim3(tiles), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>), dim3(tiles), dim3(256), lds,
+                       st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true>), dim3(tiles), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>), dim3(tiles), dim3(256), lds,
+                       st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false>), dim3(tiles), dim3(256), lds, st,
-                       p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>), dim3(tiles), dim3(256),
+                       lds, st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true>), dim3(tiles), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>), dim3(tiles), dim3(256), lds,
+                       st, p);
 }
 
 // cfg: 0..3 register-staged {128x128, 128x64, 64x64, 64x128}; 4..7 the same tiles on the
@@ -347,18 +349,26 @@ int conv_tile_n(int cfg) {
   return (cfg >= 0 && cfg < 8) ? t[cfg] : 128;
 }
 
-void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
+template <bool BNB>
+static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
   switch (cfg) {
-    case 0: launch_reg<2, 2, 64, 64>(p, st); break;    // 128 x 128
-    case 1: launch_reg<4, 1, 32, 64>(p, st); break;    // 128 x 64
-    case 2: launch_reg<2, 2, 32, 32>(p, st); break;    // 64 x 64
-    case 3: launch_reg<1, 4, 64, 32>(p, st); break;    // 64 x 128
-    case 4: launch_glds<2, 2, 64, 64, 3>(p, st); break;
-    case 5: launch_glds<4, 1, 32, 64, 3>(p, st); break;
-    case 6: launch_glds<2, 2, 32, 32, 4>(p, st); break;
-    case 7: launch_glds<1, 4, 64, 32, 3>(p, st); break;
-    default: launch_reg<2, 2, 64, 64>(p, st); break;
+    case 0: launch_reg<2, 2, 64, 64, BNB>(p, st); break;    // 128 x 128
+    case 1: launch_reg<4, 1, 32, 64, BNB>(p, st); break;    // 128 x 64
+    case 2: launch_reg<2, 2, 32, 32, BNB>(p, st); break;    // 64 x 64
+    case 3: launch_reg<1, 4, 64, 32, BNB>(p, st); break;    // 64 x 128
+    case 4: launch_glds<2, 2, 64, 64, 3, BNB>(p, st); break;
+    case 5: launch_glds<4, 1, 32, 64, 3, BNB>(p, st); break;
+    case 6: launch_glds<2, 2, 32, 32, 4, BNB>(p, st); break;
+    case 7: launch_glds<1, 4, 64, 32, 3, BNB>(p, st); break;
+    default: launch_reg<2, 2, 64, 64, BNB>(p, st); break;
   }
+}
+
+void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
+  if (p.bnb_acc != nullptr)
+    launch_cfg<true>(p, cfg, st);
+  else
+    launch_cfg<false>(p, cfg, st);
 }
 
 }  // namespace hcb

@@ -1,6 +1,12 @@
 // Shared epilogue of the implicit-GEMM conv kernels: fp32 accumulators -> (fused BN
 // statistics from registers) -> LDS staging (padded fp32 rows) -> coalesced 16-byte stores
-// with optional beta-accumulate, bias, fp32 output and strided-output pixel remap.
+// with optional beta-accumulate, bias, fp32 output, strided-output pixel remap, and the
+// fused BN-backward gating / reduction of a data-grad GEMM (ConvParams::bnb_*).
+//
+// The fused BN-backward variant (BNB, its own kernel instantiation so the plain kernels keep
+// their register budget) fetches z / y / the beta source of a chunk of up to 4 output
+// segments at once, the first chunk before the barrier, so the load latency is paid once per
+// chunk and overlaps the barrier instead of once per segment.
 #pragma once
 #include "common.h"
 #include "kernels.h"
@@ -12,12 +18,15 @@ constexpr size_t igemm_epilogue_lds(int BM, int BN, int WM) {
   return (size_t)BM * (BN + 4) * 4 + (size_t)WM * 2 * BN * 4;
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, bool BNB>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)[TM / 16][TN / 16], char* smem,
                                                int tm, int m0, int n0, int wm, int wn, int lane, int tid) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN + 4;
+  constexpr int SEGS = BN / 8;             // 16-byte output segments per tile row
+  constexpr int ITER = BM * SEGS / 256;    // segments per thread
+  static_assert(256 % SEGS == 0 && ITER >= 1, "a thread keeps one column segment across the store pass");
   const int frow = lane & 15, fq = lane >> 4;
   float* Cs = reinterpret_cast<float*>(smem);
   float* red = Cs + BM * LDC;  // [WM][2][BN] per-wave column partial sums
@@ -56,17 +65,49 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
         int col = wn * TN + j * 16 + frow;
         Cs[row * LDC + col] = acc[i][j][e];
       }
+
+  const int cs = tid % SEGS;
+  const int col = n0 + cs * 8;
+  const bool col_ok = col < p.Nout;
+  const int PQ = p.P * p.Q;
+  auto out_row = [&](int m) -> size_t {
+    if (!p.remap) return (size_t)m;
+    int n = m / PQ, r = m - n * PQ;
+    int pp = r / p.Q, qq = r - pp * p.Q;
+    return ((size_t)n * p.OH + (size_t)pp * p.osh) * p.OW + (size_t)qq * p.osw;
+  };
+  auto load_seg = [](const void* base, size_t row, int ld, int c) -> u32x4 {
+    return *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(base) + row * ld + c);
+  };
+
+  // fused BN-backward: prefetch z / y (and the beta source) of the first chunk of segments
+  // before the barrier; registers are sized for one chunk so the plain kernels are unaffected
+  constexpr int CH = BNB ? (ITER < 4 ? ITER : 4) : 1;
+  u32x4 pr[CH], pz[CH], py[CH];
+  auto prefetch = [&](int it0) {
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int m = m0 + (tid + (it0 + k) * 256) / SEGS;
+      if (col_ok && m < p.M) {
+        const size_t o = out_row(m);
+        if (p.beta) pr[k] = load_seg(p.yres, o, p.ldy, col);
+        pz[k] = load_seg(p.bnb_z, o, p.bnb_ld, col);
+        if (p.bnb_mode == 1) py[k] = load_seg(p.bnb_y, o, p.bnb_ld, col);
+      }
+    }
+  };
+  if constexpr (BNB) prefetch(0);
   __syncthreads();
 
   if (p.stats != nullptr) {
-    for (int col = tid; col < BN; col += 256) {
+    for (int c = tid; c < BN; c += 256) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
-        s1 += red[(w * 2) * BN + col];
-        s2 += red[(w * 2 + 1) * BN + col];
+        s1 += red[(w * 2) * BN + c];
+        s2 += red[(w * 2 + 1) * BN + c];
       }
-      int gc = n0 + col;
+      int gc = n0 + c;
       if (gc < p.Nout) {
         if (p.stats_R > 0) {  // atomics into replica tm % R of a [R][2][Nout] accumulator
           float* dst = p.stats + (size_t)(tm % p.stats_R) * 2 * p.Nout;
@@ -80,20 +121,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
     }
   }
 
-  const int PQ = p.P * p.Q;
-  constexpr int SEGS = BN / 8;
-  for (int sidx = tid; sidx < BM * SEGS; sidx += 256) {
-    int row = sidx / SEGS, cs = sidx - row * SEGS;
-    int m = m0 + row;
-    int col = n0 + cs * 8;
-    if (m >= p.M || col >= p.Nout) continue;
-    size_t orow = (size_t)m;
-    if (p.remap) {
-      int n = m / PQ, r = m - n * PQ;
-      int pp = r / p.Q, qq = r - pp * p.Q;
-      orow = ((size_t)n * p.OH + (size_t)pp * p.osh) * p.OW + (size_t)qq * p.osw;
-    }
-    float v[8];
+  auto stage_row = [&](int row, float* v) {
     const f32x4* src = reinterpret_cast<const f32x4*>(Cs + row * LDC + cs * 8);
     f32x4 v0 = src[0], v1 = src[1];
 #pragma unroll
@@ -101,33 +129,117 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       v[e] = v0[e];
       v[4 + e] = v1[e];
     }
-    if (p.bias != nullptr) {
+  };
+
+  if constexpr (!BNB) {
+    for (int it = 0; it < ITER; ++it) {
+      const int row = (tid + it * 256) / SEGS;
+      const int m = m0 + row;
+      if (!col_ok || m >= p.M) continue;
+      const size_t orow = out_row(m);
+      float v[8];
+      stage_row(row, v);
+      if (p.bias != nullptr) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += (col + e < p.Nout) ? p.bias[col + e] : 0.f;
-    }
-    if (p.relu) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    if (p.out_f32) {
-      float* yo = reinterpret_cast<float*>(p.y) + orow * p.ldy + col;
-      if (p.beta) {
-        const float* yi = reinterpret_cast<const float*>(p.yres) + orow * p.ldy + col;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += yi[e];
+        for (int e = 0; e < 8; ++e) v[e] += (col + e < p.Nout) ? p.bias[col + e] : 0.f;
       }
-      reinterpret_cast<f32x4*>(yo)[0] = f32x4{v[0], v[1], v[2], v[3]};
-      reinterpret_cast<f32x4*>(yo)[1] = f32x4{v[4], v[5], v[6], v[7]};
-    } else {
-      uint16_t* yo = reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col;
-      if (p.beta) {
-        const uint16_t* yi = reinterpret_cast<const uint16_t*>(p.yres) + orow * p.ldy + col;
-        float o[8];
-        unpack8(*reinterpret_cast<const u32x4*>(yi), o);
+      if (p.relu) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += o[e];
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       }
-      *reinterpret_cast<u32x4*>(yo) = pack8(v);
+      if (p.out_f32) {
+        float* yo = reinterpret_cast<float*>(p.y) + orow * p.ldy + col;
+        if (p.beta) {
+          const float* yi = reinterpret_cast<const float*>(p.yres) + orow * p.ldy + col;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += yi[e];
+        }
+        reinterpret_cast<f32x4*>(yo)[0] = f32x4{v[0], v[1], v[2], v[3]};
+        reinterpret_cast<f32x4*>(yo)[1] = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        uint16_t* yo = reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col;
+        if (p.beta) {
+          float o[8];
+          unpack8(load_seg(p.yres, orow, p.ldy, col), o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += o[e];
+        }
+        *reinterpret_cast<u32x4*>(yo) = pack8(v);
+      }
+    }
+  } else {
+    // bf16 output, no bias / relu (checked on the host)
+    float bmu[8], bis[8], bsc[8], bsh[8], bs1[8], bs2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool okc = col + e < p.Nout;
+      bmu[e] = okc ? p.bnb_mean[col + e] : 0.f;
+      bis[e] = okc ? p.bnb_invstd[col + e] : 0.f;
+      bsc[e] = okc ? p.bnb_gamma[col + e] * bis[e] : 0.f;
+      bsh[e] = okc ? p.bnb_beta[col + e] - bmu[e] * bsc[e] : 0.f;
+      bs1[e] = 0.f;
+      bs2[e] = 0.f;
+    }
+    for (int it0 = 0; it0 < ITER; it0 += CH) {
+      if (it0 > 0) prefetch(it0);
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int row = (tid + (it0 + k) * 256) / SEGS;
+        const int m = m0 + row;
+        if (!col_ok || m >= p.M) continue;
+        const size_t orow = out_row(m);
+        float v[8];
+        stage_row(row, v);
+        if (p.beta) {
+          float o[8];
+          unpack8(pr[k], o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += o[e];
+        }
+        float zf[8];
+        unpack8(pz[k], zf);
+        if (p.bnb_mode == 1) {
+          float yf[8];
+          unpack8(py[k], yf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = yf[e] > 0.f ? v[e] : 0.f;
+        } else if (p.bnb_mode == 2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (zf[e] * bsc[e] + bsh[e]) > 0.f ? v[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          bs1[e] += v[e];
+          bs2[e] += v[e] * ((zf[e] - bmu[e]) * bis[e]);
+        }
+        *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col) = pack8(v);
+      }
+    }
+    // threads sharing a column segment: LDS partials [256/SEGS][BN] (x2), column sums, atomics
+    constexpr int PR = 256 / SEGS;
+    static_assert(2 * PR * BN <= BM * LDC, "partials fit in the staging buffer");
+    float* part = Cs;
+    __syncthreads();  // all Cs reads of the store pass are done
+    const int r = tid / SEGS;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      part[r * BN + cs * 8 + e] = bs1[e];
+      part[PR * BN + r * BN + cs * 8 + e] = bs2[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float a = 0.f, b = 0.f;
+#pragma unroll 4
+      for (int rr = 0; rr < PR; ++rr) {
+        a += part[rr * BN + c];
+        b += part[PR * BN + rr * BN + c];
+      }
+      const int gc = n0 + c;
+      if (gc < p.Nout) {
+        float* dst = p.bnb_acc + (size_t)(tm % p.bnb_R) * 2 * p.Nout;
+        atomicAdd(dst + gc, a);
+        atomicAdd(dst + p.Nout + gc, b);
+      }
     }
   }
 }

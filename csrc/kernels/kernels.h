@@ -48,6 +48,16 @@ struct ConvParams {
   int relu;     // fused ReLU in the epilogue (affine layers without BN)
   int stats_R;  // 0: per-tile slab [tiles][2][Nout]; R>0: atomics into [R][2][Nout] replicas
   uint32_t x_bytes, w_bytes;
+  // Fused BN-backward reduction (a data-grad GEMM whose output is the dy of a BN layer):
+  // the epilogue gates its output with the layer's ReLU mask (bnb_mode 1: y > 0, 2: recomputed
+  // from z, 0: none), stores g instead of dy, and accumulates sum(g), sum(g * xhat) per
+  // channel into bnb_acc replicas [bnb_R][2][Nout]. z / y rows share the output's row index
+  // (after remap) with row stride bnb_ld.
+  const void* bnb_z;
+  const void* bnb_y;
+  const float *bnb_mean, *bnb_invstd, *bnb_gamma, *bnb_beta;
+  float* bnb_acc;
+  int bnb_mode, bnb_R, bnb_ld;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
 int conv_tile_m(int cfg);
@@ -102,7 +112,8 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
                           const float* invstd, const float* gamma, const float* beta,
                           const float* dgamma, const float* dbeta, int relu, hipStream_t st);
 
-// finalize-free variants: statistics accumulated in R replicas of [2][C] (fp32 atomics)
+// finalize-free variants: statistics accumulated in R replicas of [2][C] (fp32 atomics).
+// Blocks tile (row split) x (channel group) so each block only reduces its group's replicas.
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,

@@ -147,6 +147,54 @@ def test_conv_dgrad(case, accumulate):
     assert rel_err(dx, ref) < 1e-2
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[2], CONV_CASES[3], CONV_CASES[6]],
+                         ids=["1x1", "3x3", "1x1s2", "cin80"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("cfg", [2, 4])
+def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
+    """data-grad GEMM with the consuming BN layer's ReLU gating and backward sums fused into
+    its epilogue (ConvParams::bnb_*), vs the CPU gating + fp32 reductions."""
+    cin, cout, kh, kw, s, pads, H = case
+    torch.manual_seed(21)
+    spec, p, pk = make_conv(cin, cout, kh, kw, s, s, pads)
+    N = 2
+    P, Q = spec.out_hw(H, H)
+    dz = bf(torch.randn(N, P, Q, cout, device=DEV))
+    base = bf(torch.randn(N, H, H, cin, device=DEV))
+    z = bf(torch.randn(N, H, H, cin, device=DEV) * 1.5 + 0.2)
+    yact = bf(torch.relu(torch.randn(N, H, H, cin, device=DEV)))
+    mean = torch.randn(cin, device=DEV) * 0.1 + 0.2
+    invstd = torch.rand(cin, device=DEV) + 0.5
+    gamma = torch.rand(cin, device=DEV) + 0.5
+    beta = torch.randn(cin, device=DEV) * 0.2
+    saved = Fn.BNSaved(mean, invstd)
+    R = 8
+    acc = torch.zeros(R * 2 * cin, device=DEV)
+    strided_1x1 = s > 1 and kh == 1 and kw == 1
+    if strided_1x1:
+        # precondition of a fused strided-1x1 (remap) dgrad: the pixels it does not visit are 0
+        keep = torch.zeros(1, H, H, 1, dtype=torch.bool, device=DEV)
+        keep[:, ::s, ::s] = True
+        base = base * keep
+    dx = base.clone() if accumulate else (torch.zeros_like(base) if strided_1x1 else torch.empty_like(base))
+    bnb = Fn.BNBwdFuse(z, yact, saved, gamma, beta, mode, acc, R)
+    Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate, cfg=cfg, bnb=bnb)
+    ref = torch.empty(N, H, H, cin)
+    Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), ref, False)
+    if accumulate:
+        ref = ref + base.float().cpu()
+    zc = z.float().cpu()
+    cpu_bnb = Fn.BNBwdFuse(zc, yact.float().cpu(), Fn.BNSaved(mean.cpu(), invstd.cpu()), gamma.cpu(), beta.cpu(),
+                           mode, None, R)
+    g = cpu_bnb.gate_cpu(ref.clone())
+    assert rel_err(dx, g) < 1e-2
+    xhat = (zc - mean.cpu()) * invstd.cpu()
+    sums = acc.view(R, 2, cin).sum(0).cpu()
+    assert rel_err(sums[0], g.reshape(-1, cin).sum(0)) < 2e-2
+    assert rel_err(sums[1], (g * xhat).reshape(-1, cin).sum(0)) < 2e-2
+
+
 @pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}{c[3]}s{c[4]}")
 def test_conv_wgrad(case):
     cin, cout, kh, kw, s, pads, H = case
@@ -305,7 +353,7 @@ def test_synthetic_data_stats():
     assert lab.min().item() >= 0 and lab.max().item() < 1000 and lab.unique().numel() > 900
 
 
-@pytest.mark.parametrize("C", [64, 256, 2048])
+@pytest.mark.parametrize("C", [64, 256, 2048, 80, 48])
 @pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
 def test_bn_finalize_free_path(C, relu, residual):
     """conv-epilogue atomics -> bn_apply_acc (stats finalized in-kernel) and the bwd reduce /
@@ -343,6 +391,8 @@ def test_bn_finalize_free_path(C, relu, residual):
     acc_b = torch.zeros(R * 2 * C, device=DEV)
     Fn.bn_backward_acc(dy, y, z, saved, gamma, beta, mode, dg, db, dz, acc_b, R, gres)
     dzc, gresc, dgc, dbc = torch.empty(N, H, H, C), torch.empty(N, H, H, C), torch.empty(C), torch.empty(C)
-    Fn.bn_backward(dy.float().cpu(), y.float().cpu(), zc, sc, gamma.cpu(), beta.cpu(), mode, dgc, dbc, dzc, gresc)
+    # the reference uses the kernel's own batch moments so both sides gate with the same ReLU mask
+    gsv = Fn.BNSaved(saved.mean.cpu(), saved.invstd.cpu())
+    Fn.bn_backward(dy.float().cpu(), y.float().cpu(), zc, gsv, gamma.cpu(), beta.cpu(), mode, dgc, dbc, dzc, gresc)
     assert rel_err(db, dbc) < 2e-2 and rel_err(dg, dgc) < 2e-2
     assert rel_err(dz, dzc) < 3e-2 and rel_err(gres, gresc) < 1e-2

@@ -9,8 +9,14 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
   [ $rc -le 1 ] || exit $rc
 fi
-timeout -k 10 600 python tools/conv_bench.py --model resnet50 --batch 64 --tune --json gpurun_out/conv_bench.json > gpurun_out/conv_bench.log 2>&1 || { echo conv_bench failed; tail -20 gpurun_out/conv_bench.log; exit 1; }
-tail -1 gpurun_out/conv_bench.log
+if [ "${CONV_BENCH:-1}" = "1" ]; then
+  timeout -k 10 600 python tools/conv_bench.py --model resnet50 --batch 64 --tune --json gpurun_out/conv_bench.json > gpurun_out/conv_bench.log 2>&1 || { echo conv_bench failed; tail -20 gpurun_out/conv_bench.log; exit 1; }
+  tail -1 gpurun_out/conv_bench.log
+fi
+if [ -n "${AB_ENV:-}" ]; then  # A/B: the same bench with an env toggle (e.g. AB_ENV=HCB_FUSE_BN_BWD=0)
+  env $AB_ENV timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_ab.log 2>&1 || { echo "bench A/B failed"; tail -40 gpurun_out/bench_ab.log; exit 1; }
+  echo "A/B ($AB_ENV):"; tail -1 gpurun_out/bench_ab.log
+fi
 timeout -k 10 400 python bench.py --steps 30 --warmup 5 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -40 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
 cp azure_hc_intel_tf_amd/tuned/mi355x.json gpurun_out/tuned_mi355x.json 2>/dev/null
