@@ -56,7 +56,7 @@ def save_cache(path: str = DEFAULT_CACHE) -> None:
         json.dump({"arch": "gfx950", "entries": old}, f, indent=0, sort_keys=True)
 
 
-def _time(fn, reps=3) -> float:
+def _time(fn, reps=5) -> float:
     fn()
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
@@ -80,10 +80,16 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     P, Q, Cout = layer.out_shape
     N = batch
     out = []
+    M = N * P * Q
+    geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
+    keys = [Fn.fwd_key(M, Cout, spec.K), Fn.wgrad_key(Cout, spec.K, M)]
+    if layer.need_dx:
+        keys.append(Fn.fwd_key(geo[0], Cin, geo[1]))
+    if all(k in Fn._tuned for k in keys):
+        return out
     x = _bf((N, H, W, Cin), dev)
     dz = _bf((N, P, Q, Cout), dev)
     # forward
-    M = N * P * Q
     k = Fn.fwd_key(M, Cout, spec.K)
     if k not in Fn._tuned:
         y = torch.empty((N, P, Q, Cout), dtype=torch.bfloat16, device=dev)
@@ -98,7 +104,6 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     # data gradient
     if layer.need_dx:
         dx = torch.zeros((N, H, W, Cin), dtype=torch.bfloat16, device=dev)
-        geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
         k = Fn.fwd_key(geo[0], Cin, geo[1])
         if k not in Fn._tuned:
             best = None

@@ -89,7 +89,8 @@ def same_pads(size: int, k: int, s: int, d: int = 1):
 # ----------------------------------------------------------------- tile selection
 # cfg -> block tile; 0-3 register-staged main loop, 4-7 LDS-DMA ring (same tiles)
 _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
-               4: (128, 128), 5: (128, 64), 6: (64, 64), 7: (64, 128)}
+               4: (128, 128), 5: (128, 64), 6: (64, 64), 7: (64, 128),
+               8: (128, 128), 9: (128, 128), 10: (128, 64), 11: (64, 128)}
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64)}
 N_CU = 256
 _tuned: dict = {}
@@ -104,7 +105,7 @@ def wgrad_key(Nout: int, K: int, M: int):
 
 
 def fwd_candidates(N: int):
-    return [0, 3, 1, 2, 4, 7, 5, 6] if N > 64 else [1, 2, 5, 6]
+    return [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11] if N > 64 else [1, 2, 5, 6, 10]
 
 
 def wgrad_candidates(Nout: int, K: int, M: int):

@@ -37,13 +37,24 @@
 
 namespace hcb {
 
-// ---- per-thread implicit-im2col address generation, shared by both main loops
+// ---- per-thread implicit-im2col address generation, shared by both main loops.
+// k-steps are issued strictly in order (kt = 0, 1, 2, ...), so the loader keeps the current
+// filter tap / channel offset as wave-uniform state and advances it without divisions. In
+// the CBIG path (C % 64 == 0: a 64-deep k-step never straddles a tap) the per-row work is
+// two adds, two unsigned compares and a select; invalid rows carry h0 = INT_MIN/2 so the
+// bounds test rejects them without a separate flag.
 template <int AV, bool CBIG, bool LHSDIL>
 struct ALoader {
-  int pix[AV], h0[AV], w0[AV];
+  int h0[AV], w0[AV];
+  int rowoff[AV];  // byte offset of (pixel of tap (0,0)) * ldx + lane chunk, may be negative
+  int pix[AV];     // generic path: first pixel of the image, -1 = row beyond M
+  int tr, ts, tc;  // CBIG: current tap (r, s) and channel offset
 
-  __device__ __forceinline__ void init(const ConvParams& p, int m0, int tid) {
+  __device__ __forceinline__ void init(const ConvParams& p, int m0, int tid, int chunk) {
     const int PQ = p.P * p.Q;
+    tr = 0;
+    ts = 0;
+    tc = 0;
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       int m = m0 + (tid >> 3) + 32 * v;
@@ -53,39 +64,62 @@ struct ALoader {
         pix[v] = n * p.H * p.W;
         h0[v] = pp * p.stride_h - p.pad_h;
         w0[v] = qq * p.stride_w - p.pad_w;
+        rowoff[v] = ((pix[v] + h0[v] * p.W + w0[v]) * p.ldx + chunk * 8) * 2;
       } else {
         pix[v] = -1;
-        h0[v] = 0;
+        h0[v] = -0x40000000;
         w0[v] = 0;
+        rowoff[v] = 0;
       }
     }
   }
-  // byte offset of the 16-byte vector (row v, k-chunk `chunk`) of k-step kt
-  __device__ __forceinline__ void offsets(const ConvParams& p, int kt, int chunk, uint32_t (&off)[AV]) const {
-    const int k0 = kt * 64;
-    int tap, c;
-    if constexpr (CBIG) {
-      tap = k0 / p.C;
-      c = k0 - tap * p.C + chunk * 8;
-    } else {
-      int k = k0 + chunk * 8;
-      tap = k / p.C;
-      c = k - tap * p.C;
-    }
-    const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
-    const bool tap_ok = tap < p.R * p.S;
+  // byte offsets of this thread's 16-byte vectors (row v, k-chunk `chunk`) of k-step kt
+  __device__ __forceinline__ void offsets(const ConvParams& p, int kt, int chunk, uint32_t (&off)[AV]) {
+    if constexpr (CBIG && !LHSDIL) {
+      const int dh = tr * p.dil_h, dw = ts * p.dil_w;
+      const int uoff = ((dh * p.W + dw) * p.ldx + tc) * 2;
+      const bool tap_ok = tr < p.R;
 #pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      int h = h0[v] + r * p.dil_h;
-      int w = w0[v] + s * p.dil_w;
-      bool ok = tap_ok && pix[v] >= 0 && h >= 0 && w >= 0;
-      if constexpr (LHSDIL) {
-        ok = ok && (h % p.idil_h == 0) && (w % p.idil_w == 0);
-        h /= p.idil_h;
-        w /= p.idil_w;
+      for (int v = 0; v < AV; ++v) {
+        const int h = h0[v] + dh, w = w0[v] + dw;
+        const bool ok = tap_ok && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+        off[v] = ok ? (uint32_t)(rowoff[v] + uoff) : HCB_OOB;
       }
-      ok = ok && h < p.H && w < p.W;
-      off[v] = ok ? (uint32_t)((pix[v] + h * p.W + w) * p.ldx + c) * 2u : HCB_OOB;
+      // advance to the next 64-channel slab
+      tc += 64;
+      if (tc >= p.C) {
+        tc = 0;
+        if (++ts == p.S) {
+          ts = 0;
+          ++tr;
+        }
+      }
+    } else {
+      const int k0 = kt * 64;
+      int tap, c;
+      if constexpr (CBIG) {
+        tap = k0 / p.C;
+        c = k0 - tap * p.C + chunk * 8;
+      } else {
+        int k = k0 + chunk * 8;
+        tap = k / p.C;
+        c = k - tap * p.C;
+      }
+      const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+      const bool tap_ok = tap < p.R * p.S;
+#pragma unroll
+      for (int v = 0; v < AV; ++v) {
+        int h = h0[v] + r * p.dil_h;
+        int w = w0[v] + s * p.dil_w;
+        bool ok = tap_ok && pix[v] >= 0 && h >= 0 && w >= 0;
+        if constexpr (LHSDIL) {
+          ok = ok && (h % p.idil_h == 0) && (w % p.idil_w == 0);
+          h /= p.idil_h;
+          w /= p.idil_w;
+        }
+        ok = ok && h < p.H && w < p.W;
+        off[v] = ok ? (uint32_t)((pix[v] + h * p.W + w) * p.ldx + c) * 2u : HCB_OOB;
+      }
     }
   }
 };
@@ -140,7 +174,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   ALoader<AV, CBIG, LHSDIL> al;
-  al.init(p, m0, tid);
+  al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
 #pragma unroll
   for (int v = 0; v < BV; ++v) {
@@ -204,7 +238,7 @@ __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
   constexpr int AV = BM / 32, BV = BN / 32;
   constexpr int LOADS = AV + BV;  // LDS-DMA instructions per thread per stage
   constexpr int STAGE = (BM + BN) * 128;
-  static_assert(WM * WN == 4 && NST >= 2 && NST <= 4, "config");
+  static_assert(WM * WN == 4 && NST >= 2 && NST <= 6, "config");
   static_assert(LOADS * (NST - 2) <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -222,7 +256,7 @@ __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   ALoader<AV, CBIG, LHSDIL> al;
-  al.init(p, m0, tid);
+  al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
 #pragma unroll
   for (int v = 0; v < BV; ++v) {
@@ -255,8 +289,12 @@ __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
     // stage kt has landed for this thread once at most min(NST-2, nk-1-kt) later stages
     // are still outstanding; the barrier then publishes every thread's DMA.
     const int ahead = min(NST - 2, nk - 1 - kt);
-    if (ahead >= 2)
-      wait_vmcnt<2 * LOADS>();
+    if (ahead >= 4)
+      wait_vmcnt<(NST >= 6 ? 4 : 0) * LOADS>();
+    else if (ahead == 3)
+      wait_vmcnt<(NST >= 5 ? 3 : 0) * LOADS>();
+    else if (ahead == 2)
+      wait_vmcnt<(NST >= 4 ? 2 : 0) * LOADS>();
     else if (ahead == 1)
       wait_vmcnt<LOADS>();
     else
@@ -339,14 +377,16 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
 }
 
 // cfg: 0..3 register-staged {128x128, 128x64, 64x64, 64x128}; 4..7 the same tiles on the
-// LDS-DMA ring (NST 3, 3, 4, 3)
+// LDS-DMA ring (NST 3, 3, 4, 3); 8..11 deeper rings for latency-bound few-tile layers
+// (128x128 NST 4 and 5, 128x64 NST 6, 64x128 NST 6)
+constexpr int N_CONV_CFG = 12;
 int conv_tile_m(int cfg) {
-  static const int t[8] = {128, 128, 64, 64, 128, 128, 64, 64};
-  return (cfg >= 0 && cfg < 8) ? t[cfg] : 128;
+  static const int t[N_CONV_CFG] = {128, 128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64};
+  return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
-  static const int t[8] = {128, 64, 64, 128, 128, 64, 64, 128};
-  return (cfg >= 0 && cfg < 8) ? t[cfg] : 128;
+  static const int t[N_CONV_CFG] = {128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64, 128};
+  return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 
 template <bool BNB>
@@ -360,6 +400,10 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
     case 5: launch_glds<4, 1, 32, 64, 3, BNB>(p, st); break;
     case 6: launch_glds<2, 2, 32, 32, 4, BNB>(p, st); break;
     case 7: launch_glds<1, 4, 64, 32, 3, BNB>(p, st); break;
+    case 8: launch_glds<2, 2, 64, 64, 4, BNB>(p, st); break;
+    case 9: launch_glds<2, 2, 64, 64, 5, BNB>(p, st); break;
+    case 10: launch_glds<4, 1, 32, 64, 6, BNB>(p, st); break;
+    case 11: launch_glds<1, 4, 64, 32, 6, BNB>(p, st); break;
     default: launch_reg<2, 2, 64, 64, BNB>(p, st); break;
   }
 }

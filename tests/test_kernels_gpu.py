@@ -90,7 +90,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
     dz = bf(torch.randn(N, P, Q, cout, device=DEV))
     dref = torch.empty(N, H, H, cpad)
     Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), dref, False)
-    for cfg in (4, 5, 6, 7):
+    for cfg in (4, 5, 6, 7, 8, 9, 10, 11):
         y = torch.empty(N, P, Q, cout, dtype=torch.bfloat16, device=DEV)
         slab = torch.empty(math.ceil(N * P * Q / Fn._CONV_TILES[cfg][0]) * 2 * cout, device=DEV)
         Fn.conv_forward(x, spec, pk.pack, p.data, y, stats=slab, cfg=cfg)
@@ -101,7 +101,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
             assert rel_err(dx, dref) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("cfg", list(range(12)))
 def test_conv_fwd_all_tile_configs(cfg):
     torch.manual_seed(1)
     spec, p, pk = make_conv(128, 192, 3, 3, 1, 1, (1, 1, 1, 1))
