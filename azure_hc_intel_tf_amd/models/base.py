@@ -46,6 +46,13 @@ class CNNModel:
     def backward(self, dlogits: torch.Tensor) -> None:
         raise NotImplementedError
 
+    def backward_segments(self, dlogits: torch.Tensor):
+        """Backward in segments, for overlapping the gradient allreduce with the rest of the
+        backward pass: yields ``(layers, last)`` after each segment, where every parameter
+        gradient of ``layers`` is final. Default: one segment (the whole backward)."""
+        self.backward(dlogits)
+        yield None, True  # None: every gradient
+
     # -- helpers
     @property
     def act_dtype(self):
@@ -67,6 +74,17 @@ class CNNModel:
 
     def all_layers(self):
         return list(self.layers)
+
+    def grad_ranges(self, layers):
+        """Merged (offset, length) ranges of the flat gradient buffer owned by ``layers``."""
+        spans = sorted((p.offset, p.numel) for l in layers for p in getattr(l, "params", lambda: [])())
+        out = []
+        for off, n in spans:
+            if out and out[-1][0] + out[-1][1] == off:
+                out[-1] = (out[-1][0], out[-1][1] + n)
+            else:
+                out.append((off, n))
+        return out
 
     def clear(self):
         for l in self.all_layers():

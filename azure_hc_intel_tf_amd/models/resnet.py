@@ -85,6 +85,7 @@ class ResNet(CNNModel):
             for bi in range(n):
                 stride = 2 if (si > 0 and bi == 0) else 1
                 blk = Bottleneck(ps, f"stage{si + 1}/block{bi + 1}", shape, depth, bott, stride, v15)
+                blk.stage = si
                 self.blocks.append(blk)
                 shape = blk.out_shape
         self.gap = GlobalAvgPool("spatial_mean", shape)
@@ -101,10 +102,22 @@ class ResNet(CNNModel):
         return self.fc.forward(feat)
 
     def backward(self, dlogits):
+        for _ in self.backward_segments(dlogits):
+            pass
+
+    def backward_segments(self, dlogits):
+        """One segment per stage, last stage first (its ~60 % of the parameters are reduced
+        while stages 3..1 are still in backward)."""
         dfeat = self.fc.backward(dlogits)
         dx = self.gap.backward(dfeat)
+        seg = [self.fc, self.gap]
         for i in range(len(self.blocks) - 1, -1, -1):
             dx = self.blocks[i].backward(dx, self.blocks[i - 1].c3 if i > 0 else None)
+            seg += self.blocks[i].layers()
+            if i > 0 and self.blocks[i].stage != self.blocks[i - 1].stage:
+                yield seg, False
+                seg = []
         dx = self.pool.backward(dx)
         self.stem.backward(dx)
         self._last = None
+        yield seg + [self.pool, self.stem], True

@@ -134,6 +134,15 @@ class ConvBN(Layer):
         P, Q, C = self.out_shape
         return 2 * batch * P * Q * C * self.spec.kh * self.spec.kw * self.spec.cin
 
+    def params(self):
+        """Trainable ParamRefs of this layer (gradient slots in the flat buffer)."""
+        if not self.bn:
+            return [self.w, self.bias]
+        out = [self.w, self.beta]
+        if not isinstance(self.gamma, _FixedParam):
+            out.append(self.gamma)
+        return out
+
     # ------------------------------------------------------------------ forward
     def forward(self, x, out=None, residual=None):
         N = x.shape[0]
@@ -332,7 +341,7 @@ class Logits(Layer):
             C = self.ld
             geom = [B, 1, 1, C, C, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, self.cin, C, self.pack.Kpad_t, self.cin,
                     0, 1, 1, 1, 1, 0, 0]
-            cfgd = Fn.conv_cfg(B, self.cin, C)
+            cfgd = Fn.conv_plan(B, self.cin, C)[0]
             hcb.conv_igemm(dlogits, self.pack.tr, dx, None, None, None, geom, cfgd)
         else:
             g = dlogits[:, :self.ncls]
@@ -343,3 +352,6 @@ class Logits(Layer):
 
     def flops(self, batch):
         return 2 * batch * self.cin * self.ncls
+
+    def params(self):
+        return [self.w, self.b]

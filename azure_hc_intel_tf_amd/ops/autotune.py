@@ -21,6 +21,8 @@ from . import functional as Fn
 
 _DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned")
 DEFAULT_CACHE = os.path.join(_DIR, "mi355x.json")
+# bump whenever the kernel config set changes: entries of another version are re-tuned
+CACHE_VERSION = 4
 
 
 def _key_str(k) -> str:
@@ -37,6 +39,8 @@ def load_cache(path: str = DEFAULT_CACHE) -> int:
         return 0
     with open(path) as f:
         d = json.load(f)
+    if d.get("version") != CACHE_VERSION:
+        return 0
     table = {}
     for k, v in d.get("entries", {}).items():
         table[_key_parse(k)] = tuple(v) if isinstance(v, list) else v
@@ -49,11 +53,13 @@ def save_cache(path: str = DEFAULT_CACHE) -> None:
     old = {}
     if os.path.exists(path):
         with open(path) as f:
-            old = json.load(f).get("entries", {})
+            d = json.load(f)
+        if d.get("version") == CACHE_VERSION:
+            old = d.get("entries", {})
     for k, v in Fn._tuned.items():
         old[_key_str(k)] = list(v) if isinstance(v, tuple) else v
     with open(path, "w") as f:
-        json.dump({"arch": "gfx950", "entries": old}, f, indent=0, sort_keys=True)
+        json.dump({"arch": "gfx950", "version": CACHE_VERSION, "entries": old}, f, indent=0, sort_keys=True)
 
 
 def _time(fn, reps=5) -> float:
@@ -96,9 +102,12 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
         best = None
         acc = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
         for cfg in Fn.fwd_candidates(Cout):
-            t = _time(lambda: Fn.conv_forward(x, spec, layer.pack.pack, None, y, stats=acc, cfg=cfg, stats_R=8))
-            if best is None or t < best[0]:
-                best = (t, cfg)
+            for sp in Fn.splitk_candidates(cfg, M, Cout, spec.K):
+                plan = cfg if sp == 1 else [cfg, sp]
+                t = _time(lambda: Fn.conv_forward(x, spec, layer.pack.pack, None, y, stats=acc, cfg=plan,
+                                                  stats_R=8))
+                if best is None or t < best[0]:
+                    best = (t, plan)
         Fn._tuned[k] = best[1]
         out.append((k, best))
     # data gradient
@@ -108,9 +117,11 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
         if k not in Fn._tuned:
             best = None
             for cfg in Fn.fwd_candidates(Cin):
-                t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=cfg))
-                if best is None or t < best[0]:
-                    best = (t, cfg)
+                for sp in Fn.splitk_candidates(cfg, geo[0], Cin, geo[1]):
+                    plan = cfg if sp == 1 else [cfg, sp]
+                    t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=plan))
+                    if best is None or t < best[0]:
+                        best = (t, plan)
             Fn._tuned[k] = best[1]
             out.append((k, best))
     # weight gradient

@@ -90,7 +90,8 @@ def same_pads(size: int, k: int, s: int, d: int = 1):
 # cfg -> block tile; 0-3 register-staged main loop, 4-7 LDS-DMA ring (same tiles)
 _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                4: (128, 128), 5: (128, 64), 6: (64, 64), 7: (64, 128),
-               8: (128, 128), 9: (128, 128), 10: (128, 64), 11: (64, 128)}
+               8: (128, 128), 9: (128, 128), 10: (128, 64), 11: (64, 128),
+               12: (128, 128), 13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (64, 128)}
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64)}
 N_CU = 256
 _tuned: dict = {}
@@ -105,7 +106,10 @@ def wgrad_key(Nout: int, K: int, M: int):
 
 
 def fwd_candidates(N: int):
-    return [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11] if N > 64 else [1, 2, 5, 6, 10]
+    if N <= 64:
+        return [1, 2, 5, 6, 10]
+    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16]
+    return c + [15] if N > 128 else c
 
 
 def wgrad_candidates(Nout: int, K: int, M: int):
@@ -122,9 +126,47 @@ def wgrad_candidates(Nout: int, K: int, M: int):
     return out
 
 
-def conv_cfg(M: int, N: int, K: int) -> int:
-    """Block tile for C[M,N] (+K): the autotuned choice if known, else the biggest tile that
-    still gives >= 2 workgroups per CU."""
+# split-K scratch (fp32 partial-tile slabs + self-resetting per-tile tickets), one per process
+SPLITK_WS_FLOATS = 32 << 20
+SPLITK_MAX_TILES = 1 << 16
+_splitk = {}
+
+
+def ensure_splitk_workspace(device) -> None:
+    dev = torch.device(device)
+    if _splitk.get("dev") == dev:
+        return
+    ws = torch.empty(SPLITK_WS_FLOATS, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(SPLITK_MAX_TILES, dtype=torch.int32, device=dev)
+    _ext.ops().set_splitk_workspace(ws, cnt)
+    _splitk.update(dev=dev, ws=ws, cnt=cnt)
+
+
+def splitk_candidates(cfg: int, M: int, N: int, K: int):
+    """split-K factors worth timing for an LDS-DMA config: only while the grid is below ~2
+    workgroups per CU and every split keeps >= 4 k-steps."""
+    if cfg < 4:
+        return [1]
+    bm, bn = _CONV_TILES[cfg]
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    ksteps = math.ceil(K / 64)
+    out = [1]
+    for s in (2, 3, 4, 6, 8):
+        if tiles * (s - 1) >= 2 * N_CU or ksteps // s < 4 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
+            break
+        out.append(s)
+    return out
+
+
+def conv_plan(M: int, N: int, K: int):
+    """(cfg, splits) for C[M,N] (+K)."""
+    c = conv_cfg(M, N, K)
+    return (c[0], c[1]) if isinstance(c, (tuple, list)) else (c, 1)
+
+
+def conv_cfg(M: int, N: int, K: int):
+    """Block tile for C[M,N] (+K): the autotuned choice if known (an int cfg or a [cfg, splits]
+    pair), else the biggest tile that still gives >= 2 workgroups per CU."""
     key = fwd_key(M, N, K)
     if key in _tuned:
         return _tuned[key]
@@ -172,12 +214,11 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
     P, Q = spec.out_hw(H, W)
     if x.is_cuda:
         M = N * P * Q
-        if cfg is None:
-            cfg = conv_cfg(M, spec.cout, spec.K)
+        cfg, splits = _plan(cfg, M, spec.cout, spec.K, x.device)
         out_f32 = out.dtype == torch.float32
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
                 spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1, 0,
-                1 if out_f32 else 0, 1 if relu else 0, int(stats_R)]
+                1 if out_f32 else 0, 1 if relu else 0, int(stats_R), splits]
         _ext.ops().conv_igemm(x, wpack, out, None, bias, stats, geom, cfg)
         return out
     xt = x.permute(0, 3, 1, 2)
@@ -189,6 +230,19 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
         y = torch.relu(y)
     out.copy_(y.permute(0, 2, 3, 1))
     return out
+
+
+def _plan(cfg, M, N, K, device):
+    """Normalise a cfg argument (None = tuned / heuristic, int, or (cfg, splits))."""
+    if cfg is None:
+        cfg, splits = conv_plan(M, N, K)
+    elif isinstance(cfg, (tuple, list)):
+        cfg, splits = cfg
+    else:
+        splits = 1
+    if splits > 1:
+        ensure_splitk_workspace(device)
+    return int(cfg), int(splits)
 
 
 def relu_backward(dy, y, dz):
@@ -204,7 +258,7 @@ def conv_stats_slab(x_shape, spec: ConvSpec, device, cfg=None):
     P, Q = spec.out_hw(H, W)
     M = N * P * Q
     if cfg is None:
-        cfg = conv_cfg(M, spec.cout, spec.K)
+        cfg = conv_plan(M, spec.cout, spec.K)[0]
     bm = _CONV_TILES[cfg][0]
     T = math.ceil(M / bm)
     return torch.empty(T * 2 * spec.cout, dtype=torch.float32, device=device), T, cfg
@@ -255,8 +309,8 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
             geom = [N, P, Q, Cdz, ld(dz), H, W, spec.kh, spec.kw, 1, 1, pt, pl, spec.dh, spec.dw,
                     spec.sh, spec.sw, spec.cin_pad, K, Kpad, ld(dx), 0, H, W, 1, 1,
                     1 if accumulate else 0, 0]
-        if cfg is None:
-            cfg = conv_cfg(M, spec.cin_pad, K)
+        cfg, splits = _plan(cfg, M, spec.cin_pad, K, dz.device)
+        geom = geom + [0, 0, splits]
         if bnb is not None:
             _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
                                       bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,

@@ -95,6 +95,13 @@ class Communicator:
         self._cc.bucket_allreduce_(self.h, flat, buckets, compress, scale, average)
         return flat
 
+    def bucket_allreduce_async_(self, flat, buckets, compress=0, scale=1.0, average=False):
+        self._cc.bucket_allreduce_async_(self.h, flat, buckets, compress, scale, average)
+        return flat
+
+    def join_(self):
+        self._cc.join_(self.h)
+
     def barrier(self):
         self._cc.barrier(self.h)
 
@@ -137,6 +144,16 @@ class NativeReducer:
             return flat
         self.comm.bucket_allreduce_(flat, self._bucket_table(flat.numel()), self.compress, 1.0, self.average)
         return flat
+
+    # -- overlap interface: reduce finished gradient ranges while backward continues
+    def allreduce_ranges_async_(self, flat, ranges):
+        if self.comm.world == 1 and not self.compress:
+            return
+        table = torch.tensor([list(r) for r in ranges], dtype=torch.int64).view(-1, 2)
+        self.comm.bucket_allreduce_async_(flat, table, self.compress, 1.0, self.average)
+
+    def join(self):
+        self.comm.join_()
 
     def broadcast_(self, t, root=0):
         if self.comm.world > 1:

@@ -78,6 +78,32 @@ class TorchDistReducer:
             flat.mul_(1.0 / world)
         return flat
 
+    # -- overlap interface (trainer: reduce finished gradient ranges while backward continues)
+    def allreduce_ranges_async_(self, flat: torch.Tensor, ranges) -> None:
+        if dist.get_world_size(self.group) == 1:
+            return
+        pend = getattr(self, "_pending", None)
+        if pend is None:
+            pend = self._pending = []
+        if self.compression and (self._comm_buf is None or self._comm_buf.numel() != flat.numel()):
+            dt = torch.float16 if self.compression == "fp16" else torch.bfloat16
+            self._comm_buf = torch.empty(flat.numel(), dtype=dt, device=flat.device)
+        for off, n in ranges:
+            view = flat[off:off + n]
+            if self.compression:
+                cb = self._comm_buf[off:off + n]
+                cb.copy_(view)
+                pend.append((view, cb, dist.all_reduce(cb, group=self.group, async_op=True)))
+            else:
+                pend.append((view, None, dist.all_reduce(view, group=self.group, async_op=True)))
+
+    def join(self) -> None:
+        for view, cb, work in getattr(self, "_pending", None) or []:
+            work.wait()
+            if cb is not None:
+                view.copy_(cb)
+        self._pending = []
+
     def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
         if dist.get_world_size(self.group) > 1:
             dist.broadcast(t, src=root, group=self.group)

@@ -12,13 +12,17 @@ run-tf-sing-ucx-openmpi.sh:62-81):
 
 On the GPU the whole sequence (≈500-1000 kernels for ResNet-50) is captured once in a HIP
 graph (torch.cuda.CUDAGraph == hipGraph on ROCm) and replayed every step, so Python and
-launch overhead vanish. With more than one worker the gradient allreduce runs between two
-graphs, (a) fwd+bwd and (b) optimizer, on the communication engine (see
-``parallel/``), so collectives never need to be captured.
+launch overhead vanish. With more than one worker the step is captured as one graph per
+backward SEGMENT (``model.backward_segments``: one per ResNet stage, last stage first) plus
+an optimizer graph; after each segment's replay the gradient ranges it finished are handed
+to the communication engine (``parallel/``) asynchronously on its own stream, so the
+allreduce of stage 4's gradients overlaps the backward of stages 3..1 and only the last
+segment's (small) reduction is exposed. Collectives are never captured.
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Optional
 
 import torch
@@ -81,10 +85,16 @@ class Trainer:
         self._g_fb = None
         self._g_opt = None
         self._g_all = None
+        self._segs = None
+        self._seg_ranges = {}
         self._static = None
+        # overlap the allreduce with backward (segmented graphs + async reducer)
+        self.overlap = (reducer is not None and world_size > 1 and not forward_only
+                        and hasattr(reducer, "allreduce_ranges_async_")
+                        and os.environ.get("HCB_OVERLAP", "1") != "0")
 
     # ---------------------------------------------------------------- pieces
-    def _forward_backward(self, images, labels):
+    def _forward(self, images, labels):
         ps = self.ps
         if not self.forward_only:
             ps.zero_grad()
@@ -92,10 +102,19 @@ class Trainer:
         ps.repack()
         logits = self.model.forward(images)
         Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B)
+
+    def _forward_backward(self, images, labels):
+        self._forward(images, labels)
         if self.forward_only:
             self.model.clear()
             return
         self.model.backward(self.dlogits)
+
+    def _ranges(self, i, layers):
+        if i not in self._seg_ranges:
+            self._seg_ranges[i] = ([(0, self.ps.grad.numel())] if layers is None
+                                   else self.model.grad_ranges(layers))
+        return self._seg_ranges[i]
 
     def _optimizer(self):
         if self.forward_only:
@@ -111,6 +130,13 @@ class Trainer:
             self.reducer.allreduce_(self.ps.grad)
 
     def _eager_step(self, images, labels):
+        if self.overlap:
+            self._forward(images, labels)
+            for i, (layers, _) in enumerate(self.model.backward_segments(self.dlogits)):
+                self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
+            self.reducer.join()
+            self._optimizer()
+            return
         self._forward_backward(images, labels)
         self._reduce()
         self._optimizer()
@@ -120,7 +146,27 @@ class Trainer:
         torch.cuda.synchronize()
         single = self.reducer is None or self.world <= 1 or getattr(self.reducer, "graph_safe", False)
         pool = torch.cuda.graph_pool_handle()
-        if single:
+        if self.overlap:
+            # one graph per backward segment (the first also holds the forward), replayed in
+            # capture order (they share one memory pool)
+            segs = []
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self._forward(images, labels)
+                gen = self.model.backward_segments(self.dlogits)
+                layers, last = next(gen)
+            segs.append((g, self._ranges(0, layers)))
+            while not last:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    layers, last = next(gen)
+                segs.append((g, self._ranges(len(segs), layers)))
+            gen.close()
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=pool):
+                self._optimizer()
+            self._segs, self._g_opt = segs, g2
+        elif single:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 self._forward_backward(images, labels)
@@ -147,7 +193,7 @@ class Trainer:
         else:
             if self._static is not None and (images is not self._static[0] or labels is not self._static[1]):
                 raise ValueError("graph-captured trainer needs the same (static) input buffers every step")
-            if self._g_all is None and self._g_fb is None:
+            if self._g_all is None and self._g_fb is None and self._segs is None:
                 if self.steps_done < self.graph_warmup:
                     self._eager_step(images, labels)
                     self.steps_done += 1
@@ -155,6 +201,12 @@ class Trainer:
                 self._capture(images, labels)
             if self._g_all is not None:
                 self._g_all.replay()
+            elif self._segs is not None:
+                for g, rng in self._segs:
+                    g.replay()
+                    self.reducer.allreduce_ranges_async_(self.ps.grad, rng)
+                self.reducer.join()
+                self._g_opt.replay()
             else:
                 self._g_fb.replay()
                 self._reduce()

@@ -19,6 +19,12 @@ namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// raw pointers (the Python side owns and keeps the tensors alive; no static Tensor dtor at exit)
+float* g_splitk_ws = nullptr;
+int64_t g_splitk_ws_bytes = 0;
+unsigned* g_splitk_cnt = nullptr;
+int64_t g_splitk_cnt_n = 0;
+
 void check_cuda(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), "hcb: ", name, " must be a GPU tensor");
 }
@@ -47,7 +53,7 @@ void check_align16(const void* p, const char* name) {
 hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                             const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
                             at::IntArrayRef g, int64_t cfg) {
-  TORCH_CHECK(g.size() >= 28 && g.size() <= 30, "hcb.conv_igemm: geom must have 28 (+relu, +stats_R) entries");
+  TORCH_CHECK(g.size() >= 28 && g.size() <= 31, "hcb.conv_igemm: geom must have 28 (+relu, +stats_R, +splits) entries");
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_cuda(y, "y");
@@ -61,6 +67,7 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   p.beta = g[26]; p.out_f32 = g[27];
   p.relu = g.size() > 28 ? (int)g[28] : 0;
   p.stats_R = g.size() > 29 ? (int)g[29] : 0;
+  p.splits = g.size() > 30 ? (int)g[30] : 1;
   p.M = p.N * p.P * p.Q;
   TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0 && p.ldx >= p.C, "hcb.conv_igemm: C, ldx must be multiples of 8");
   TORCH_CHECK(p.Kpad % 64 == 0 && p.Kpad >= p.K && p.K == p.R * p.S * p.C,
@@ -108,7 +115,30 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   }
   p.x_bytes = (uint32_t)xb;
   p.w_bytes = (uint32_t)wb;
+  TORCH_CHECK(p.splits >= 1 && p.splits <= p.Kpad / 64, "hcb.conv_igemm: 1 <= splits <= k-steps");
+  if (p.splits > 1) {
+    TORCH_CHECK(cfg >= 4, "hcb.conv_igemm: split-K needs an LDS-DMA config (cfg >= 4)");
+    TORCH_CHECK(g_splitk_ws != nullptr && g_splitk_cnt != nullptr, "hcb.conv_igemm: split-K workspace not set");
+    const int bm = hcb::conv_tile_m((int)cfg), bn = hcb::conv_tile_n((int)cfg);
+    const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * ((p.Nout + bn - 1) / bn);
+    TORCH_CHECK(tiles * p.splits * bm * bn * 4 <= g_splitk_ws_bytes, "hcb.conv_igemm: split-K workspace too small");
+    TORCH_CHECK(tiles <= g_splitk_cnt_n, "hcb.conv_igemm: split-K counter array too small");
+    p.ws = g_splitk_ws;
+    p.cnt = g_splitk_cnt;
+  }
   return p;
+}
+
+// split-K scratch shared by every conv launch of the process (one compute stream): fp32 slabs
+// and zero-initialised per-tile tickets that the kernels leave zeroed
+void set_splitk_workspace(const Tensor& ws, const Tensor& cnt) {
+  check_f32(ws, "ws");
+  check_cuda(cnt, "cnt");
+  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.is_contiguous() && ws.is_contiguous(), "hcb: bad split-K workspace");
+  g_splitk_ws = ws.data_ptr<float>();
+  g_splitk_ws_bytes = ws.numel() * 4;
+  g_splitk_cnt = reinterpret_cast<unsigned*>(cnt.data_ptr<int>());
+  g_splitk_cnt_n = cnt.numel();
 }
 
 void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
@@ -580,6 +610,7 @@ TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg) -> ()");
   m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
+  m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
   m.def("bn_stats(Tensor x, int M, int C, int ldx, Tensor(a!) slab) -> ()");
   m.def("bn_partials(int M, int C) -> int", bn_partials);
@@ -613,6 +644,7 @@ TORCH_LIBRARY(hcb, m) {
 TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("conv_igemm", conv_igemm);
   m.impl("conv_igemm_bnb", conv_igemm_bnb);
+  m.impl("set_splitk_workspace", set_splitk_workspace);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("bn_stats", bn_stats);
   m.impl("bn_finalize", bn_finalize);

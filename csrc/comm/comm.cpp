@@ -350,8 +350,8 @@ void reduce_scatter_(int64_t h, const Tensor& in, const Tensor& out, bool averag
 // buckets: int64 CPU tensor [nb][2] of (offset, length) in elements, issued in order.
 // compress: 0 none, 1 bf16, 2 fp16 (fp16 goes through an fp32->fp16 cast kernel pair)
 // scale: multiplied in during pack (e.g. 1/world for averaging when compressing).
-void bucket_allreduce_(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale,
-                       bool average) {
+void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale, bool average,
+                 bool do_join) {
   Comm* c = get(h);
   TORCH_CHECK(c->comm, "hcb_comm: communicator aborted");
   TORCH_CHECK(flat.is_cuda() && flat.is_contiguous() && flat.scalar_type() == at::kFloat,
@@ -400,7 +400,7 @@ void bucket_allreduce_(int64_t h, const Tensor& flat, const Tensor& buckets, int
     }
   }
   HCB_HIP(hipEventRecord(c->join_ev, c->stream));
-  HCB_HIP(hipStreamWaitEvent(cur, c->join_ev, 0));
+  if (do_join) HCB_HIP(hipStreamWaitEvent(cur, c->join_ev, 0));
   if (!cap) {
     std::lock_guard<std::mutex> lk(c->mu);
     c->watch_ev = c->join_ev;
@@ -409,6 +409,25 @@ void bucket_allreduce_(int64_t h, const Tensor& flat, const Tensor& buckets, int
     c->watch_cycle = c->cycle;
   }
   c->cycle++;
+}
+
+void bucket_allreduce_(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale,
+                       bool average) {
+  bucket_impl(h, flat, buckets, compress, scale, average, true);
+}
+
+// Overlap form: the comm stream waits for the caller's stream (everything enqueued so far,
+// e.g. a replayed backward segment) but the caller does NOT wait for the reduction; call
+// join_() before consuming the reduced buffer. Successive async calls queue in order on the
+// comm stream, so one join covers them all.
+void bucket_allreduce_async_(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale,
+                             bool average) {
+  bucket_impl(h, flat, buckets, compress, scale, average, false);
+}
+
+void join_(int64_t h) {
+  Comm* c = get(h);
+  HCB_HIP(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), c->join_ev, 0));
 }
 
 void barrier(int64_t h) {
@@ -447,6 +466,9 @@ TORCH_LIBRARY(hcb_comm, m) {
   m.def("reduce_scatter_(int h, Tensor input, Tensor(a!) output, bool average) -> ()", reduce_scatter_);
   m.def("bucket_allreduce_(int h, Tensor(a!) flat, Tensor buckets, int compress, float scale, bool average) -> ()",
         bucket_allreduce_);
+  m.def("bucket_allreduce_async_(int h, Tensor(a!) flat, Tensor buckets, int compress, float scale, bool average) -> ()",
+        bucket_allreduce_async_);
+  m.def("join_(int h) -> ()", join_);
   m.def("barrier(int h) -> ()", barrier);
   m.def("rank(int h) -> int", comm_rank);
   m.def("size(int h) -> int", comm_size);

@@ -43,7 +43,7 @@ namespace hcb {
 // the CBIG path (C % 64 == 0: a 64-deep k-step never straddles a tap) the per-row work is
 // two adds, two unsigned compares and a select; invalid rows carry h0 = INT_MIN/2 so the
 // bounds test rejects them without a separate flag.
-template <int AV, bool CBIG, bool LHSDIL>
+template <int AV, bool CBIG, bool LHSDIL, int RP = 32>  // RP: rows covered per load pass (threads / 8)
 struct ALoader {
   int h0[AV], w0[AV];
   int rowoff[AV];  // byte offset of (pixel of tap (0,0)) * ldx + lane chunk, may be negative
@@ -57,7 +57,7 @@ struct ALoader {
     tc = 0;
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
-      int m = m0 + (tid >> 3) + 32 * v;
+      int m = m0 + (tid >> 3) + RP * v;
       if (m < p.M) {
         int n = m / PQ, r = m - n * PQ;
         int pp = r / p.Q, qq = r - pp * p.Q;
@@ -72,6 +72,14 @@ struct ALoader {
         rowoff[v] = 0;
       }
     }
+  }
+  // position the incremental tap state at k-step kt0 (a split-K block's first k-step)
+  __device__ __forceinline__ void seek(const ConvParams& p, int kt0) {
+    const int k0 = kt0 * 64;
+    const int tap = k0 / p.C;
+    tc = k0 - tap * p.C;
+    tr = tap / p.S;
+    ts = tap - tr * p.S;
   }
   // byte offsets of this thread's 16-byte vectors (row v, k-chunk `chunk`) of k-step kt
   __device__ __forceinline__ void offsets(const ConvParams& p, int kt, int chunk, uint32_t (&off)[AV]) {
@@ -232,13 +240,15 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB>
-__global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
+__global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
-  constexpr int AV = BM / 32, BV = BN / 32;
+  constexpr int NT = WM * WN * 64, RP = NT / 8;  // threads; tile rows per load pass
+  constexpr int AV = BM / RP, BV = BN / RP;
   constexpr int LOADS = AV + BV;  // LDS-DMA instructions per thread per stage
   constexpr int STAGE = (BM + BN) * 128;
-  static_assert(WM * WN == 4 && NST >= 2 && NST <= 6, "config");
+  static_assert((WM * WN == 4 || WM * WN == 8) && NST >= 2 && NST <= 6, "config");
+  static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 2) <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -246,21 +256,24 @@ __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
   const int wid = wave_id_uniform();
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_n = (p.Nout + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // a tile's splits are neighbours: same XCD
+  const int S = p.splits;
+  const int tile = bid / S, split = bid - tile * S;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  // lane-linear LDS image: lane -> (row = (tid>>3)+32v, position tid&7); the lane fetches the
-  // GLOBAL chunk that the swizzled read expects at that position (involution).
+  // lane-linear LDS image: lane -> (row = (tid>>3)+RP*v, position tid&7); the lane fetches the
+  // GLOBAL chunk that the swizzled read expects at that position (involution; RP*v and the
+  // wave's 8-row base are multiples of 16, so (row>>1)&7 == (tid>>4)&7).
   const int chunk = (tid & 7) ^ ((tid >> 4) & 7);
 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
-  ALoader<AV, CBIG, LHSDIL> al;
+  ALoader<AV, CBIG, LHSDIL, RP> al;
   al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
 #pragma unroll
   for (int v = 0; v < BV; ++v) {
-    int j = n0 + (tid >> 3) + 32 * v;
+    int j = n0 + (tid >> 3) + RP * v;
     b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
   }
   f32x4 acc[MI][NI];
@@ -274,17 +287,19 @@ __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
     al.offsets(p, kt, chunk, off);
     char* sbase = smem + stage * STAGE;
 #pragma unroll
-    for (int v = 0; v < AV; ++v) glds16(xr, sbase + (wid * 8 + 32 * v) * 128, off[v]);
+    for (int v = 0; v < AV; ++v) glds16(xr, sbase + (wid * 8 + RP * v) * 128, off[v]);
 #pragma unroll
     for (int v = 0; v < BV; ++v)
-      glds16(wr, sbase + BM * 128 + (wid * 8 + 32 * v) * 128,
+      glds16(wr, sbase + BM * 128 + (wid * 8 + RP * v) * 128,
              b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
   };
 
-  const int nk = p.Kpad / BK;
+  const int nk_all = p.Kpad / BK;
+  const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's k-steps
+  if (kb > 0) al.seek(p, kb);
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
-    if (s < nk) issue(s, s);
+    if (s < nk) issue(s, kb + s);
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for this thread once at most min(NST-2, nk-1-kt) later stages
     // are still outstanding; the barrier then publishes every thread's DMA.
@@ -301,12 +316,48 @@ __global__ __launch_bounds__(256) void conv_igemm_glds_kernel(ConvParams p) {
       wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, kt + NST - 1);
+    if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, kb + kt + NST - 1);
     const char* sb = smem + (kt % NST) * STAGE;
     mfma_tile_step<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + BM * 128),
                                    acc, wm, wn, lane);
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
+  if (S > 1) {
+    // split-K hand-off (cdna guide Guideline 16, counter form): park the partial tile, publish
+    // it with one agent-scope release + ticket; the last arriver acquires and sums the others.
+    constexpr int FR = MI * NI;  // f32x4 fragments per thread
+    f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)tile * S * FR * NT;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) slab[((size_t)split * FR + i * NI + j) * NT + tid] = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned t = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == (unsigned)(S - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    const int last = *flag;
+    __syncthreads();  // the flag word is epilogue staging space next
+    if (!last) return;
+    for (int s2 = 0; s2 < S; ++s2) {
+      if (s2 == split) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] += slab[((size_t)s2 * FR + i * NI + j) * NT + tid];
+    }
+  }
   igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
 }
 
@@ -347,8 +398,8 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
 
 template <int WM, int WN, int TM, int TN, int NST, bool BNB>
 static void launch_glds(const ConvParams& p, hipStream_t st) {
-  constexpr int BM = WM * TM, BN = WN * TN;
-  int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
+  constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
+  int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
   size_t lds_main = (size_t)NST * (BM + BN) * 128;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
@@ -363,29 +414,31 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>), dim3(tiles), dim3(256), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>), dim3(tiles), dim3(256), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>), dim3(tiles), dim3(256),
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>), dim3(tiles), dim3(NT),
                        lds, st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>), dim3(tiles), dim3(256), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>), dim3(tiles), dim3(NT), lds,
                        st, p);
 }
 
 // cfg: 0..3 register-staged {128x128, 128x64, 64x64, 64x128}; 4..7 the same tiles on the
 // LDS-DMA ring (NST 3, 3, 4, 3); 8..11 deeper rings for latency-bound few-tile layers
-// (128x128 NST 4 and 5, 128x64 NST 6, 64x128 NST 6)
-constexpr int N_CONV_CFG = 12;
+// (128x128 NST 4 and 5, 128x64 NST 6, 64x128 NST 6); 12..16 eight-wave workgroups (two
+// waves per SIMD when a layer has only ~1 tile per CU): 128x128 as 2x4 waves of 64x32 and as
+// 4x2 of 32x64, 256x128 (4x2 of 64x64), 128x256 (2x4 of 64x64), 64x128 (2x4 of 32x32)
+constexpr int N_CONV_CFG = 17;
 int conv_tile_m(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64};
+  static const int t[N_CONV_CFG] = {128, 128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64, 128, 128, 256, 128, 64};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64, 128};
+  static const int t[N_CONV_CFG] = {128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64, 128, 128, 128, 128, 256, 128};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 
@@ -404,6 +457,11 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
     case 9: launch_glds<2, 2, 64, 64, 5, BNB>(p, st); break;
     case 10: launch_glds<4, 1, 32, 64, 6, BNB>(p, st); break;
     case 11: launch_glds<1, 4, 64, 32, 6, BNB>(p, st); break;
+    case 12: launch_glds<2, 4, 64, 32, 3, BNB>(p, st); break;
+    case 13: launch_glds<4, 2, 32, 64, 3, BNB>(p, st); break;
+    case 14: launch_glds<4, 2, 64, 64, 3, BNB>(p, st); break;
+    case 15: launch_glds<2, 4, 64, 64, 3, BNB>(p, st); break;
+    case 16: launch_glds<2, 4, 32, 32, 4, BNB>(p, st); break;
     default: launch_reg<2, 2, 64, 64, BNB>(p, st); break;
   }
 }

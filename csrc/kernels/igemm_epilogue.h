@@ -25,8 +25,9 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN + 4;
   constexpr int SEGS = BN / 8;             // 16-byte output segments per tile row
-  constexpr int ITER = BM * SEGS / 256;    // segments per thread
-  static_assert(256 % SEGS == 0 && ITER >= 1, "a thread keeps one column segment across the store pass");
+  constexpr int NT = WM * WN * 64;         // threads of the workgroup
+  constexpr int ITER = BM * SEGS / NT;     // segments per thread
+  static_assert(NT % SEGS == 0 && ITER >= 1, "a thread keeps one column segment across the store pass");
   const int frow = lane & 15, fq = lane >> 4;
   float* Cs = reinterpret_cast<float*>(smem);
   float* red = Cs + BM * LDC;  // [WM][2][BN] per-wave column partial sums
@@ -87,7 +88,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   auto prefetch = [&](int it0) {
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
-      const int m = m0 + (tid + (it0 + k) * 256) / SEGS;
+      const int m = m0 + (tid + (it0 + k) * NT) / SEGS;
       if (col_ok && m < p.M) {
         const size_t o = out_row(m);
         if (p.beta) pr[k] = load_seg(p.yres, o, p.ldy, col);
@@ -100,7 +101,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   __syncthreads();
 
   if (p.stats != nullptr) {
-    for (int c = tid; c < BN; c += 256) {
+    for (int c = tid; c < BN; c += NT) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
@@ -133,7 +134,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
 
   if constexpr (!BNB) {
     for (int it = 0; it < ITER; ++it) {
-      const int row = (tid + it * 256) / SEGS;
+      const int row = (tid + it * NT) / SEGS;
       const int m = m0 + row;
       if (!col_ok || m >= p.M) continue;
       const size_t orow = out_row(m);
@@ -184,7 +185,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       if (it0 > 0) prefetch(it0);
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
-        const int row = (tid + (it0 + k) * 256) / SEGS;
+        const int row = (tid + (it0 + k) * NT) / SEGS;
         const int m = m0 + row;
         if (!col_ok || m >= p.M) continue;
         const size_t orow = out_row(m);
@@ -215,8 +216,8 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
         *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col) = pack8(v);
       }
     }
-    // threads sharing a column segment: LDS partials [256/SEGS][BN] (x2), column sums, atomics
-    constexpr int PR = 256 / SEGS;
+    // threads sharing a column segment: LDS partials [NT/SEGS][BN] (x2), column sums, atomics
+    constexpr int PR = NT / SEGS;
     static_assert(2 * PR * BN <= BM * LDC, "partials fit in the staging buffer");
     float* part = Cs;
     __syncthreads();  // all Cs reads of the store pass are done
@@ -227,7 +228,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       part[PR * BN + r * BN + cs * 8 + e] = bs2[e];
     }
     __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
+    for (int c = tid; c < BN; c += NT) {
       float a = 0.f, b = 0.f;
 #pragma unroll 4
       for (int rr = 0; rr < PR; ++rr) {

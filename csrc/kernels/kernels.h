@@ -58,6 +58,13 @@ struct ConvParams {
   const float *bnb_mean, *bnb_invstd, *bnb_gamma, *bnb_beta;
   float* bnb_acc;
   int bnb_mode, bnb_R, bnb_ld;
+  // In-launch split-K (LDS-DMA kernels): `splits` blocks per output tile each reduce a
+  // contiguous k-step range; all but the last arriver park fp32 partials in ws slabs
+  // [tile][split][tile elems], the last one (agent-scope ticket in cnt[tile], self-resetting)
+  // sums them and runs the epilogue.
+  int splits;
+  float* ws;
+  unsigned* cnt;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
 int conv_tile_m(int cfg);

@@ -40,3 +40,21 @@ def test_native_comm_one_rank(tmp_path, monkeypatch):
     torch.cuda.synchronize()
     assert torch.allclose(g, g0.bfloat16().float())
     r.close()
+
+
+def test_native_async_range_allreduce_overlap_one_rank():
+    """the overlap interface: async range reductions forked off the compute stream, one join"""
+    from azure_hc_intel_tf_amd.parallel.native import NativeReducer
+
+    r = NativeReducer(compression="bf16")
+    g = torch.randn(500_000, device="cuda")
+    g0 = g.clone()
+    r.allreduce_ranges_async_(g, [(300_000, 200_000)])
+    g[:1000].mul_(2.0)  # compute-stream work between the two hand-offs
+    r.allreduce_ranges_async_(g, [(0, 100_000), (100_000, 200_000)])
+    r.join()
+    torch.cuda.synchronize()
+    ref = g0.clone()
+    ref[:1000] *= 2.0
+    assert torch.allclose(g, ref.bfloat16().float())
+    r.close()

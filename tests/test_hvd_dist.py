@@ -119,3 +119,47 @@ def test_make_buckets_cover_buffer_in_reverse():
 
     b = make_buckets(1000, 256)
     assert b[0] == (744, 256) and sum(n for _, n in b) == 1000 and b[-1][0] == 0
+
+
+def _overlap_matches_serial(hvd):
+    """segmented backward + async range allreduce == one allreduce after the whole backward"""
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.parallel import make_reducer
+    from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+    masters = []
+    for overlap in (True, False):
+        m = create_model("resnet50", image_size=32, device="cpu", seed=7 + hvd.rank())
+        hvd.broadcast_global_variables(m, 0)
+        img, lab = synthetic_batch(m, 2, seed=hvd.rank())
+        img = (img - 127) / 60
+        t = Trainer(m, 2, constant_lr(0.05), reducer=make_reducer("torch", bucket_bytes=1 << 20),
+                    world_size=hvd.size())
+        t.overlap = overlap
+        for _ in range(2):
+            t.step(img, lab)
+        masters.append(m.ps.master.clone())
+    assert torch.allclose(masters[0], masters[1], rtol=1e-5, atol=1e-6)
+
+
+def test_overlapped_allreduce_matches_serial():
+    run(2, _overlap_matches_serial)
+
+
+def test_backward_segments_cover_every_gradient_once():
+    from azure_hc_intel_tf_amd.models import create_model
+
+    for name in ("resnet50", "resnet50_v1.5"):
+        m = create_model(name, image_size=32, device="cpu")
+        # the segment ranges only depend on which layers each segment lists
+        layers_all = []
+        for blk in reversed(m.blocks):
+            layers_all.append(blk.layers())
+        cover = torch.zeros(m.ps.grad.numel(), dtype=torch.int32)
+        ranges = m.grad_ranges([l for ls in layers_all for l in ls] + [m.fc, m.stem])
+        for off, n in ranges:
+            cover[off:off + n] += 1
+        # every parameter exactly once (the buffer may carry alignment padding between tensors)
+        assert int(cover.max()) == 1 and int(cover.sum()) == sum(p.numel for l in m.all_layers()
+                                                                  for p in getattr(l, "params", lambda: [])()), name
+        assert int(cover.sum()) >= m.num_params() - 64, name

@@ -90,7 +90,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
     dz = bf(torch.randn(N, P, Q, cout, device=DEV))
     dref = torch.empty(N, H, H, cpad)
     Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), dref, False)
-    for cfg in (4, 5, 6, 7, 8, 9, 10, 11):
+    for cfg in range(4, 17):
         y = torch.empty(N, P, Q, cout, dtype=torch.bfloat16, device=DEV)
         slab = torch.empty(math.ceil(N * P * Q / Fn._CONV_TILES[cfg][0]) * 2 * cout, device=DEV)
         Fn.conv_forward(x, spec, pk.pack, p.data, y, stats=slab, cfg=cfg)
@@ -101,7 +101,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
             assert rel_err(dx, dref) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("cfg", list(range(12)))
+@pytest.mark.parametrize("cfg", list(range(17)))
 def test_conv_fwd_all_tile_configs(cfg):
     torch.manual_seed(1)
     spec, p, pk = make_conv(128, 192, 3, 3, 1, 1, (1, 1, 1, 1))
@@ -109,6 +109,32 @@ def test_conv_fwd_all_tile_configs(cfg):
     y = torch.empty(2, 13, 13, 192, dtype=torch.bfloat16, device=DEV)
     Fn.conv_forward(x, spec, pk.pack, p.data, y, cfg=cfg)
     assert rel_err(y, cpu_ref_conv(x, spec, bf(p.data))) < 1e-2
+
+
+@pytest.mark.parametrize("plan", [(4, 2), (4, 3), (12, 2), (13, 4), (14, 2), (16, 3), (6, 5)])
+def test_conv_split_k_in_launch_reduction(plan):
+    """split-K: partial tiles parked in the workspace, the last arriver (agent-scope ticket)
+    sums them and runs the normal epilogue (BN statistics, beta-accumulate, BN-bwd fusion)."""
+    torch.manual_seed(7)
+    spec, p, pk = make_conv(128, 256, 3, 3, 1, 1, (1, 1, 1, 1))
+    N, H = 4, 14
+    x = bf(torch.randn(N, H, H, 128, device=DEV))
+    y = torch.empty(N, H, H, 256, dtype=torch.bfloat16, device=DEV)
+    acc = torch.zeros(8 * 2 * 256, device=DEV)
+    for rep in range(2):  # second pass checks that the tickets were left re-armed
+        acc.zero_()
+        Fn.conv_forward(x, spec, pk.pack, p.data, y, stats=acc, stats_R=8, cfg=plan)
+        ref = cpu_ref_conv(x, spec, bf(p.data))
+        assert rel_err(y, ref) < 1e-2, rep
+        assert rel_err(acc.view(8, 2, 256).sum(0)[0], ref.reshape(-1, 256).sum(0)) < 2e-2
+    dz = bf(torch.randn(N, H, H, 256, device=DEV))
+    base = bf(torch.randn(N, H, H, 128, device=DEV))
+    dx = base.clone()
+    Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, True, cfg=plan)
+    dref = torch.empty(N, H, H, 128)
+    Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), dref, False)
+    assert rel_err(dx, dref + base.float().cpu()) < 1e-2
+    assert int(Fn._splitk["cnt"].abs().sum().item()) == 0
 
 
 def test_conv_fwd_channel_slice_views():
@@ -151,7 +177,7 @@ def test_conv_dgrad(case, accumulate):
                          ids=["1x1", "3x3", "1x1s2", "cin80"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [2, 4])
+@pytest.mark.parametrize("cfg", [2, 4, 12])
 def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
     """data-grad GEMM with the consuming BN layer's ReLU gating and backward sums fused into
     its epilogue (ConvParams::bnb_*), vs the CPU gating + fp32 reductions."""
