@@ -123,9 +123,25 @@ def build_comm(verbose: bool = False, jobs: int = 8) -> str:
     return COMM_SO
 
 
+RCCL_BENCH = os.path.join(REPO, "tools", "rccl_bench", "rccl_allreduce_bench")
+
+
+def build_tools(verbose: bool = False) -> str:
+    """tools/rccl_bench: the OSU-style RCCL collective benchmark (standalone executable)."""
+    src = RCCL_BENCH + ".hip"
+    if not os.path.exists(src):
+        return ""
+    if _newer(RCCL_BENCH, [src]):
+        _run([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O2", "-std=c++17", src, "-o",
+              RCCL_BENCH, "-L" + os.path.join(ROCM, "lib"), "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib")],
+             verbose)
+    return RCCL_BENCH
+
+
 def build_all(verbose: bool = False) -> None:
     build_kernels(verbose)
     build_comm(verbose)
+    build_tools(verbose)
 
 
 if __name__ == "__main__":

@@ -132,7 +132,13 @@ class BenchmarkCNN:
         self.trainer = Trainer(self.model, self.batch_size, self._lr_fn(), momentum=mom,
                                weight_decay=p.weight_decay, reducer=reducer, world_size=self.size,
                                use_graph=bool(p.use_hip_graph) and self.on_gpu and p.horovod_device != "cpu",
-                               forward_only=bool(p.forward_only))
+                               forward_only=bool(p.forward_only),
+                               # --use_fp16: the GPU's 16-bit compute type is bf16 (same MFMA rate
+                               # as fp16, fp32 exponent range); the loss-scaling semantics of the
+                               # reference flags are kept (static scale or automatic scaling)
+                               loss_scale=p.fp16_loss_scale if p.use_fp16 else None,
+                               dynamic_loss_scale=bool(p.use_fp16 and p.fp16_enable_auto_loss_scale),
+                               loss_scale_interval=p.fp16_inc_loss_scale_every_n)
         if p.horovod_device == "cpu" and self.size > 1 and self.on_gpu:
             self.trainer.reducer = _HostStagedReducer(reducer)
 

@@ -66,6 +66,8 @@ FLAGS: List[Flag] = [
     Flag("num_gpus", 1, int, "GPUs per process (horovod: 1)"),
     Flag("use_fp16", False, parse_bool, "fp16 compute (bf16 is the default GPU compute type)"),
     Flag("fp16_loss_scale", 128.0, float, "static loss scale for --use_fp16"),
+    Flag("fp16_enable_auto_loss_scale", False, parse_bool, "dynamic loss scaling for --use_fp16"),
+    Flag("fp16_inc_loss_scale_every_n", 1000, int, "double the auto loss scale after N clean steps"),
     Flag("init_learning_rate", None, float, "constant learning rate (overrides the model schedule)"),
     Flag("momentum", 0.9, float, "momentum for --optimizer=momentum"),
     Flag("weight_decay", 0.00004, float, "L2 weight decay (coupled, tf_cnn_benchmarks semantics)"),

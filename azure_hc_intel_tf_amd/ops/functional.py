@@ -547,12 +547,15 @@ def gap_backward(dy, dx):
 
 
 # ------------------------------------------------------------------------- loss
-def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale):
-    """Per-row cross entropy (into row_loss) and dlogits = (softmax - onehot) * scale."""
+def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None):
+    """Per-row cross entropy (into row_loss) and dlogits = (softmax - onehot) * scale
+    (* scale_dev[0], a device-resident loss scale, when given)."""
     B = labels.numel()
     if logits.is_cuda:
-        _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale)
+        _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale, scale_dev)
         return
+    if scale_dev is not None:
+        scale = scale * float(scale_dev.reshape(-1)[0])
     lg = logits[:, :ncls].float()
     lse = torch.logsumexp(lg, dim=1)
     row_loss.copy_(lse - lg.gather(1, labels.view(-1, 1)).view(-1))
@@ -571,12 +574,46 @@ def colsum(g, M, N, out):
 
 
 # -------------------------------------------------------------------- optimizer
+def nonfinite(g, flag):
+    """flag[0] = 1 if g holds an Inf/NaN (flag must be zeroed by the caller)."""
+    if g.is_cuda:
+        _ext.ops().nonfinite(g, flag)
+        return
+    if not bool(torch.isfinite(g).all()):
+        flag.view(-1)[0] = 1.0
+
+
+def loss_scale_update(hyper, world: int, dynamic: bool):
+    """hyper = [lr, mu, wd, grad_scale, found_inf, loss_scale, good_steps, interval]: dynamic
+    loss-scale step (halve on overflow, double after `interval` clean steps), then
+    grad_scale = 1 / (world * loss_scale)."""
+    if hyper.is_cuda:
+        _ext.ops().loss_scale_update(hyper, float(world), bool(dynamic))
+        return
+    h = hyper
+    S = float(h[5])
+    if dynamic:
+        if float(h[4]) != 0.0:
+            S = max(S * 0.5, 1.0)
+            h[6] = 0.0
+        else:
+            h[6] += 1.0
+            if float(h[6]) >= float(h[7]):
+                S *= 2.0
+                h[6] = 0.0
+        h[5] = S
+    h[3] = 1.0 / (world * S)
+
+
 def sgd_momentum(w, mom, g, n_decay, hyper, l2=None, nesterov=False):
-    """TF ApplyMomentum on the flat parameter buffer: hyper = [lr, momentum, wd, grad_scale]."""
+    """TF ApplyMomentum on the flat parameter buffer: hyper = [lr, momentum, wd, grad_scale
+    (, found_inf, ...)]; a set found_inf skips the update (loss scaling)."""
     if w.is_cuda:
         _ext.ops().sgd_momentum(w, mom, g, n_decay, hyper, l2, nesterov)
         return
-    lr, mu, wd, gs = [float(v) for v in hyper.tolist()]
+    if hyper.numel() > 4 and float(hyper[4]) != 0.0:
+        return
+    lr, mu, wd, gs = [float(v) for v in hyper[:4].tolist()]
     gg = g * gs
     if n_decay > 0:
         if l2 is not None:

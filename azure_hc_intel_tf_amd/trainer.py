@@ -59,7 +59,9 @@ def constant_lr(v: float):
 class Trainer:
     def __init__(self, model, batch_size: int, lr_fn: Callable[[int], float], momentum: float = 0.9,
                  weight_decay: float = 4e-5, reducer=None, world_size: int = 1, use_graph: bool = True,
-                 nesterov: bool = False, graph_warmup: int = 2, forward_only: bool = False):
+                 nesterov: bool = False, graph_warmup: int = 2, forward_only: bool = False,
+                 loss_scale: Optional[float] = None, dynamic_loss_scale: bool = False,
+                 loss_scale_interval: int = 1000):
         self.model = model
         self.ps = model.ps
         self.B = batch_size
@@ -75,8 +77,17 @@ class Trainer:
         self.graph_warmup = graph_warmup
         ld = model.fc.ld if hasattr(model, "fc") else (model.num_classes + 7) // 8 * 8
         self.ld = ld
-        self.hyper = torch.tensor([0.0, momentum, weight_decay, 1.0 / world_size], dtype=torch.float32,
-                                  device=self.dev)
+        # loss scaling (tf_cnn_benchmarks --use_fp16 --fp16_loss_scale /
+        # --fp16_enable_auto_loss_scale): dlogits scaled by S on the device, gradients unscaled
+        # in the optimizer, the step skipped on Inf/NaN; all state device-resident so the
+        # captured graph needs no host round trip.
+        self.loss_scaling = loss_scale is not None or dynamic_loss_scale
+        self.dynamic_ls = dynamic_loss_scale
+        S = float(loss_scale or (2.0 ** 15 if dynamic_loss_scale else 1.0))
+        h = [0.0, momentum, weight_decay, 1.0 / (world_size * S if self.loss_scaling else world_size)]
+        if self.loss_scaling:
+            h += [0.0, S, 0.0, float(loss_scale_interval)]
+        self.hyper = torch.tensor(h, dtype=torch.float32, device=self.dev)
         self.row_loss = torch.zeros(batch_size, dtype=torch.float32, device=self.dev)
         self.dlogits = torch.zeros((batch_size, ld), dtype=model.act_dtype, device=self.dev)
         self.l2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
@@ -101,7 +112,8 @@ class Trainer:
         ps.zero_stats()
         ps.repack()
         logits = self.model.forward(images)
-        Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B)
+        Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B,
+                        self.hyper[5:6] if self.loss_scaling else None)
 
     def _forward_backward(self, images, labels):
         self._forward(images, labels)
@@ -121,8 +133,13 @@ class Trainer:
             self.loss.copy_(self.row_loss.mean().view(1))
             return
         self.l2.zero_()
+        if self.loss_scaling:
+            self.hyper[4:5].zero_()
+            Fn.nonfinite(self.ps.grad, self.hyper[4:5])
         Fn.sgd_momentum(self.ps.master, self.ps.momentum, self.ps.grad, self.ps.n_decay, self.hyper, self.l2,
                         self.nesterov)
+        if self.loss_scaling:
+            Fn.loss_scale_update(self.hyper, self.world, self.dynamic_ls)
         self.loss.copy_((self.row_loss.mean() + 0.5 * self.wd * self.l2).view(1))
 
     def _reduce(self):
@@ -187,7 +204,7 @@ class Trainer:
 
     def step(self, images, labels):
         """One training step; returns the device tensor holding total_loss of this step."""
-        self.hyper[0:1].fill_(float(self.lr_fn(self.steps_done)))
+        self.hyper[0:1].fill_(float(self.lr_fn(self.steps_done)))  # host write, outside the graph
         if not self.use_graph:
             self._eager_step(images, labels)
         else:

@@ -408,7 +408,8 @@ void gap_bwd(const Tensor& dy, const Tensor& dx, int64_t N, int64_t HW, int64_t 
 }
 
 void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_t ncls,
-                  const Tensor& row_loss, const Tensor& dlogits, int64_t lddl, double scale) {
+                  const Tensor& row_loss, const Tensor& dlogits, int64_t lddl, double scale,
+                  const c10::optional<Tensor>& scale_dev) {
   check_f32(logits, "logits");
   check_cuda(labels, "labels");
   TORCH_CHECK(labels.scalar_type() == at::kLong, "hcb.softmax_xent: labels int64");
@@ -419,7 +420,21 @@ void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_
   TORCH_CHECK(row_loss.numel() >= B, "hcb.softmax_xent: row_loss");
   hcb::launch_softmax_xent(logits.data_ptr<float>(), (int)ld, labels.data_ptr<int64_t>(), (int)B, (int)ncls,
                            row_loss.data_ptr<float>(), dlogits.data_ptr(), (int)lddl, (float)scale,
-                           cur_stream());
+                           scale_dev.has_value() ? scale_dev->data_ptr<float>() : nullptr, cur_stream());
+}
+
+void nonfinite(const Tensor& g, const Tensor& flag) {
+  check_f32(g, "g");
+  check_f32(flag, "flag");
+  TORCH_CHECK(g.is_contiguous() && flag.numel() >= 1, "hcb.nonfinite: args");
+  check_align16(g.data_ptr(), "g");
+  hcb::launch_nonfinite(g.data_ptr<float>(), g.numel(), flag.data_ptr<float>(), cur_stream());
+}
+
+void loss_scale_update(const Tensor& hyper, double world, bool dynamic) {
+  check_f32(hyper, "hyper");
+  TORCH_CHECK(hyper.numel() >= 8 && hyper.is_contiguous(), "hcb.loss_scale_update: hyper[8]");
+  hcb::launch_loss_scale_update(hyper.data_ptr<float>(), (float)world, dynamic ? 1 : 0, cur_stream());
 }
 
 void colsum(const Tensor& g, int64_t ld, int64_t M, int64_t N, const Tensor& out) {
@@ -444,7 +459,7 @@ void sgd_momentum(const Tensor& w, const Tensor& mom, const Tensor& g, int64_t n
   check_align16(g.data_ptr(), "g");
   hcb::launch_sgd_momentum(w.data_ptr<float>(), mom.data_ptr<float>(), g.data_ptr<float>(), w.numel(),
                            n_decay, hyper.data_ptr<float>(), l2.has_value() ? l2->data_ptr<float>() : nullptr,
-                           nesterov ? 1 : 0, cur_stream());
+                           nesterov ? 1 : 0, (int)hyper.numel(), cur_stream());
 }
 
 void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, int64_t max_work) {
@@ -623,7 +638,9 @@ TORCH_LIBRARY(hcb, m) {
   m.def("pool_bwd(Tensor dy, Tensor x, Tensor y, Tensor? idx, Tensor(a!) dx, int[] geom, bool accumulate) -> ()");
   m.def("gap_fwd(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx, int N, int HW, int C) -> ()");
-  m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale) -> ()");
+  m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale, Tensor? scale_dev=None) -> ()");
+  m.def("nonfinite(Tensor g, Tensor(a!) flag) -> ()");
+  m.def("loss_scale_update(Tensor(a!) hyper, float world, bool dynamic) -> ()");
   m.def("colsum(Tensor g, int ld, int M, int N, Tensor(a!) out) -> ()");
   m.def("sgd_momentum(Tensor(a!) w, Tensor(b!) mom, Tensor g, int n_decay, Tensor hyper, Tensor(c!)? l2, bool nesterov) -> ()");
   m.def("weight_pack(Tensor master, Tensor(a!) pack, Tensor table, int max_work) -> ()");
@@ -644,6 +661,8 @@ TORCH_LIBRARY(hcb, m) {
 TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("conv_igemm", conv_igemm);
   m.impl("conv_igemm_bnb", conv_igemm_bnb);
+  m.impl("nonfinite", nonfinite);
+  m.impl("loss_scale_update", loss_scale_update);
   m.impl("set_splitk_workspace", set_splitk_workspace);
   m.impl("conv_wgrad", conv_wgrad);
   m.impl("bn_stats", bn_stats);

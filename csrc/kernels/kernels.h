@@ -146,14 +146,18 @@ void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t 
 
 // ---------------------------------------------------------------- loss / fc helpers
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
-                         float* row_loss, void* dlogits, int lddl, float scale, hipStream_t st);
+                         float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
+                         hipStream_t st);
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st);
 
 // ---------------------------------------------------------------- optimizer / weights
-// hyper (device fp32): [lr, momentum, weight_decay, grad_scale] so a captured graph
-// picks up a new learning rate every replay
+// hyper (device fp32): [lr, momentum, weight_decay, grad_scale(, found_inf, loss_scale,
+// good_steps, interval)] so a captured graph picks up a new learning rate every replay; with
+// hyper_n > 4 the update is skipped when found_inf != 0 (loss scaling)
 void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
-                         const float* hyper, float* l2_out, int nesterov, hipStream_t st);
+                         const float* hyper, float* l2_out, int nesterov, int hyper_n, hipStream_t st);
+void launch_nonfinite(const float* g, int64_t n, float* flag, hipStream_t st);
+void launch_loss_scale_update(float* hyper, float world, int dynamic, hipStream_t st);
 struct WPackEntry {  // all int64 so the table is a plain int64 tensor [n][9]
   int64_t src_off;   // fp32 master offset (elements)
   int64_t pack_off;  // bf16 packed [Nout][Kpad] offset (elements), -1 = skip

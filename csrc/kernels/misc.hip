@@ -24,8 +24,10 @@ namespace hcb {
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits, int ld,
                                                            const int64_t* __restrict__ labels,
                                                            int ncls, float* row_loss,
-                                                           uint16_t* dl, int lddl, float scale) {
+                                                           uint16_t* dl, int lddl, float scale,
+                                                           const float* scale_dev) {
   __shared__ float red[8];
+  if (scale_dev != nullptr) scale *= *scale_dev;  // device-resident loss scale
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float* lr = logits + (size_t)row * ld;
   float mx = -INFINITY;
@@ -73,8 +75,11 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w
                                                            const float* __restrict__ g, int64_t n,
                                                            int64_t n_decay,
                                                            const float* __restrict__ hyper,
-                                                           float* l2_out, int nesterov) {
+                                                           float* l2_out, int nesterov, int hyper_n) {
   __shared__ float red[4];
+  // loss scaling: hyper[4] = "non-finite gradient seen" -> skip the whole update (TF
+  // LossScaleOptimizer semantics); the flag is wave-uniform so every block exits together
+  if (hyper_n > 4 && hyper[4] != 0.f) return;
   const float lr = hyper[0], mu = hyper[1], wd = hyper[2], gscale = hyper[3];
   float l2 = 0.f;
   const int64_t n4 = n >> 2;
@@ -273,18 +278,59 @@ static int grid_for(int64_t n) {
 }
 
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
-                         float* row_loss, void* dlogits, int lddl, float scale, hipStream_t st) {
+                         float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
+                         hipStream_t st) {
   hipLaunchKernelGGL(softmax_xent_kernel, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls,
-                     row_loss, (uint16_t*)dlogits, lddl, scale);
+                     row_loss, (uint16_t*)dlogits, lddl, scale, scale_dev);
+}
+
+// ------------------------------------------------------------------ loss scaling
+// flag[0] = 1 when any gradient element is Inf/NaN (the caller zeroes the flag first)
+__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, int64_t n, float* flag) {
+  int bad = 0;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 v = reinterpret_cast<const f32x4*>(g)[i];
+    bad |= !(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]) && isfinite(v[3]));
+  }
+  for (int64_t j = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(g[j]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = 1.f;  // benign race: every writer stores 1
+}
+// hyper = [lr, mu, wd, grad_scale, found_inf, loss_scale, good_steps, interval]; one thread.
+// dynamic: halve on overflow (floor 1), double after `interval` clean steps; then
+// grad_scale = 1 / (world * loss_scale) for the next step.
+__global__ void loss_scale_update_kernel(float* hyper, float world, int dynamic) {
+  float S = hyper[5];
+  if (dynamic) {
+    if (hyper[4] != 0.f) {
+      S = fmaxf(S * 0.5f, 1.f);
+      hyper[6] = 0.f;
+    } else {
+      hyper[6] += 1.f;
+      if (hyper[6] >= hyper[7]) {
+        S *= 2.f;
+        hyper[6] = 0.f;
+      }
+    }
+    hyper[5] = S;
+  }
+  hyper[3] = 1.f / (world * S);
+}
+void launch_nonfinite(const float* g, int64_t n, float* flag, hipStream_t st) {
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, g, n, flag);
+}
+void launch_loss_scale_update(float* hyper, float world, int dynamic, hipStream_t st) {
+  hipLaunchKernelGGL(loss_scale_update_kernel, dim3(1), dim3(1), 0, st, hyper, world, dynamic);
 }
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st) {
   hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256), dim3(256), 0, st, g, ld, M, N, is_f32,
                      out);
 }
 void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
-                         const float* hyper, float* l2_out, int nesterov, hipStream_t st) {
+                         const float* hyper, float* l2_out, int nesterov, int hyper_n, hipStream_t st) {
   hipLaunchKernelGGL(sgd_momentum_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, w, mom, g,
-                     n, n_decay, hyper, l2_out, nesterov);
+                     n, n_decay, hyper, l2_out, nesterov, hyper_n);
 }
 void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st) {
   hipLaunchKernelGGL(l2norm_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, out);

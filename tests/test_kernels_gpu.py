@@ -422,3 +422,30 @@ def test_bn_finalize_free_path(C, relu, residual):
     Fn.bn_backward(dy.float().cpu(), y.float().cpu(), zc, gsv, gamma.cpu(), beta.cpu(), mode, dgc, dbc, dzc, gresc)
     assert rel_err(db, dbc) < 2e-2 and rel_err(dg, dgc) < 2e-2
     assert rel_err(dz, dzc) < 3e-2 and rel_err(gres, gresc) < 1e-2
+
+
+def test_loss_scale_ops_gpu():
+    """device-side loss scaling: scaled dlogits, Inf/NaN detection, skipped update, scale step"""
+    torch.manual_seed(31)
+    B, ncls, ldl = 8, 1001, 1008
+    logits = torch.randn(B, ldl, device=DEV)
+    labels = torch.randint(0, ncls, (B,), device=DEV)
+    rl, rl2 = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    d1 = torch.empty(B, ldl, dtype=torch.bfloat16, device=DEV)
+    d2 = torch.empty_like(d1)
+    S = torch.tensor([64.0], device=DEV)
+    Fn.softmax_xent(logits, labels, ncls, rl, d1, 1.0 / B)
+    Fn.softmax_xent(logits, labels, ncls, rl2, d2, 1.0 / B, S)
+    assert torch.allclose(d2.float(), d1.float() * 64, rtol=1e-2, atol=1e-4) and torch.equal(rl, rl2)
+    h = torch.tensor([0.1, 0.9, 0.0, 1.0 / 1024, 0.0, 1024.0, 0.0, 1000.0], device=DEV)
+    g = torch.ones(100_003, device=DEV)
+    w, mom = torch.ones_like(g), torch.zeros_like(g)
+    Fn.nonfinite(g, h[4:5])
+    assert float(h[4]) == 0.0
+    g[77_777] = float("nan")
+    Fn.nonfinite(g, h[4:5])
+    assert float(h[4]) == 1.0
+    Fn.sgd_momentum(w, mom, g, 0, h)
+    assert torch.equal(w, torch.ones_like(w))
+    Fn.loss_scale_update(h, 1, True)
+    assert float(h[5]) == 512.0 and abs(float(h[3]) - 1 / 512) < 1e-9
