@@ -502,6 +502,17 @@ def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False, argmax=No
 def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, accumulate=False, argmax=None):
     pt, pb, pl, pr = pads
     if x.is_cuda:
+        # the kernel walks x / dx with one pixel stride and y / dy with another: align views
+        if ld(y) != ld(dy):
+            y = y.contiguous() if ld(dy) == y.shape[3] else y
+            dy = dy.contiguous() if ld(y) != ld(dy) else dy
+        if ld(dx) != ld(x):
+            tmp = dx.contiguous() if accumulate else torch.empty(dx.shape, dtype=dx.dtype, device=dx.device)
+            xc = x.contiguous()
+            _ext.ops().pool_bwd(dy, xc, y, argmax, tmp, pool_geom(xc, dy, kh, kw, sh, sw, pt, pl, is_max, incl_pad),
+                                accumulate)
+            dx.copy_(tmp)
+            return dx
         _ext.ops().pool_bwd(dy, x, y, argmax, dx, pool_geom(x, dy, kh, kw, sh, sw, pt, pl, is_max, incl_pad),
                             accumulate)
         return dx

@@ -241,7 +241,7 @@ void bn_stats(const Tensor& x, int64_t M, int64_t C, int64_t ldx, const Tensor& 
   check_bf16(x, "x");
   check_f32(slab, "slab");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0, "hcb.bn_stats: C % 8 == 0, C <= 2048");
-  check_range(x, M * ldx * 2, "x");
+  check_range(x, ((M - 1) * ldx + C) * 2, "x");
   int T = hcb::bn_num_partials((int)M, (int)C);
   TORCH_CHECK(slab.numel() >= (int64_t)T * 2 * C, "hcb.bn_stats: slab too small");
   hcb::launch_bn_stats(x.data_ptr(), (int)M, (int)C, (int)ldx, slab.data_ptr<float>(), T, cur_stream());
@@ -278,7 +278,7 @@ void bn_apply(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, const 
   check_bf16(x, "x");
   check_bf16(y, "y");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldy % 8 == 0, "hcb.bn_apply: C/ld");
-  check_range(x, M * ldx * 2, "x");
+  check_range(x, ((M - 1) * ldx + C) * 2, "x");
   check_range(y, ((M - 1) * ldy + C) * 2, "y");
   const void* rp = nullptr;
   if (res.has_value()) {
@@ -362,8 +362,8 @@ void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx
   check_bf16(x, "x");
   check_bf16(y, "y");
   TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_fwd: C/ld % 8");
-  check_range(x, g[0] * g[1] * g[2] * g[4] * 2, "x");
-  check_range(y, g[0] * g[5] * g[6] * g[7] * 2, "y");
+  check_range(x, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "x");
+  check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "y");
   void* ip = nullptr;
   if (idx.has_value()) {
     TORCH_CHECK(idx->scalar_type() == at::kByte && idx->is_contiguous() && idx->numel() >= g[0] * g[5] * g[6] * g[3],
@@ -381,10 +381,10 @@ void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::opt
   check_bf16(x, "x");
   check_bf16(y, "y");
   check_bf16(dx, "dx");
-  check_range(x, g[0] * g[1] * g[2] * g[4] * 2, "x");
-  check_range(dx, g[0] * g[1] * g[2] * g[4] * 2, "dx");
-  check_range(y, g[0] * g[5] * g[6] * g[7] * 2, "y");
-  check_range(dy, g[0] * g[5] * g[6] * g[7] * 2, "dy");
+  check_range(x, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "x");
+  check_range(dx, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "dx");
+  check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "y");
+  check_range(dy, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "dy");
   hcb::launch_pool_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), dx.data_ptr(), g[0], g[1], g[2], g[3],
                        g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], g[15],
                        accumulate ? 1 : 0, idx.has_value() ? idx->data_ptr() : nullptr, cur_stream());
