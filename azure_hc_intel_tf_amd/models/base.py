@@ -50,7 +50,10 @@ class CNNModel:
         """Backward in segments, for overlapping the gradient allreduce with the rest of the
         backward pass: yields ``(layers, last)`` after each segment, where every parameter
         gradient of ``layers`` is final. Default: one segment (the whole backward)."""
+        from ..nn.layers import join_side_streams
+
         self.backward(dlogits)
+        join_side_streams()
         yield None, True  # None: every gradient
 
     # -- helpers

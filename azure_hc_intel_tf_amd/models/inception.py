@@ -18,7 +18,7 @@ from typing import List
 
 import torch
 
-from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_act
+from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_act, join_side_streams
 from .base import CNNModel
 
 BN_KW = dict(eps=1e-3, decay=0.999, scale=False)
@@ -199,3 +199,4 @@ class InceptionV3(CNNModel):
                 dx, _ = l.backward(dx) if l.need_dx else (l.backward(dx)[0], None)
             else:
                 dx = l.backward(dx)
+        join_side_streams()

@@ -14,7 +14,7 @@ BN: decay 0.9, epsilon 1e-5, scale=True. ResNet-50 v1: 25,559,081 trainable para
 """
 from __future__ import annotations
 
-from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool
+from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, join_side_streams
 from .base import CNNModel
 
 LAYER_COUNTS = {18: None, 50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}
@@ -115,9 +115,11 @@ class ResNet(CNNModel):
             dx = self.blocks[i].backward(dx, self.blocks[i - 1].c3 if i > 0 else None)
             seg += self.blocks[i].layers()
             if i > 0 and self.blocks[i].stage != self.blocks[i - 1].stage:
+                join_side_streams()  # the segment's weight gradients are final
                 yield seg, False
                 seg = []
         dx = self.pool.backward(dx)
         self.stem.backward(dx)
         self._last = None
+        join_side_streams()
         yield seg + [self.pool, self.stem], True

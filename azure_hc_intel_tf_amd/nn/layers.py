@@ -58,6 +58,32 @@ def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
 STAT_R = 8  # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
 FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
+# HCB_WGRAD_STREAM=1: run weight-gradient GEMMs on a second HIP stream, concurrent with the
+# data-grad chain (the critical path of backward), captured as parallel graph branches.
+# Off by default: measured on MI355X (ResNet-50 bs=64) the split-K-tuned GEMMs already fill
+# the 256 CUs, and the concurrent pairs contend (7594 vs 7699 img/s).
+WGRAD_STREAM = os.environ.get("HCB_WGRAD_STREAM", "0") == "1"
+_SIDE = {}
+_SIDE_USED = set()
+
+
+def wgrad_stream(dev) -> "torch.cuda.Stream":
+    """The side stream of ``dev``, forked from the current stream (waits for all work so far)."""
+    idx = torch.device(dev).index or 0
+    s = _SIDE.get(idx)
+    if s is None:
+        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
+    s.wait_stream(torch.cuda.current_stream(idx))
+    _SIDE_USED.add(idx)
+    return s
+
+
+def join_side_streams():
+    """Make the current stream wait for every forked weight-gradient stream (before the
+    gradients are reduced / applied, and before a graph capture ends)."""
+    for idx in list(_SIDE_USED):
+        torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
+    _SIDE_USED.clear()
 
 
 class _FixedParam:
@@ -221,7 +247,14 @@ class ConvBN(Layer):
             Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
                 gres = dz
-        Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(C, -1) if dz.is_cuda else self.w.grad)
+        if dz.is_cuda and WGRAD_STREAM:
+            with torch.cuda.stream(wgrad_stream(dev)):
+                Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(C, -1))
+            # the allocator must not hand dz / x to the main stream before the wgrad has read them
+            dz.record_stream(_SIDE[dev.index or 0])
+            x.record_stream(_SIDE[dev.index or 0])
+        else:
+            Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(C, -1) if dz.is_cuda else self.w.grad)
         if self.need_dx:
             H, W, Cin = self.in_shape
             if dx is None:

@@ -193,6 +193,8 @@ class ParamStore:
             if pk.want_tr:
                 pk.tr_off = poff
                 poff += _align(pk.C * pk.Kpad_t)
+            # the pack kernel moves 8-channel vectors (fp32 float4 pairs -> one 16-byte bf16 store)
+            assert pk.C % 8 == 0 and pk.Kpad % 64 == 0, f"pack of {pk.param.name}: C % 8, Kpad % 64"
             rows.append([pk.param.offset, pk.pack_off, pk.tr_off, pk.Nout, pk.R, pk.S, pk.C, pk.Kpad, pk.Kpad_t])
             work = pk.Nout * pk.Kpad + (pk.C * pk.Kpad_t if pk.want_tr else 0)
             self.pack_max_work = max(self.pack_max_work, work)

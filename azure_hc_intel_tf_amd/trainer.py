@@ -29,6 +29,7 @@ import torch
 
 from .ops import functional as Fn
 from .ops import _ext
+from .nn.layers import join_side_streams
 
 
 def resnet_lr_schedule(global_batch: int, num_examples_per_epoch: int = 1281167, base_lr: float = 0.128,
@@ -121,6 +122,7 @@ class Trainer:
             self.model.clear()
             return
         self.model.backward(self.dlogits)
+        join_side_streams()
 
     def _ranges(self, i, layers):
         if i not in self._seg_ranges:

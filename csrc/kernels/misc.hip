@@ -137,35 +137,80 @@ __global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ x
 }
 
 // ------------------------------------------------------------------ weights
+// Per entry the work is (A) the row-padded copy [Nout][K] -> [Nout][Kpad] in 8-element vectors
+// (two 16-byte reads, one 16-byte write per lane; pad columns stay zero from allocation) and
+// (B) the flipped/transposed data-grad operand [C][tap*Nout + kk] <- W[kk][R-1-r][S-1-s][c],
+// a 64x64 LDS-tiled transpose per (tap, kk-tile, c-tile) so both the fp32 reads (along c) and
+// the bf16 writes (along kk) are coalesced. Blocks grid-stride over A chunks then B tiles.
 __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ master,
                                                           uint16_t* __restrict__ pack,
                                                           const WPackEntry* __restrict__ ents) {
+  __shared__ float tile[64][65];
   const WPackEntry e = ents[blockIdx.y];
   const int R = (int)e.R, S = (int)e.S, C = (int)e.C, Nout = (int)e.Nout;
   const int Kpad = (int)e.Kpad, Kpad_t = (int)e.Kpad_t;
-  const int K = R * S * C;
-  const int Kt = R * S * Nout;
+  const int K = R * S * C, K8 = K / 8;
   const float* src = master + e.src_off;
-  const int n1 = e.pack_off >= 0 ? Nout * Kpad : 0;
-  const int n2 = e.tr_off >= 0 ? C * Kpad_t : 0;
-  // 32-bit index math (every conv weight is < 2^31 elements); packed part is a straight
-  // row-padded copy, the transposed part reads the master through L2 (weights are small)
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n1 + n2; i += gridDim.x * blockDim.x) {
-    if (i < n1) {
-      int j = i / Kpad, k = i - j * Kpad;
-      float v = k < K ? src[j * K + k] : 0.f;
-      pack[e.pack_off + i] = f2bf(v);
-    } else {
-      int t = i - n1;
-      int c = t / Kpad_t, k = t - c * Kpad_t;
-      float v = 0.f;
-      if (k < Kt) {
-        int tap = k / Nout, kk = k - tap * Nout;
-        int rr = tap / S, ss = tap - rr * S;
-        v = src[((kk * R + (R - 1 - rr)) * S + (S - 1 - ss)) * C + c];
+  const int tid = threadIdx.x;
+  const int nA = e.pack_off >= 0 ? (Nout * K8 + 255) / 256 : 0;
+  const int tkk = (Nout + 63) / 64, tc = (C + 63) / 64;
+  const int nB = e.tr_off >= 0 ? R * S * tkk * tc : 0;
+  for (int u = blockIdx.x; u < nA + nB; u += gridDim.x) {
+    if (u < nA) {
+      const int i = u * 256 + tid;
+      if (i < Nout * K8) {
+        const int j = i / K8, k8 = i - j * K8;
+        const float4* s4 = reinterpret_cast<const float4*>(src + (size_t)j * K + k8 * 8);
+        const float4 a = s4[0], b = s4[1];
+        u32x4 v;
+        v[0] = pack2(a.x, a.y);
+        v[1] = pack2(a.z, a.w);
+        v[2] = pack2(b.x, b.y);
+        v[3] = pack2(b.z, b.w);
+        *reinterpret_cast<u32x4*>(pack + e.pack_off + (size_t)j * Kpad + k8 * 8) = v;
       }
-      pack[e.tr_off + t] = f2bf(v);
+      continue;
     }
+    int t = u - nA;
+    const int ci = t % tc;
+    t /= tc;
+    const int ki = t % tkk;
+    const int tap = t / tkk;
+    const int rr = tap / S, ss = tap - rr * S;
+    const int kk0 = ki * 64, c0 = ci * 64;
+    // load W[kk0+row][R-1-rr][S-1-ss][c0 .. c0+63] (fp32, float4 along c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tid >> 4) + 16 * q, c4 = (tid & 15) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kk0 + row < Nout && c0 + c4 < C)
+        v = *reinterpret_cast<const float4*>(src + ((size_t)((kk0 + row) * R + (R - 1 - rr)) * S + (S - 1 - ss)) * C +
+                                             c0 + c4);
+      tile[row][c4] = v.x;
+      tile[row][c4 + 1] = v.y;
+      tile[row][c4 + 2] = v.z;
+      tile[row][c4 + 3] = v.w;
+    }
+    __syncthreads();
+    {
+      const int c = tid >> 2, k16 = (tid & 3) * 16;
+      if (c0 + c < C) {
+        const size_t o = (size_t)e.tr_off + (size_t)(c0 + c) * Kpad_t + (size_t)tap * Nout + kk0 + k16;
+        if (kk0 + k16 + 16 <= Nout && (o & 7) == 0) {
+          u32x4 v0, v1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v0[q] = pack2(tile[k16 + 2 * q][c], tile[k16 + 2 * q + 1][c]);
+            v1[q] = pack2(tile[k16 + 8 + 2 * q][c], tile[k16 + 9 + 2 * q][c]);
+          }
+          reinterpret_cast<u32x4*>(pack + o)[0] = v0;
+          reinterpret_cast<u32x4*>(pack + o)[1] = v1;
+        } else {
+          for (int q = 0; q < 16 && kk0 + k16 + q < Nout; ++q) pack[o + q] = f2bf(tile[k16 + q][c]);
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -337,8 +382,8 @@ void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st) {
 }
 void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
                         int n_entries, int64_t max_work, hipStream_t st) {
-  int gx = grid_for(max_work);
-  if (gx > 1024) gx = 1024;
+  int64_t units = max_work / 2048 + 2;  // A chunks are 2048 elements, B tiles 4096
+  int gx = units > 1024 ? 1024 : (int)units;
   hipLaunchKernelGGL(weight_pack_kernel, dim3(gx, n_entries), dim3(256), 0, st, master, pack,
                      entries_dev);
 }

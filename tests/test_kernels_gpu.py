@@ -353,17 +353,21 @@ def test_sgd_momentum_flat():
     assert abs(l2.item() - l2c.item()) / l2c.item() < 1e-4
 
 
-def test_weight_pack_transposed_flip():
+@pytest.mark.parametrize("cin,cout,k", [(16, 24, 3), (136, 200, 3), (64, 128, 1), (256, 1001, 1), (8, 64, 7)])
+def test_weight_pack_transposed_flip(cin, cout, k):
+    """Vector copy + LDS-tiled transpose of the weight pack kernel (partial and full 64x64
+    tiles, odd Nout) against a torch reference."""
     torch.manual_seed(10)
-    spec, p, pk = make_conv(16, 24, 3, 3, 1, 1, (1, 1, 1, 1))
+    spec, p, pk = make_conv(cin, cout, k, k, 1, 1, (k // 2,) * 4)
     w = p.data.cpu()
-    packed = pk.pack.view(24, spec.Kpad).float().cpu()
-    assert torch.allclose(packed[:, :spec.K], bf(w).float().reshape(24, -1))
-    assert packed[:, spec.K:].abs().max() == 0
-    tr = pk.tr.view(16, spec.Kpad_t).float().cpu()
+    packed = pk.pack.view(cout, spec.Kpad).float().cpu()
+    assert torch.allclose(packed[:, :spec.K], bf(w).float().reshape(cout, -1))
+    assert spec.K == spec.Kpad or packed[:, spec.K:].abs().max() == 0
+    tr = pk.tr.view(cin, spec.Kpad_t).float().cpu()
     # tr[c][(r'*S+s')*Cout + k] = W[k][R-1-r'][S-1-s'][c]
-    ref = bf(w).float().flip(1).flip(2).permute(3, 1, 2, 0).reshape(16, -1)
+    ref = bf(w).float().flip(1).flip(2).permute(3, 1, 2, 0).reshape(cin, -1)
     assert torch.allclose(tr[:, :spec.Kt], ref)
+    assert spec.Kt == spec.Kpad_t or tr[:, spec.Kt:].abs().max() == 0
 
 
 def test_synthetic_data_stats():
