@@ -6,6 +6,8 @@ box with the repo snapshot):
 * ``_hcb_kernels.so`` -- the hand-written CDNA4 kernels (``csrc/kernels/*.hip``, compiled
   with ``hipcc --offload-arch=gfx950``) plus their ``torch.library`` registrations
   (``csrc/bindings.cpp``), loaded with ``torch.ops.load_library``.
+* ``_hcb_data*.so`` -- the native real-data pipeline core (TFRecord / tf.Example / crop
+  windows / prefetch threads; ``csrc/data/*.cpp``).
 * ``_hcb_comm.so`` -- the C++ communication runtime (RCCL communicator, bucketed
   allreduce engine, Chrome-trace timeline, stall watchdog; ``csrc/comm/*.cpp``).
 
@@ -123,6 +125,30 @@ def build_comm(verbose: bool = False, jobs: int = 8) -> str:
     return COMM_SO
 
 
+def _data_so() -> str:
+    import sysconfig
+
+    return os.path.join(PKG_DIR, "_hcb_data" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_data(verbose: bool = False) -> str:
+    """``_hcb_data`` -- the native half of the real-data input pipeline (TFRecord reader /
+    writer with CRC-32C, tf.Example parsing, crop-window sampling, prefetch threads;
+    ``csrc/data/*.cpp``), a plain CPython extension (pybind11, no torch dependency)."""
+    import sysconfig
+
+    import pybind11
+
+    srcs = sorted(glob.glob(os.path.join(CSRC, "data", "*.cpp")))
+    if not srcs:
+        return ""
+    so = _data_so()
+    if _newer(so, srcs + _headers()):
+        _run(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-I" + pybind11.get_include(),
+              "-I" + sysconfig.get_paths()["include"], *srcs, "-o", so, "-lpthread"], verbose)
+    return so
+
+
 RCCL_BENCH = os.path.join(REPO, "tools", "rccl_bench", "rccl_allreduce_bench")
 
 
@@ -141,6 +167,7 @@ def build_tools(verbose: bool = False) -> str:
 def build_all(verbose: bool = False) -> None:
     build_kernels(verbose)
     build_comm(verbose)
+    build_data(verbose)
     build_tools(verbose)
 
 

@@ -62,6 +62,8 @@ FLAGS: List[Flag] = [
     Flag("local_parameter_device", "gpu", str, "accepted for compatibility", noop_on_gpu=True),
     Flag("data_dir", None, str, "real-data directory; absent = synthetic ImageNet"),
     Flag("data_name", None, str, "dataset name (imagenet)"),
+    Flag("datasets_num_private_threads", None, int, "TFRecord reader threads per worker (real data)"),
+    Flag("num_decode_threads", None, int, "JPEG decode threads per worker (real data)"),
     # --- tf_cnn_benchmarks flags used by the BASELINE configs / common runs
     Flag("num_gpus", 1, int, "GPUs per process (horovod: 1)"),
     Flag("use_fp16", False, parse_bool, "fp16 compute (bf16 is the default GPU compute type)"),

@@ -601,6 +601,38 @@ void synth_labels(const Tensor& out, int64_t ncls, int64_t seed) {
   hcb::launch_synth_labels(out.data_ptr<int64_t>(), (int)out.numel(), (int)ncls, (uint64_t)seed, cur_stream());
 }
 
+// desc_host: the CPU copy of desc, used to check every crop lies inside src before launching
+void preprocess_images(const Tensor& src, const Tensor& desc, const Tensor& desc_host, const Tensor& out,
+                       at::ArrayRef<double> scale, at::ArrayRef<double> bias) {
+  check_cuda(src, "src");
+  check_cuda(desc, "desc");
+  check_bf16(out, "out");
+  TORCH_CHECK(src.scalar_type() == at::kByte && src.is_contiguous(), "hcb.preprocess_images: src uint8 contiguous");
+  TORCH_CHECK(desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 4 && desc.is_contiguous(),
+              "hcb.preprocess_images: desc int64 [B][4]");
+  TORCH_CHECK(!desc_host.is_cuda() && desc_host.scalar_type() == at::kLong && desc_host.is_contiguous() &&
+                  desc_host.sizes() == desc.sizes(),
+              "hcb.preprocess_images: desc_host must be the CPU copy of desc");
+  TORCH_CHECK(out.dim() == 4 && out.is_contiguous() && out.size(1) == out.size(2) && out.size(3) % 8 == 0 &&
+                  out.size(3) >= 8,
+              "hcb.preprocess_images: out [B][S][S][Cpad] contiguous, Cpad % 8 == 0");
+  TORCH_CHECK(scale.size() == 3 && bias.size() == 3, "hcb.preprocess_images: 3 scales / biases");
+  const int64_t B = desc.size(0);
+  TORCH_CHECK(B <= out.size(0), "hcb.preprocess_images: more crops than output images");
+  const int64_t* d = desc_host.data_ptr<int64_t>();
+  for (int64_t i = 0; i < B; ++i) {
+    TORCH_CHECK(d[4 * i] >= 0 && d[4 * i + 1] > 0 && d[4 * i + 2] > 0 &&
+                    d[4 * i] + d[4 * i + 1] * d[4 * i + 2] * 3 <= src.numel(),
+                "hcb.preprocess_images: crop ", i, " outside the staging buffer");
+  }
+  TORCH_CHECK(out.size(1) * out.size(1) < (1ll << 31), "hcb.preprocess_images: image too large");
+  const float sc[3] = {(float)scale[0], (float)scale[1], (float)scale[2]};
+  const float bi[3] = {(float)bias[0], (float)bias[1], (float)bias[2]};
+  if (B == 0) return;
+  hcb::launch_preprocess_images(src.data_ptr<uint8_t>(), desc.data_ptr<int64_t>(), (int)B, out.data_ptr(),
+                                (int)out.size(1), (int)out.size(3), sc, bi, cur_stream());
+}
+
 void bucket_pack(const Tensor& src, const Tensor& dst, double scale) {
   check_f32(src, "src");
   check_cuda(dst, "dst");
@@ -652,6 +684,7 @@ TORCH_LIBRARY(hcb, m) {
   m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg) -> ()");
   m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
+  m.def("preprocess_images(Tensor src, Tensor desc, Tensor desc_host, Tensor(a!) out, float[] scale, float[] bias) -> ()");
   m.def("synth_images(Tensor(a!) out, int C, int Cpad, float mean, float std, int seed) -> ()");
   m.def("synth_labels(Tensor(a!) out, int ncls, int seed) -> ()");
   m.def("bucket_pack(Tensor src, Tensor(a!) dst, float scale) -> ()");
@@ -688,6 +721,7 @@ TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("bn_bwd_apply_acc", bn_bwd_apply_acc);
   m.impl("l2norm_sq", l2norm_sq);
   m.impl("synth_images", synth_images);
+  m.impl("preprocess_images", preprocess_images);
   m.impl("synth_labels", synth_labels);
   m.impl("bucket_pack", bucket_pack);
   m.impl("bucket_unpack", bucket_unpack);

@@ -177,6 +177,10 @@ void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st);
 void launch_synth_images(void* out, int64_t n_pix, int C, int Cpad, float mean, float std,
                          uint64_t seed, hipStream_t st);
 void launch_synth_labels(int64_t* out, int n, int ncls, uint64_t seed, hipStream_t st);
+// real data: batch of RGB uint8 crops (desc [B][4] = byte offset, h, w, flip) -> bilinear resize
+// to S x S, optional horizontal flip, x*scale[c]+bias[c], NHWC bf16 with Cpad channels
+void launch_preprocess_images(const uint8_t* src, const int64_t* desc, int B, void* out, int S, int Cpad,
+                              const float* scale, const float* bias, hipStream_t st);
 
 // ---------------------------------------------------------------- gradient buckets
 void launch_bucket_pack(const float* src, void* dst, int64_t n, float scale, int to_bf16,
