@@ -91,6 +91,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     keys = [Fn.fwd_key(M, Cout, spec.K), Fn.wgrad_key(Cout, spec.K, M)]
     if layer.need_dx:
         keys.append(Fn.fwd_key(geo[0], Cin, geo[1]))
+        keys.append(Fn.dgb_key(geo[0], Cin, geo[1]))
     if all(k in Fn._tuned for k in keys):
         return out
     x = _bf((N, H, W, Cin), dev)
@@ -120,6 +121,24 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
                 for sp in Fn.splitk_candidates(cfg, geo[0], Cin, geo[1]):
                     plan = cfg if sp == 1 else [cfg, sp]
                     t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=plan))
+                    if best is None or t < best[0]:
+                        best = (t, plan)
+            Fn._tuned[k] = best[1]
+            out.append((k, best))
+        # the same GEMM with the fused BN-backward epilogue (ReLU mask from y, residual
+        # beta-accumulate: the heaviest epilogue), used when a BN layer consumes this dx
+        k = Fn.dgb_key(geo[0], Cin, geo[1])
+        if k not in Fn._tuned:
+            z = _bf((N, H, W, Cin), dev)
+            yv = _bf((N, H, W, Cin), dev)
+            stats = [torch.rand(Cin, device=dev) + 0.5 for _ in range(4)]
+            bacc = torch.zeros(8 * 2 * Cin, dtype=torch.float32, device=dev)
+            bnb = Fn.BNBwdFuse(z, yv, Fn.BNSaved(stats[0], stats[1]), stats[2], stats[3], 1, bacc, 8)
+            best = None
+            for cfg in Fn.fwd_candidates(Cin):
+                for sp in Fn.splitk_candidates(cfg, geo[0], Cin, geo[1]):
+                    plan = cfg if sp == 1 else [cfg, sp]
+                    t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, True, cfg=plan, bnb=bnb))
                     if best is None or t < best[0]:
                         best = (t, plan)
             Fn._tuned[k] = best[1]

@@ -92,13 +92,21 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                4: (128, 128), 5: (128, 64), 6: (64, 64), 7: (64, 128),
                8: (128, 128), 9: (128, 128), 10: (128, 64), 11: (64, 128),
                12: (128, 128), 13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (64, 128)}
-_WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64)}
+# weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring
+_WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
+                6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128)}
 N_CU = 256
 _tuned: dict = {}
 
 
 def fwd_key(M: int, N: int, K: int):
     return ("fwd", M, N, K)
+
+
+def dgb_key(M: int, N: int, K: int):
+    """Data-grad GEMM with the fused BN-backward epilogue (its own tuning entry: the epilogue
+    reads z / y / the beta source, which moves the best tile away from the plain GEMM's)."""
+    return ("dgb", M, N, K)
 
 
 def wgrad_key(Nout: int, K: int, M: int):
@@ -309,6 +317,8 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
             geom = [N, P, Q, Cdz, ld(dz), H, W, spec.kh, spec.kw, 1, 1, pt, pl, spec.dh, spec.dw,
                     spec.sh, spec.sw, spec.cin_pad, K, Kpad, ld(dx), 0, H, W, 1, 1,
                     1 if accumulate else 0, 0]
+        if cfg is None and bnb is not None:
+            cfg = _tuned.get(dgb_key(M, spec.cin_pad, K))
         cfg, splits = _plan(cfg, M, spec.cin_pad, K, dz.device)
         geom = geom + [0, 0, splits]
         if bnb is not None:

@@ -37,6 +37,10 @@
 
 namespace hcb {
 
+// data-grad GEMMs with at most this many 64-deep k-steps issue their fused BN-backward
+// epilogue loads before the main loop (EpiPrefetch)
+constexpr int EARLY_EPI_KSTEPS = 2;
+
 // ---- per-thread implicit-im2col address generation, shared by both main loops.
 // k-steps are issued strictly in order (kt = 0, 1, 2, ...), so the loader keeps the current
 // filter tap / channel offset as wave-uniform state and advances it without divisions. In
@@ -220,6 +224,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   };
 
   const int nk = p.Kpad / BK;
+  EpiPrefetch<WM, WN, TM, TN, BNB> pre;
+  const bool early = BNB && nk <= EARLY_EPI_KSTEPS;
+  if (early) pre.load(p, 0, m0, n0, tid);
   gload(0);
   lstore(0);
   __syncthreads();
@@ -230,7 +237,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
-  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
+  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early);
 }
 
 // ============================================================== LDS-DMA multi-stage main loop
@@ -297,6 +304,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
   const int nk_all = p.Kpad / BK;
   const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's k-steps
   if (kb > 0) al.seek(p, kb);
+  EpiPrefetch<WM, WN, TM, TN, BNB> pre;
+  const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS;
+  if (early) pre.load(p, 0, m0, n0, tid);
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
     if (s < nk) issue(s, kb + s);
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
         for (int j = 0; j < NI; ++j) acc[i][j] += slab[((size_t)s2 * FR + i * NI + j) * NT + tid];
     }
   }
-  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid);
+  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early);
 }
 
 // ============================================================== launch

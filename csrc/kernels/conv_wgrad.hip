@@ -199,6 +199,220 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   }
 }
 
+// ============================================================== LDS-DMA multi-stage variant
+// Same GEMM, but both operands stream global -> LDS with buffer_load ... lds (no register
+// staging) into an NST-deep ring, with counted s_waitcnt vmcnt + raw s_barrier keeping NST-2
+// stages in flight (the conv_igemm_glds scheme). Each wave instruction fills RPI whole LDS rows
+// (1 KiB); a lane fetches the GLOBAL 16-byte chunk that the swizzled transpose read expects at
+// its LDS position (the 32-byte-slot XOR is an involution, applied to the source chunk). Wave
+// tiles up to 64x64 halve the LDS bytes read per MFMA against the 32x32 register-staged
+// kernel, which is LDS-read bound.
+template <int N>
+__device__ __forceinline__ void wg_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG>
+__global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradParams p) {
+  constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int NW = WM * WN;
+  constexpr int ACPR = BM / 8, BCPR = BN / 8;        // 16-byte chunks per LDS row
+  constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;  // LDS rows filled by one wave instruction
+  constexpr int AI = BK / ARPI / NW, BI = BK / BRPI / NW;  // instructions per wave per stage
+  constexpr int LOADS = AI + BI;
+  constexpr int STAGE = BK * (BM + BN) * 2;
+  static_assert(AI * ARPI * NW == BK && BI * BRPI * NW == BK && AI >= 1 && BI >= 1, "tile / wave mapping");
+  static_assert(NST >= 2 && NST <= 5 && LOADS * (NST - 2) <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = wave_id_uniform();
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_m = (p.Nout + BM - 1) / BM;
+  const int tiles_n = (p.K + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int i0 = tm * BM, j0 = tn * BN;
+  const int nkt = (p.M + BK - 1) / BK;
+  const int kt_begin = split * p.ksteps_per_split;
+  const int kt_end = min(kt_begin + p.ksteps_per_split, nkt);
+  if (kt_begin >= kt_end) return;  // uniform per workgroup
+
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(p.dy, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+
+  // per instruction v: this lane's LDS row within the stage and the global column it fetches
+  int a_row[AI], a_col[AI];
+#pragma unroll
+  for (int v = 0; v < AI; ++v) {
+    const int row = (wid * AI + v) * ARPI + lane / ACPR, pos = lane % ACPR;
+    const int chunk = (((pos >> 1) ^ wg_swz<BM / 16>(row)) << 1) | (pos & 1);
+    a_row[v] = row;
+    a_col[v] = i0 + chunk * 8;
+  }
+  int b_row[BI], b_c[BI], b_dh[BI], b_dw[BI];
+  bool b_ok[BI];
+#pragma unroll
+  for (int v = 0; v < BI; ++v) {
+    const int row = (wid * BI + v) * BRPI + lane / BCPR, pos = lane % BCPR;
+    const int chunk = (((pos >> 1) ^ wg_swz<BN / 16>(row)) << 1) | (pos & 1);
+    const int col = j0 + chunk * 8;
+    int tap, c;
+    if constexpr (CBIG) {
+      tap = j0 / p.C;
+      c = j0 - tap * p.C + chunk * 8;
+    } else {
+      tap = (int)fdiv((uint32_t)col, p.fd_c);
+      c = col - tap * p.C;
+    }
+    const int r = (int)fdiv((uint32_t)tap, p.fd_s), s = tap - r * p.S;
+    b_row[v] = row;
+    b_c[v] = c;
+    b_dh[v] = r * p.dil_h - p.pad_h;
+    b_dw[v] = s * p.dil_w - p.pad_w;
+    b_ok[v] = col < p.K;
+  }
+
+  auto issue = [&](int stage, int kt) {
+    const int mb = kt * BK;
+    char* sA = smem + stage * STAGE;
+    char* sB = sA + BK * BM * 2;
+#pragma unroll
+    for (int v = 0; v < AI; ++v) {
+      const int m = mb + a_row[v];
+      const uint32_t off = (a_col[v] < p.Nout && m < p.M) ? (uint32_t)(m * p.ldy + a_col[v]) * 2u : HCB_OOB;
+      glds16(dyr, sA + (wid * AI + v) * ARPI * BM * 2, off);
+    }
+#pragma unroll
+    for (int v = 0; v < BI; ++v) {
+      const int m = mb + b_row[v];
+      uint32_t off = HCB_OOB;
+      if (b_ok[v] && m < p.M) {
+        const int n = (int)fdiv((uint32_t)m, p.fd_pq);
+        const int rem = m - n * p.P * p.Q;
+        const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
+        const int qq = rem - pp * p.Q;
+        const int h = pp * p.stride_h + b_dh[v], w = qq * p.stride_w + b_dw[v];
+        if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W)
+          off = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c[v]) * 2u;
+      }
+      glds16(xr, sB + (wid * BI + v) * BRPI * BN * 2, off);
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed fragment reads (lane supplies row + q4, columns col + 4*p4), swizzled slots
+  const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
+  auto tr_read_a = [&](const char* base, int row, int col) -> short4v {
+    const int rr = row + q4, cb = (col + 4 * p4) * 2;
+    const int slot = (cb >> 5) ^ wg_swz<BM / 16>(rr);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BM * 2 + slot * 32 + (cb & 31)));
+  };
+  auto tr_read_b = [&](const char* base, int row, int col) -> short4v {
+    const int rr = row + q4, cb = (col + 4 * p4) * 2;
+    const int slot = (cb >> 5) ^ wg_swz<BN / 16>(rr);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BN * 2 + slot * 32 + (cb & 31)));
+  };
+
+  const int nk = kt_end - kt_begin;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, kt_begin + s);
+  for (int k = 0; k < nk; ++k) {
+    // stage k has landed for this thread once at most min(NST-2, nk-1-k) later stages are
+    // outstanding; the barrier then publishes every thread's DMA
+    const int ahead = min(NST - 2, nk - 1 - k);
+    if (ahead >= 3)
+      wg_wait_vmcnt<(NST >= 5 ? 3 : 0) * LOADS>();
+    else if (ahead == 2)
+      wg_wait_vmcnt<(NST >= 4 ? 2 : 0) * LOADS>();
+    else if (ahead == 1)
+      wg_wait_vmcnt<LOADS>();
+    else
+      wg_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + NST - 1 < nk) issue((k + NST - 1) % NST, kt_begin + k + NST - 1);
+    const char* Ab = smem + (k % NST) * STAGE;
+    const char* Bb = Ab + BK * BM * 2;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int col = wm * TM + i * 16;
+        short4v lo = tr_read_a(Ab, ks * 32 + 8 * g, col);
+        short4v hi = tr_read_a(Ab, ks * 32 + 8 * g + 4, col);
+        short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, t);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = wn * TN + j * 16;
+        short4v lo = tr_read_b(Bb, ks * 32 + 8 * g, col);
+        short4v hi = tr_read_b(Bb, ks * 32 + 8 * g + 4, col);
+        short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, t);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every wave is done with the ring before the epilogue reuses LDS
+
+  constexpr int LDC = BN + 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * TM + i * 16 + g * 4 + e;
+        const int col = wn * TN + j * 16 + li;
+        Cs[row * LDC + col] = acc[i][j][e];
+      }
+  __syncthreads();
+  for (int idx = tid; idx < BM * BN; idx += NW * 64) {
+    const int row = idx / BN, col = idx - row * BN;
+    const int gi = i0 + row, gj = j0 + col;
+    if (gi < p.Nout && gj < p.K) atomicAdd(p.dw + (size_t)gi * p.K + gj, Cs[row * LDC + col]);
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int NST>
+static void wlaunch_glds(const WgradParams& p, int splits, hipStream_t st) {
+  constexpr int BM = WM * TM, BN = WN * TN;
+  const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
+  const size_t lds_main = (size_t)NST * 64 * (BM + BN) * 2;
+  const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
+  const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_glds_kernel<WM, WN, TM, TN, NST, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_glds_kernel<WM, WN, TM, TN, NST, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
+  }
+  dim3 grid(tiles * splits);
+  if ((p.C % BN) == 0)
+    hipLaunchKernelGGL((conv_wgrad_glds_kernel<WM, WN, TM, TN, NST, true>), grid, dim3(WM * WN * 64), lds, st, p);
+  else
+    hipLaunchKernelGGL((conv_wgrad_glds_kernel<WM, WN, TM, TN, NST, false>), grid, dim3(WM * WN * 64), lds, st, p);
+}
+
 template <int WM, int WN, int TM, int TN>
 static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
@@ -227,13 +441,31 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
   }
 }
 
-int wgrad_tile_m(int cfg) { return cfg == 0 ? 128 : (cfg == 1 ? 64 : 64); }
-int wgrad_tile_n(int cfg) { return cfg == 0 ? 128 : (cfg == 1 ? 128 : 64); }
+// cfg 0..2: register-staged {128x128, 64x128, 64x64}; 3..9: LDS-DMA ring {128x128 (4 waves of
+// 64x64, NST 4), 128x128 (8 waves of 64x32), 256x128 (8 waves of 64x64), 128x256 (8 waves of
+// 64x64), 64x128 (8 waves of 32x32, NST 4), 64x64 (4 waves, NST 4), 64x128 (4 waves of 64x32,
+// NST 4)}
+constexpr int N_WGRAD_CFG = 10;
+int wgrad_tile_m(int cfg) {
+  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64};
+  return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
+}
+int wgrad_tile_n(int cfg) {
+  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128};
+  return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
+}
 
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st) {
   switch (cfg) {
     case 0: wlaunch<2, 2, 64, 64>(p, splits, st); break;  // 128 x 128
     case 1: wlaunch<1, 4, 64, 32>(p, splits, st); break;  // 64 x 128
+    case 3: wlaunch_glds<2, 2, 64, 64, 4>(p, splits, st); break;
+    case 4: wlaunch_glds<2, 4, 64, 32, 3>(p, splits, st); break;
+    case 5: wlaunch_glds<4, 2, 64, 64, 3>(p, splits, st); break;
+    case 6: wlaunch_glds<2, 4, 64, 64, 3>(p, splits, st); break;
+    case 7: wlaunch_glds<2, 4, 32, 32, 4>(p, splits, st); break;
+    case 8: wlaunch_glds<2, 2, 32, 32, 4>(p, splits, st); break;
+    case 9: wlaunch_glds<1, 4, 64, 32, 4>(p, splits, st); break;
     default: wlaunch<2, 2, 32, 32>(p, splits, st); break; // 64 x 64
   }
 }

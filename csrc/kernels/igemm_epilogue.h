@@ -18,9 +18,47 @@ constexpr size_t igemm_epilogue_lds(int BM, int BN, int WM) {
   return (size_t)BM * (BN + 4) * 4 + (size_t)WM * 2 * BN * 4;
 }
 
+// Output row of GEMM row m (strided-output remap for strided 1x1 data gradients).
+__device__ __forceinline__ size_t epi_out_row(const ConvParams& p, int m) {
+  if (!p.remap) return (size_t)m;
+  const int PQ = p.P * p.Q;
+  int n = m / PQ, r = m - n * PQ;
+  int pp = r / p.Q, qq = r - pp * p.Q;
+  return ((size_t)n * p.OH + (size_t)pp * p.osh) * p.OW + (size_t)qq * p.osw;
+}
+
+// Register prefetch of the fused BN-backward epilogue operands (z, y and the beta source) for
+// one chunk of CH output segments per thread. A kernel with a short main loop issues the first
+// chunk BEFORE its main loop, so these loads share one memory latency with the A/B tiles
+// instead of paying a second one after the MFMAs (the stage-1 data-grad GEMMs have a single
+// 64-deep k-step and are bound by exactly this latency).
+template <int WM, int WN, int TM, int TN, bool BNB>
+struct EpiPrefetch {
+  static constexpr int BM = WM * TM, BN = WN * TN, SEGS = BN / 8, NT = WM * WN * 64;
+  static constexpr int ITER = BM * SEGS / NT;
+  static constexpr int CH = BNB ? (ITER < 4 ? ITER : 4) : 1;
+  u32x4 pr[CH], pz[CH], py[CH];
+  __device__ __forceinline__ void load(const ConvParams& p, int it0, int m0, int n0, int tid) {
+    const int col = n0 + (tid % SEGS) * 8;
+    if (col >= p.Nout) return;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int m = m0 + (tid + (it0 + k) * NT) / SEGS;
+      if (m < p.M) {
+        const size_t o = epi_out_row(p, m);
+        if (p.beta) pr[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.yres) + o * p.ldy + col);
+        pz[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_z) + o * p.bnb_ld + col);
+        if (p.bnb_mode == 1)
+          py[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_y) + o * p.bnb_ld + col);
+      }
+    }
+  }
+};
+
 template <int WM, int WN, int TM, int TN, bool BNB>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)[TM / 16][TN / 16], char* smem,
-                                               int tm, int m0, int n0, int wm, int wn, int lane, int tid) {
+                                               int tm, int m0, int n0, int wm, int wn, int lane, int tid,
+                                               EpiPrefetch<WM, WN, TM, TN, BNB>& pre, bool prefetched) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN + 4;
@@ -71,33 +109,18 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   const int col = n0 + cs * 8;
   const bool col_ok = col < p.Nout;
   const int PQ = p.P * p.Q;
-  auto out_row = [&](int m) -> size_t {
-    if (!p.remap) return (size_t)m;
-    int n = m / PQ, r = m - n * PQ;
-    int pp = r / p.Q, qq = r - pp * p.Q;
-    return ((size_t)n * p.OH + (size_t)pp * p.osh) * p.OW + (size_t)qq * p.osw;
-  };
+  auto out_row = [&](int m) -> size_t { return epi_out_row(p, m); };
   auto load_seg = [](const void* base, size_t row, int ld, int c) -> u32x4 {
     return *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(base) + row * ld + c);
   };
+  (void)PQ;
 
-  // fused BN-backward: prefetch z / y (and the beta source) of the first chunk of segments
-  // before the barrier; registers are sized for one chunk so the plain kernels are unaffected
-  constexpr int CH = BNB ? (ITER < 4 ? ITER : 4) : 1;
-  u32x4 pr[CH], pz[CH], py[CH];
-  auto prefetch = [&](int it0) {
-#pragma unroll
-    for (int k = 0; k < CH; ++k) {
-      const int m = m0 + (tid + (it0 + k) * NT) / SEGS;
-      if (col_ok && m < p.M) {
-        const size_t o = out_row(m);
-        if (p.beta) pr[k] = load_seg(p.yres, o, p.ldy, col);
-        pz[k] = load_seg(p.bnb_z, o, p.bnb_ld, col);
-        if (p.bnb_mode == 1) py[k] = load_seg(p.bnb_y, o, p.bnb_ld, col);
-      }
-    }
-  };
-  if constexpr (BNB) prefetch(0);
+  // fused BN-backward: the first chunk of z / y / beta-source segments is in flight before
+  // the barrier (or since before the main loop); registers hold one chunk
+  constexpr int CH = EpiPrefetch<WM, WN, TM, TN, BNB>::CH;
+  if constexpr (BNB) {
+    if (!prefetched) pre.load(p, 0, m0, n0, tid);
+  }
   __syncthreads();
 
   if (p.stats != nullptr) {
@@ -182,7 +205,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       bs2[e] = 0.f;
     }
     for (int it0 = 0; it0 < ITER; it0 += CH) {
-      if (it0 > 0) prefetch(it0);
+      if (it0 > 0) pre.load(p, it0, m0, n0, tid);
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
         const int row = (tid + (it0 + k) * NT) / SEGS;
@@ -193,15 +216,15 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
         stage_row(row, v);
         if (p.beta) {
           float o[8];
-          unpack8(pr[k], o);
+          unpack8(pre.pr[k], o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += o[e];
         }
         float zf[8];
-        unpack8(pz[k], zf);
+        unpack8(pre.pz[k], zf);
         if (p.bnb_mode == 1) {
           float yf[8];
-          unpack8(py[k], yf);
+          unpack8(pre.py[k], yf);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = yf[e] > 0.f ? v[e] : 0.f;
         } else if (p.bnb_mode == 2) {

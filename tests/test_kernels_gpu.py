@@ -238,6 +238,27 @@ def test_conv_wgrad(case):
     assert rel_err(dw, ref) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", list(range(10)))
+def test_conv_wgrad_all_configs(cfg):
+    """Every weight-grad tile config (register-staged 0-2, LDS-DMA ring 3-9) with split-K on
+    1x1 / 3x3 / strided / odd-channel geometries (partial tiles in Nout, K and pixels)."""
+    torch.manual_seed(6)
+    for cin, cout, k, s, pads, H, splits in [(64, 256, 1, 1, (0, 0, 0, 0), 14, 3),
+                                             (128, 128, 3, 2, (1, 1, 1, 1), 15, 2),
+                                             (80, 192, 3, 1, (0, 0, 0, 0), 11, 1),
+                                             (256, 72, 1, 1, (0, 0, 0, 0), 9, 4)]:
+        spec, p, pk = make_conv(cin, cout, k, k, s, s, pads)
+        N = 3
+        P, Q = spec.out_hw(H, H)
+        x = bf(torch.randn(N, H, H, cin, device=DEV))
+        dz = bf(torch.randn(N, P, Q, cout, device=DEV))
+        dw = torch.zeros(cout, spec.K, dtype=torch.float32, device=DEV)
+        Fn.conv_wgrad(dz, x, spec, dw, cfg=(cfg, splits))
+        ref = torch.zeros(cout, k, k, cin)
+        Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
+        assert rel_err(dw, ref.view(cout, -1)) < 1e-2, (cfg, cin, cout, k)
+
+
 def test_conv_wgrad_split_k_large_reduction():
     torch.manual_seed(5)
     spec, p, pk = make_conv(64, 64, 3, 3, 1, 1, (1, 1, 1, 1))
