@@ -103,6 +103,14 @@ class BenchmarkCNN:
         if p.num_epochs:
             self.num_batches = int(math.ceil(p.num_epochs * 1281167 / (self.batch_size * self.size)))
         self.step_offset = 0
+        if self.on_gpu and p.autotune:
+            # per-shape kernel configs (cached in tuned/mi355x.json; new shapes timed once here)
+            from ..ops import autotune
+
+            autotune.load_cache()
+            n = autotune.tune_model(self.model, self.batch_size, save=(self.rank == 0))
+            if n and self.rank == 0:
+                log_fn(f"Autotuned {n} conv problems")
         self._build_trainer()
 
     # ------------------------------------------------------------------ setup pieces

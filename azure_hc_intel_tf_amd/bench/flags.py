@@ -91,6 +91,7 @@ FLAGS: List[Flag] = [
     Flag("image_size", 0, int, "override the model's input resolution (0 = model default)"),
     # --- MI355X engine knobs
     Flag("use_hip_graph", True, parse_bool, "capture the training step in a HIP graph"),
+    Flag("autotune", True, parse_bool, "time the conv kernel configs of untuned shapes before the run"),
     Flag("comm_engine", "torch", str, "gradient allreduce engine: native (C++ RCCL) | torch",
          choices=["native", "torch"]),
     Flag("gradient_compression", "none", str, "none | fp16 | bf16 (Horovod Compression)",

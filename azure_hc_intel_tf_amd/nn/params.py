@@ -193,14 +193,15 @@ class ParamStore:
             if pk.want_tr:
                 pk.tr_off = poff
                 poff += _align(pk.C * pk.Kpad_t)
-            # the pack kernel moves 8-channel vectors (fp32 float4 pairs -> one 16-byte bf16 store)
-            assert pk.C % 8 == 0 and pk.Kpad % 64 == 0, f"pack of {pk.param.name}: C % 8, Kpad % 64"
             rows.append([pk.param.offset, pk.pack_off, pk.tr_off, pk.Nout, pk.R, pk.S, pk.C, pk.Kpad, pk.Kpad_t])
             work = pk.Nout * pk.Kpad + (pk.C * pk.Kpad_t if pk.want_tr else 0)
             self.pack_max_work = max(self.pack_max_work, work)
         self.pack_total = poff
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.packs:
+            # the pack kernel moves 8-channel vectors (fp32 float4 pairs -> one 16-byte bf16 store)
+            for pk in self.packs:
+                assert pk.C % 8 == 0 and pk.Kpad % 64 == 0, f"pack of {pk.param.name}: C % 8, Kpad % 64"
             self.pack_buf = torch.zeros(max(poff, ALIGN), dtype=dtype_pack, device=device)
             self.pack_table = torch.tensor(rows, dtype=torch.int64, device=device)
             for pk in self.packs:

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--no_tune", action="store_true", help="skip per-shape kernel autotuning")
     ap.add_argument("--compression", default=None, choices=[None, "fp16", "bf16"])
     ap.add_argument("--engine", default="native", choices=["native", "torch"])
+    ap.add_argument("--use_fp16", action="store_true",
+                    help="tf_cnn_benchmarks --use_fp16: 16-bit compute (bf16 on MI355X) with automatic loss scaling")
     args = ap.parse_args()
 
     import torch
@@ -94,7 +96,7 @@ def main():
         reducer.broadcast_(model.ps.buf, 0)
     images, labels = synthetic_batch(model, B, seed=rank)
     trainer = Trainer(model, B, resnet_lr_schedule(B * world), reducer=reducer, world_size=world,
-                      use_graph=not args.no_graph)
+                      use_graph=not args.no_graph, dynamic_loss_scale=args.use_fp16)
 
     def barrier():
         if world > 1:
@@ -122,7 +124,7 @@ def main():
     if rank == 0:
         res = {
             "metric": "images/sec (whole node) ResNet-50 bs=64/worker at 1/2/4/8 MI355X"
-            if args.model == "resnet50" else f"images/sec (whole node) {args.model} bs={B}/worker",
+            if (args.model == "resnet50" and B == 64) else f"images/sec (whole node) {args.model} bs={B}/worker",
             "value": round(ips, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -138,6 +140,7 @@ def main():
                        "image_size": model.image_size, "parallelism": f"dp{world}",
                        "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": not args.no_graph,
                        "engine": args.engine if world > 1 else None, "compression": args.compression,
+                       "loss_scaling": "dynamic" if args.use_fp16 else None,
                        "final_loss": round(loss, 4)},
         }
         print(json.dumps(res), flush=True)

@@ -362,6 +362,7 @@ void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx
   check_bf16(x, "x");
   check_bf16(y, "y");
   TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_fwd: C/ld % 8");
+  TORCH_CHECK(g[0] * g[5] * g[6] * (g[3] / 8) < (1ll << 31), "hcb.pool_fwd: 32-bit index range");
   check_range(x, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "x");
   check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "y");
   void* ip = nullptr;
@@ -385,6 +386,11 @@ void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::opt
   check_range(dx, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "dx");
   check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "y");
   check_range(dy, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "dy");
+  TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_bwd: C/ld % 8");
+  TORCH_CHECK(g[0] * g[1] * g[2] * (g[3] / 8) < (1ll << 31), "hcb.pool_bwd: 32-bit index range");
+  if (idx.has_value())
+    TORCH_CHECK(idx->scalar_type() == at::kByte && idx->is_contiguous() && idx->numel() >= g[0] * g[5] * g[6] * g[3],
+                "hcb.pool_bwd: idx must be contiguous uint8 [N,P,Q,C]");
   hcb::launch_pool_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), dx.data_ptr(), g[0], g[1], g[2], g[3],
                        g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], g[15],
                        accumulate ? 1 : 0, idx.has_value() ? idx->data_ptr() : nullptr, cur_stream());

@@ -18,16 +18,16 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const uint16_t* __restric
                                                        int ldy, int kh, int kw, int sh, int sw,
                                                        int ph, int pw, int is_max, int incl_pad,
                                                        uint8_t* __restrict__ amax) {
-  const int CV = C >> 3;
-  const long total = (long)N * P * Q * CV;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
-    int cv = (int)(idx % CV);
-    long pix = idx / CV;
-    int q = (int)(pix % Q);
-    long t = pix / Q;
-    int p = (int)(t % P);
-    int n = (int)(t / P);
+  // 32-bit index math (the host checks N*P*Q*C/8 < 2^31): 64-bit div/mod is emulated
+  const unsigned CV = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int cv = (int)(idx % CV);
+    const unsigned pix = idx / CV;
+    const int q = (int)(pix % (unsigned)Q);
+    const unsigned t = pix / (unsigned)Q;
+    const int p = (int)(t % (unsigned)P);
+    const int n = (int)(t / (unsigned)P);
     int h0 = p * sh - ph, w0 = q * sw - pw;
     float acc[8];
     int arg[8];
@@ -80,16 +80,15 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(
     const uint16_t* __restrict__ y, uint16_t* __restrict__ dx, int N, int H, int W, int C, int ldx,
     int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
     int incl_pad, int accum, const uint8_t* __restrict__ amax) {
-  const int CV = C >> 3;
-  const long total = (long)N * H * W * CV;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
-    int cv = (int)(idx % CV);
-    long pix = idx / CV;
-    int w = (int)(pix % W);
-    long t = pix / W;
-    int h = (int)(t % H);
-    int n = (int)(t / H);
+  const unsigned CV = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * H * W * CV;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int cv = (int)(idx % CV);
+    const unsigned pix = idx / CV;
+    const int w = (int)(pix % (unsigned)W);
+    const unsigned t = pix / (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
     float xv[8], g[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = 0.f;
@@ -167,6 +166,65 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(
   }
 }
 
+// Max-pool backward from the recorded argmax when at most NPW x NPW windows cover a pixel
+// (ceil(k/s) <= NPW; ResNet's 3x3/2: 2x2): the candidate windows are unrolled so all their dy /
+// argmax loads are in flight together instead of one loop trip at a time.
+template <int NPW>
+__global__ __launch_bounds__(256) void maxpool_bwd_amax_kernel(
+    const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N, int H, int W, int C, int ldx, int P, int Q,
+    int ldy, int kw, int sh, int sw, int ph, int pw, int accum, const uint8_t* __restrict__ amax) {
+  const unsigned CV = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * H * W * CV;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int cv = (int)(idx % CV);
+    const unsigned pix = idx / CV;
+    const int w = (int)(pix % (unsigned)W);
+    const unsigned t = pix / (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
+    // windows p with p*sh - ph <= h, i.e. p <= (h+ph)/sh, and h < p*sh - ph + kh
+    const int p_hi = (h + ph) / sh, q_hi = (w + pw) / sw;
+    u32x4 d[NPW][NPW];
+    u32x2 a[NPW][NPW];
+    bool ok[NPW][NPW];
+#pragma unroll
+    for (int i = 0; i < NPW; ++i)
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) {
+        const int p = p_hi - i, q = q_hi - j;
+        const int h0 = p * sh - ph, w0 = q * sw - pw;
+        ok[i][j] = p >= 0 && q >= 0 && p < P && q < Q && h - h0 < kw && w - w0 < kw;  // kh == kw
+        const size_t o = ((size_t)(n * P + (ok[i][j] ? p : 0)) * Q + (ok[i][j] ? q : 0));
+        d[i][j] = *reinterpret_cast<const u32x4*>(dy + o * ldy + cv * 8);
+        a[i][j] = *reinterpret_cast<const u32x2*>(amax + o * C + cv * 8);
+      }
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i)
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) {
+        const int p = p_hi - i, q = q_hi - j;
+        const int mine = (h - (p * sh - ph)) * kw + (w - (q * sw - pw));
+        if (!ok[i][j]) continue;
+        float f[8];
+        unpack8(d[i][j], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((a[i][j][e >> 2] >> (8 * (e & 3))) & 0xff) == mine) g[e] += f[e];
+      }
+    uint16_t* dp = dx + ((size_t)(n * H + h) * W + w) * ldx + cv * 8;
+    if (accum) {
+      float o[8];
+      unpack8(*reinterpret_cast<const u32x4*>(dp), o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] += o[e];
+    }
+    *reinterpret_cast<u32x4*>(dp) = pack8(g);
+  }
+}
+
 // global average pool [N][HW][C] -> [N][C]
 __global__ __launch_bounds__(256) void gap_fwd_kernel(const uint16_t* __restrict__ x,
                                                       uint16_t* __restrict__ y, int N, int HW,
@@ -227,6 +285,11 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
                      int pw, int is_max, int count_include_pad, int accum, const void* idx,
                      hipStream_t st) {
   long total = (long)N * H * W * (C / 8);
+  if (is_max && idx != nullptr && (kh + sh - 1) / sh <= 2 && (kw + sw - 1) / sw <= 2 && kh == kw && sh == sw) {
+    hipLaunchKernelGGL(maxpool_bwd_amax_kernel<2>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
+                       (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx);
+    return;
+  }
   hipLaunchKernelGGL(pool_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
                      (const uint16_t*)x, (const uint16_t*)y, (uint16_t*)dx, N, H, W, C, ldx, P, Q,
                      ldy, kh, kw, sh, sw, ph, pw, is_max, count_include_pad, accum,
