@@ -23,7 +23,8 @@ import torch
 
 from .flags import Params, noop_flags_set, parse_flags
 
-MODEL_DEFAULT_BATCH = {"inception3": 32, "trivial": 32}
+MODEL_DEFAULT_BATCH = {"inception3": 32, "trivial": 32, "alexnet": 512, "googlenet": 32, "overfeat": 32,
+                       "lenet": 32, "vgg11": 32, "vgg16": 32, "vgg19": 32}
 
 
 def log_fn(msg: str = ""):
@@ -123,7 +124,10 @@ class BenchmarkCNN:
         gb = self.batch_size * self.size
         if self.model_name.startswith("resnet"):
             return resnet_lr_schedule(gb)
-        return constant_lr(0.005 * gb / 32.0)
+        # tf_cnn_benchmarks Model defaults: a constant rate scaled by global batch / the
+        # model's default batch size
+        m = self.model
+        return constant_lr(getattr(m, "default_lr", 0.005) * gb / float(getattr(m, "default_batch_size", 32)))
 
     def _build_trainer(self):
         from ..parallel import make_reducer

@@ -43,7 +43,8 @@ FLAGS: List[Flag] = [
     Flag("batch_size", 0, int, "per-device (per-worker) batch size; 0 = model default"),
     Flag("num_warmup_batches", None, int, "untimed warmup steps (default: model/device dependent)"),
     Flag("num_batches", 100, int, "timed steps"),
-    Flag("model", "trivial", str, "model name (resnet50, resnet50_v1.5, resnet101, resnet152, inception3, trivial)"),
+    Flag("model", "trivial", str, "model name: resnet50|101|152[_v1.5], inception3, vgg11|16|19, alexnet, googlenet, "
+         "overfeat, lenet, trivial"),
     Flag("num_intra_threads", 0, int, "host intra-op threads (CPU path: torch.set_num_threads)"),
     Flag("num_inter_threads", 0, int, "host inter-op threads (CPU path)"),
     Flag("kmp_blocktime", 0, int, "KMP_BLOCKTIME for the CPU path", noop_on_gpu=True),

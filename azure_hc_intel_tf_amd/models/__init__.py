@@ -22,6 +22,15 @@ def _trivial(**kw):
     return Trivial(**kw)
 
 
+def _seq(cls_name, **fixed):
+    def make(**kw):
+        from . import sequential
+
+        return getattr(sequential, cls_name)(**fixed, **kw)
+
+    return make
+
+
 _MODELS = {
     "resnet50": _resnet(50, "v1"),
     "resnet50_v1.5": _resnet(50, "v1.5"),
@@ -31,6 +40,13 @@ _MODELS = {
     "resnet152_v1.5": _resnet(152, "v1.5"),
     "inception3": _inception3,
     "trivial": _trivial,
+    "vgg11": _seq("VGG", depth=11),
+    "vgg16": _seq("VGG", depth=16),
+    "vgg19": _seq("VGG", depth=19),
+    "alexnet": _seq("AlexNet"),
+    "overfeat": _seq("OverFeat"),
+    "lenet": _seq("LeNet"),
+    "googlenet": _seq("GoogLeNet"),
 }
 
 

@@ -35,7 +35,8 @@ class InceptionModule:
     """Columns of ('conv', C, kh, kw[, sh, sw, mode]) / ('mpool'|'apool', kh, kw, sh, sw, mode) /
     ('share',) -- the convnet_builder.inception_module DSL. Column outputs are concatenated."""
 
-    def __init__(self, ps, name, in_shape, cols):
+    def __init__(self, ps, name, in_shape, cols, conv_kw=None):
+        conv_kw = dict(relu=True, **BN_KW) if conv_kw is None else conv_kw
         self.name = name
         self.in_shape = in_shape
         self.nodes: List[_Node] = []
@@ -54,7 +55,7 @@ class InceptionModule:
                     if kind == "conv":
                         _, c, kh, kw = spec[:4]
                         sh, sw, mode = (spec[4], spec[5], spec[6]) if len(spec) > 4 else (1, 1, "SAME")
-                        layer = ConvBN(ps, lname, shape, c, kh, kw, sh, sw, mode, relu=True, **BN_KW)
+                        layer = ConvBN(ps, lname, shape, c, kh, kw, sh, sw, mode, **conv_kw)
                     elif kind in ("mpool", "apool"):
                         _, kh, kw, sh, sw, mode = spec
                         layer = Pool(lname, shape, kh, kw, sh, sw, mode, is_max=(kind == "mpool"))

@@ -116,7 +116,7 @@ class ConvBN(Layer):
     def __init__(self, ps: ParamStore, name: str, in_shape, cout: int, kh: int, kw: int, sh: int = 1,
                  sw: int = 1, mode="SAME", relu: bool = True, bn: bool = True, need_dx: bool = True,
                  eps: float = 1e-5, decay: float = 0.9, logical_cin: Optional[int] = None,
-                 dilation: int = 1, scale: bool = True):
+                 dilation: int = 1, scale: bool = True, init: str = "variance_scaling"):
         H, W, cin = in_shape
         self.name = name
         self.in_shape = in_shape
@@ -133,9 +133,9 @@ class ConvBN(Layer):
         self.decay = decay
         lc = logical_cin or cin
         fan_in = kh * kw * lc
-        self.w = ps.add(f"{name}/conv2d/kernel", (cout, kh, kw, cin), True,
-                        ps.variance_scaling(fan_in, lc if lc != cin else -1),
-                        logical_numel=cout * kh * kw * lc)
+        winit = (ps.glorot_uniform(fan_in, kh * kw * cout, lc if lc != cin else -1) if init == "glorot"
+                 else ps.variance_scaling(fan_in, lc if lc != cin else -1))
+        self.w = ps.add(f"{name}/conv2d/kernel", (cout, kh, kw, cin), True, winit, logical_numel=cout * kh * kw * lc)
         self.pack = ps.add_pack(self.w, cout, kh, kw, cin, self.spec.Kpad, self.spec.Kpad_t, want_tr=need_dx)
         if bn:
             if scale:
@@ -241,6 +241,8 @@ class ConvBN(Layer):
                                self.beta.grad, dz, gres)
         else:
             if self.relu:
+                if dy.is_cuda and not (dy.is_contiguous() and y.is_contiguous()):
+                    dy, y = dy.contiguous(), y.contiguous()  # concat-window views (GoogLeNet)
                 dz = Fn.relu_backward(dy, y, empty_act((N, P, Q, C), dev))
             else:
                 dz = dy if dy.is_contiguous() else dy.contiguous()
@@ -309,6 +311,48 @@ class Pool(Layer):
 
     def clear(self):
         self._saved = None
+
+
+class Dropout(Layer):
+    """tf_cnn_benchmarks ``cnn.dropout(keep_prob=0.5)`` after the hidden affine layers of
+    AlexNet / VGG / OverFeat. Identity when ``keep == 1`` or in forward-only mode."""
+
+    def __init__(self, name, in_shape, keep: float = 0.5, seed: int = 0):
+        self.name = name
+        self.in_shape = in_shape
+        self.out_shape = in_shape
+        self.keep = keep
+        self.seed = seed
+        self.training = True
+        self._step = None
+        self._mask = None
+
+    def forward(self, x):
+        if self.keep >= 1.0 or not self.training:
+            self._mask = None
+            return x
+        if self._step is None or self._step.device != x.device:
+            self._step = torch.zeros(1, dtype=torch.int64, device=x.device)
+        y = torch.empty_like(x)
+        if x.is_cuda:
+            mask = torch.empty((x.numel() + 7) // 8, dtype=torch.uint8, device=x.device)
+        else:
+            mask = torch.empty(x.shape, dtype=torch.bool)
+        Fn.dropout_forward(x, y, mask, self.keep, self.seed, self._step)
+        self._step.add_(1)  # device-side: a replayed graph advances it too
+        self._mask = mask
+        return y
+
+    def backward(self, dy):
+        if self._mask is None:
+            return dy
+        dx = torch.empty_like(dy)
+        Fn.dropout_backward(dy.contiguous(), self._mask, dx, self.keep)
+        self._mask = None
+        return dx
+
+    def clear(self):
+        self._mask = None
 
 
 class GlobalAvgPool(Layer):

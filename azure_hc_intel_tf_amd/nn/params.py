@@ -141,6 +141,21 @@ class ParamStore:
 
         return f
 
+    def glorot_uniform(self, fan_in: int, fan_out: int, logical_c: int = -1):
+        """tf.glorot_uniform_initializer() -- the tf.layers default kernel initializer, which
+        tf_cnn_benchmarks' convnet_builder uses for the conv / affine layers of the models
+        without batch norm (VGG, AlexNet, OverFeat, LeNet, GoogLeNet)."""
+        limit = math.sqrt(6.0 / (fan_in + fan_out))
+        gen = self.gen
+
+        def f(t):
+            v = torch.empty(t.shape, dtype=torch.float32).uniform_(-limit, limit, generator=gen)
+            if logical_c > 0 and t.dim() == 4 and t.shape[3] > logical_c:
+                v[..., logical_c:] = 0
+            t.copy_(v)
+
+        return f
+
     @staticmethod
     def const(v: float):
         return lambda t: t.fill_(v)

@@ -586,6 +586,29 @@ def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None)
     dlogits[:, :ncls].copy_(p * scale)
 
 
+def dropout_forward(x, y, mask, keep: float, seed: int, step):
+    """y = x * m / keep with m ~ Bernoulli(keep) (tf.nn.dropout). GPU: the mask is a hash of
+    (seed, step[0], index), one bit per element in ``mask`` (uint8, numel/8); ``step`` is a
+    device int64 counter so captured-graph replays draw fresh masks. CPU: ``mask`` is a bool
+    tensor of x's shape drawn from a generator seeded with (seed, step)."""
+    if x.is_cuda:
+        _ext.ops().dropout_fwd(x, y, mask, float(keep), int(seed), step)
+        return y
+    g = torch.Generator().manual_seed(int(seed) * 1000003 + int(step[0]))
+    m = torch.rand(x.shape, generator=g) < keep
+    mask.copy_(m)
+    y.copy_(x * m.to(x.dtype) / keep)
+    return y
+
+
+def dropout_backward(dy, mask, dx, keep: float):
+    if dy.is_cuda:
+        _ext.ops().dropout_bwd(dy, mask, dx, float(keep))
+        return dx
+    dx.copy_(dy * mask.to(dy.dtype) / keep)
+    return dx
+
+
 def colsum(g, M, N, out):
     if g.is_cuda:
         _ext.ops().colsum(g, ld(g), M, N, out)

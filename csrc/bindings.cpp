@@ -448,7 +448,11 @@ void colsum(const Tensor& g, int64_t ld, int64_t M, int64_t N, const Tensor& out
   check_f32(out, "out");
   bool f32 = g.scalar_type() == at::kFloat;
   TORCH_CHECK(f32 || g.scalar_type() == at::kBFloat16, "hcb.colsum: dtype");
-  check_range(g, ((M - 1) * ld + N) * (f32 ? 4 : 2), "g");
+  // the kernel reads whole 8-column vectors: rows padded to 8 columns, 16-byte aligned
+  TORCH_CHECK(ld % 8 == 0 && ld >= ((N + 7) / 8) * 8, "hcb.colsum: ld must be a multiple of 8 covering N");
+  check_range(g, ((M - 1) * ld + ((N + 7) / 8) * 8) * (f32 ? 4 : 2), "g");
+  check_align16(g.data_ptr(), "g");
+  TORCH_CHECK(out.numel() >= N, "hcb.colsum: out too small");
   hcb::launch_colsum2(g.data_ptr(), (int)ld, (int)M, (int)N, f32 ? 1 : 0, out.data_ptr<float>(), cur_stream());
 }
 
@@ -582,6 +586,33 @@ void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
   hcb::launch_relu_bwd(dy.data_ptr(), y.data_ptr(), dz.data_ptr(), dy.numel(), cur_stream());
 }
 
+void dropout_fwd(const Tensor& x, const Tensor& y, const Tensor& mask, double keep, int64_t seed, const Tensor& step) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  check_cuda(mask, "mask");
+  check_cuda(step, "step");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && mask.is_contiguous(), "hcb.dropout_fwd: contiguous");
+  TORCH_CHECK(x.numel() == y.numel() && x.numel() % 8 == 0 && mask.scalar_type() == at::kByte &&
+                  mask.numel() * 8 >= x.numel(),
+              "hcb.dropout_fwd: sizes (mask: one bit per element)");
+  TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() >= 1, "hcb.dropout_fwd: step int64");
+  TORCH_CHECK(keep > 0.0 && keep <= 1.0, "hcb.dropout_fwd: 0 < keep <= 1");
+  hcb::launch_dropout_fwd(x.data_ptr(), y.data_ptr(), mask.data_ptr<uint8_t>(), x.numel(), (float)keep, (uint64_t)seed,
+                          step.data_ptr<int64_t>(), cur_stream());
+}
+
+void dropout_bwd(const Tensor& dy, const Tensor& mask, const Tensor& dx, double keep) {
+  check_bf16(dy, "dy");
+  check_bf16(dx, "dx");
+  check_cuda(mask, "mask");
+  TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous() && mask.is_contiguous(), "hcb.dropout_bwd: contiguous");
+  TORCH_CHECK(dy.numel() == dx.numel() && dy.numel() % 8 == 0 && mask.scalar_type() == at::kByte &&
+                  mask.numel() * 8 >= dy.numel(),
+              "hcb.dropout_bwd: sizes");
+  TORCH_CHECK(keep > 0.0 && keep <= 1.0, "hcb.dropout_bwd: 0 < keep <= 1");
+  hcb::launch_dropout_bwd(dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), dy.numel(), (float)keep, cur_stream());
+}
+
 void scale_f32(const Tensor& x, double s) {
   check_f32(x, "x");
   TORCH_CHECK(x.is_contiguous(), "hcb.scale_f32: contiguous");
@@ -691,6 +722,8 @@ TORCH_LIBRARY(hcb, m) {
   m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
   m.def("preprocess_images(Tensor src, Tensor desc, Tensor desc_host, Tensor(a!) out, float[] scale, float[] bias) -> ()");
+  m.def("dropout_fwd(Tensor x, Tensor(a!) y, Tensor(b!) mask, float keep, int seed, Tensor step) -> ()");
+  m.def("dropout_bwd(Tensor dy, Tensor mask, Tensor(a!) dx, float keep) -> ()");
   m.def("synth_images(Tensor(a!) out, int C, int Cpad, float mean, float std, int seed) -> ()");
   m.def("synth_labels(Tensor(a!) out, int ncls, int seed) -> ()");
   m.def("bucket_pack(Tensor src, Tensor(a!) dst, float scale) -> ()");
@@ -727,6 +760,8 @@ TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("bn_bwd_apply_acc", bn_bwd_apply_acc);
   m.impl("l2norm_sq", l2norm_sq);
   m.impl("synth_images", synth_images);
+  m.impl("dropout_fwd", dropout_fwd);
+  m.impl("dropout_bwd", dropout_bwd);
   m.impl("preprocess_images", preprocess_images);
   m.impl("synth_labels", synth_labels);
   m.impl("bucket_pack", bucket_pack);

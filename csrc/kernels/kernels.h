@@ -166,6 +166,10 @@ struct WPackEntry {  // all int64 so the table is a plain int64 tensor [n][9]
 };
 void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
                         int n_entries, int64_t max_work, hipStream_t st);
+// dropout on bf16 activations (n % 8 == 0): mask = 1 bit per element packed 8 per byte
+void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
+                        const int64_t* step, hipStream_t st);
+void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float keep, hipStream_t st);
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 void launch_add_bf16(const void* a, const void* b, void* y, int64_t n, hipStream_t st);

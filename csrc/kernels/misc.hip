@@ -54,22 +54,46 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   }
 }
 
-// column sums: out[n] = sum_m g[m][n] (bf16 or fp32 input), fp32 out
+// column sums: out[n] += sum_m g[m][n] (bf16 or fp32 input, fp32 out; `out` is zeroed by the
+// caller). A block covers 256 columns (32 lanes x 8-column vectors) and 8 row lanes that
+// stride over M; the 8 row partials meet in LDS and one fp32 atomic per column and block
+// publishes them. (The bias gradient of a conv over a 224x224 map reduces 3.2 M rows.)
 __global__ __launch_bounds__(256) void colsum_kernel(const void* g, int ld, int M, int N, int is_f32,
                                                      float* out) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int m = 0; m < M; ++m) {
-    if (is_f32)
-      s += reinterpret_cast<const float*>(g)[(size_t)m * ld + n];
-    else
-      s += bf2f(reinterpret_cast<const uint16_t*>(g)[(size_t)m * ld + n]);
+  __shared__ float part[8][257];
+  const int lane = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c0 = (blockIdx.y * 32 + lane) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < N) {
+    for (int m = blockIdx.x * 8 + rl; m < M; m += gridDim.x * 8) {
+      float f[8];
+      if (is_f32) {
+        const f32x4* r = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(g) + (size_t)m * ld + c0);
+        const f32x4 a = r[0], b = r[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          f[e] = a[e];
+          f[4 + e] = b[e];
+        }
+      } else {
+        unpack8(*reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(g) + (size_t)m * ld + c0), f);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += f[e];
+    }
   }
-  out[n] = s;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[rl][lane * 8 + e] = acc[e];
+  __syncthreads();
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s += part[r][threadIdx.x];
+    atomicAdd(out + c, s);
+  }
 }
 
-// ------------------------------------------------------------------ optimizer
 __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w,
                                                            float* __restrict__ mom,
                                                            const float* __restrict__ g, int64_t n,
@@ -211,6 +235,49 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
       }
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ dropout
+// tf.nn.dropout semantics: keep with probability `keep`, scale kept values by 1/keep. The mask
+// bit of element i is a counter-based hash of (seed, step, i) -- no RNG state to carry -- and
+// `step` is read from device memory so every replay of a captured graph draws a new mask.
+__device__ __forceinline__ uint32_t dropout_mix32(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+__global__ __launch_bounds__(256) void dropout_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ mask, int64_t n8, uint32_t thresh,
+                                                          float inv_keep, uint64_t seed,
+                                                          const int64_t* __restrict__ step) {
+  const uint64_t base = seed * 0x9E3779B97F4A7C15ull + (uint64_t)(*step) * 0xD1B54A32D192ED03ull;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const u32x4*>(x)[i], f);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool keep = dropout_mix32(base + (uint64_t)(i * 8 + e)) < thresh;
+      f[e] = keep ? f[e] * inv_keep : 0.f;
+      bits |= (keep ? 1u : 0u) << e;
+    }
+    reinterpret_cast<u32x4*>(y)[i] = pack8(f);
+    mask[i] = (uint8_t)bits;
+  }
+}
+
+__global__ __launch_bounds__(256) void dropout_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ mask, uint16_t* __restrict__ dx,
+                                                          int64_t n8, float inv_keep) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const u32x4*>(dy)[i], f);
+    const uint32_t bits = mask[i];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = ((bits >> e) & 1u) ? f[e] * inv_keep : 0.f;
+    reinterpret_cast<u32x4*>(dx)[i] = pack8(f);
   }
 }
 
@@ -369,8 +436,13 @@ void launch_loss_scale_update(float* hyper, float world, int dynamic, hipStream_
   hipLaunchKernelGGL(loss_scale_update_kernel, dim3(1), dim3(1), 0, st, hyper, world, dynamic);
 }
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256), dim3(256), 0, st, g, ld, M, N, is_f32,
-                     out);
+  const int gy = (N + 255) / 256;
+  int gx = (M + 63) / 64;  // >= 8 rows per thread
+  const int cap = (2048 + gy - 1) / gy;
+  if (gx > cap) gx = cap;
+  if (gx < 1) gx = 1;
+  (void)hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, st, g, ld, M, N, is_f32, out);
 }
 void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
                          const float* hyper, float* l2_out, int nesterov, int hyper_n, hipStream_t st) {
@@ -386,6 +458,16 @@ void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* e
   int gx = units > 1024 ? 1024 : (int)units;
   hipLaunchKernelGGL(weight_pack_kernel, dim3(gx, n_entries), dim3(256), 0, st, master, pack,
                      entries_dev);
+}
+void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
+                        const int64_t* step, hipStream_t st) {
+  const uint32_t thresh = keep >= 1.f ? 0xffffffffu : (uint32_t)((double)keep * 4294967296.0);
+  hipLaunchKernelGGL(dropout_fwd_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y,
+                     mask, n / 8, thresh, 1.f / keep, seed, step);
+}
+void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float keep, hipStream_t st) {
+  hipLaunchKernelGGL(dropout_bwd_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)dy, mask,
+                     (uint16_t*)dx, n / 8, 1.f / keep);
 }
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);

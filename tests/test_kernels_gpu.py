@@ -359,6 +359,20 @@ def test_gap_and_softmax_and_colsum():
     assert rel_err(cs, dl.float().cpu()[:, :ncls].sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("M,N,f32", [(200_003, 64, False), (1_000, 1001, False), (5_000, 24, True), (3, 256, False)])
+def test_colsum_large_reductions(M, N, f32):
+    """bias gradients: the parallel column sum over up to millions of rows (row-strided
+    vectors, LDS partials, one atomic per column and block)."""
+    torch.manual_seed(13)
+    ldg = (N + 7) // 8 * 8
+    g = torch.randn(M, ldg, device=DEV)
+    g = g if f32 else bf(g)
+    out = torch.full((N,), 123.0, device=DEV)  # overwritten, not accumulated
+    Fn.colsum(g, M, N, out)
+    ref = g.float().cpu()[:, :N].double().sum(0)
+    assert rel_err(out, ref.float()) < 1e-4
+
+
 def test_sgd_momentum_flat():
     torch.manual_seed(9)
     n, nd = 100_003, 60_000
