@@ -10,6 +10,15 @@ def _resnet(depth, version):
     return lambda **kw: ResNet(depth=depth, version=version, **kw)
 
 
+def _resnet_v2(depth):
+    def make(**kw):
+        from .resnet import ResNetV2
+
+        return ResNetV2(depth=depth, **kw)
+
+    return make
+
+
 def _inception3(**kw):
     from .inception import InceptionV3
 
@@ -38,6 +47,9 @@ _MODELS = {
     "resnet101_v1.5": _resnet(101, "v1.5"),
     "resnet152": _resnet(152, "v1"),
     "resnet152_v1.5": _resnet(152, "v1.5"),
+    "resnet50_v2": _resnet_v2(50),
+    "resnet101_v2": _resnet_v2(101),
+    "resnet152_v2": _resnet_v2(152),
     "inception3": _inception3,
     "trivial": _trivial,
     "vgg11": _seq("VGG", depth=11),

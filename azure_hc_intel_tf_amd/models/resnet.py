@@ -8,13 +8,14 @@ Architecture (tf_cnn_benchmarks resnet_model semantics):
      depths 256/512/1024/2048, bottleneck widths 64/128/256/512,
      v1: stride on the first 1x1 of the first block of stages 2-4,
      v1.5: stride on the 3x3 instead; projection shortcut (1x1 conv + BN) when the
-     channel count changes
+     channel count changes; v2 (``ResNetV2``): pre-activation blocks
   -> spatial mean -> affine 2048 -> 1001 classes (ImageNet + background).
 BN: decay 0.9, epsilon 1e-5, scale=True. ResNet-50 v1: 25,559,081 trainable params.
 """
 from __future__ import annotations
 
-from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, join_side_streams
+from ..nn.layers import BNReLU, ConvBN, GlobalAvgPool, Logits, Pool, join_side_streams
+from ..ops import functional as Fn
 from .base import CNNModel
 
 LAYER_COUNTS = {18: None, 50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}
@@ -123,3 +124,93 @@ class ResNet(CNNModel):
         self._last = None
         join_side_streams()
         yield seg + [self.pool, self.stem], True
+
+
+class PreActBottleneck:
+    """tf_cnn_benchmarks ``bottleneck_block_v2`` (pre-activation ResNet): preact = relu(BN(x));
+    shortcut = x (identity) or a bias-free 1x1 projection of preact; 1x1 (stride) conv+BN+ReLU
+    -> 3x3 conv+BN+ReLU -> bias-free 1x1 conv whose GEMM epilogue adds the shortcut."""
+
+    def __init__(self, ps, name, in_shape, depth, bottleneck, stride):
+        H, W, C = in_shape
+        self.pre = BNReLU(ps, f"{name}/preact", in_shape)
+        self.proj = C != depth
+        if self.proj:
+            self.sc = ConvBN(ps, f"{name}/shortcut", in_shape, depth, 1, 1, stride, stride, "SAME", relu=False,
+                             bn=False, bias=False)
+        else:
+            assert stride == 1, "identity shortcut with stride is not used by these ResNets"
+            self.sc = None
+        self.c1 = ConvBN(ps, f"{name}/conv1", in_shape, bottleneck, 1, 1, stride, stride, "SAME")
+        self.c2 = ConvBN(ps, f"{name}/conv2", self.c1.out_shape, bottleneck, 3, 3, 1, 1, "SAME_RESNET")
+        self.c3 = ConvBN(ps, f"{name}/conv3", self.c2.out_shape, depth, 1, 1, 1, 1, "SAME", relu=False, bn=False,
+                         bias=False)
+        self.in_shape = in_shape
+        self.out_shape = self.c3.out_shape
+
+    def layers(self):
+        return [l for l in (self.pre, self.sc, self.c1, self.c2, self.c3) if l is not None]
+
+    def forward(self, x):
+        a = self.pre.forward(x)
+        sc = self.sc.forward(a) if self.proj else x
+        h = self.c2.forward(self.c1.forward(a))
+        return self.c3.forward(h, residual=sc)
+
+    def backward(self, dy):
+        d2, gres = self.c3.backward(dy, want_gres=True)  # gres = dy: the shortcut's gradient
+        d1, _ = self.c2.backward(d2)
+        if self.proj:
+            da, _ = self.sc.backward(gres)
+            self.c1.backward(d1, dx=da, accumulate=True)
+            return self.pre.backward(da)
+        da, _ = self.c1.backward(d1)
+        dx = self.pre.backward(da)
+        return Fn.add(dx, gres)  # identity shortcut: d(x) += dy
+
+
+class ResNetV2(CNNModel):
+    """ResNet v2 (``--model=resnet50_v2`` / 101 / 152): stem conv+BN+ReLU, max pool, the
+    pre-activation bottleneck stages (stride on the first 1x1, as tf_cnn_benchmarks), a final
+    BN + ReLU, spatial mean, affine."""
+
+    default_image_size = 224
+
+    def __init__(self, depth: int = 50, **kw):
+        self.depth = depth
+        self.name = f"resnet{depth}_v2"
+        super().__init__(**kw)
+
+    def build(self):
+        ps = self.ps
+        S = self.image_size
+        self.stem = ConvBN(ps, "conv0", (S, S, self.image_channels), 64, 7, 7, 2, 2, "SAME_RESNET", relu=True,
+                           need_dx=False, logical_cin=3)
+        self.pool = Pool("mpool0", self.stem.out_shape, 3, 3, 2, 2, "SAME", is_max=True)
+        shape = self.pool.out_shape
+        self.blocks = []
+        for si, (n, depth, bott) in enumerate(zip(LAYER_COUNTS[self.depth], (256, 512, 1024, 2048),
+                                                  (64, 128, 256, 512))):
+            for bi in range(n):
+                stride = 2 if (si > 0 and bi == 0) else 1
+                blk = PreActBottleneck(ps, f"stage{si + 1}/block{bi + 1}", shape, depth, bott, stride)
+                self.blocks.append(blk)
+                shape = blk.out_shape
+        self.post = BNReLU(ps, "postnorm", shape)
+        self.gap = GlobalAvgPool("spatial_mean", shape)
+        self.fc = Logits(ps, "logits", shape[2], self.num_classes)
+        self.layers = ([self.stem, self.pool] + [l for b in self.blocks for l in b.layers()]
+                       + [self.post, self.gap, self.fc])
+
+    def forward(self, images):
+        x = self.pool.forward(self.stem.forward(images))
+        for b in self.blocks:
+            x = b.forward(x)
+        return self.fc.forward(self.gap.forward(self.post.forward(x)))
+
+    def backward(self, dlogits):
+        dx = self.post.backward(self.gap.backward(self.fc.backward(dlogits)))
+        for b in reversed(self.blocks):
+            dx = b.backward(dx)
+        self.stem.backward(self.pool.backward(dx))
+        join_side_streams()

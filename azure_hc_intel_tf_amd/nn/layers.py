@@ -116,7 +116,7 @@ class ConvBN(Layer):
     def __init__(self, ps: ParamStore, name: str, in_shape, cout: int, kh: int, kw: int, sh: int = 1,
                  sw: int = 1, mode="SAME", relu: bool = True, bn: bool = True, need_dx: bool = True,
                  eps: float = 1e-5, decay: float = 0.9, logical_cin: Optional[int] = None,
-                 dilation: int = 1, scale: bool = True, init: str = "variance_scaling"):
+                 dilation: int = 1, scale: bool = True, init: str = "variance_scaling", bias: bool = True):
         H, W, cin = in_shape
         self.name = name
         self.in_shape = in_shape
@@ -152,7 +152,8 @@ class ConvBN(Layer):
             self.sv_mean = ps.add_stat(f"{name}/bn_mean", (cout,))
             self.sv_invstd = ps.add_stat(f"{name}/bn_invstd", (cout,))
         else:
-            self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0))
+            # ResNet-v2's un-normalised convs (shortcut, conv3) have no bias in tf_cnn_benchmarks
+            self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0)) if bias else None
         self._saved = None
         self._pre_reduced = False
 
@@ -163,7 +164,7 @@ class ConvBN(Layer):
     def params(self):
         """Trainable ParamRefs of this layer (gradient slots in the flat buffer)."""
         if not self.bn:
-            return [self.w, self.bias]
+            return [self.w, self.bias] if self.bias is not None else [self.w]
         out = [self.w, self.beta]
         if not isinstance(self.gamma, _FixedParam):
             out.append(self.gamma)
@@ -190,10 +191,10 @@ class ConvBN(Layer):
                                       self.decay, self.eps, y, self.relu, residual=residual)
             self._saved = (x, z, y, saved, residual is not None)
             return y
-        assert residual is None, "conv without BN: no residual input"
+        assert residual is None or not self.relu, "conv without BN: residual add only without ReLU"
         y = out if out is not None else empty_act((N, P, Q, C), dev)
-        Fn.conv_forward(x, self.spec, self.pack.pack if x.is_cuda else None, self.w.data, y, bias=self.bias.data,
-                        relu=self.relu)
+        Fn.conv_forward(x, self.spec, self.pack.pack if x.is_cuda else None, self.w.data, y,
+                        bias=self.bias.data if self.bias is not None else None, relu=self.relu, residual=residual)
         self._saved = (x, None, y, None, False)
         return y
 
@@ -246,7 +247,8 @@ class ConvBN(Layer):
                 dz = Fn.relu_backward(dy, y, empty_act((N, P, Q, C), dev))
             else:
                 dz = dy if dy.is_contiguous() else dy.contiguous()
-            Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
+            if self.bias is not None:
+                Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
                 gres = dz
         if dz.is_cuda and WGRAD_STREAM:
@@ -306,6 +308,49 @@ class Pool(Layer):
             accumulate = False
         Fn.pool_backward(dy, x, y, dx, *self.k, *self.s, self.pads, self.is_max, self.incl_pad, accumulate,
                          argmax=amax)
+        self._saved = None
+        return dx
+
+    def clear(self):
+        self._saved = None
+
+
+class BNReLU(Layer):
+    """Standalone training-mode BatchNorm (+ ReLU) on an activation: the pre-activation of
+    ResNet v2 blocks (tf_cnn_benchmarks ``bottleneck_block_v2``: preact = relu(batch_norm(x)))
+    and its final BN. Statistics come from a reduction kernel over the input (there is no
+    producing GEMM epilogue to fuse them into)."""
+
+    def __init__(self, ps: ParamStore, name: str, in_shape, relu: bool = True, eps: float = 1e-5,
+                 decay: float = 0.9):
+        self.name = name
+        self.in_shape = in_shape
+        self.out_shape = in_shape
+        C = in_shape[2]
+        self.relu = relu
+        self.eps = eps
+        self.decay = decay
+        self.gamma = ps.add(f"{name}/batchnorm/gamma", (C,), False, ParamStore.const(1.0))
+        self.beta = ps.add(f"{name}/batchnorm/beta", (C,), False, ParamStore.const(0.0))
+        self.rmean = ps.add_buffer(f"{name}/batchnorm/moving_mean", (C,), 0.0)
+        self.rvar = ps.add_buffer(f"{name}/batchnorm/moving_variance", (C,), 1.0)
+        self._saved = None
+
+    def params(self):
+        return [self.beta, self.gamma]
+
+    def forward(self, x):
+        y = empty_act(tuple(x.shape), x.device)
+        saved = Fn.bn_forward(x, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
+                              self.eps, y, self.relu)
+        self._saved = (x, y, saved)
+        return y
+
+    def backward(self, dy):
+        x, y, saved = self._saved
+        dx = empty_act(tuple(x.shape), dy.device)
+        Fn.bn_backward(dy if dy.is_contiguous() else dy.contiguous(), y, x, saved, self.gamma.data, self.beta.data,
+                       1 if self.relu else 0, self.gamma.grad, self.beta.grad, dx)
         self._saved = None
         return dx
 

@@ -215,7 +215,7 @@ def set_tuned(table: dict) -> None:
 
 # ---------------------------------------------------------------- conv forward
 def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None, relu=False,
-                 stats_R: int = 0):
+                 stats_R: int = 0, residual=None):
     """out[N,P,Q,cout] = conv(x, W) (+bias) [ReLU]. GPU: fp32 acc, bf16 (or fp32) out + fused BN
     statistics: per-tile slab (stats_R=0) or fp32 atomics into stats_R replicas of [2][cout]."""
     N, H, W, _ = x.shape
@@ -225,9 +225,11 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
         cfg, splits = _plan(cfg, M, spec.cout, spec.K, x.device)
         out_f32 = out.dtype == torch.float32
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
-                spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1, 0,
-                1 if out_f32 else 0, 1 if relu else 0, int(stats_R), splits]
-        _ext.ops().conv_igemm(x, wpack, out, None, bias, stats, geom, cfg)
+                spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1,
+                1 if residual is not None else 0, 1 if out_f32 else 0, 1 if relu else 0, int(stats_R), splits]
+        if residual is not None:  # beta-accumulate epilogue: out = conv(x) + residual (same layout)
+            assert ld(residual) == ld(out) and residual.shape == out.shape
+        _ext.ops().conv_igemm(x, wpack, out, residual, bias, stats, geom, cfg)
         return out
     xt = x.permute(0, 3, 1, 2)
     if spec.pt or spec.pb or spec.pl or spec.pr:
@@ -236,7 +238,10 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
     y = F.conv2d(xt, wt, bias=None if bias is None else bias.to(x.dtype), stride=(spec.sh, spec.sw), dilation=(spec.dh, spec.dw))
     if relu:
         y = torch.relu(y)
-    out.copy_(y.permute(0, 2, 3, 1))
+    y = y.permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual
+    out.copy_(y)
     return out
 
 
@@ -584,6 +589,17 @@ def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None)
     p[torch.arange(B), labels] -= 1.0
     dlogits.zero_()
     dlogits[:, :ncls].copy_(p * scale)
+
+
+def add(a, b, out=None):
+    """out = a + b on activations (bf16 HIP kernel on the GPU)."""
+    out = torch.empty_like(a) if out is None else out
+    if a.is_cuda:
+        a, b = a.contiguous(), b.contiguous()
+        _ext.ops().add_bf16(a, b, out)
+        return out
+    torch.add(a, b, out=out)
+    return out
 
 
 def dropout_forward(x, y, mask, keep: float, seed: int, step):

@@ -16,7 +16,8 @@ def rel_err(a, b):
 
 
 @pytest.mark.parametrize("name,size,batch", [("resnet50", 128, 16), ("resnet50_v1.5", 128, 16),
-                                             ("inception3", 299, 4), ("trivial", 64, 16)])
+                                             ("inception3", 299, 4), ("trivial", 64, 16),
+                                             ("resnet50_v2", 128, 16)])
 def test_model_gpu_forward_and_descent(name, size, batch):
     """At random init the gradients of this BN network are chaotic in the rounding (an fp32
     CPU run already differs from fp64 autograd by ~1% and bf16 rounding decorrelates deep

@@ -46,3 +46,44 @@ def test_training_reduces_loss():
     for _ in range(6):
         last = float(t.step(img, lab))
     assert last < first
+
+
+def _bnrelu_ref(layer, x, params, relu=True):
+    z = torch.nn.functional.batch_norm(x, None, None, params[layer.gamma.name], params[layer.beta.name],
+                                       training=True, eps=layer.eps)
+    return torch.relu(z) if relu else z
+
+
+def resnet_v2_ref(model, images_nhwc, params):
+    from reference_models import conv_ref, convbn_ref, pool_ref
+
+    x = images_nhwc.permute(0, 3, 1, 2)
+    x = pool_ref(model.pool, convbn_ref(model.stem, x, params))
+    for b in model.blocks:
+        a = _bnrelu_ref(b.pre, x, params)
+        sc = conv_ref(b.sc, a, params) if b.proj else x
+        h = convbn_ref(b.c2, convbn_ref(b.c1, a, params), params)
+        x = conv_ref(b.c3, h, params) + sc
+    x = _bnrelu_ref(model.post, x, params)
+    feat = x.mean(dim=(2, 3))
+    w = params[model.fc.w.name].view(model.fc.ncls, -1)
+    return feat @ w.t() + params[model.fc.b.name]
+
+
+def test_resnet_v2_grads_match_autograd(monkeypatch):
+    """Pre-activation ResNet-50 v2: standalone BN+ReLU layers, bias-free convs, shortcut
+    added in the last conv's epilogue, identity-shortcut gradient fan-in."""
+    monkeypatch.setenv("HCB_CPU_DTYPE", "float64")
+    torch.manual_seed(0)
+    m = create_model("resnet50_v2", image_size=64, device="cpu")
+    img, lab = synthetic_batch(m, 4)
+    img = ((img - 127.0) / 60.0).double()
+    loss_ref, grads_ref, _ = reference_grads(m, img, lab, resnet_v2_ref)
+    t = Trainer(m, 4, constant_lr(0.0), weight_decay=0.0)
+    t._forward_backward(img, lab)
+    assert torch.allclose(t.row_loss.mean().double(), loss_ref, rtol=1e-5, atol=1e-6)
+    for p in m.ps.params:
+        r = grads_ref[p.name]
+        err = (p.grad - r).abs().max().item()
+        scale = r.abs().max().item() + 1e-6
+        assert err <= 1e-4 * scale + 1e-6, f"{p.name}: max err {err} vs scale {scale}"
