@@ -24,8 +24,11 @@ def native():
     global _MOD
     if _MOD is not None:
         return _MOD
-    if _PKG not in sys.path:
-        sys.path.insert(0, _PKG)
+    # HCB_DATA_LIB_DIR: load another build of the library (e.g. the ASan/UBSan build of
+    # tools/sanitize_data.sh) instead of the in-tree one
+    d = os.environ.get("HCB_DATA_LIB_DIR") or _PKG
+    if d not in sys.path:
+        sys.path.insert(0, d)
     try:
         _MOD = importlib.import_module("_hcb_data")
     except ImportError:

@@ -89,6 +89,17 @@ class CNNModel:
                 out.append((off, n))
         return out
 
+    def set_training(self, training: bool) -> None:
+        """Training (batch-statistics BN, dropout on) or inference mode (moving-statistics BN,
+        dropout off) -- tf_cnn_benchmarks' phase_train, False under ``--forward_only``."""
+        todo = list(self.all_layers())
+        while todo:
+            l = todo.pop()
+            if hasattr(l, "layers") and callable(l.layers):
+                todo += l.layers()
+            if hasattr(l, "training"):
+                l.training = training
+
     def clear(self):
         for l in self.all_layers():
             if hasattr(l, "clear"):

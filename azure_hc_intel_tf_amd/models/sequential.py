@@ -114,10 +114,6 @@ class SequentialCNN(CNNModel):
                 dx = l.backward(dx)
         join_side_streams()
 
-    def set_training(self, training: bool):
-        for l in self.seq:
-            if isinstance(l, Dropout):
-                l.training = training
 
 
 def _vgg_specs(counts):

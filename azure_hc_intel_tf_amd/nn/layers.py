@@ -156,6 +156,7 @@ class ConvBN(Layer):
             self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0)) if bias else None
         self._saved = None
         self._pre_reduced = False
+        self.training = True  # False: inference BN from the moving statistics (forward-only)
 
     def flops(self, batch: int) -> int:
         P, Q, C = self.out_shape
@@ -175,6 +176,14 @@ class ConvBN(Layer):
         N = x.shape[0]
         P, Q, C = self.out_shape
         dev = x.device
+        if self.bn and not self.training:
+            z = empty_act((N, P, Q, C), dev)
+            y = out if out is not None else empty_act((N, P, Q, C), dev)
+            Fn.conv_forward(x, self.spec, self.pack.pack if x.is_cuda else None, self.w.data, z)
+            Fn.bn_inference(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.eps, y,
+                            self.relu, residual=residual)
+            self._saved = None
+            return y
         if self.bn:
             z = empty_act((N, P, Q, C), dev)
             y = out if out is not None else empty_act((N, P, Q, C), dev)
@@ -335,12 +344,16 @@ class BNReLU(Layer):
         self.rmean = ps.add_buffer(f"{name}/batchnorm/moving_mean", (C,), 0.0)
         self.rvar = ps.add_buffer(f"{name}/batchnorm/moving_variance", (C,), 1.0)
         self._saved = None
+        self.training = True
 
     def params(self):
         return [self.beta, self.gamma]
 
     def forward(self, x):
         y = empty_act(tuple(x.shape), x.device)
+        if not self.training:
+            return Fn.bn_inference(x, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.eps, y,
+                                   self.relu)
         saved = Fn.bn_forward(x, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
                               self.eps, y, self.relu)
         self._saved = (x, y, saved)

@@ -378,6 +378,22 @@ class BNSaved:
         self.invstd = invstd
 
 
+def bn_inference(z, gamma, beta, running_mean, running_var, eps, out, relu: bool, residual=None):
+    """Inference BN (``--forward_only``: tf_cnn_benchmarks builds the model with
+    phase_train=False): out = act(gamma*(z-moving_mean)/sqrt(moving_var+eps) + beta [+ res])."""
+    invstd = torch.rsqrt(running_var + eps)
+    N, H, W, C = z.shape
+    if z.is_cuda:
+        _ext.ops().bn_apply(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0,
+                            N * H * W, C, running_mean, invstd, gamma, beta, 1 if relu else 0)
+        return out
+    y = (z - running_mean) * (invstd * gamma) + beta
+    if residual is not None:
+        y = y + residual
+    out.copy_(torch.relu(y) if relu else y)
+    return out
+
+
 def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, relu: bool,
                residual=None, stats=None, stats_T: int = 0):
     """Training BN: batch stats (from a fused conv slab when given), running-stat update,

@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from .compression import Compression  # noqa: F401  (re-export)
+from .monitor import tracked
 from .reducer import fusion_threshold_bytes, make_buckets
 
 _state = {"initialized": False, "owns_pg": False, "cpu_group": None}
@@ -75,6 +76,9 @@ def is_initialized() -> bool:
 
 
 def shutdown() -> None:
+    from . import monitor as _monitor
+
+    _monitor.reset()  # stop the stall inspector, write HOROVOD_TIMELINE
     if _state["owns_pg"] and dist.is_initialized():
         dist.destroy_process_group()
     _state.update(initialized=False, owns_pg=False, cpu_group=None)
@@ -134,7 +138,8 @@ def allreduce_(tensor: torch.Tensor, average: Optional[bool] = None, name: Optio
     if not _dist() or size() == 1:
         return tensor
     c, ctx = compression.compress(tensor)
-    dist.all_reduce(c, group=_group_for(c))
+    with tracked(f"allreduce.{name or 'tensor'}", c.numel() * c.element_size()):
+        dist.all_reduce(c, group=_group_for(c))
     out = compression.decompress(c, ctx)
     if average:
         out = out / size() if not out.is_floating_point() else out.mul_(1.0 / size())

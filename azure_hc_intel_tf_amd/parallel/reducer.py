@@ -19,6 +19,8 @@ from typing import List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from .monitor import monitor, tracked
+
 DEFAULT_FUSION_BYTES = 128 * 1024 * 1024
 
 
@@ -65,15 +67,16 @@ class TorchDistReducer:
             dt = torch.float16 if self.compression == "fp16" else torch.bfloat16
             if self._comm_buf is None or self._comm_buf.numel() != flat.numel():
                 self._comm_buf = torch.empty(flat.numel(), dtype=dt, device=flat.device)
-        for off, n in self._buckets:
+        for bi, (off, n) in enumerate(self._buckets):
             view = flat[off:off + n]
-            if self.compression:
-                cb = self._comm_buf[off:off + n]
-                cb.copy_(view)
-                dist.all_reduce(cb, group=self.group)
-                view.copy_(cb)
-            else:
-                dist.all_reduce(view, group=self.group)
+            with tracked(f"allreduce.bucket{bi}", n * esz):
+                if self.compression:
+                    cb = self._comm_buf[off:off + n]
+                    cb.copy_(view)
+                    dist.all_reduce(cb, group=self.group)
+                    view.copy_(cb)
+                else:
+                    dist.all_reduce(view, group=self.group)
         if self.average:
             flat.mul_(1.0 / world)
         return flat
@@ -90,16 +93,18 @@ class TorchDistReducer:
             self._comm_buf = torch.empty(flat.numel(), dtype=dt, device=flat.device)
         for off, n in ranges:
             view = flat[off:off + n]
+            tid = monitor().begin(f"allreduce.range{off}", n * (2 if self.compression else 4))
             if self.compression:
                 cb = self._comm_buf[off:off + n]
                 cb.copy_(view)
-                pend.append((view, cb, dist.all_reduce(cb, group=self.group, async_op=True)))
+                pend.append((view, cb, dist.all_reduce(cb, group=self.group, async_op=True), tid))
             else:
-                pend.append((view, None, dist.all_reduce(view, group=self.group, async_op=True)))
+                pend.append((view, None, dist.all_reduce(view, group=self.group, async_op=True), tid))
 
     def join(self) -> None:
-        for view, cb, work in getattr(self, "_pending", None) or []:
+        for view, cb, work, tid in getattr(self, "_pending", None) or []:
             work.wait()
+            monitor().end(tid)
             if cb is not None:
                 view.copy_(cb)
         self._pending = []

@@ -74,6 +74,8 @@ class Trainer:
         self.world = world_size
         self.nesterov = nesterov
         self.forward_only = forward_only
+        if forward_only and hasattr(model, "set_training"):
+            model.set_training(False)  # inference BN / no dropout (tf_cnn_benchmarks phase_train=False)
         self.use_graph = use_graph and self.dev.type == "cuda"
         self.graph_warmup = graph_warmup
         ld = model.fc.ld if hasattr(model, "fc") else (model.num_classes + 7) // 8 * 8

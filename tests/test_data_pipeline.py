@@ -216,3 +216,12 @@ def test_cli_real_data_cpu_end_to_end(fake_dir, tmp_path):
 
     s = json.loads(out.read_text())
     assert s["data"] == "imagenet-tfrecord" and s["num_batches"] == 3
+
+
+def test_native_data_library_under_asan_ubsan(tmp_path):
+    """Host sanitizers over the C++ data core (GPU sanitizers are unavailable on the pool):
+    ASan + UBSan build driven through corrupted records, junk Example bytes, crop sampling
+    and prefetcher start/stop."""
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "sanitize_data.sh"), str(tmp_path)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "sanitize_data: ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -163,3 +163,63 @@ def test_backward_segments_cover_every_gradient_once():
         assert int(cover.max()) == 1 and int(cover.sum()) == sum(p.numel for l in m.all_layers()
                                                                   for p in getattr(l, "params", lambda: [])()), name
         assert int(cover.sum()) >= m.num_params() - 64, name
+
+
+def _stall_and_timeline(hvd):
+    import time
+
+    r = hvd.rank()
+    if r == 1:
+        time.sleep(2.5)  # fault injection: rank 1 joins the collective late
+    t = torch.full((1000,), float(r))
+    hvd.allreduce_(t, average=False, name="grad")
+    assert torch.all(t == 1.0)
+    from azure_hc_intel_tf_amd.parallel.monitor import monitor
+
+    if r == 0:
+        assert monitor().stalls >= 1
+        assert monitor().timeline is not None
+
+
+def test_stall_inspector_and_timeline(tmp_path, monkeypatch, capfd):
+    """Horovod's stall inspector / HOROVOD_TIMELINE on the gloo path: a late rank is reported
+    while the collective is outstanding, and every collective lands in the Chrome trace."""
+    tl = tmp_path / "timeline.json"
+    monkeypatch.setenv("HOROVOD_TIMELINE", str(tl))
+    monkeypatch.setenv("HOROVOD_STALL_CHECK_TIME_SECONDS", "0.5")
+    run(2, _stall_and_timeline)
+    import json
+
+    ev = json.loads(tl.read_text())
+    assert any(e["name"] == "allreduce.grad" and e["ph"] == "X" and e["args"]["bytes"] == 4000 for e in ev)
+    assert json.loads((tmp_path / "timeline.json.rank1").read_text())
+    assert "stall inspector" in capfd.readouterr().err
+
+
+def _stall_abort(hvd):
+    import time
+
+    if hvd.rank() == 1:
+        time.sleep(30)  # never joins in time
+    hvd.allreduce_(torch.ones(4))
+
+
+def test_stall_abort_exits_the_stuck_rank(monkeypatch):
+    """HCB_STALL_ABORT_SECONDS: the waiting rank exits with the stall code instead of hanging."""
+    import multiprocessing
+
+    monkeypatch.setenv("HOROVOD_STALL_CHECK_TIME_SECONDS", "0.3")
+    monkeypatch.setenv("HCB_STALL_ABORT_SECONDS", "1.5")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    p0 = ctx.Process(target=_worker, args=(0, 2, port, _stall_abort, q))
+    p1 = ctx.Process(target=_worker, args=(1, 2, port, _stall_abort, q))
+    p0.start()
+    p1.start()
+    p0.join(timeout=60)
+    from azure_hc_intel_tf_amd.parallel.monitor import STALL_EXIT_CODE
+
+    assert p0.exitcode == STALL_EXIT_CODE
+    p1.kill()
+    p1.join(timeout=30)

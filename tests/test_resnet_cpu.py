@@ -87,3 +87,56 @@ def test_resnet_v2_grads_match_autograd(monkeypatch):
         err = (p.grad - r).abs().max().item()
         scale = r.abs().max().item() + 1e-6
         assert err <= 1e-4 * scale + 1e-6, f"{p.name}: max err {err} vs scale {scale}"
+
+
+def test_forward_only_uses_moving_statistics(monkeypatch):
+    """--forward_only: BN runs in inference mode from the moving statistics (phase_train=False)."""
+    monkeypatch.setenv("HCB_CPU_DTYPE", "float64")
+    from reference_models import conv_ref, pool_ref
+
+    torch.manual_seed(2)
+    m = create_model("resnet50", image_size=64, device="cpu")
+    # non-trivial moving statistics
+    for l in m.all_layers():
+        if getattr(l, "bn", False):
+            l.rmean.data.normal_(0.0, 0.1)
+            l.rvar.data.uniform_(0.5, 2.0)
+    img, lab = synthetic_batch(m, 2)
+    img = ((img - 127.0) / 60.0).double()
+    t = Trainer(m, 2, constant_lr(0.0), forward_only=True)
+    t._forward(img, lab)
+    params = {p.name: p.data.double() for p in m.ps.params}
+
+    def cbn(layer, x, residual=None):
+        z = conv_ref(layer, x, params)
+        z = torch.nn.functional.batch_norm(z, layer.rmean.data.double(), layer.rvar.data.double(),
+                                           params[layer.gamma.name], params[layer.beta.name], training=False,
+                                           eps=layer.eps)
+        if residual is not None:
+            z = z + residual
+        return torch.relu(z) if layer.relu else z
+
+    x = pool_ref(m.pool, cbn(m.stem, img.permute(0, 3, 1, 2)))
+    for b in m.blocks:
+        sc = cbn(b.sc, x) if b.proj else x
+        x = cbn(b.c3, cbn(b.c2, cbn(b.c1, x)), residual=sc)
+    logits = x.mean(dim=(2, 3)) @ params[m.fc.w.name].view(m.fc.ncls, -1).t() + params[m.fc.b.name]
+    ref = torch.nn.functional.cross_entropy(logits, lab, reduction="none")
+    assert torch.allclose(t.row_loss.double(), ref, rtol=1e-6, atol=1e-7)
+
+
+def test_cpu_training_is_bitwise_deterministic():
+    """Same seed, same data -> bitwise-identical losses and weights (fp32 CPU path; the GPU
+    path reduces BN statistics / weight gradients with fp32 atomics, so it is reproducible to
+    rounding, not bitwise)."""
+    def run():
+        torch.manual_seed(0)
+        m = create_model("resnet50", image_size=32, device="cpu", seed=7)
+        img, lab = synthetic_batch(m, 4, seed=3)
+        img = (img - 127.0) / 60.0
+        t = Trainer(m, 4, constant_lr(0.05))
+        losses = [float(t.step(img, lab)) for _ in range(3)]
+        return losses, m.ps.master.clone()
+
+    (l1, w1), (l2, w2) = run(), run()
+    assert l1 == l2 and torch.equal(w1, w2)
