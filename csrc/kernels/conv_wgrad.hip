@@ -27,6 +27,25 @@ __device__ __forceinline__ int wg_swz(int row) {
   else return ((row >> 1) & 1) | ((row >> 2) & 2);
 }
 
+// Adds the LDS-staged fp32 tile into dw: a plain read-modify-write when this workgroup is the
+// tile's only writer (no split-K), fp32 atomics otherwise. (Measured alternative, dropped:
+// split-K partial slabs + a last-arriver sum instead of atomics was 1.2-3x slower on the
+// ResNet-50 layers -- the serial tail reduction costs more than the atomics.)
+__device__ __forceinline__ void wgrad_store_tile(const WgradParams& p, const float* Cs, int LDC, int BM, int BN, int i0,
+                                                 int j0, int tid, int nthreads, bool sole_writer) {
+  for (int idx = tid; idx < BM * BN; idx += nthreads) {
+    const int row = idx / BN, col = idx - row * BN;
+    const int gi = i0 + row, gj = j0 + col;
+    if (gi < p.Nout && gj < p.K) {
+      float* d = p.dw + (size_t)gi * p.K + gj;
+      if (sole_writer)
+        *d += Cs[row * LDC + col];
+      else
+        atomicAdd(d, Cs[row * LDC + col]);
+    }
+  }
+}
+
 template <int WM, int WN, int TM, int TN, bool CBIG>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
@@ -192,11 +211,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
         Cs[row * LDC + col] = acc[i][j][e];
       }
   __syncthreads();
-  for (int idx = tid; idx < BM * BN; idx += 256) {
-    int row = idx / BN, col = idx - row * BN;
-    int gi = i0 + row, gj = j0 + col;
-    if (gi < p.Nout && gj < p.K) atomicAdd(p.dw + (size_t)gi * p.K + gj, Cs[row * LDC + col]);
-  }
+  wgrad_store_tile(p, Cs, LDC, BM, BN, i0, j0, tid, 256, gridDim.x == ntiles);
 }
 
 // ============================================================== LDS-DMA multi-stage variant
@@ -384,11 +399,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradPara
         Cs[row * LDC + col] = acc[i][j][e];
       }
   __syncthreads();
-  for (int idx = tid; idx < BM * BN; idx += NW * 64) {
-    const int row = idx / BN, col = idx - row * BN;
-    const int gi = i0 + row, gj = j0 + col;
-    if (gi < p.Nout && gj < p.K) atomicAdd(p.dw + (size_t)gi * p.K + gj, Cs[row * LDC + col]);
-  }
+  wgrad_store_tile(p, Cs, LDC, BM, BN, i0, j0, tid, NW * 64, gridDim.x == ntiles);
 }
 
 template <int WM, int WN, int TM, int TN, int NST>
