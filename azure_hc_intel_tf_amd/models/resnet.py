@@ -14,6 +14,7 @@ BN: decay 0.9, epsilon 1e-5, scale=True. ResNet-50 v1: 25,559,081 trainable para
 """
 from __future__ import annotations
 
+from ..nn import layers as L
 from ..nn.layers import BNReLU, ConvBN, GlobalAvgPool, Logits, Pool, join_side_streams
 from ..ops import functional as Fn
 from .base import CNNModel
@@ -93,9 +94,13 @@ class ResNet(CNNModel):
         self.fc = Logits(ps, "logits", shape[2], self.num_classes)
         self.layers = [self.stem, self.pool] + [l for b in self.blocks for l in b.layers()] + [self.gap, self.fc]
 
+    def _stem_pool(self, images):
+        if images.is_cuda and L.FUSE_STEM_POOL and self.stem.training:
+            return self.stem.forward_maxpool(images, self.pool)
+        return self.pool.forward(self.stem.forward(images))
+
     def forward(self, images):
-        x = self.stem.forward(images)
-        x = self.pool.forward(x)
+        x = self._stem_pool(images)
         for b in self.blocks:
             x = b.forward(x)
         self._last = x
@@ -203,7 +208,7 @@ class ResNetV2(CNNModel):
                        + [self.post, self.gap, self.fc])
 
     def forward(self, images):
-        x = self.pool.forward(self.stem.forward(images))
+        x = ResNet._stem_pool(self, images)
         for b in self.blocks:
             x = b.forward(x)
         return self.fc.forward(self.gap.forward(self.post.forward(x)))

@@ -55,6 +55,8 @@ def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
     raise ValueError(mode)
 
 
+# ResNet stem: BN+ReLU+max pool in one kernel on the GPU (HCB_FUSE_STEM_POOL=0 to disable)
+FUSE_STEM_POOL = os.environ.get("HCB_FUSE_STEM_POOL", "1") != "0"
 STAT_R = 8  # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
 FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
@@ -205,6 +207,25 @@ class ConvBN(Layer):
         Fn.conv_forward(x, self.spec, self.pack.pack if x.is_cuda else None, self.w.data, y,
                         bias=self.bias.data if self.bias is not None else None, relu=self.relu, residual=residual)
         self._saved = (x, None, y, None, False)
+        return y
+
+    def forward_maxpool(self, x, pool: "Pool"):
+        """GPU training forward of conv -> BN -> ReLU -> max pool (the ResNet stem) in two
+        launches: the conv (BN statistics in its epilogue) and one BN+ReLU+pool kernel. The
+        full-size BN+ReLU activation is never written; ``pool`` keeps the argmax for its
+        backward and this layer recomputes the ReLU mask from z."""
+        assert self.bn and self.relu and x.is_cuda and pool.is_max and self.training
+        N = x.shape[0]
+        P, Q, C = self.out_shape
+        z = empty_act((N, P, Q, C), x.device)
+        Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data, stats_R=STAT_R)
+        y = empty_act((N,) + tuple(pool.out_shape), x.device)
+        amax = torch.empty((N,) + tuple(pool.out_shape), dtype=torch.uint8, device=x.device)
+        saved = Fn.bn_relu_maxpool_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
+                                       self.eps, self.acc_f.data, STAT_R, self.sv_mean.data, self.sv_invstd.data, y,
+                                       amax, *pool.k, *pool.s, pool.pads)
+        self._saved = (x, z, None, saved, False)
+        pool._saved = (z, y, amax)  # the argmax backward reads only shapes from x / y
         return y
 
     # ------------------------------------------------------------------ backward

@@ -443,6 +443,18 @@ def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out
     return BNSaved(saved_mean, saved_invstd)
 
 
+def bn_relu_maxpool_acc(z, gamma, beta, running_mean, running_var, momentum, eps, acc, R: int, saved_mean,
+                        saved_invstd, out, argmax, kh, kw, sh, sw, pads):
+    """GPU: BN (conv-epilogue statistics in ``acc``) + ReLU + max pool in one kernel; writes the
+    pooled ``out`` and the uint8 window ``argmax`` only (the BN+ReLU activation is not stored)."""
+    N, H, W, C = z.shape
+    _, P, Q, _ = out.shape
+    pt, pb, pl, pr = pads
+    _ext.ops().bn_relu_maxpool_acc(z, out, argmax, [N, H, W, C, P, Q, ld(out), kh, kw, sh, sw, pt, pl], acc, R, eps,
+                                   momentum, gamma, beta, saved_mean, saved_invstd, running_mean, running_var)
+    return BNSaved(saved_mean, saved_invstd)
+
+
 def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, acc, R: int,
                     gres=None, pre_reduced: bool = False):
     """GPU BN(+ReLU) backward with the dgamma/dbeta reduction accumulated in ``acc`` replicas

@@ -356,6 +356,34 @@ void bn_bwd_apply(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y
                             dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu, cur_stream());
 }
 
+// geom = [N,H,W,C,P,Q,ldy,kh,kw,sh,sw,ph,pw]; z contiguous [N,H,W,C]
+void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, at::IntArrayRef g, const Tensor& acc,
+                         int64_t R, double eps, double momentum, const Tensor& gamma, const Tensor& beta,
+                         const Tensor& saved_mean, const Tensor& saved_invstd, const Tensor& run_mean,
+                         const Tensor& run_var) {
+  TORCH_CHECK(g.size() == 13, "hcb.bn_relu_maxpool_acc: geom");
+  check_bf16(z, "z");
+  check_bf16(y, "y");
+  check_cuda(amax, "amax");
+  const int64_t N = g[0], H = g[1], W = g[2], C = g[3], P = g[4], Q = g[5], ldy = g[6];
+  TORCH_CHECK(z.is_contiguous() && z.numel() == N * H * W * C, "hcb.bn_relu_maxpool_acc: z contiguous [N,H,W,C]");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldy % 8 == 0 && ldy >= C, "hcb.bn_relu_maxpool_acc: C / ldy");
+  TORCH_CHECK(g[7] * g[8] <= 255, "hcb.bn_relu_maxpool_acc: window too large for the uint8 argmax");
+  check_range(y, ((N * P * Q - 1) * ldy + C) * 2, "y");
+  TORCH_CHECK(amax.scalar_type() == at::kByte && amax.is_contiguous() && amax.numel() >= N * P * Q * C,
+              "hcb.bn_relu_maxpool_acc: amax uint8 [N,P,Q,C]");
+  TORCH_CHECK(N * P * Q < (1ll << 31) && N * H * W < (1ll << 31), "hcb.bn_relu_maxpool_acc: 32-bit index range");
+  for (const Tensor* t : {&acc, &gamma, &beta, &saved_mean, &saved_invstd, &run_mean, &run_var}) check_f32(*t, "bn");
+  TORCH_CHECK(acc.numel() >= R * 2 * C && gamma.numel() >= C && beta.numel() >= C && saved_mean.numel() >= C &&
+                  saved_invstd.numel() >= C && run_mean.numel() >= C && run_var.numel() >= C,
+              "hcb.bn_relu_maxpool_acc: per-channel tensors too small");
+  hcb::launch_bn_relu_maxpool_acc(z.data_ptr(), N, H, W, C, y.data_ptr(), P, Q, ldy, amax.data_ptr(), g[7], g[8], g[9],
+                                  g[10], g[11], g[12], acc.data_ptr<float>(), R, (float)eps, (float)momentum,
+                                  gamma.data_ptr<float>(), beta.data_ptr<float>(), saved_mean.data_ptr<float>(),
+                                  saved_invstd.data_ptr<float>(), run_mean.data_ptr<float>(),
+                                  run_var.data_ptr<float>(), cur_stream());
+}
+
 // geom = [N,H,W,C,ldx,P,Q,ldy,kh,kw,sh,sw,ph,pw,is_max,incl_pad]
 void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx, at::IntArrayRef g) {
   TORCH_CHECK(g.size() == 16, "hcb.pool_fwd: geom");
@@ -722,6 +750,9 @@ TORCH_LIBRARY(hcb, m) {
   m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
   m.def("preprocess_images(Tensor src, Tensor desc, Tensor desc_host, Tensor(a!) out, float[] scale, float[] bias) -> ()");
+  m.def("bn_relu_maxpool_acc(Tensor z, Tensor(a!) y, Tensor(b!) amax, int[] geom, Tensor acc, int R, float eps, "
+        "float momentum, Tensor gamma, Tensor beta, Tensor(c!) saved_mean, Tensor(d!) saved_invstd, "
+        "Tensor(e!) run_mean, Tensor(f!) run_var) -> ()");
   m.def("dropout_fwd(Tensor x, Tensor(a!) y, Tensor(b!) mask, float keep, int seed, Tensor step) -> ()");
   m.def("dropout_bwd(Tensor dy, Tensor mask, Tensor(a!) dx, float keep) -> ()");
   m.def("synth_images(Tensor(a!) out, int C, int Cpad, float mean, float std, int seed) -> ()");
@@ -761,6 +792,7 @@ TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("l2norm_sq", l2norm_sq);
   m.impl("synth_images", synth_images);
   m.impl("dropout_fwd", dropout_fwd);
+  m.impl("bn_relu_maxpool_acc", bn_relu_maxpool_acc);
   m.impl("dropout_bwd", dropout_bwd);
   m.impl("preprocess_images", preprocess_images);
   m.impl("synth_labels", synth_labels);

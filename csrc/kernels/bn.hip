@@ -712,6 +712,85 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
   }
 }
 
+// ResNet stem: BN (statistics from the conv epilogue's replicas) + ReLU + max pool in one pass.
+// The BN+ReLU output is never written: each thread normalises the (<= kh x kw) window elements
+// of one pooled pixel x 8 channels, keeps the max and the first-max window position (the
+// argmax the pool backward gathers with), and stores only the pooled tensor. The backward
+// recomputes the ReLU mask from z (mode 2), so nothing else needs the full-size activation.
+__global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
+    const uint16_t* __restrict__ z, int H, int W, int C, int CVB, uint16_t* __restrict__ y, int P, int Q, int ldy,
+    uint8_t* __restrict__ amax, int kh, int kw, int sh, int sw, int ph, int pw, int Nimg, int M,
+    const float* __restrict__ acc, int R, float eps, float momentum, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var) {
+  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
+  const GroupMap gm = groupmap(CVB);
+  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
+  const float inv_n = 1.f / (float)M;
+  if (blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
+      const int c = gm.c0 + i;
+      const float mu = sums[i] * inv_n;
+      const float var = fmaxf(sums[gm.CB + i] * inv_n - mu * mu, 0.f);
+      saved_mean[c] = mu;
+      saved_invstd[c] = rsqrtf(var + eps);
+      if (run_mean != nullptr) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * mu;
+        run_var[c] = momentum * run_var[c] + (1.f - momentum) * unb;
+      }
+    }
+  }
+  if (gm.r0 >= gm.rows) return;
+  float sc[8], sft[8];
+  const int cl = (threadIdx.x % CVB) * 8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float mu = sums[cl + e] * inv_n;
+    const float var = fmaxf(sums[gm.CB + cl + e] * inv_n - mu * mu, 0.f);
+    const float s = gamma[gm.c0 + cl + e] * rsqrtf(var + eps);
+    sc[e] = s;
+    sft[e] = beta[gm.c0 + cl + e] - mu * s;
+  }
+  const unsigned PQ = (unsigned)P * Q, total = (unsigned)Nimg * PQ;
+  for (unsigned op = blockIdx.x * gm.rows + gm.r0; op < total; op += gridDim.x * gm.rows) {
+    const int n = (int)(op / PQ);
+    const int rem = (int)(op - (unsigned)n * PQ);
+    const int p = rem / Q, q = rem - p * Q;
+    const int h0 = p * sh - ph, w0 = q * sw - pw;
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      arg[e] = 255;
+    }
+    for (int r = 0; r < kh; ++r) {
+      const int h = h0 + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < kw; ++s) {
+        const int w = w0 + s;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(z + ((size_t)(n * H + h) * W + w) * C + gm.cv * 8), f);
+        const int pos = r * kw + s;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = fmaxf(f[e] * sc[e] + sft[e], 0.f);
+          if (v > best[e]) {  // strict: the FIRST maximal element keeps the gradient
+            best[e] = v;
+            arg[e] = pos;
+          }
+        }
+      }
+    }
+    *reinterpret_cast<u32x4*>(y + (size_t)op * ldy + gm.cv * 8) = pack8(best);
+    u32x2 a;
+    a[0] = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+    a[1] = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+    *reinterpret_cast<u32x2*>(amax + (size_t)op * C + gm.cv * 8) = a;
+  }
+}
+
 // (row splits) x (channel groups); ~2048 blocks in total, each thread >= 1 row
 static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
   const int CV = C / 8;
@@ -736,6 +815,17 @@ void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* r
   hipLaunchKernelGGL(bn_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x, ldx,
                      (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta,
                      relu, saved_mean, saved_invstd, run_mean, run_var);
+}
+
+void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
+                                int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
+                                float momentum, const float* gamma, const float* beta, float* saved_mean,
+                                float* saved_invstd, float* run_mean, float* run_var, hipStream_t st) {
+  int cvb;
+  dim3 grid = bn_grid_groups(N * P * Q, C, &cvb);
+  hipLaunchKernelGGL(bn_relu_maxpool_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W,
+                     C, cvb, (uint16_t*)y, P, Q, ldy, (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps,
+                     momentum, gamma, beta, saved_mean, saved_invstd, run_mean, run_var);
 }
 
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,

@@ -125,6 +125,12 @@ void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* r
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
                          hipStream_t st);
+// BN(acc statistics) + ReLU + max pool (NHWC, C contiguous): pooled y [N,P,Q] (row stride ldy) and
+// the uint8 window argmax [N,P,Q,C]; the BN+ReLU activation itself is not materialised
+void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
+                                int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
+                                float momentum, const float* gamma, const float* beta, float* saved_mean,
+                                float* saved_invstd, float* run_mean, float* run_var, hipStream_t st);
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
                               int relu, float* acc, int R, void* gout, int ldg, hipStream_t st);

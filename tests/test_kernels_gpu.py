@@ -488,3 +488,37 @@ def test_loss_scale_ops_gpu():
     assert torch.equal(w, torch.ones_like(w))
     Fn.loss_scale_update(h, 1, True)
     assert float(h[5]) == 512.0 and abs(float(h[3]) - 1 / 512) < 1e-9
+
+
+def test_fused_stem_bn_relu_maxpool_matches_unfused():
+    """ResNet stem: conv -> [BN + ReLU + max pool in one kernel] against conv -> BN+ReLU -> pool,
+    forward values, running statistics, and the backward through the argmax + BN."""
+    from azure_hc_intel_tf_amd.nn.layers import ConvBN, Pool
+    from azure_hc_intel_tf_amd.nn.params import ParamStore
+
+    torch.manual_seed(21)
+    res = []
+    for fused in (False, True):
+        ps = ParamStore(seed=3)
+        stem = ConvBN(ps, "conv0", (64, 64, 8), 64, 7, 7, 2, 2, "SAME_RESNET", relu=True, need_dx=False,
+                      logical_cin=3)
+        pool = Pool("mpool0", stem.out_shape, 3, 3, 2, 2, "SAME", is_max=True)
+        ps.finalize(DEV)
+        ps.repack()
+        ps.zero_stats()
+        ps.zero_grad()
+        g = torch.Generator().manual_seed(5)
+        x = bf(torch.randn(4, 64, 64, 8, generator=g).to(DEV))
+        x[..., 3:] = 0
+        y = stem.forward_maxpool(x, pool) if fused else pool.forward(stem.forward(x))
+        dy = bf(torch.randn(y.shape, generator=g).to(DEV))
+        stem.backward(pool.backward(dy))
+        torch.cuda.synchronize()
+        res.append((y.float().cpu(), stem.rmean.data.cpu().clone(), stem.w.grad.float().cpu().clone(),
+                    stem.gamma.grad.cpu().clone()))
+    (y0, rm0, gw0, gg0), (y1, rm1, gw1, gg1) = res
+    assert torch.equal(y0, y1)
+    assert torch.allclose(rm0, rm1, atol=1e-6)
+    # the fused kernel picks the window max in fp32, the unfused pool among bf16-rounded values:
+    # near-ties (common with 8-bit mantissas) route a few gradients to a neighbouring pixel
+    assert rel_err(gw1, gw0) < 5e-2 and rel_err(gg1, gg0) < 5e-2

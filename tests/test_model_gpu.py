@@ -56,13 +56,16 @@ def test_model_gpu_forward_and_descent(name, size, batch):
 
 
 def test_graph_training_step_runs_and_learns():
+    # Loss on one repeated batch plateaus near ln(#labels in batch) for a few steps before it
+    # drops; seed the init and run long enough to leave the plateau.
+    torch.manual_seed(0)
     m = create_model("resnet50", image_size=96, device="cuda")
     img, lab = synthetic_batch(m, 16)
     t = Trainer(m, 16, constant_lr(0.02), use_graph=True, graph_warmup=2)
-    losses = [float(t.step(img, lab)) for _ in range(12)]
+    losses = [float(t.step(img, lab)) for _ in range(16)]
     assert all(torch.isfinite(torch.tensor(losses)))
     assert t._g_all is not None
-    assert losses[-1] < losses[2]
+    assert min(losses[-3:]) < 0.8 * losses[2]
 
 
 def test_full_size_resnet50_step_bs64():
