@@ -526,12 +526,20 @@ __device__ __forceinline__ GroupMap groupmap(int CVB) {
 }
 
 // block-cooperative: sums[i] = sum_r acc[r][0][c0+i], sums[CB+i] = sum_r acc[r][1][c0+i]
+// The replica loads are issued 8 at a time (one L2 round trip, not R dependent ones): in the
+// small late-stage layers this reduction is on the critical path of a one-wave kernel.
 __device__ __forceinline__ void reduce_group_replicas(const float* acc, int R, int C, int c0, int CB,
                                                       float* sums) {
   for (int i = threadIdx.x; i < 2 * CB; i += blockDim.x) {
     const int off = i < CB ? c0 + i : C + c0 + (i - CB);
     float s = 0.f;
-    for (int r = 0; r < R; ++r) s += acc[(size_t)r * 2 * C + off];
+    for (int r0 = 0; r0 < R; r0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = r0 + r < R ? acc[(size_t)(r0 + r) * 2 * C + off] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s += v[r];
+    }
     sums[i] = s;
   }
   __syncthreads();
@@ -544,6 +552,31 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     float* saved_invstd, float* run_mean, float* run_var) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
   const GroupMap gm = groupmap(CVB);
+  const bool active = gm.r0 < gm.rows;
+  const int cl = (threadIdx.x % CVB) * 8;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx));
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx));
+  const int stride = gridDim.x * gm.rows;
+  int m0 = blockIdx.x * gm.rows + gm.r0;
+  u32x4 xv[BN_U], rv[BN_U];
+  auto load_rows = [&](int mb) {
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      int m = mb + u * stride;
+      xv[u] = buf_load16(xr, m < M ? (uint32_t)((size_t)m * ldx + gm.cv * 8) * 2u : HCB_OOB);
+      if (res != nullptr) rv[u] = buf_load16(rr, m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * 2u : HCB_OOB);
+    }
+  };
+  // First rows and the affine parameters are in flight while the statistics are reduced.
+  float gam[8], bet[8];
+  if (active) {
+    load_rows(m0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gam[e] = gamma[gm.c0 + cl + e];
+      bet[e] = beta[gm.c0 + cl + e];
+    }
+  }
   reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
   const float inv_n = 1.f / (float)M;
   if (blockIdx.x == 0) {
@@ -560,28 +593,18 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
       }
     }
   }
-  if (gm.r0 >= gm.rows) return;
+  if (!active) return;
   float sc[8], sh[8];
-  const int cl = (threadIdx.x % CVB) * 8;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     float mu = sums[cl + e] * inv_n;
     float var = fmaxf(sums[gm.CB + cl + e] * inv_n - mu * mu, 0.f);
-    float s = gamma[gm.c0 + cl + e] * rsqrtf(var + eps);
+    float s = gam[e] * rsqrtf(var + eps);
     sc[e] = s;
-    sh[e] = beta[gm.c0 + cl + e] - mu * s;
+    sh[e] = bet[e] - mu * s;
   }
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx));
-  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx));
-  const int stride = gridDim.x * gm.rows;
-  for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
-    u32x4 xv[BN_U], rv[BN_U];
-#pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
-      int m = m0 + u * stride;
-      xv[u] = buf_load16(xr, m < M ? (uint32_t)((size_t)m * ldx + gm.cv * 8) * 2u : HCB_OOB);
-      if (res != nullptr) rv[u] = buf_load16(rr, m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * 2u : HCB_OOB);
-    }
+  for (; m0 < M; m0 += BN_U * stride) {
+    if (m0 != blockIdx.x * gm.rows + gm.r0) load_rows(m0);
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       int m = m0 + u * stride;
@@ -672,6 +695,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     int R, float* dgamma, float* dbeta, int relu) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]: dbeta, dgamma
   const GroupMap gm = groupmap(CVB);
+  const bool active = gm.r0 < gm.rows;
+  BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
+             make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, gm.cv};
+  const int stride = gridDim.x * gm.rows;
+  const int mfirst = blockIdx.x * gm.rows + gm.r0;
+  u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
+  float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
+  // First rows and the per-channel parameters are in flight while dgamma/dbeta are reduced.
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) src.load(mfirst + u * stride, M, relu, dv[u], xv[u], yv[u]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int c = gm.cv * 8 + e;
+      mu[e] = mean[c];
+      is[e] = invstd[c];
+      sc[e] = gamma[c];
+      sh[e] = beta[c];
+    }
+  }
   reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
@@ -679,27 +722,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
       dgamma[gm.c0 + i] = sums[gm.CB + i];
     }
   }
-  if (gm.r0 >= gm.rows) return;
-  float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
+  if (!active) return;
   const float invM = 1.f / (float)M;
   const int cl = (threadIdx.x % CVB) * 8;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    int c = gm.cv * 8 + e;
-    mu[e] = mean[c];
-    is[e] = invstd[c];
-    sc[e] = gamma[c] * is[e];
-    sh[e] = beta[c] - mu[e] * sc[e];
+    sc[e] = sc[e] * is[e];
+    sh[e] = sh[e] - mu[e] * sc[e];
     k1[e] = sums[cl + e] * invM;
     k2[e] = sums[gm.CB + cl + e] * invM;
   }
-  BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
-             make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, gm.cv};
-  const int stride = gridDim.x * gm.rows;
-  for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
-    u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
+  for (int m0 = mfirst; m0 < M; m0 += BN_U * stride) {
+    if (m0 != mfirst) {
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+      for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+    }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const int m = m0 + u * stride;

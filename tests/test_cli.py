@@ -111,3 +111,20 @@ def test_cpu_benchmark_end_to_end(tmp_path):
     # resume continues from the saved step
     out2 = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert out2.returncode == 0 and "Restored checkpoint at step 4" in out2.stdout
+
+
+def test_launcher_propagates_rank_failure(tmp_path):
+    """Fault injection (--fault_rank/--fault_step) under the per-GPU launcher: rank 1 dies at step 2
+    while rank 0 waits in the next allreduce; the launcher must tear rank 0 down and exit with the
+    failing rank's code instead of hanging (MPI_Abort semantics, SURVEY.md §5 failure detection)."""
+    import time
+    cmd = [sys.executable, "-m", "azure_hc_intel_tf_amd.launch.launcher", "--nproc_per_node", "2", "--no_pin",
+           "--", sys.executable, os.path.join(ROOT, "tf_cnn_benchmarks.py"), "--device=cpu", "--model=trivial",
+           "--batch_size=2", "--image_size=32", "--num_batches=50", "--num_warmup_batches=1",
+           "--variable_update=horovod", "--horovod_device=cpu", "--fault_rank=1", "--fault_step=2"]
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
+                         env=dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1"))
+    assert out.returncode == 17, out.stdout[-2000:] + out.stderr[-2000:]
+    assert "[fault injection] rank 1 aborting at step 2" in out.stdout
+    assert time.time() - t0 < 200
