@@ -1,7 +1,8 @@
 """Model base class: a ParamStore plus explicit forward / backward over NHWC activations."""
 from __future__ import annotations
 
-from typing import List
+import os
+from typing import Callable, List, Sequence, Tuple
 
 import torch
 
@@ -55,6 +56,32 @@ class CNNModel:
         self.backward(dlogits)
         join_side_streams()
         yield None, True  # None: every gradient
+
+    @staticmethod
+    def _param_count(layers) -> int:
+        return sum(p.numel for l in layers for p in getattr(l, "params", lambda: [])())
+
+    def _segments_from_units(self, dx, head: Sequence, units: Sequence[Tuple[Callable, Sequence]],
+                             tail: Sequence = ()):
+        """Generic segmented backward. ``head``: layers whose backward already ran (their
+        gradients are final); ``units``: (fn(dx) -> dx, layers) in backward order; ``tail``:
+        parameter-free layers that are never back-propagated through. A segment is closed
+        (yielded) once it owns >= HCB_SEGMENT_PARAMS parameters (default 2M = 8 MB fp32), so
+        the first reductions start while most of the backward is still ahead."""
+        from ..nn.layers import join_side_streams
+
+        thr = int(os.environ.get("HCB_SEGMENT_PARAMS", 2_000_000))
+        seg, n = list(head), self._param_count(head)
+        for i, (fn, layers) in enumerate(units):
+            dx = fn(dx)
+            seg += list(layers)
+            n += self._param_count(layers)
+            if i < len(units) - 1 and n >= thr:
+                join_side_streams()  # the segment's weight gradients are final
+                yield seg, False
+                seg, n = [], 0
+        join_side_streams()
+        yield seg + list(tail), True
 
     # -- helpers
     @property

@@ -191,6 +191,18 @@ class InceptionV3(CNNModel):
             x = m.forward(x)
         return self.fc.forward(self.gap.forward(x))
 
+    def backward_segments(self, dlogits):
+        """Segments of whole inception modules (last first; the 8x8 'E' modules and the
+        logits hold most of the parameters), then the stem."""
+        dx = self.gap.backward(self.fc.backward(dlogits))
+        units = [(m.backward, m.layers()) for m in reversed(self.modules)]
+        for l in reversed(self.stem):
+            if isinstance(l, ConvBN):
+                units.append((lambda d, l=l: l.backward(d)[0], [l]))
+            else:
+                units.append((l.backward, [l]))
+        yield from self._segments_from_units(dx, [self.fc, self.gap], units)
+
     def backward(self, dlogits):
         dx = self.gap.backward(self.fc.backward(dlogits))
         for m in reversed(self.modules):

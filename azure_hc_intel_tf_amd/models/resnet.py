@@ -213,6 +213,12 @@ class ResNetV2(CNNModel):
             x = b.forward(x)
         return self.fc.forward(self.gap.forward(self.post.forward(x)))
 
+    def backward_segments(self, dlogits):
+        dx = self.post.backward(self.gap.backward(self.fc.backward(dlogits)))
+        units = [(b.backward, b.layers()) for b in reversed(self.blocks)]
+        units.append((lambda d: self.stem.backward(self.pool.backward(d)), [self.pool, self.stem]))
+        yield from self._segments_from_units(dx, [self.fc, self.gap, self.post], units)
+
     def backward(self, dlogits):
         dx = self.post.backward(self.gap.backward(self.fc.backward(dlogits)))
         for b in reversed(self.blocks):

@@ -103,6 +103,19 @@ class SequentialCNN(CNNModel):
         self._last_shape = tuple(x.shape)
         return self.fc.forward(x.reshape(x.shape[0], -1))
 
+    def backward_segments(self, dlogits):
+        dx = self.fc.backward(dlogits).reshape(self._last_shape)
+        units, rest = [], list(reversed(self.seq))
+        while rest:
+            l = rest.pop(0)
+            if isinstance(l, ConvBN):
+                units.append((lambda d, l=l: l.backward(d)[0], [l]))
+                if not l.need_dx:
+                    break  # the input conv: nothing below it needs a gradient
+            else:
+                units.append((l.backward, l.layers() if isinstance(l, InceptionModule) else [l]))
+        yield from self._segments_from_units(dx, [self.fc], units, tail=rest)
+
     def backward(self, dlogits):
         dx = self.fc.backward(dlogits).reshape(self._last_shape)
         for l in reversed(self.seq):

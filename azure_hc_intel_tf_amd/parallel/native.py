@@ -120,7 +120,9 @@ class Communicator:
 class NativeReducer:
     """Flat-buffer gradient allreduce on the C++ RCCL engine."""
 
-    def __init__(self, compression=None, bucket_bytes=None, average=False):
+    def __init__(self, compression=None, bucket_bytes=None, average=False, force=False):
+        """``force``: run the collectives even on a 1-rank communicator (where they are the
+        identity), so the multi-GPU code path can be exercised and timed on one GPU."""
         if compression not in (None, "none", "bf16", "fp16"):
             raise ValueError(compression)
         # fp16 wire format maps to bf16 on MI355X: same 2 bytes, fp32 exponent range
@@ -128,7 +130,10 @@ class NativeReducer:
         self.bucket_bytes = bucket_bytes or fusion_threshold_bytes()
         self.average = average
         self.comm = Communicator()
-        self.graph_safe = os.environ.get("HCB_GRAPH_COMM", "0") == "1"
+        # collectives captured inside the training-step graph (default); HCB_GRAPH_COMM=0
+        # replays one graph per backward segment and launches the reductions from the host
+        self.graph_safe = os.environ.get("HCB_GRAPH_COMM", "1") == "1"
+        self.force = force
         self._buckets = None
 
     def _bucket_table(self, numel):
@@ -140,14 +145,16 @@ class NativeReducer:
         return self._buckets
 
     def allreduce_(self, flat):
-        if self.comm.world == 1 and not self.compress:
+        if self.comm.world == 1 and not self.compress and not self.force:
             return flat
         self.comm.bucket_allreduce_(flat, self._bucket_table(flat.numel()), self.compress, 1.0, self.average)
         return flat
 
     # -- overlap interface: reduce finished gradient ranges while backward continues
     def allreduce_ranges_async_(self, flat, ranges):
-        if self.comm.world == 1 and not self.compress:
+        if self.comm.world == 1 and not self.compress and not self.force:
+            return
+        if os.environ.get("HCB_COMM_NOOP") == "1":  # debug: segmented step without collectives
             return
         table = torch.tensor([list(r) for r in ranges], dtype=torch.int64).view(-1, 2)
         self.comm.bucket_allreduce_async_(flat, table, self.compress, 1.0, self.average)

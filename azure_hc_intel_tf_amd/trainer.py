@@ -62,7 +62,7 @@ class Trainer:
                  weight_decay: float = 4e-5, reducer=None, world_size: int = 1, use_graph: bool = True,
                  nesterov: bool = False, graph_warmup: int = 2, forward_only: bool = False,
                  loss_scale: Optional[float] = None, dynamic_loss_scale: bool = False,
-                 loss_scale_interval: int = 1000):
+                 loss_scale_interval: int = 1000, force_overlap: bool = False):
         self.model = model
         self.ps = model.ps
         self.B = batch_size
@@ -103,7 +103,8 @@ class Trainer:
         self._seg_ranges = {}
         self._static = None
         # overlap the allreduce with backward (segmented graphs + async reducer)
-        self.overlap = (reducer is not None and world_size > 1 and not forward_only
+        # (force_overlap: take the segmented multi-GPU path on one rank -- tests / N=1 timing)
+        self.overlap = (reducer is not None and (world_size > 1 or force_overlap) and not forward_only
                         and hasattr(reducer, "allreduce_ranges_async_")
                         and os.environ.get("HCB_OVERLAP", "1") != "0")
 
@@ -167,7 +168,24 @@ class Trainer:
         torch.cuda.synchronize()
         single = self.reducer is None or self.world <= 1 or getattr(self.reducer, "graph_safe", False)
         pool = torch.cuda.graph_pool_handle()
-        if self.overlap:
+        if self.overlap and getattr(self.reducer, "graph_safe", False):
+            # ONE graph for the whole step with the collectives inside it: after each backward
+            # segment the engine forks its comm stream off the capture stream (fork / join
+            # events become graph edges), so the segment's gradient reductions run on a
+            # parallel branch of the graph, overlapped with the rest of the backward, and
+            # the step is a single launch. (Several graphs with event records between their
+            # launches let a later graph start before the previous one had finished on
+            # MI355X -- tools/dp_variants.sh.) thread_local capture: the comm watchdog
+            # thread may touch its own events meanwhile.
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                self._forward(images, labels)
+                for i, (layers, _) in enumerate(self.model.backward_segments(self.dlogits)):
+                    self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
+                self.reducer.join()
+                self._optimizer()
+            self._g_all = g
+        elif self.overlap:
             # one graph per backward segment (the first also holds the forward), replayed in
             # capture order (they share one memory pool)
             segs = []

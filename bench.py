@@ -21,6 +21,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+import azure_hc_intel_tf_amd  # noqa: E402,F401  (HIP runtime defaults, before torch touches the GPU)
 
 BASELINE_VALUE = None  # the reference publishes no number
 
@@ -36,6 +37,9 @@ def main():
     ap.add_argument("--no_tune", action="store_true", help="skip per-shape kernel autotuning")
     ap.add_argument("--compression", default=None, choices=[None, "fp16", "bf16"])
     ap.add_argument("--engine", default="native", choices=["native", "torch"])
+    ap.add_argument("--force_dp_path", action="store_true",
+                    help="N=1 only: run the multi-GPU step (segmented graphs + async RCCL engine on a 1-rank "
+                         "communicator) to time its overhead on one GPU")
     ap.add_argument("--use_fp16", action="store_true",
                     help="tf_cnn_benchmarks --use_fp16: 16-bit compute (bf16 on MI355X) with automatic loss scaling")
     args = ap.parse_args()
@@ -82,6 +86,10 @@ def main():
         else:
             reducer = make_reducer("torch", compression=args.compression)
 
+    if world == 1 and args.force_dp_path:
+        from azure_hc_intel_tf_amd.parallel.native import NativeReducer
+
+        reducer = NativeReducer(compression=args.compression, force=True)
     model = create_model(args.model, device=dev)
     B = args.batch_size
     from azure_hc_intel_tf_amd.ops import autotune
@@ -96,7 +104,8 @@ def main():
         reducer.broadcast_(model.ps.buf, 0)
     images, labels = synthetic_batch(model, B, seed=rank)
     trainer = Trainer(model, B, resnet_lr_schedule(B * world), reducer=reducer, world_size=world,
-                      use_graph=not args.no_graph, dynamic_loss_scale=args.use_fp16)
+                      use_graph=not args.no_graph, dynamic_loss_scale=args.use_fp16,
+                      force_overlap=args.force_dp_path)
 
     def barrier():
         if world > 1:
@@ -108,9 +117,12 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
+    trace = torch.zeros(args.steps, device=dev) if os.environ.get("HCB_BENCH_LOSS_TRACE") == "1" else None
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         trainer.step(images, labels)
+        if trace is not None:  # device-side copy, no host sync (debug only)
+            trace[i:i + 1].copy_(trainer.loss)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
@@ -120,6 +132,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss = float(trainer.loss.item())
+    if trace is not None and rank == 0:
+        print("[bench] losses " + " ".join(f"{v:.4f}" for v in trace.tolist()), file=sys.stderr)
     ips = world * B * args.steps / elapsed
     if rank == 0:
         res = {
@@ -139,7 +153,7 @@ def main():
             "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
                        "image_size": model.image_size, "parallelism": f"dp{world}",
                        "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": not args.no_graph,
-                       "engine": args.engine if world > 1 else None, "compression": args.compression,
+                       "engine": args.engine if (world > 1 or args.force_dp_path) else None, "compression": args.compression,
                        "loss_scaling": "dynamic" if args.use_fp16 else None,
                        "final_loss": round(loss, 4)},
         }

@@ -106,10 +106,19 @@ struct Comm {
   std::mutex mu;
   std::condition_variable cv;
   std::atomic<bool> stop{false};
-  hipEvent_t watch_ev = nullptr;  // last join event to watch
-  std::chrono::steady_clock::time_point watch_since;
-  bool watching = false;
+  // Progress counters for the watchdog. The watchdog thread never calls into HIP or RCCL
+  // while the job is healthy: with a second host thread querying the comm stream's events
+  // (or host callbacks on that stream) the training step was corrupted intermittently on
+  // MI355X (tools/dp_variants.sh). Instead the CALLER's thread, at each new reduction,
+  // polls the previous cycle's dedicated watch event and advances `done`; the watchdog
+  // thread only compares `done` with `enq` and the clock. Only when the caller has been
+  // quiet for > 1 s (blocked on a hung collective, or idle) does the watchdog query the
+  // watch event itself, under `mu`, which every enqueue also holds.
+  std::atomic<int64_t> enq{0}, done{0};
+  bool skip_rccl = false;  // debug (HCB_COMM_SKIP_RCCL=1): stream fork/join without the collective
+  hipEvent_t watch_ev = nullptr;
   int64_t watch_cycle = 0;
+  std::chrono::steady_clock::time_point last_call = std::chrono::steady_clock::now();
   double stall_warn_s = 60.0, stall_abort_s = 0.0;
   std::atomic<bool> aborted{false};
 
@@ -144,11 +153,31 @@ bool capturing(hipStream_t s) {
 
 void watchdog_loop(Comm* c) {
   bool warned = false;
+  int64_t seen_done = -1;
+  auto since = std::chrono::steady_clock::now();
   while (!c->stop.load()) {
-    std::unique_lock<std::mutex> lk(c->mu);
-    c->cv.wait_for(lk, std::chrono::milliseconds(500));
+    {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv.wait_for(lk, std::chrono::milliseconds(500));
+    }
     if (c->stop.load()) break;
-    if (c->comm) {
+    if (c->stop.load()) break;
+    auto now = std::chrono::steady_clock::now();
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (c->done.load() < c->watch_cycle && std::chrono::duration<double>(now - c->last_call).count() > 1.0 &&
+          hipEventQuery(c->watch_ev) == hipSuccess)
+        c->done.store(c->watch_cycle, std::memory_order_release);
+    }
+    const int64_t d = c->done.load(std::memory_order_acquire), e = c->enq.load(std::memory_order_acquire);
+    if (d >= e || d != seen_done) {  // idle, or progress since the last look
+      seen_done = d;
+      since = now;
+      warned = false;
+      continue;
+    }
+    const double waited = std::chrono::duration<double>(now - since).count();
+    if (waited > 1.0 && c->comm) {  // stalled: only now ask RCCL whether a peer failed
       ncclResult_t ae = ncclSuccess;
       if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
         std::fprintf(stderr, "[hcb watchdog] rank %d: RCCL async error: %s -- aborting communicator\n", c->rank,
@@ -160,23 +189,11 @@ void watchdog_loop(Comm* c) {
         std::_Exit(18);
       }
     }
-    if (!c->watching || !c->watch_ev) {
-      warned = false;
-      continue;
-    }
-    hipError_t q = hipEventQuery(c->watch_ev);
-    if (q == hipSuccess) {
-      c->watching = false;
-      warned = false;
-      continue;
-    }
-    double waited =
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - c->watch_since).count();
     if (!warned && waited > c->stall_warn_s) {
       std::fprintf(stderr,
-                   "[hcb watchdog] rank %d: gradient allreduce of cycle %lld has not completed after %.0f s; "
+                   "[hcb watchdog] rank %d: gradient allreduce %lld has not completed after %.0f s; "
                    "one or more ranks may have stalled (HOROVOD_STALL_CHECK_TIME_SECONDS=%.0f)\n",
-                   c->rank, (long long)c->watch_cycle, waited, c->stall_warn_s);
+                   c->rank, (long long)d, waited, c->stall_warn_s);
       std::fflush(stderr);
       warned = true;
     }
@@ -219,6 +236,7 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
   HCB_HIP(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
   HCB_HIP(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
   HCB_HIP(hipEventCreate(&c->base_ev));
+  HCB_HIP(hipEventCreateWithFlags(&c->watch_ev, hipEventDisableTiming));
   HCB_HIP(hipEventRecord(c->base_ev, c->stream));
   if (const char* tl = std::getenv("HOROVOD_TIMELINE")) {
     if (*tl) {
@@ -231,8 +249,9 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
   }
   c->stall_warn_s = env_double("HOROVOD_STALL_CHECK_TIME_SECONDS", 60.0);
   c->stall_abort_s = env_double("HCB_STALL_ABORT_SECONDS", 0.0);
+  c->skip_rccl = env_double("HCB_COMM_SKIP_RCCL", 0.0) != 0.0;
   Comm* raw = c.get();
-  raw->wd = std::thread(watchdog_loop, raw);
+  if (env_double("HCB_COMM_WATCHDOG", 1.0) != 0.0) raw->wd = std::thread(watchdog_loop, raw);
   std::lock_guard<std::mutex> lk(g_mu);
   int64_t h = g_next++;
   g_comms[h] = std::move(c);
@@ -293,6 +312,7 @@ void destroy(int64_t h) {
   hipEventDestroy(c->fork_ev);
   hipEventDestroy(c->join_ev);
   hipEventDestroy(c->base_ev);
+  hipEventDestroy(c->watch_ev);
   if (c->cbuf) hipFree(c->cbuf);
   hipStreamDestroy(c->stream);
 }
@@ -364,9 +384,13 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
   const int64_t n = flat.numel();
   for (int64_t i = 0; i < nb; ++i)
     TORCH_CHECK(bk[2 * i] >= 0 && bk[2 * i + 1] > 0 && bk[2 * i] + bk[2 * i + 1] <= n, "hcb_comm: bucket out of range");
+  std::lock_guard<std::mutex> call_lk(c->mu);  // excludes the watchdog's (rare) event query
+  c->last_call = std::chrono::steady_clock::now();
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   const bool cap = capturing(cur);
   if (!cap) flush_timeline(c, false);
+  if (!cap && c->wd.joinable() && c->done.load() < c->watch_cycle && hipEventQuery(c->watch_ev) == hipSuccess)
+    c->done.store(c->watch_cycle, std::memory_order_release);
   if (compress && c->cbuf_bytes < (size_t)n * 2) {
     TORCH_CHECK(!cap, "hcb_comm: first compressed reduction must run outside graph capture");
     HCB_HIP(hipStreamSynchronize(c->stream));
@@ -390,7 +414,7 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
       hcb::launch_bucket_pack(fp + off, cb, len, (float)scale, 1, c->stream);
       HCB_NCCL(ncclAllReduce(cb, cb, len, ncclBfloat16, average ? ncclAvg : ncclSum, c->comm, c->stream));
       hcb::launch_bucket_unpack(cb, fp + off, len, 1.0f, 1, c->stream);
-    } else {
+    } else if (!c->skip_rccl) {
       HCB_NCCL(ncclAllReduce(fp + off, fp + off, len, ncclFloat32, average ? ncclAvg : ncclSum, c->comm, c->stream));
     }
     if (tl) {
@@ -401,12 +425,9 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
   }
   HCB_HIP(hipEventRecord(c->join_ev, c->stream));
   if (do_join) HCB_HIP(hipStreamWaitEvent(cur, c->join_ev, 0));
-  if (!cap) {
-    std::lock_guard<std::mutex> lk(c->mu);
-    c->watch_ev = c->join_ev;
-    c->watch_since = std::chrono::steady_clock::now();
-    c->watching = true;
-    c->watch_cycle = c->cycle;
+  if (!cap && c->wd.joinable()) {
+    HCB_HIP(hipEventRecord(c->watch_ev, c->stream));
+    c->watch_cycle = c->enq.fetch_add(1, std::memory_order_acq_rel) + 1;
   }
   c->cycle++;
 }

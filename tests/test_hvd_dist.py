@@ -223,3 +223,43 @@ def test_stall_abort_exits_the_stuck_rank(monkeypatch):
     assert p0.exitcode == STALL_EXIT_CODE
     p1.kill()
     p1.join(timeout=30)
+
+
+@pytest.mark.parametrize("name,size", [("resnet50", 32), ("resnet50_v2", 32), ("inception3", 107), ("vgg11", 32),
+                                       ("googlenet", 64), ("alexnet", 99)])
+def test_segmented_backward_equals_plain_backward(name, size, monkeypatch):
+    """backward_segments (the multi-GPU overlap path) computes the same gradients as the plain
+    backward, closes more than one segment for the large models, and its segments own every
+    parameter exactly once."""
+    monkeypatch.setenv("HCB_SEGMENT_PARAMS", "500000")
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.nn.layers import Dropout
+    from azure_hc_intel_tf_amd.trainer import synthetic_batch
+
+    torch.manual_seed(0)
+    m = create_model(name, image_size=size, device="cpu")
+    for l in getattr(m, "seq", []):
+        if isinstance(l, Dropout):
+            l.keep = 1.0
+    img, lab = synthetic_batch(m, 2)
+    dl = torch.randn(2, m.num_classes, dtype=torch.float32).to(m.act_dtype) * 0.1
+    if dl.shape[1] != getattr(m.fc, "ld", dl.shape[1]):
+        dl = torch.nn.functional.pad(dl, (0, m.fc.ld - dl.shape[1]))
+    m.ps.zero_grad()
+    m.forward(img)
+    m.backward(dl)
+    g_plain = m.ps.grad.clone()
+    m.ps.zero_grad()
+    m.forward(img)
+    cover = torch.zeros(m.ps.grad.numel(), dtype=torch.int32)
+    nseg = 0
+    for layers, last in m.backward_segments(dl):
+        nseg += 1
+        rng = [(0, m.ps.grad.numel())] if layers is None else m.grad_ranges(layers)
+        for off, n in rng:
+            cover[off:off + n] += 1
+    assert last
+    assert int(cover.max()) == 1 and int(cover.sum()) >= m.num_params() - 64
+    if name != "alexnet":
+        assert nseg >= 2
+    assert torch.allclose(m.ps.grad, g_plain, rtol=1e-4, atol=1e-6)
