@@ -177,15 +177,25 @@ class Trainer:
             # launches let a later graph start before the previous one had finished on
             # MI355X -- tools/dp_variants.sh.) thread_local capture: the comm watchdog
             # thread may touch its own events meanwhile.
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
-                self._forward(images, labels)
-                for i, (layers, _) in enumerate(self.model.backward_segments(self.dlogits)):
-                    self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
-                self.reducer.join()
-                self._optimizer()
-            self._g_all = g
-        elif self.overlap:
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                    self._forward(images, labels)
+                    for i, (layers, _) in enumerate(self.model.backward_segments(self.dlogits)):
+                        self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
+                    self.reducer.join()
+                    self._optimizer()
+                self._g_all = g
+                self._static = (images, labels)
+                torch.cuda.synchronize()
+                return
+            except RuntimeError as e:  # collectives not capturable here: per-segment graphs
+                print(f"[trainer] capturing the collectives failed ({e}); replaying one graph per "
+                      "backward segment instead", flush=True)
+                torch.cuda.synchronize()
+                self.reducer.graph_safe = False
+                pool = torch.cuda.graph_pool_handle()
+        if self.overlap and not getattr(self.reducer, "graph_safe", False):
             # one graph per backward segment (the first also holds the forward), replayed in
             # capture order (they share one memory pool)
             segs = []
@@ -205,7 +215,7 @@ class Trainer:
             with torch.cuda.graph(g2, pool=pool):
                 self._optimizer()
             self._segs, self._g_opt = segs, g2
-        elif single:
+        elif single and not self.overlap:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 self._forward_backward(images, labels)
