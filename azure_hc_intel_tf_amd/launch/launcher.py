@@ -34,12 +34,86 @@ def fabric_env(fabric: str) -> Dict[str, str]:
     raise ValueError(f"unknown fabric {fabric!r} (expected ib or sock)")
 
 
-def cpu_shares(n_workers: int, cpus: Optional[List[int]] = None) -> List[List[int]]:
+def _parse_cpulist(text: str) -> List[int]:
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out += list(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return out
+
+
+def _read(path: str) -> Optional[str]:
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def gpu_numa_nodes(sysfs: str = "/sys") -> List[int]:
+    """NUMA node of every GPU in HIP device order (the KFD topology's GPU agents, in node
+    order), from the agent's PCI location -> /sys/bus/pci/devices/<bdf>/numa_node. -1 where
+    unknown; [] without a KFD topology (no GPU driver, e.g. CPU-only hosts)."""
+    root = os.path.join(sysfs, "class/kfd/kfd/topology/nodes")
+    try:
+        nodes = sorted(int(n) for n in os.listdir(root) if n.isdigit())
+    except OSError:
+        return []
+    out = []
+    for n in nodes:
+        props = _read(os.path.join(root, str(n), "properties"))
+        if props is None:
+            out.append(-1)  # an agent we may not read: keep the device index aligned
+            continue
+        kv = dict(line.split()[:2] for line in props.splitlines() if len(line.split()) >= 2)
+        if int(kv.get("simd_count", "0")) == 0:
+            continue  # CPU agent
+        loc, dom = int(kv.get("location_id", "0")), int(kv.get("domain", "0"))
+        bdf = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+        numa = _read(os.path.join(sysfs, "bus/pci/devices", bdf, "numa_node"))
+        out.append(int(numa) if numa is not None and numa.strip().lstrip("-").isdigit() else -1)
+    return out
+
+
+def cpu_shares(n_workers: int, cpus: Optional[List[int]] = None, sysfs: str = "/sys") -> List[List[int]]:
+    """CPU set per local worker: the cores of its GPU's NUMA node, split evenly between the
+    workers whose GPUs share that node (the reference's ``--map-by ppr:W:socket,pe=C``,
+    run-tf-sing-ucx-openmpi.sh:102, made GPU-affine); contiguous equal shares of the allowed
+    CPUs when the topology is unknown."""
     cpus = sorted(cpus if cpus is not None else os.sched_getaffinity(0))
     if n_workers <= 0:
         return []
     per = max(len(cpus) // n_workers, 1)
-    return [cpus[i * per:(i + 1) * per] or cpus for i in range(n_workers)]
+    flat = [cpus[i * per:(i + 1) * per] or cpus for i in range(n_workers)]
+    numa = gpu_numa_nodes(sysfs)
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    if vis and numa:
+        try:
+            numa = [numa[int(i)] for i in vis.split(",") if i.strip() != ""]
+        except (ValueError, IndexError):
+            return flat
+    if len(numa) < n_workers or any(n < 0 for n in numa[:n_workers]):
+        return flat
+    allowed = set(cpus)
+    by_node = {}
+    for w in range(n_workers):
+        by_node.setdefault(numa[w], []).append(w)
+    shares: List[List[int]] = [[] for _ in range(n_workers)]
+    for node, ws in by_node.items():
+        text = _read(os.path.join(sysfs, "devices/system/node", f"node{node}", "cpulist"))
+        node_cpus = [c for c in _parse_cpulist(text)] if text else []
+        node_cpus = sorted(c for c in node_cpus if c in allowed)
+        if len(node_cpus) < len(ws):
+            return flat
+        k = len(node_cpus) // len(ws)
+        for j, w in enumerate(ws):
+            shares[w] = node_cpus[j * k:(j + 1) * k]
+    return shares
 
 
 def free_port() -> int:

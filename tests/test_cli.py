@@ -128,3 +128,34 @@ def test_launcher_propagates_rank_failure(tmp_path):
     assert out.returncode == 17, out.stdout[-2000:] + out.stderr[-2000:]
     assert "[fault injection] rank 1 aborting at step 2" in out.stdout
     assert time.time() - t0 < 200
+
+
+def test_cpu_shares_follow_gpu_numa_nodes(tmp_path):
+    """Each worker is pinned to the cores of its GPU's NUMA node (fake sysfs: 4 GPUs, two per
+    socket, behind two CPU agents)."""
+    sysfs = tmp_path
+    topo = sysfs / "class/kfd/kfd/topology/nodes"
+    cpu_props = "cpu_cores_count 64\nsimd_count 0\nlocation_id 0\ndomain 0\n"
+    gpus = [(0x1100, 0), (0x2100, 0), (0x9100, 1), (0xa100, 1)]
+    (topo / "0").mkdir(parents=True)
+    (topo / "0" / "properties").write_text(cpu_props)
+    (topo / "1").mkdir()
+    (topo / "1" / "properties").write_text(cpu_props)
+    for i, (loc, node) in enumerate(gpus):
+        d = topo / str(i + 2)
+        d.mkdir()
+        d.joinpath("properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nlocation_id {loc}\ndomain 0\n")
+        bdf = f"0000:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+        (sysfs / "bus/pci/devices" / bdf).mkdir(parents=True)
+        (sysfs / "bus/pci/devices" / bdf / "numa_node").write_text(f"{node}\n")
+    for node, cl in ((0, "0-7,16-23"), (1, "8-15,24-31")):
+        (sysfs / f"devices/system/node/node{node}").mkdir(parents=True)
+        (sysfs / f"devices/system/node/node{node}/cpulist").write_text(cl + "\n")
+    from azure_hc_intel_tf_amd.launch.launcher import gpu_numa_nodes
+
+    assert gpu_numa_nodes(str(sysfs)) == [0, 0, 1, 1]
+    sh = cpu_shares(4, list(range(32)), sysfs=str(sysfs))
+    assert sh[0] == [0, 1, 2, 3, 4, 5, 6, 7] and sh[1] == [16, 17, 18, 19, 20, 21, 22, 23]
+    assert sh[2] == list(range(8, 16)) and sh[3] == list(range(24, 32))
+    # unknown topology: contiguous equal shares
+    assert cpu_shares(2, list(range(8)), sysfs=str(tmp_path / "none")) == [[0, 1, 2, 3], [4, 5, 6, 7]]
