@@ -125,7 +125,7 @@ def wgrad_candidates(Nout: int, K: int, M: int):
     out = []
     for c, (bm, bn) in _WGRAD_TILES.items():
         tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
-        for s in (1, 2, 4, 8, 16, 32, 64, 128):
+        for s in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512):
             if s > 1 and ksteps // s < 2:
                 break
             if tiles * s > 8 * N_CU:

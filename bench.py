@@ -149,7 +149,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": (ips / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16",
-            "data": "synthetic (truncated-normal ImageNet 224x224, random-init weights)",
+            "data": f"synthetic (truncated-normal ImageNet {model.image_size}x{model.image_size}, random-init weights)",
             "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
                        "image_size": model.image_size, "parallelism": f"dp{world}",
                        "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": not args.no_graph,
