@@ -11,6 +11,8 @@
 // [T][2][C] (the conv epilogue writes the same slab format, so stats can be fused into
 // the producing GEMM), then a finalize kernel that sums the slab in fp64 — no float
 // atomics, bitwise reproducible.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -837,7 +839,18 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
   int need = (M + rows - 1) / rows;
   int target = 2048 / groups;
   if (target < 1) target = 1;
-  int s = need < target ? need : target;
+  // Small tensors: give every thread up to BN_U rows (all loads in flight at once) rather than
+  // one row per thread -- fewer workgroups to dispatch and one memory round trip, while the
+  // grid still covers every CU. HCB_BN_ROWS_PER_THREAD=1 restores one row per thread.
+  static const int rpt = [] {
+    const char* e = std::getenv("HCB_BN_ROWS_PER_THREAD");
+    const int v = e ? std::atoi(e) : BN_U;
+    return v < 1 ? 1 : (v > BN_U ? BN_U : v);
+  }();
+  int floor_s = (256 + groups - 1) / groups;
+  int want = (need + rpt - 1) / rpt;
+  if (want < floor_s) want = floor_s < need ? floor_s : need;
+  int s = want < target ? want : target;
   if (s < 1) s = 1;
   *cvb_out = cvb;
   return dim3(s, groups);
