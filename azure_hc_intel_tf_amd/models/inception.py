@@ -68,6 +68,18 @@ class InceptionModule:
                 shape = node.layer.out_shape
             self.terminals.append(cur[-1])
             prev_col = cur
+        # consumers of every node's output (a terminal's concat slice counts as one): a conv whose
+        # input comes from a single-consumer conv produces that conv's whole dy, so the
+        # producer's BN-backward reduction is fused into the consumer's data-grad epilogue
+        cons = {}
+        for n in self.nodes:
+            if n.src is not None:
+                cons[id(n.src)] = cons.get(id(n.src), 0) + 1
+        for t in self.terminals:
+            cons[id(t)] = cons.get(id(t), 0) + 1
+        self._fuse_src = {id(n) for n in self.nodes
+                          if n.src is not None and cons.get(id(n.src)) == 1
+                          and isinstance(n.layer, ConvBN) and isinstance(n.src.layer, ConvBN) and n.src.layer.bn}
         outs = [t.layer.out_shape for t in self.terminals]
         H, W = outs[0][0], outs[0][1]
         assert all(o[0] == H and o[1] == W for o in outs), f"{name}: branch spatial mismatch {outs}"
@@ -109,6 +121,9 @@ class InceptionModule:
                     dx, _ = n.layer.backward(g, dx=dx, accumulate=dx is not None)
                 else:
                     dx = n.layer.backward(g, dx=dx, accumulate=dx is not None)
+            elif id(n) in self._fuse_src:
+                r, _ = n.layer.backward(g, dx_bn=n.src.layer)
+                grads[id(n.src)] = (r, True)
             else:
                 prev = grads.get(id(n.src))
                 tgt = prev[0] if prev is not None else None
@@ -196,9 +211,10 @@ class InceptionV3(CNNModel):
         logits hold most of the parameters), then the stem."""
         dx = self.gap.backward(self.fc.backward(dlogits))
         units = [(m.backward, m.layers()) for m in reversed(self.modules)]
-        for l in reversed(self.stem):
+        for i in range(len(self.stem) - 1, -1, -1):
+            l, below = self.stem[i], self._stem_bn_below(i)
             if isinstance(l, ConvBN):
-                units.append((lambda d, l=l: l.backward(d)[0], [l]))
+                units.append((lambda d, l=l, b=below: l.backward(d, dx_bn=b)[0], [l]))
             else:
                 units.append((l.backward, [l]))
         yield from self._segments_from_units(dx, [self.fc, self.gap], units)
@@ -207,9 +223,19 @@ class InceptionV3(CNNModel):
         dx = self.gap.backward(self.fc.backward(dlogits))
         for m in reversed(self.modules):
             dx = m.backward(dx)
-        for l in reversed(self.stem):
+        for i in range(len(self.stem) - 1, -1, -1):
+            l = self.stem[i]
             if isinstance(l, ConvBN):
-                dx, _ = l.backward(dx) if l.need_dx else (l.backward(dx)[0], None)
+                dx, _ = l.backward(dx, dx_bn=self._stem_bn_below(i))
             else:
                 dx = l.backward(dx)
         join_side_streams()
+
+    def _stem_bn_below(self, i):
+        """The conv+BN feeding stem layer i directly (its BN-backward reduction is fused into
+        layer i's data-grad epilogue), else None."""
+        l = self.stem[i]
+        if i > 0 and isinstance(l, ConvBN) and l.need_dx and isinstance(self.stem[i - 1], ConvBN) \
+                and self.stem[i - 1].bn:
+            return self.stem[i - 1]
+        return None
