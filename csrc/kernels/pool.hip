@@ -166,6 +166,135 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(
   }
 }
 
+// 3x3 stride-1 pools (Inception's 3x3/1 'SAME' average-pool branches and the 3x3/1 max pool of
+// the last module): all nine window loads are issued before any is used -- raw buffer loads
+// whose out-of-range offset returns zero stand in for the halo -- instead of one dependent
+// load per loop trip of the generic kernel.
+template <bool IS_MAX>
+__global__ __launch_bounds__(256) void pool3s1_fwd_kernel(const uint16_t* __restrict__ x, uint32_t x_bytes,
+                                                          uint16_t* __restrict__ y, int N, int H, int W, int C,
+                                                          int ldx, int P, int Q, int ldy, int ph, int pw,
+                                                          int incl_pad, uint8_t* __restrict__ amax) {
+  const unsigned CV = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, x_bytes);
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int cv = (int)(idx % CV);
+    const unsigned pix = idx / CV;
+    const int q = (int)(pix % (unsigned)Q);
+    const unsigned t = pix / (unsigned)Q;
+    const int p = (int)(t % (unsigned)P);
+    const int n = (int)(t / (unsigned)P);
+    const int h0 = p - ph, w0 = q - pw;
+    u32x4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int h = h0 + r, w = w0 + s2;
+        const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        ok[r * 3 + s2] = in;
+        v[r * 3 + s2] = buf_load16(xr, in ? (uint32_t)(((n * H + h) * W + w) * ldx + cv * 8) * 2u : HCB_OOB);
+      }
+    float acc[8];
+    if constexpr (IS_MAX) {
+      int arg[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[e] = -INFINITY;
+        arg[e] = 255;
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        if (!ok[k]) continue;
+        float f[8];
+        unpack8(v[k], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (f[e] > acc[e]) {  // strict: the FIRST maximal element keeps the gradient
+            acc[e] = f[e];
+            arg[e] = k;
+          }
+      }
+      if (amax != nullptr) {
+        u32x2 a;
+        a[0] = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+        a[1] = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+        *reinterpret_cast<u32x2*>(amax + ((size_t)(n * P + p) * Q + q) * C + cv * 8) = a;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {  // out-of-range taps loaded zeros
+        float f[8];
+        unpack8(v[k], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+      }
+      const int vr = ((unsigned)h0 < (unsigned)H) + ((unsigned)(h0 + 1) < (unsigned)H) +
+                     ((unsigned)(h0 + 2) < (unsigned)H);
+      const int vc = ((unsigned)w0 < (unsigned)W) + ((unsigned)(w0 + 1) < (unsigned)W) + ((unsigned)(w0 + 2) < (unsigned)W);
+      const float inv = 1.f / (float)(incl_pad ? 9 : (vr * vc > 0 ? vr * vc : 1));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    }
+    *reinterpret_cast<u32x4*>(y + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8) = pack8(acc);
+  }
+}
+
+// Average-pool 3x3/1 backward as a gather: the (up to) nine windows covering a pixel, each
+// scaled by 1 / (its valid-tap count), all loads in flight together.
+__global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const uint16_t* __restrict__ dy, uint32_t dy_bytes,
+                                                             uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                             int ldx, int P, int Q, int ldy, int ph, int pw,
+                                                             int incl_pad, int accum) {
+  const unsigned CV = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * H * W * CV;
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(dy, dy_bytes);
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int cv = (int)(idx % CV);
+    const unsigned pix = idx / CV;
+    const int w = (int)(pix % (unsigned)W);
+    const unsigned t = pix / (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
+    u32x4 d[9];
+    float sc[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int p = h + ph - i, q = w + pw - j;  // windows p - ph <= h <= p - ph + 2
+        const bool in = (unsigned)p < (unsigned)P && (unsigned)q < (unsigned)Q;
+        d[i * 3 + j] = buf_load16(dr, in ? (uint32_t)(((n * P + p) * Q + q) * ldy + cv * 8) * 2u : HCB_OOB);
+        const int hs = p - ph, ws = q - pw;
+        const int vr = ((unsigned)hs < (unsigned)H) + ((unsigned)(hs + 1) < (unsigned)H) + ((unsigned)(hs + 2) < (unsigned)H);
+        const int vc = ((unsigned)ws < (unsigned)W) + ((unsigned)(ws + 1) < (unsigned)W) + ((unsigned)(ws + 2) < (unsigned)W);
+        sc[i * 3 + j] = in ? 1.f / (float)(incl_pad ? 9 : (vr * vc > 0 ? vr * vc : 1)) : 0.f;
+      }
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      float f[8];
+      unpack8(d[k], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] += f[e] * sc[k];
+    }
+    uint16_t* dp = dx + ((size_t)(n * H + h) * W + w) * ldx + cv * 8;
+    if (accum) {
+      float o[8];
+      unpack8(*reinterpret_cast<const u32x4*>(dp), o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] += o[e];
+    }
+    *reinterpret_cast<u32x4*>(dp) = pack8(g);
+  }
+}
+
 // Max-pool backward from the recorded argmax when at most NPW x NPW windows cover a pixel
 // (ceil(k/s) <= NPW; ResNet's 3x3/2: 2x2): the candidate windows are unrolled so all their dy /
 // argmax loads are in flight together instead of one loop trip at a time.
@@ -275,6 +404,18 @@ void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx
                      int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
                      int count_include_pad, void* idx, hipStream_t st) {
   long total = (long)N * P * Q * (C / 8);
+  const long xbytes = (long)N * H * W * ldx * 2;
+  if (kh == 3 && kw == 3 && sh == 1 && sw == 1 && xbytes < 0x7fffffffL) {
+    if (is_max)
+      hipLaunchKernelGGL(pool3s1_fwd_kernel<true>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)x,
+                         (uint32_t)xbytes, (uint16_t*)y, N, H, W, C, ldx, P, Q, ldy, ph, pw, count_include_pad,
+                         (uint8_t*)idx);
+    else
+      hipLaunchKernelGGL(pool3s1_fwd_kernel<false>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)x,
+                         (uint32_t)xbytes, (uint16_t*)y, N, H, W, C, ldx, P, Q, ldy, ph, pw, count_include_pad,
+                         (uint8_t*)idx);
+    return;
+  }
   hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)x,
                      (uint16_t*)y, N, H, W, C, ldx, P, Q, ldy, kh, kw, sh, sw, ph, pw, is_max,
                      count_include_pad, (uint8_t*)idx);
@@ -288,6 +429,17 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
   if (is_max && idx != nullptr && (kh + sh - 1) / sh <= 2 && (kw + sw - 1) / sw <= 2 && kh == kw && sh == sw) {
     hipLaunchKernelGGL(maxpool_bwd_amax_kernel<2>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
                        (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx);
+    return;
+  }
+  if (is_max && idx != nullptr && (kh + sh - 1) / sh <= 3 && (kw + sw - 1) / sw <= 3 && kh == kw && sh == sw) {
+    hipLaunchKernelGGL(maxpool_bwd_amax_kernel<3>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
+                       (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx);
+    return;
+  }
+  const long dybytes = (long)N * P * Q * ldy * 2;
+  if (!is_max && kh == 3 && kw == 3 && sh == 1 && sw == 1 && dybytes < 0x7fffffffL) {
+    hipLaunchKernelGGL(avgpool3s1_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
+                       (uint32_t)dybytes, (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, ph, pw, count_include_pad, accum);
     return;
   }
   hipLaunchKernelGGL(pool_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,

@@ -305,7 +305,8 @@ def test_bn_fwd_bwd(C, relu, residual):
     assert rel_err(gres, gresc) < 1e-2
 
 
-@pytest.mark.parametrize("kind", ["max3s2same", "avg3s1same", "max3s2valid", "avg8valid"])
+@pytest.mark.parametrize("kind", ["max3s2same", "avg3s1same", "max3s2valid", "avg8valid", "max3s1same",
+                                  "avg3s1valid"])
 def test_pool_fwd_bwd(kind):
     from azure_hc_intel_tf_amd.nn.layers import Pool
 
@@ -317,6 +318,10 @@ def test_pool_fwd_bwd(kind):
         layer = Pool("p", (H, H, C), 3, 3, 1, 1, "SAME", is_max=False)
     elif kind == "max3s2valid":
         layer = Pool("p", (H, H, C), 3, 3, 2, 2, "VALID", is_max=True)
+    elif kind == "max3s1same":  # Inception's last module (3x3/1 kernels, argmax over 3x3 windows)
+        layer = Pool("p", (H, H, C), 3, 3, 1, 1, "SAME", is_max=True)
+    elif kind == "avg3s1valid":
+        layer = Pool("p", (H, H, C), 3, 3, 1, 1, "VALID", is_max=False)
     else:
         H = 8
         layer = Pool("p", (H, H, C), 8, 8, 1, 1, "VALID", is_max=False)
