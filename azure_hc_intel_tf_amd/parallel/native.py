@@ -135,6 +135,13 @@ class NativeReducer:
         self.graph_safe = os.environ.get("HCB_GRAPH_COMM", "1") == "1"
         self.force = force
         self._buckets = None
+        # opt-in one-shot xGMI allreduce for small fp32 ranges (single node only)
+        self.xgmi, self.xgmi_bytes = None, int(os.environ.get("HCB_XGMI_BYTES", "0"))
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", self.comm.world))
+        if self.xgmi_bytes > 0 and not self.compress and 1 < self.comm.world == local:
+            from .xgmi import XgmiAllreduce
+
+            self.xgmi = XgmiAllreduce(capacity_bytes=self.xgmi_bytes)
 
     def _bucket_table(self, numel):
         if self._buckets is None or self._numel != numel:
@@ -156,6 +163,13 @@ class NativeReducer:
             return
         if os.environ.get("HCB_COMM_NOOP") == "1":  # debug: segmented step without collectives
             return
+        if self.xgmi is not None:  # small ranges: one hop over xGMI on the caller's stream
+            small = [r for r in ranges if r[1] * 4 <= self.xgmi_bytes]
+            for off, n in small:
+                self.xgmi.allreduce_(flat[off:off + n], average=self.average)
+            ranges = [r for r in ranges if r[1] * 4 > self.xgmi_bytes]
+            if not ranges:
+                return
         table = torch.tensor([list(r) for r in ranges], dtype=torch.int64).view(-1, 2)
         self.comm.bucket_allreduce_async_(flat, table, self.compress, 1.0, self.average)
 
@@ -168,4 +182,6 @@ class NativeReducer:
         return t
 
     def close(self):
+        if self.xgmi is not None:
+            self.xgmi.close()
         self.comm.close()

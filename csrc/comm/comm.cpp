@@ -458,6 +458,115 @@ void barrier(int64_t h) {
   HCB_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStream().stream()));
 }
 
+// ------------------------------------------------------------ one-shot xGMI allreduce
+// IPC-shared staging regions (csrc/kernels/xgmi.hip has the protocol). Independent of the
+// RCCL communicator: handles are exchanged by the Python side over torch.distributed.
+struct Xgmi {
+  int rank = 0, world = 1, device = 0;
+  int64_t cap = 0;                  // floats per slot
+  float* region = nullptr;          // own region: 2 slots + flags
+  unsigned* err = nullptr;          // device error word (spin timeout)
+  std::vector<float*> peers;        // every rank's region as mapped here (own = region)
+  std::vector<bool> opened;
+};
+std::mutex g_xmu;
+std::map<int64_t, std::unique_ptr<Xgmi>> g_xgmi;
+int64_t g_xnext = 1;
+
+Xgmi* xget(int64_t h) {
+  std::lock_guard<std::mutex> lk(g_xmu);
+  auto it = g_xgmi.find(h);
+  TORCH_CHECK(it != g_xgmi.end(), "hcb_comm: invalid xgmi handle ", h);
+  return it->second.get();
+}
+
+int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, int64_t device) {
+  TORCH_CHECK(world >= 1 && world <= hcb::xgmi_max_ranks() && rank >= 0 && rank < world,
+              "hcb_comm.xgmi_create: 1..", hcb::xgmi_max_ranks(), " ranks");
+  TORCH_CHECK(cap > 0 && cap % 4 == 0, "hcb_comm.xgmi_create: capacity must be a positive multiple of 4 floats");
+  auto x = std::make_unique<Xgmi>();
+  x->rank = (int)rank;
+  x->world = (int)world;
+  x->device = (int)device;
+  x->cap = cap;
+  HCB_HIP(hipSetDevice(x->device));
+  const size_t bytes = (size_t)2 * cap * 4 + 256;
+  HCB_HIP(hipMalloc(&x->region, bytes));
+  HCB_HIP(hipMemset(x->region, 0, bytes));
+  HCB_HIP(hipMalloc(&x->err, 4));
+  HCB_HIP(hipMemset(x->err, 0, 4));
+  HCB_HIP(hipDeviceSynchronize());
+  x->peers.assign(world, nullptr);
+  x->opened.assign(world, false);
+  x->peers[rank] = x->region;
+  std::lock_guard<std::mutex> lk(g_xmu);
+  int64_t h = g_xnext++;
+  g_xgmi[h] = std::move(x);
+  return h;
+}
+
+Tensor xgmi_handle(int64_t h) {
+  Xgmi* x = xget(h);
+  hipIpcMemHandle_t mh;
+  HCB_HIP(hipIpcGetMemHandle(&mh, x->region));
+  Tensor t = at::empty({(int64_t)sizeof(mh)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &mh, sizeof(mh));
+  return t;
+}
+
+void xgmi_open(int64_t h, const Tensor& handles) {
+  Xgmi* x = xget(h);
+  TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.dim() == 2 &&
+                  handles.size(0) == x->world && handles.size(1) == (int64_t)sizeof(hipIpcMemHandle_t),
+              "hcb_comm.xgmi_open: handles uint8 [world][", sizeof(hipIpcMemHandle_t), "] on CPU");
+  HCB_HIP(hipSetDevice(x->device));
+  for (int r = 0; r < x->world; ++r) {
+    if (r == x->rank) continue;
+    hipIpcMemHandle_t mh;
+    std::memcpy(&mh, handles.data_ptr<uint8_t>() + (size_t)r * sizeof(mh), sizeof(mh));
+    void* p = nullptr;
+    HCB_HIP(hipIpcOpenMemHandle(&p, mh, hipIpcMemLazyEnablePeerAccess));
+    x->peers[r] = static_cast<float*>(p);
+    x->opened[r] = true;
+  }
+}
+
+void xgmi_allreduce_(int64_t h, const Tensor& t, double scale) {
+  Xgmi* x = xget(h);
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat,
+              "hcb_comm.xgmi_allreduce_: contiguous fp32 GPU tensor");
+  TORCH_CHECK(t.numel() <= x->cap, "hcb_comm.xgmi_allreduce_: ", t.numel(), " floats > capacity ", x->cap);
+  for (int r = 0; r < x->world; ++r) TORCH_CHECK(x->peers[r] != nullptr, "hcb_comm.xgmi: peer ", r, " not opened");
+  if (t.numel() == 0) return;
+  std::vector<const float*> b(x->peers.begin(), x->peers.end());
+  hcb::launch_xgmi_allreduce(b.data(), x->world, x->rank, t.data_ptr<float>(), t.data_ptr<float>(), t.numel(),
+                             x->cap, (float)scale, x->err, c10::hip::getCurrentHIPStream().stream());
+}
+
+int64_t xgmi_error(int64_t h) {
+  Xgmi* x = xget(h);
+  unsigned v = 0;
+  HCB_HIP(hipMemcpy(&v, x->err, 4, hipMemcpyDeviceToHost));
+  return (int64_t)v;
+}
+
+void xgmi_destroy(int64_t h) {
+  std::unique_ptr<Xgmi> x;
+  {
+    std::lock_guard<std::mutex> lk(g_xmu);
+    auto it = g_xgmi.find(h);
+    if (it == g_xgmi.end()) return;
+    x = std::move(it->second);
+    g_xgmi.erase(it);
+  }
+  hipSetDevice(x->device);
+  hipDeviceSynchronize();
+  for (int r = 0; r < x->world; ++r)
+    if (x->opened[r]) hipIpcCloseMemHandle(x->peers[r]);
+  hipFree(x->region);
+  hipFree(x->err);
+}
+
 int64_t comm_rank(int64_t h) { return get(h)->rank; }
 int64_t comm_size(int64_t h) { return get(h)->world; }
 
@@ -495,4 +604,10 @@ TORCH_LIBRARY(hcb_comm, m) {
   m.def("size(int h) -> int", comm_size);
   m.def("abort(int h) -> ()", abort_comm);
   m.def("version() -> str", version);
+  m.def("xgmi_create(int rank, int world, int cap, int device) -> int", xgmi_create);
+  m.def("xgmi_handle(int h) -> Tensor", xgmi_handle);
+  m.def("xgmi_open(int h, Tensor handles) -> ()", xgmi_open);
+  m.def("xgmi_allreduce_(int h, Tensor(a!) t, float scale) -> ()", xgmi_allreduce_);
+  m.def("xgmi_error(int h) -> int", xgmi_error);
+  m.def("xgmi_destroy(int h) -> ()", xgmi_destroy);
 }

@@ -103,3 +103,57 @@ def test_segmented_overlap_step_matches_single_graph(model_name):
     assert torch.isfinite(b).all()
     assert torch.allclose(a[:4], b[:4], rtol=3e-2, atol=3e-2), (runs[0], runs[1])
     assert b[-1] < 0.9 * b[0] and a[-1] < 0.9 * a[0], (runs[0], runs[1])
+
+
+def _xgmi_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)  # every rank on the one GPU of the box: IPC maps within the device
+    from azure_hc_intel_tf_amd.parallel.xgmi import XgmiAllreduce
+
+    x = XgmiAllreduce(capacity_bytes=1 << 20)
+    ok = True
+    for it, n in enumerate([1, 7, 4096, 100_003, 262_144, 5, 65_536]):  # > 2 epochs per slot
+        t = torch.arange(n, dtype=torch.float32, device="cuda") * (rank + 1) + it
+        x.allreduce_(t, average=(it % 2 == 1))
+        ref = torch.arange(n, dtype=torch.float32, device="cuda") * sum(range(1, world + 1)) + it * world
+        if it % 2 == 1:
+            ref /= world
+        torch.cuda.synchronize()
+        ok = ok and torch.allclose(t, ref, rtol=1e-6, atol=1e-3)
+    err = x.error()
+    x.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, bool(ok), err))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_xgmi_one_shot_allreduce_two_processes_one_gpu(world):
+    """The IPC one-shot allreduce protocol (publish / bounded wait / system-scope reads, slot
+    alternation across epochs, in-place, average) with `world` processes sharing the GPU."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_xgmi_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = [q.get(timeout=100) for _ in range(world)]
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert all(ok and err == 0 for _, ok, err in res), res
