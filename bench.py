@@ -53,6 +53,10 @@ def main():
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)
         sys.exit(2)
+    # rehearsal knobs for a one-GPU box (never used by the driver): every rank on device 0
+    # and gloo instead of RCCL, which refuses two ranks on one device
+    if os.environ.get("HCB_BENCH_ONE_DEVICE") == "1":
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -63,7 +67,12 @@ def main():
     _ext.load()
     reducer = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("HCB_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+            args.engine = "torch"
         from azure_hc_intel_tf_amd.parallel import make_reducer
 
         if args.engine == "native":
