@@ -402,6 +402,167 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradPara
   wgrad_store_tile(p, Cs, LDC, BM, BN, i0, j0, tid, NW * 64, gridDim.x == ntiles);
 }
 
+// ============================================================== intra-workgroup split-K variant
+// 64x64 output tile, 4 waves, each wave owns the WHOLE tile and one 32-deep quarter of a
+// 128-deep k-step (the waves' partial tiles are summed through LDS at the end). Against the
+// 2x2 arrangement of 32x32 wave tiles this halves the transposed LDS fragment bytes per MFMA
+// (16 reads feed 16 MFMAs per wave, not 8 reads 4 MFMAs): that kernel is LDS-read bound.
+__global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
+  constexpr int BM = 64, BN = 64, BK = 128;
+  constexpr int AVR = BM / 8, BVR = BN / 8;          // 16-byte vectors per LDS row (8)
+  constexpr int AV = BK * AVR / 256, BV = BK * BVR / 256;  // 4 + 4 per thread per k-step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* As = smem;                   // [2][BK][BM] bf16
+  char* Bs = smem + 2 * BK * BM * 2;  // [2][BK][BN]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tiles_m = (p.Nout + BM - 1) / BM;
+  const int tiles_n = (p.K + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int i0 = tm * BM, j0 = tn * BN;
+
+  // this split's pixel rows (the host plans splits in 64-row units)
+  const int mbeg = split * p.ksteps_per_split * 64;
+  const int mend = min(mbeg + p.ksteps_per_split * 64, p.M);
+  if (mbeg >= mend) return;  // uniform per workgroup
+  const int nk = (mend - mbeg + BK - 1) / BK;
+
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(p.dy, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const int a_cv = tid % AVR, a_r0 = tid / AVR;
+  constexpr int A_RSTEP = 256 / AVR;
+  const int a_col = i0 + a_cv * 8;
+  const bool a_colok = a_col < p.Nout;
+  const int b_cv = tid % BVR, b_r0 = tid / BVR;
+  constexpr int B_RSTEP = 256 / BVR;
+  const int b_col = j0 + b_cv * 8;
+  const bool b_colok = b_col < p.K;
+  int tap = (int)fdiv((uint32_t)b_col, p.fd_c);
+  const int b_c = b_col - tap * p.C;
+  const int b_r = (int)fdiv((uint32_t)tap, p.fd_s), b_s = tap - b_r * p.S;
+  const int b_dh = b_r * p.dil_h - p.pad_h, b_dw = b_s * p.dil_w - p.pad_w;
+
+  u32x4 ra[AV], rb[BV];
+  auto gload = [&](int kt) {
+    const int mb = mbeg + kt * BK;
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int m = mb + a_r0 + A_RSTEP * v;
+      ra[v] = buf_load16(dyr, (a_colok && m < mend) ? (uint32_t)(m * p.ldy + a_col) * 2u : HCB_OOB);
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int m = mb + b_r0 + B_RSTEP * v;
+      uint32_t off = HCB_OOB;
+      if (b_colok && m < mend) {
+        const int n = (int)fdiv((uint32_t)m, p.fd_pq);
+        const int rem = m - n * p.P * p.Q;
+        const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
+        const int qq = rem - pp * p.Q;
+        const int h = pp * p.stride_h + b_dh, w = qq * p.stride_w + b_dw;
+        if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W)
+          off = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c) * 2u;
+      }
+      rb[v] = buf_load16(xr, off);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int row = a_r0 + A_RSTEP * v;
+      const int slot = (a_cv >> 1) ^ wg_swz<BM / 16>(row);
+      *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + row * BM * 2 + slot * 32 + (a_cv & 1) * 16) = ra[v];
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int row = b_r0 + B_RSTEP * v;
+      const int slot = (b_cv >> 1) ^ wg_swz<BN / 16>(row);
+      *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + row * BN * 2 + slot * 32 + (b_cv & 1) * 16) = rb[v];
+    }
+  };
+
+  const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
+  auto tr_read = [&](const char* base, int row, int col) -> short4v {
+    const int rr = row + q4, cb = (col + 4 * p4) * 2;
+    const int slot = (cb >> 5) ^ wg_swz<BM / 16>(rr);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BM * 2 + slot * 32 + (cb & 31)));
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  const int krow = wid * 32;  // this wave's quarter of every k-step
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* Ab = As + cur * BK * BM * 2;
+    const char* Bb = Bs + cur * BK * BN * 2;
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      short4v lo = tr_read(Ab, krow + 8 * g, i * 16);
+      short4v hi = tr_read(Ab, krow + 8 * g + 4, i * 16);
+      short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[i] = __builtin_bit_cast(bf16x8, t);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      short4v lo = tr_read(Bb, krow + 8 * g, j * 16);
+      short4v hi = tr_read(Bb, krow + 8 * g + 4, j * 16);
+      short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[j] = __builtin_bit_cast(bf16x8, t);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // the four waves' partial tiles -> LDS, summed by all threads, then stored / atomically added
+  constexpr int LDC = BN + 4;
+  float* Cs = reinterpret_cast<float*>(smem);  // [4][BM][LDC]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Cs[(wid * BM + i * 16 + g * 4 + e) * LDC + j * 16 + li] = acc[i][j][e];
+  __syncthreads();
+  for (int idx = tid; idx < BM * BN; idx += 256) {
+    const int row = idx / BN, col = idx - row * BN;
+    Cs[row * LDC + col] += Cs[(BM + row) * LDC + col] + Cs[(2 * BM + row) * LDC + col] + Cs[(3 * BM + row) * LDC + col];
+  }
+  __syncthreads();
+  wgrad_store_tile(p, Cs, LDC, BM, BN, i0, j0, tid, 256, gridDim.x == ntiles);
+}
+
+static void wlaunch_kq(const WgradParams& p, int splits, hipStream_t st) {
+  const int tiles = ((p.Nout + 63) / 64) * ((p.K + 63) / 64);
+  const size_t lds_main = (size_t)2 * 128 * (64 + 64) * 2;
+  const size_t lds_epi = (size_t)4 * 64 * (64 + 4) * 4;
+  const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    once = true;
+  }
+  hipLaunchKernelGGL(conv_wgrad_kq_kernel, dim3(tiles * splits), dim3(256), lds, st, p);
+}
+
 template <int WM, int WN, int TM, int TN, int NST>
 static void wlaunch_glds(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
@@ -456,13 +617,13 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
 // 64x64, NST 4), 128x128 (8 waves of 64x32), 256x128 (8 waves of 64x64), 128x256 (8 waves of
 // 64x64), 64x128 (8 waves of 32x32, NST 4), 64x64 (4 waves, NST 4), 64x128 (4 waves of 64x32,
 // NST 4)}
-constexpr int N_WGRAD_CFG = 10;
+constexpr int N_WGRAD_CFG = 11;  // 10: 64x64, intra-workgroup k-split (conv_wgrad_kq_kernel)
 int wgrad_tile_m(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64};
+  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64, 64};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 int wgrad_tile_n(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128};
+  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128, 64};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 
@@ -477,6 +638,7 @@ void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st
     case 7: wlaunch_glds<2, 4, 32, 32, 4>(p, splits, st); break;
     case 8: wlaunch_glds<2, 2, 32, 32, 4>(p, splits, st); break;
     case 9: wlaunch_glds<1, 4, 64, 32, 4>(p, splits, st); break;
+    case 10: wlaunch_kq(p, splits, st); break;
     default: wlaunch<2, 2, 32, 32>(p, splits, st); break; // 64 x 64
   }
 }
