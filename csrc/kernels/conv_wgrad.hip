@@ -403,19 +403,25 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradPara
 }
 
 // ============================================================== intra-workgroup split-K variant
-// 64x64 output tile, 4 waves, each wave owns the WHOLE tile and one 32-deep quarter of a
-// 128-deep k-step (the waves' partial tiles are summed through LDS at the end). Against the
-// 2x2 arrangement of 32x32 wave tiles this halves the transposed LDS fragment bytes per MFMA
-// (16 reads feed 16 MFMAs per wave, not 8 reads 4 MFMAs): that kernel is LDS-read bound.
+// 4 waves, each with a 64x64 wave tile: WMt x WNt waves tile the output block and KS waves
+// share each (BM x BN) block, splitting every 128-deep k-step (128 / KS rows each); their
+// partial tiles are summed through LDS at the end. <1,1,4>: every wave owns the whole 64x64
+// tile over a 32-deep quarter -- against the 2x2 arrangement of 32x32 wave tiles this halves
+// the transposed LDS fragment bytes per MFMA (16 reads feed 16 MFMAs per wave, not 8 reads 4
+// MFMAs), and that kernel is LDS-read bound. <2,1,2> / <1,2,2>: 128x64 / 64x128 blocks.
+template <int WMt, int WNt, int KS>
 __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
-  constexpr int BM = 64, BN = 64, BK = 128;
-  constexpr int AVR = BM / 8, BVR = BN / 8;          // 16-byte vectors per LDS row (8)
-  constexpr int AV = BK * AVR / 256, BV = BK * BVR / 256;  // 4 + 4 per thread per k-step
+  static_assert(WMt * WNt * KS == 4, "4 waves");
+  constexpr int BM = 64 * WMt, BN = 64 * WNt, BK = 128, KW = BK / KS;  // KW: k rows per wave
+  constexpr int AVR = BM / 8, BVR = BN / 8;                // 16-byte vectors per LDS row
+  constexpr int AV = BK * AVR / 256, BV = BK * BVR / 256;  // vectors per thread per k-step
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* As = smem;                   // [2][BK][BM] bf16
+  char* As = smem;                    // [2][BK][BM] bf16
   char* Bs = smem + 2 * BK * BM * 2;  // [2][BK][BN]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid % KS, wmn = wid / KS;  // k share, output sub-tile
+  const int wm = wmn / WNt, wn = wmn % WNt;
   const int tiles_m = (p.Nout + BM - 1) / BM;
   const int tiles_n = (p.K + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
@@ -485,10 +491,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
   };
 
   const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
-  auto tr_read = [&](const char* base, int row, int col) -> short4v {
+  auto tr_read_a = [&](const char* base, int row, int col) -> short4v {
     const int rr = row + q4, cb = (col + 4 * p4) * 2;
     const int slot = (cb >> 5) ^ wg_swz<BM / 16>(rr);
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BM * 2 + slot * 32 + (cb & 31)));
+  };
+  auto tr_read_b = [&](const char* base, int row, int col) -> short4v {
+    const int rr = row + q4, cb = (col + 4 * p4) * 2;
+    const int slot = (cb >> 5) ^ wg_swz<BN / 16>(rr);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BN * 2 + slot * 32 + (cb & 31)));
   };
 
   f32x4 acc[4][4];
@@ -500,67 +511,77 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
   gload(0);
   lstore(0);
   __syncthreads();
-  const int krow = wid * 32;  // this wave's quarter of every k-step
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
     const char* Ab = As + cur * BK * BM * 2;
     const char* Bb = Bs + cur * BK * BN * 2;
-    bf16x8 af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      short4v lo = tr_read(Ab, krow + 8 * g, i * 16);
-      short4v hi = tr_read(Ab, krow + 8 * g + 4, i * 16);
-      short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      af[i] = __builtin_bit_cast(bf16x8, t);
+    for (int ks = 0; ks < KW / 32; ++ks) {
+      const int krow = wk * KW + ks * 32;
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        short4v lo = tr_read_a(Ab, krow + 8 * g, wm * 64 + i * 16);
+        short4v hi = tr_read_a(Ab, krow + 8 * g + 4, wm * 64 + i * 16);
+        short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, t);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        short4v lo = tr_read_b(Bb, krow + 8 * g, wn * 64 + j * 16);
+        short4v hi = tr_read_b(Bb, krow + 8 * g + 4, wn * 64 + j * 16);
+        short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, t);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      short4v lo = tr_read(Bb, krow + 8 * g, j * 16);
-      short4v hi = tr_read(Bb, krow + 8 * g + 4, j * 16);
-      short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      bfr[j] = __builtin_bit_cast(bf16x8, t);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
 
-  // the four waves' partial tiles -> LDS, summed by all threads, then stored / atomically added
+  // the KS k-shares' partial tiles -> LDS, summed, then stored / atomically added
   constexpr int LDC = BN + 4;
-  float* Cs = reinterpret_cast<float*>(smem);  // [4][BM][LDC]
+  float* Cs = reinterpret_cast<float*>(smem);  // [KS][BM][LDC]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        Cs[(wid * BM + i * 16 + g * 4 + e) * LDC + j * 16 + li] = acc[i][j][e];
+        Cs[(wk * BM + wm * 64 + i * 16 + g * 4 + e) * LDC + wn * 64 + j * 16 + li] = acc[i][j][e];
   __syncthreads();
-  for (int idx = tid; idx < BM * BN; idx += 256) {
-    const int row = idx / BN, col = idx - row * BN;
-    Cs[row * LDC + col] += Cs[(BM + row) * LDC + col] + Cs[(2 * BM + row) * LDC + col] + Cs[(3 * BM + row) * LDC + col];
+  if constexpr (KS > 1) {
+    for (int idx = tid; idx < BM * BN; idx += 256) {
+      const int row = idx / BN, col = idx - row * BN;
+      float v = Cs[row * LDC + col];
+#pragma unroll
+      for (int k = 1; k < KS; ++k) v += Cs[(k * BM + row) * LDC + col];
+      Cs[row * LDC + col] = v;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   wgrad_store_tile(p, Cs, LDC, BM, BN, i0, j0, tid, 256, gridDim.x == ntiles);
 }
 
+template <int WMt, int WNt, int KS>
 static void wlaunch_kq(const WgradParams& p, int splits, hipStream_t st) {
-  const int tiles = ((p.Nout + 63) / 64) * ((p.K + 63) / 64);
-  const size_t lds_main = (size_t)2 * 128 * (64 + 64) * 2;
-  const size_t lds_epi = (size_t)4 * 64 * (64 + 4) * 4;
+  constexpr int BM = 64 * WMt, BN = 64 * WNt;
+  const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
+  const size_t lds_main = (size_t)2 * 128 * (BM + BN) * 2;
+  const size_t lds_epi = (size_t)KS * BM * (BN + 4) * 4;
   const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
-  hipLaunchKernelGGL(conv_wgrad_kq_kernel, dim3(tiles * splits), dim3(256), lds, st, p);
+  hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS>), dim3(tiles * splits), dim3(256), lds, st, p);
 }
 
 template <int WM, int WN, int TM, int TN, int NST>
@@ -617,13 +638,13 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
 // 64x64, NST 4), 128x128 (8 waves of 64x32), 256x128 (8 waves of 64x64), 128x256 (8 waves of
 // 64x64), 64x128 (8 waves of 32x32, NST 4), 64x64 (4 waves, NST 4), 64x128 (4 waves of 64x32,
 // NST 4)}
-constexpr int N_WGRAD_CFG = 11;  // 10: 64x64, intra-workgroup k-split (conv_wgrad_kq_kernel)
+constexpr int N_WGRAD_CFG = 13;  // 10-12: intra-workgroup k-split 64x64, 128x64, 64x128
 int wgrad_tile_m(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64, 64};
+  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64, 64, 128, 64};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 int wgrad_tile_n(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128, 64};
+  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128, 64, 64, 128};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 
@@ -638,7 +659,9 @@ void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st
     case 7: wlaunch_glds<2, 4, 32, 32, 4>(p, splits, st); break;
     case 8: wlaunch_glds<2, 2, 32, 32, 4>(p, splits, st); break;
     case 9: wlaunch_glds<1, 4, 64, 32, 4>(p, splits, st); break;
-    case 10: wlaunch_kq(p, splits, st); break;
+    case 10: wlaunch_kq<1, 1, 4>(p, splits, st); break;
+    case 11: wlaunch_kq<2, 1, 2>(p, splits, st); break;
+    case 12: wlaunch_kq<1, 2, 2>(p, splits, st); break;
     default: wlaunch<2, 2, 32, 32>(p, splits, st); break; // 64 x 64
   }
 }

@@ -238,10 +238,10 @@ def test_conv_wgrad(case):
     assert rel_err(dw, ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(11)))
+@pytest.mark.parametrize("cfg", list(range(13)))
 def test_conv_wgrad_all_configs(cfg):
     """Every weight-grad tile config (register-staged 0-2, LDS-DMA ring 3-9, intra-workgroup
-    k-split 10) with split-K on
+    k-split 10-12) with split-K on
     1x1 / 3x3 / strided / odd-channel geometries (partial tiles in Nout, K and pixels)."""
     torch.manual_seed(6)
     for cin, cout, k, s, pads, H, splits in [(64, 256, 1, 1, (0, 0, 0, 0), 14, 3),
