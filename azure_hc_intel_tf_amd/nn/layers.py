@@ -60,6 +60,11 @@ FUSE_STEM_POOL = os.environ.get("HCB_FUSE_STEM_POOL", "1") != "0"
 STAT_R = 8  # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
 FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
+# HCB_RELU_BITMASK=1: residual+ReLU BN outputs also store a 1-bit ReLU mask and the fused
+# backward epilogue reads it instead of the bf16 output (bnb mode 3, 1/16 of the bytes).
+# Off by default: measured on MI355X (ResNet-50 bs=64) 8385 vs 8394 img/s -- the stage-1
+# data-grad epilogues are not bound by that read (profiles/relu_bitmask_ab_r1.txt).
+RELU_BITMASK = os.environ.get("HCB_RELU_BITMASK", "0") == "1"
 # HCB_WGRAD_STREAM=1: run weight-gradient GEMMs on a second HIP stream, concurrent with the
 # data-grad chain (the critical path of backward), captured as parallel graph branches.
 # Off by default: measured on MI355X (ResNet-50 bs=64) the split-K-tuned GEMMs already fill
@@ -157,6 +162,7 @@ class ConvBN(Layer):
             # ResNet-v2's un-normalised convs (shortcut, conv3) have no bias in tf_cnn_benchmarks
             self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0)) if bias else None
         self._saved = None
+        self._mask = None
         self._pre_reduced = False
         self.training = True  # False: inference BN from the moving statistics (forward-only)
 
@@ -193,9 +199,15 @@ class ConvBN(Layer):
                 # conv epilogue accumulates the batch statistics; the apply kernel finalizes them
                 Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data,
                                 stats_R=STAT_R)
+                # residual + ReLU outputs keep a bit mask for the fused backward (mode 3)
+                mask = None
+                if (RELU_BITMASK and self.relu and residual is not None and FUSE_BN_BWD
+                        and Fn.ld(z) == C and Fn.ld(y) == C):
+                    mask = torch.empty((N * P * Q, C // 8), dtype=torch.uint8, device=dev)
                 saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
                                           self.decay, self.eps, y, self.relu, self.acc_f.data, STAT_R,
-                                          self.sv_mean.data, self.sv_invstd.data, residual=residual)
+                                          self.sv_mean.data, self.sv_invstd.data, residual=residual, mask=mask)
+                self._mask = mask
             else:
                 Fn.conv_forward(x, self.spec, None, self.w.data, z)
                 saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
@@ -236,6 +248,8 @@ class ConvBN(Layer):
         x, z, y, saved, had_res = self._saved
         mode = (1 if had_res else 2) if self.relu else 0
         self._pre_reduced = True
+        if mode == 1 and self._mask is not None:
+            return Fn.BNBwdFuse(z, self._mask, saved, self.gamma.data, self.beta.data, 3, self.acc_b.data, STAT_R)
         return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, self.acc_b.data, STAT_R)
 
     def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False, dx_bn=None):
@@ -298,6 +312,7 @@ class ConvBN(Layer):
             bnb = dx_bn.bwd_fuse_request() if dx_bn is not None else None
             Fn.conv_dgrad(dz, self.spec, self.pack.tr, self.w.data, dx, accumulate, bnb=bnb)
         self._saved = None
+        self._mask = None
         return dx, gres
 
     def clear(self):

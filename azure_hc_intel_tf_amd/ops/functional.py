@@ -293,10 +293,27 @@ class BNBwdFuse:
         """CPU semantics of the fused epilogue's gating (the reductions stay in bn_backward)."""
         if self.mode == 1:
             g.mul_((self.y > 0).to(g.dtype))
+        elif self.mode == 3:
+            g.mul_(unpack_relu_mask(self.y, g.shape).to(g.dtype))
         elif self.mode == 2:
             xhat = (self.z - self.saved.mean) * self.saved.invstd
             g.mul_(((xhat * self.gamma + self.beta) > 0).to(g.dtype))
         return g
+
+
+def pack_relu_mask(y):
+    """Reference packer of the bn_apply_acc ReLU bit mask: y[..., C] -> uint8 [M, C/8]."""
+    C = y.shape[-1]
+    b = (y.reshape(-1, C // 8, 8).float() > 0).to(torch.int32)
+    w = (1 << torch.arange(8, dtype=torch.int32, device=y.device))
+    return (b * w).sum(-1).to(torch.uint8)
+
+
+def unpack_relu_mask(mask, shape):
+    """uint8 [M, C/8] ReLU bit mask (bit e of byte j = channel 8j+e) -> bool tensor ``shape``."""
+    bits = torch.arange(8, dtype=torch.int32, device=mask.device)
+    m = ((mask.to(torch.int32).unsqueeze(-1) >> bits) & 1).bool()
+    return m.reshape(shape)
 
 
 def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None, bnb: "BNBwdFuse" = None):
@@ -329,7 +346,7 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
         geom = geom + [0, 0, splits]
         if bnb is not None:
             _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
-                                      bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
+                                      bnb.y if bnb.mode in (1, 3) else None, ld(bnb.z), bnb.saved.mean,
                                       bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
         else:
             _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg)
@@ -432,15 +449,17 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
 
 
 def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out, relu: bool, acc, R: int,
-                   saved_mean, saved_invstd, residual=None):
+                   saved_mean, saved_invstd, residual=None, mask=None):
     """GPU BN forward whose batch statistics were accumulated by the producing conv's epilogue
     into ``acc`` (R replicas of [2][C]); mean/invstd are derived inside the apply kernel (no
-    finalize launch) and written to saved_mean / saved_invstd for the backward."""
+    finalize launch) and written to saved_mean / saved_invstd for the backward. ``mask``
+    (uint8 [M, C/8]): also store the output's ReLU bit mask, which the mode-3 fused
+    BN-backward epilogue reads instead of the full bf16 output (1/16 of the bytes)."""
     N, H, W, C = z.shape
     M = N * H * W
     _ext.ops().bn_apply_acc(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0, M, C,
                             acc, R, eps, momentum, gamma, beta, 1 if relu else 0, saved_mean, saved_invstd,
-                            running_mean, running_var)
+                            running_mean, running_var, mask)
     return BNSaved(saved_mean, saved_invstd)
 
 

@@ -157,7 +157,7 @@ void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10
                     const Tensor& acc, int64_t R, int64_t mode) {
   hcb::ConvParams p = conv_params(x, w, y, yres, c10::nullopt, c10::nullopt, g, cfg);
   TORCH_CHECK(!p.out_f32 && !p.relu && p.bias == nullptr, "hcb.conv_igemm_bnb: bf16 output without bias/relu");
-  TORCH_CHECK(mode >= 0 && mode <= 2 && R >= 1, "hcb.conv_igemm_bnb: bad mode / R");
+  TORCH_CHECK(mode >= 0 && mode <= 3 && R >= 1, "hcb.conv_igemm_bnb: bad mode / R");
   TORCH_CHECK(ld % 8 == 0 && ld >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm_bnb: bad ld");
   int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
   int64_t need = (rows - 1) * ld * 2 + ((p.Nout + 7) / 8) * 8 * 2;
@@ -170,6 +170,12 @@ void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10
     check_bf16(*yact, "y");
     check_range(*yact, need, "y");
     check_align16(yact->data_ptr(), "y");
+    p.bnb_y = yact->data_ptr();
+  } else if (mode == 3) {
+    TORCH_CHECK(yact.has_value(), "hcb.conv_igemm_bnb: mode 3 needs the ReLU bit mask");
+    TORCH_CHECK(yact->scalar_type() == at::kByte && yact->is_cuda() && yact->is_contiguous(),
+                "hcb.conv_igemm_bnb: mask must be a contiguous uint8 GPU tensor");
+    TORCH_CHECK(yact->numel() >= rows * (ld / 8), "hcb.conv_igemm_bnb: mask too small");
     p.bnb_y = yact->data_ptr();
   }
   for (const Tensor* t : {&mean, &invstd, &gamma, &beta}) {
@@ -531,7 +537,8 @@ void add_bf16(const Tensor& a, const Tensor& b, const Tensor& y) {
 void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, const c10::optional<Tensor>& res,
                   int64_t ldr, int64_t M, int64_t C, const Tensor& acc, int64_t R, double eps, double momentum,
                   const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& saved_mean,
-                  const Tensor& saved_invstd, const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv) {
+                  const Tensor& saved_invstd, const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv,
+                  const c10::optional<Tensor>& mask) {
   check_bf16(x, "x");
   check_bf16(y, "y");
   check_f32(acc, "acc");
@@ -546,11 +553,18 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
     check_range(*res, ((M - 1) * ldr + C) * 2, "res");
     rp = res->data_ptr();
   }
+  void* mp = nullptr;
+  if (mask.has_value()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_cuda() && mask->is_contiguous(),
+                "hcb.bn_apply_acc: mask must be a contiguous uint8 GPU tensor");
+    TORCH_CHECK(mask->numel() >= M * (C / 8), "hcb.bn_apply_acc: mask too small");
+    mp = mask->data_ptr();
+  }
   hcb::launch_bn_apply_acc(x.data_ptr(), (int)ldx, y.data_ptr(), (int)ldy, rp, (int)ldr, (int)M, (int)C,
                            acc.data_ptr<float>(), (int)R, (float)eps, (float)momentum, gamma.data_ptr<float>(),
                            beta.data_ptr<float>(), (int)relu, saved_mean.data_ptr<float>(),
                            saved_invstd.data_ptr<float>(), rm.has_value() ? rm->data_ptr<float>() : nullptr,
-                           rv.has_value() ? rv->data_ptr<float>() : nullptr, cur_stream());
+                           rv.has_value() ? rv->data_ptr<float>() : nullptr, mp, cur_stream());
 }
 
 void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
@@ -745,7 +759,7 @@ TORCH_LIBRARY(hcb, m) {
   m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");
   m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
-  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var) -> ()");
+  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor(f!)? mask=None) -> ()");
   m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg) -> ()");
   m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");

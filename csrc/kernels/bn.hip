@@ -551,7 +551,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ y, int ldy, const uint16_t* __restrict__ res,
     int ldr, int M, int C, int CVB, const float* __restrict__ acc, int R, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
-    float* saved_invstd, float* run_mean, float* run_var) {
+    float* saved_invstd, float* run_mean, float* run_var, uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
@@ -624,7 +624,19 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
       }
-      if (m < M) *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + gm.cv * 8) = pack8(f);
+      if (m < M) {
+        const u32x4 o = pack8(f);
+        *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + gm.cv * 8) = o;
+        if (mask != nullptr) {  // bit e: the STORED bf16 value is > 0 (same test as mode 1)
+          uint32_t bits = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t h = (o[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+            bits |= ((h - 1u) < 0x7f80u ? 1u : 0u) << e;  // 0 < bf16 <= +inf
+          }
+          mask[(size_t)m * (C >> 3) + gm.cv] = (uint8_t)bits;
+        }
+      }
     }
   }
 }
@@ -859,12 +871,12 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         hipStream_t st) {
+                         void* mask, hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   hipLaunchKernelGGL(bn_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x, ldx,
                      (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta,
-                     relu, saved_mean, saved_invstd, run_mean, run_var);
+                     relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask);
 }
 
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,

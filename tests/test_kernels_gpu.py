@@ -175,7 +175,7 @@ def test_conv_dgrad(case, accumulate):
 
 @pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[2], CONV_CASES[3], CONV_CASES[6]],
                          ids=["1x1", "3x3", "1x1s2", "cin80"])
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("cfg", [2, 4, 12])
 def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
@@ -204,7 +204,8 @@ def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
         keep[:, ::s, ::s] = True
         base = base * keep
     dx = base.clone() if accumulate else (torch.zeros_like(base) if strided_1x1 else torch.empty_like(base))
-    bnb = Fn.BNBwdFuse(z, yact, saved, gamma, beta, mode, acc, R)
+    gate = Fn.pack_relu_mask(yact) if mode == 3 else yact  # mode 3: 1-bit ReLU mask of y
+    bnb = Fn.BNBwdFuse(z, gate, saved, gamma, beta, mode, acc, R)
     Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate, cfg=cfg, bnb=bnb)
     ref = torch.empty(N, H, H, cin)
     Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), ref, False)
@@ -212,7 +213,7 @@ def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
         ref = ref + base.float().cpu()
     zc = z.float().cpu()
     cpu_bnb = Fn.BNBwdFuse(zc, yact.float().cpu(), Fn.BNSaved(mean.cpu(), invstd.cpu()), gamma.cpu(), beta.cpu(),
-                           mode, None, R)
+                           1 if mode == 3 else mode, None, R)
     g = cpu_bnb.gate_cpu(ref.clone())
     assert rel_err(dx, g) < 1e-2
     xhat = (zc - mean.cpu()) * invstd.cpu()
@@ -443,7 +444,12 @@ def test_bn_finalize_free_path(C, relu, residual):
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     mean, invstd = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
     y = torch.empty_like(z)
-    saved = Fn.bn_forward_acc(z, gamma, beta, rm, rv, 0.9, 1e-5, y, relu, acc_f, R, mean, invstd, residual=res)
+    mask = torch.full((N * H * H, C // 8), 0xAA, dtype=torch.uint8, device=DEV)
+    saved = Fn.bn_forward_acc(z, gamma, beta, rm, rv, 0.9, 1e-5, y, relu, acc_f, R, mean, invstd, residual=res,
+                              mask=mask)
+    # the ReLU bit mask (read by the mode-3 fused backward) is exactly the stored output's y > 0
+    assert torch.equal(mask, Fn.pack_relu_mask(y))
+    assert torch.equal(Fn.unpack_relu_mask(mask, y.shape), y > 0)
     zc = z.float().cpu()
     yc = torch.empty(N, H, H, C)
     rmc, rvc = torch.zeros(C), torch.ones(C)
