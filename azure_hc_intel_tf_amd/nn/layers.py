@@ -60,6 +60,10 @@ FUSE_STEM_POOL = os.environ.get("HCB_FUSE_STEM_POOL", "1") != "0"
 STAT_R = 8  # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
 FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
+# ...only when the data-grad GEMM's reduction depth (cout * kh * kw of the producing conv) is at
+# least this: a shallow GEMM (stage-1 1x1, K=64) is all epilogue, and the fused gating +
+# reductions there cost more than a separate BN-backward reduce pass
+FUSE_BN_BWD_MIN_K = int(os.environ.get("HCB_FUSE_BN_BWD_MIN_K", "0"))
 # HCB_RELU_BITMASK=1: residual+ReLU BN outputs also store a 1-bit ReLU mask and the fused
 # backward epilogue reads it instead of the bf16 output (bnb mode 3, 1/16 of the bytes).
 # Off by default: measured on MI355X (ResNet-50 bs=64) 8385 vs 8394 img/s -- the stage-1
@@ -309,7 +313,8 @@ class ConvBN(Layer):
                 strided_1x1 = (self.spec.sh > 1 or self.spec.sw > 1) and self.spec.kh == 1 and self.spec.kw == 1
                 dx = empty_act((N, H, W, Cin), dev, zero=strided_1x1 and dev.type == "cuda")
                 accumulate = False
-            bnb = dx_bn.bwd_fuse_request() if dx_bn is not None else None
+            fuse = dx_bn is not None and self.spec.cout * self.spec.kh * self.spec.kw >= FUSE_BN_BWD_MIN_K
+            bnb = dx_bn.bwd_fuse_request() if fuse else None
             Fn.conv_dgrad(dz, self.spec, self.pack.tr, self.w.data, dx, accumulate, bnb=bnb)
         self._saved = None
         self._mask = None
