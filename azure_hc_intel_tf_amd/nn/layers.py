@@ -57,7 +57,8 @@ def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
 
 # ResNet stem: BN+ReLU+max pool in one kernel on the GPU (HCB_FUSE_STEM_POOL=0 to disable)
 FUSE_STEM_POOL = os.environ.get("HCB_FUSE_STEM_POOL", "1") != "0"
-STAT_R = 8  # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
+# replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
+STAT_R = max(1, int(os.environ.get("HCB_STAT_R", "8")))
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
 FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
 # ...only when the data-grad GEMM's reduction depth (cout * kh * kw of the producing conv) is at
