@@ -8,6 +8,7 @@ box with the repo snapshot):
   (``csrc/bindings.cpp``), loaded with ``torch.ops.load_library``.
 * ``_hcb_data*.so`` -- the native real-data pipeline core (TFRecord / tf.Example / crop
   windows / prefetch threads; ``csrc/data/*.cpp``).
+* ``_hcb_engine_cpu*.so`` -- the bucket engine core on an in-process fake fabric (CPU tests).
 * ``_hcb_comm.so`` -- the C++ communication runtime (RCCL communicator, bucketed
   allreduce engine, Chrome-trace timeline, stall watchdog; ``csrc/comm/*.cpp``).
 
@@ -149,6 +150,30 @@ def build_data(verbose: bool = False) -> str:
     return so
 
 
+def _engine_cpu_so() -> str:
+    import sysconfig
+
+    return os.path.join(PKG_DIR, "_hcb_engine_cpu" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_engine_cpu(verbose: bool = False) -> str:
+    """``_hcb_engine_cpu`` -- the gradient bucket engine core (``csrc/comm/engine.h``, the same
+    code the RCCL library runs) on an in-process fake fabric of emulated ranks
+    (``csrc/engine_cpu/*.cpp``): the CPU test suite's fake backend (pybind11, no torch/HIP)."""
+    import sysconfig
+
+    import pybind11
+
+    srcs = sorted(glob.glob(os.path.join(CSRC, "engine_cpu", "*.cpp")))
+    if not srcs:
+        return ""
+    so = _engine_cpu_so()
+    if _newer(so, srcs + _headers()):
+        _run(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-I" + CSRC, "-I" + pybind11.get_include(),
+              "-I" + sysconfig.get_paths()["include"], *srcs, "-o", so, "-lpthread"], verbose)
+    return so
+
+
 RCCL_BENCH = os.path.join(REPO, "tools", "rccl_bench", "rccl_allreduce_bench")
 
 
@@ -168,6 +193,7 @@ def build_all(verbose: bool = False) -> None:
     build_kernels(verbose)
     build_comm(verbose)
     build_data(verbose)
+    build_engine_cpu(verbose)
     build_tools(verbose)
 
 

@@ -227,7 +227,9 @@ class BenchmarkCNN:
         if p.trace_file:
             self._trace_one_step(images, labels, p.trace_file)
 
-        log_fn("Step\tImg/sec\ttotal_loss") if self.rank == 0 else None
+        acc = bool(p.print_training_accuracy)
+        if self.rank == 0:  # tf_cnn_benchmarks header (+ accuracy columns with --print_training_accuracy)
+            log_fn("Step\tImg/sec\ttotal_loss" + ("\ttop_1_accuracy\ttop_5_accuracy" if acc else ""))
         step_times: List[float] = []
         use_events = self.on_gpu
         evs = []
@@ -262,7 +264,11 @@ class BenchmarkCNN:
                         k = len(step_times)
                         step_times.append(evs[k].elapsed_time(evs[k + 1]) / 1000.0)
                 if self.rank == 0:
-                    log_fn("%i\t%s\t%.3f" % (step, get_perf_timing_str(self.batch_size, step_times), loss))
+                    line = "%i\t%s\t%.3f" % (step, get_perf_timing_str(self.batch_size, step_times), loss)
+                    if acc:
+                        t1, t5 = self.trainer.accuracy(labels)
+                        line += "\t%.3f\t%.3f" % (float(t1), float(t5))
+                    log_fn(line)
                 if not math.isfinite(loss):
                     raise RuntimeError(f"non-finite loss at step {step}")
             if p.train_dir and self.rank == 0:
@@ -284,16 +290,26 @@ class BenchmarkCNN:
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             elapsed_max = float(t.item())
         images_per_sec = self.size * self.batch_size * self.num_batches / elapsed_max
+        own_images_per_sec = self.size * self.batch_size * self.num_batches / elapsed
         final_loss = float(self.trainer.loss.item())
+        comm = None
+        if self.size > 1 and self.on_gpu and p.comm_profile:
+            comm = self.trainer.comm_profile(images, labels)
+        if self.reducer is not None and hasattr(self.reducer, "check_errors"):
+            self.reducer.check_errors()
         if loader is not None:
             loader.close()
         if p.train_dir and self.rank == 0:
             checkpoint.save(p.train_dir, self.step_offset + self.num_warmup_batches + self.num_batches,
                             self.model.ps)
+        # every worker prints its own total, as tf_cnn_benchmarks does under mpirun
+        # (run-tf-sing-ucx-openmpi.sh:99-113); rank 0 reports the job figure (slowest rank)
         if self.rank == 0:
             log_fn("-" * 64)
             log_fn("total images/sec: %.2f" % images_per_sec)
             log_fn("-" * 64)
+        else:
+            log_fn("[rank %d] total images/sec: %.2f" % (self.rank, own_images_per_sec))
         summary = {
             "model": self.model_name, "device": "MI355X" if self.on_gpu else platform.processor() or "cpu",
             "workers": self.size, "batch_size_per_worker": self.batch_size,
@@ -307,7 +323,18 @@ class BenchmarkCNN:
             "input_decode_s": loader.decode_s if loader else None,
             "variable_update": p.variable_update, "comm_engine": p.comm_engine if self.size > 1 else None,
             "gradient_compression": p.gradient_compression, "hip_graph": self.trainer.use_graph,
+            "fusion_threshold_bytes": getattr(self.reducer, "bucket_bytes", None),
+            "comm": comm,
         }
+        if self.size > 1:
+            per_rank = torch.tensor([own_images_per_sec], dtype=torch.float64,
+                                    device=self.device if self.on_gpu else "cpu")
+            allr = [torch.zeros_like(per_rank) for _ in range(self.size)]
+            torch.distributed.all_gather(allr, per_rank)
+            summary["per_rank_images_per_sec"] = [round(float(x.item()), 2) for x in allr]
+        if acc:
+            t1, t5 = self.trainer.accuracy(labels)
+            summary["top_1_accuracy"], summary["top_5_accuracy"] = float(t1), float(t5)
         self.summary = summary
         if self.rank == 0:
             out = p.json_summary

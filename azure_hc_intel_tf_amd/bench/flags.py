@@ -93,11 +93,14 @@ FLAGS: List[Flag] = [
     # --- MI355X engine knobs
     Flag("use_hip_graph", True, parse_bool, "capture the training step in a HIP graph"),
     Flag("autotune", True, parse_bool, "time the conv kernel configs of untuned shapes before the run"),
-    Flag("comm_engine", "torch", str, "gradient allreduce engine: native (C++ RCCL) | torch",
+    Flag("comm_engine", "native", str, "gradient allreduce engine: native (C++ RCCL bucket engine, the one "
+         "bench.py measures) | torch (torch.distributed)",
          choices=["native", "torch"]),
     Flag("gradient_compression", "none", str, "none | fp16 | bf16 (Horovod Compression)",
          choices=["none", "fp16", "bf16"]),
     Flag("json_summary", None, str, "write the run summary JSON to this path"),
+    Flag("comm_profile", True, parse_bool, "after the timed run (N>1, GPU): measure allreduce time, exposed "
+         "communication and overlap % for the JSON summary"),
     Flag("fault_rank", -1, int, "fault injection: rank that aborts (testing)"),
     Flag("fault_step", -1, int, "fault injection: step at which --fault_rank aborts"),
 ]

@@ -117,6 +117,24 @@ def tf_args(plan: Plan, env=os.environ) -> List[str]:
     return a
 
 
+def flavor_settings(flavor: str) -> Dict[str, object]:
+    """What distinguishes the two reference runners, mapped onto the per-GPU launcher.
+
+    * ucx-openmpi (run-tf-sing-ucx-openmpi.sh:99-106): ``--map-by ppr:W:socket,pe=C`` core
+      pinning, ``-x HOROVOD_MPI_THREADS_DISABLE=1``, quiet transport.
+    * libfabric-intelmpi (run-tf-sing-libfabric-intelmpi.sh:94-105): ``mpiexec.hydra -ppn W``
+      with NO pinning, ``-genv I_MPI_DEBUG 5`` (transport selection printed at start-up; here
+      ``NCCL_DEBUG=INFO`` with the INIT / NET / TUNING subsystems, RCCL's equivalent), and no
+      HOROVOD_MPI_THREADS_DISABLE.
+    """
+    if flavor == "ucx-openmpi":
+        return {"pin": True, "env": {"HOROVOD_MPI_THREADS_DISABLE": "1"}, "unset": []}
+    if flavor == "libfabric-intelmpi":
+        return {"pin": False, "env": {"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT,NET,TUNING"},
+                "unset": ["HOROVOD_MPI_THREADS_DISABLE"]}
+    raise ValueError(flavor)
+
+
 def node_rank_from_hostfile(path: str) -> (List[str], int):
     hosts = [l.split()[0] for l in open(path) if l.strip() and not l.startswith("#")]
     me = {socket.gethostname(), socket.getfqdn(), "127.0.0.1", "localhost"}
@@ -155,11 +173,12 @@ def main(argv=None) -> int:
                 return 2
         else:
             hosts, node_rank = node_rank_from_hostfile(hf)
+    fl = flavor_settings(a.flavor)
     launcher = [sys.executable, "-m", "azure_hc_intel_tf_amd.launch.launcher",
                 f"--nproc_per_node={plan.workers_per_node}", f"--nnodes={plan.num_nodes}",
                 f"--node_rank={node_rank}", f"--master_addr={hosts[0]}", f"--fabric={plan.fabric}",
-                f"--omp_threads={plan.intra_t}", "--",
-                sys.executable, os.path.join(REPO, "tf_cnn_benchmarks.py")] + targs
+                f"--omp_threads={plan.intra_t}"] + ([] if fl["pin"] else ["--no_pin"]) + [
+                "--", sys.executable, os.path.join(REPO, "tf_cnn_benchmarks.py")] + targs
     # config echo (run-tf-sing-ucx-openmpi.sh:52-58,97,111)
     print(f"NUM_NODES: {plan.num_nodes}  WORKERS_PER_SOCKET: {plan.workers_per_socket}  "
           f"NUM_SOCKETS: {plan.sockets}  CORES_PER_SOCKET: {plan.cores_per_socket}")
@@ -167,15 +186,22 @@ def main(argv=None) -> int:
           f"INTRA_T: {plan.intra_t}  INTER_T: {plan.inter_t}  TOTAL_WORKERS: {plan.total_workers}")
     print(f"BATCH_SIZE: {plan.batch_size}  FABRIC: {plan.fabric} ({'RCCL P2P/xGMI' if plan.fabric == 'ib' else 'RCCL sockets'})"
           f"  DEVICE: {plan.device}  FLAVOR: {a.flavor}")
+    print("ENV: " + " ".join(f"{k}={v}" for k, v in sorted(fl["env"].items())) +
+          (f"  (unset {' '.join(fl['unset'])})" if fl["unset"] else "") +
+          f"  PINNING: {'per-GPU NUMA cores' if fl['pin'] else 'none'}")
     print("COMMAND: " + " ".join(shlex.quote(c) for c in launcher), flush=True)
     if env.get("DRY_RUN") == "1":
         return 0
     log_dir = env.get("LOG_DIR", os.path.join(REPO, "gpurun_out", "logs"))
     os.makedirs(log_dir, exist_ok=True)
     log = os.path.join(log_dir, f"tfmn-{plan.num_nodes}n-{plan.batch_size}b-synthetic-{plan.fabric}-r1.log")
+    child_env = dict(env, PYTHONPATH=REPO + os.pathsep + env.get("PYTHONPATH", ""))
+    for k in fl["unset"]:
+        child_env.pop(k, None)
+    for k, v in fl["env"].items():
+        child_env.setdefault(k, v)
     with open(log, "w") as lf:
-        p = subprocess.Popen(launcher, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
-                             env=dict(env, PYTHONPATH=REPO + os.pathsep + env.get("PYTHONPATH", "")))
+        p = subprocess.Popen(launcher, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=child_env)
         for line in p.stdout:
             sys.stdout.write(line)
             lf.write(line)

@@ -10,6 +10,23 @@ from ..nn.layers import act_dtype
 from ..nn.params import ParamStore
 
 
+# activation / GEMM-operand precisions the GPU path implements (the CPU path is fp32/fp64)
+GPU_COMPUTE_DTYPES = ("bf16",)
+
+
+def check_compute_dtype(compute_dtype, device) -> str:
+    """Validate a requested compute precision; never substitute one precision for another."""
+    if torch.device(device).type != "cuda":
+        if compute_dtype not in (None, "fp32"):
+            raise ValueError(f"the CPU path computes in fp32, not {compute_dtype}")
+        return "fp32"
+    cd = compute_dtype or "bf16"
+    if cd not in GPU_COMPUTE_DTYPES:
+        raise NotImplementedError(f"compute dtype {cd!r} is not implemented on the GPU path "
+                                  f"(available: {', '.join(GPU_COMPUTE_DTYPES)})")
+    return cd
+
+
 class CNNModel:
     """Subclasses build their layers in ``build()`` using ``self.ps`` and implement
     ``forward(images) -> logits`` and ``backward(dlogits)``.
@@ -24,8 +41,9 @@ class CNNModel:
     default_lr_per_256 = 0.1  # tf_cnn_benchmarks: lr = 0.1 * global_batch / 256 for ResNets
 
     def __init__(self, num_classes: int = 1001, image_size: int = None, device="cpu", seed: int = 1234,
-                 image_channels: int = None):
+                 image_channels: int = None, compute_dtype: str = None):
         self.num_classes = num_classes
+        self.compute_dtype = check_compute_dtype(compute_dtype, device)
         self.image_size = image_size or self.default_image_size
         self.device = torch.device(device)
         if image_channels is None:

@@ -1,6 +1,6 @@
 """Data-parallel communication: Horovod-compatible API (``hvd``), gradient reducers and the
 native C++ RCCL bucket engine."""
-from .reducer import TorchDistReducer, fusion_threshold_bytes, make_buckets
+from .reducer import TorchDistReducer, fusion_threshold_bytes, make_buckets, split_ranges
 
 
 def make_reducer(engine: str = "torch", compression=None, group=None, **kw):
@@ -15,4 +15,4 @@ def make_reducer(engine: str = "torch", compression=None, group=None, **kw):
     raise ValueError(f"unknown engine {engine!r}")
 
 
-__all__ = ["make_reducer", "TorchDistReducer", "fusion_threshold_bytes", "make_buckets"]
+__all__ = ["make_reducer", "TorchDistReducer", "fusion_threshold_bytes", "make_buckets", "split_ranges"]

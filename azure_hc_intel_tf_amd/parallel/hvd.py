@@ -271,6 +271,7 @@ class DistributedOptimizer(torch.optim.Optimizer):
         self._bucket_of = {}
         self._buckets: List[List[torch.Tensor]] = []
         self._pending: Dict[int, int] = {}
+        self._launched = set()
         limit = fusion_threshold_bytes()
         cur, cur_bytes = [], 0
         for p in reversed(params):  # backward produces the last layers' grads first
@@ -306,13 +307,27 @@ class DistributedOptimizer(torch.optim.Optimizer):
         bi = self._bucket_of[p]
         self._pending[bi] = self._pending.get(bi, 0) + 1
         if self._pending[bi] == len(self._buckets[bi]):
-            grads = [q.grad for q in self._buckets[bi]]
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            c, ctx = self._compression.compress(flat)
-            work = dist.all_reduce(c, async_op=True, group=_group_for(c))
-            self._handles.append((work, c, ctx, flat, grads))
+            self._launch(bi)
+
+    def _launch(self, bi):
+        ps = self._buckets[bi]
+        for q in ps:  # a parameter that got no gradient this step contributes zeros (Horovod)
+            if q.grad is None:
+                q.grad = torch.zeros_like(q)
+        grads = [q.grad for q in ps]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        c, ctx = self._compression.compress(flat)
+        work = dist.all_reduce(c, async_op=True, group=_group_for(c))
+        self._handles.append((work, c, ctx, flat, grads))
+        self._launched.add(bi)
 
     def synchronize(self):
+        # buckets whose parameters did not all receive a gradient (unused branch, frozen layer)
+        # were never launched from the hooks: reduce them now, in bucket order -- the same on
+        # every rank -- instead of silently stepping with local gradients
+        for bi in range(len(self._buckets)):
+            if bi not in self._launched:
+                self._launch(bi)
         for work, c, ctx, flat, grads in self._handles:
             work.wait()
             out = self._compression.decompress(c, ctx)
@@ -324,6 +339,7 @@ class DistributedOptimizer(torch.optim.Optimizer):
                 o += g.numel()
         self._handles.clear()
         self._pending.clear()
+        self._launched.clear()
 
     def step(self, closure=None):
         self._counter += 1

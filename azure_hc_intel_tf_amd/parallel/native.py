@@ -3,10 +3,12 @@
 ``NativeReducer`` owns one RCCL communicator (created from an ncclUniqueId exchanged through
 the torch.distributed TCP store -- no MPI) and reduces the flat gradient buffer bucket by
 bucket on a dedicated high-priority comm stream forked from / joined to the compute stream.
-Bucket size: ``HOROVOD_FUSION_THRESHOLD``. Optional bf16 compression (pack kernel -> bf16
-allreduce -> unpack kernel, all on the comm stream). ``HOROVOD_TIMELINE`` writes a Chrome
-trace of the bucket reductions; the watchdog honours ``HOROVOD_STALL_CHECK_TIME_SECONDS`` and
-``HCB_STALL_ABORT_SECONDS``.
+Every gradient range handed to it (a whole backward segment on the overlap path) is cut by
+the C++ engine into buckets of at most ``HOROVOD_FUSION_THRESHOLD`` wire bytes
+(csrc/comm/engine.h). Optional Horovod compression: bf16 or IEEE fp16 on the wire (pack
+kernel -> 16-bit allreduce -> unpack kernel, all on the comm stream). ``HOROVOD_TIMELINE``
+writes a Chrome trace of the bucket reductions; the watchdog honours
+``HOROVOD_STALL_CHECK_TIME_SECONDS`` and ``HCB_STALL_ABORT_SECONDS``.
 """
 from __future__ import annotations
 
@@ -99,11 +101,21 @@ class Communicator:
         self._cc.bucket_allreduce_async_(self.h, flat, buckets, compress, scale, average)
         return flat
 
+    def set_fusion_threshold(self, nbytes: int):
+        self._cc.set_fusion_threshold(self.h, int(nbytes))
+
+    def buckets_issued(self) -> int:
+        return int(self._cc.buckets_issued(self.h))
+
     def join_(self):
         self._cc.join_(self.h)
 
     def barrier(self):
         self._cc.barrier(self.h)
+
+    def size(self) -> int:
+        """Rank count as reported by the RCCL communicator itself."""
+        return int(self._cc.size(self.h))
 
     def close(self):
         if getattr(self, "h", None) is not None:
@@ -125,11 +137,12 @@ class NativeReducer:
         identity), so the multi-GPU code path can be exercised and timed on one GPU."""
         if compression not in (None, "none", "bf16", "fp16"):
             raise ValueError(compression)
-        # fp16 wire format maps to bf16 on MI355X: same 2 bytes, fp32 exponent range
-        self.compress = 0 if compression in (None, "none") else 1
+        # wire formats: 0 fp32, 1 bf16, 2 IEEE fp16 (Horovod Compression.fp16)
+        self.compress = {None: 0, "none": 0, "bf16": 1, "fp16": 2}[compression]
         self.bucket_bytes = bucket_bytes or fusion_threshold_bytes()
         self.average = average
         self.comm = Communicator()
+        self.comm.set_fusion_threshold(self.bucket_bytes)
         # collectives captured inside the training-step graph (default); HCB_GRAPH_COMM=0
         # replays one graph per backward segment and launches the reductions from the host
         self.graph_safe = os.environ.get("HCB_GRAPH_COMM", "1") == "1"
@@ -144,6 +157,8 @@ class NativeReducer:
             self.xgmi = XgmiAllreduce(capacity_bytes=self.xgmi_bytes)
 
     def _bucket_table(self, numel):
+        # whole-buffer form: buckets from the END of the buffer first (the engine cuts each
+        # of them again only if it exceeds the threshold)
         if self._buckets is None or self._numel != numel:
             esz = 2 if self.compress else 4
             b = make_buckets(numel, max(self.bucket_bytes // esz, 64))
@@ -175,6 +190,13 @@ class NativeReducer:
 
     def join(self):
         self.comm.join_()
+
+    def check_errors(self):
+        """Raise if the one-shot xGMI path timed out waiting for a peer (its output was
+        poisoned with NaN on the device). Synchronises; call outside the timed loop."""
+        if self.xgmi is not None and self.xgmi.error():
+            raise RuntimeError("xGMI allreduce: a peer did not publish within HCB_XGMI_SPIN; gradients of "
+                               "that step were poisoned (NaN) instead of being reduced unsynchronised")
 
     def broadcast_(self, t, root=0):
         if self.comm.world > 1:

@@ -44,6 +44,27 @@ def make_buckets(numel: int, bucket_elems: int, align: int = 64) -> List[Tuple[i
     return out
 
 
+def split_ranges(ranges, bucket_elems: int, align: int = 64) -> List[Tuple[int, int]]:
+    """Cut every (offset, length) range into equal pieces of at most ``bucket_elems`` elements,
+    in order (the same rule as the C++ engine's plan_buckets, csrc/comm/engine.h), so the
+    HOROVOD_FUSION_THRESHOLD bounds each collective on the overlapped path too."""
+    out = []
+    m = max(align, bucket_elems // align * align) if bucket_elems > 0 else 0
+    for off, n in ranges:
+        if n <= 0:
+            continue
+        if m <= 0:
+            out.append((off, n))
+            continue
+        pieces = (n + m - 1) // m
+        per = min(m, ((n + pieces - 1) // pieces + align - 1) // align * align)
+        s = 0
+        while s < n:
+            out.append((off + s, min(per, n - s)))
+            s += per
+    return out
+
+
 class TorchDistReducer:
     graph_safe = False
 
@@ -91,9 +112,10 @@ class TorchDistReducer:
         if self.compression and (self._comm_buf is None or self._comm_buf.numel() != flat.numel()):
             dt = torch.float16 if self.compression == "fp16" else torch.bfloat16
             self._comm_buf = torch.empty(flat.numel(), dtype=dt, device=flat.device)
-        for off, n in ranges:
+        esz = 2 if self.compression else 4
+        for off, n in split_ranges(ranges, self.bucket_bytes // esz):
             view = flat[off:off + n]
-            tid = monitor().begin(f"allreduce.range{off}", n * (2 if self.compression else 4))
+            tid = monitor().begin(f"allreduce.range{off}", n * esz)
             if self.compression:
                 cb = self._comm_buf[off:off + n]
                 cb.copy_(view)

@@ -17,7 +17,15 @@ backward SEGMENT (``model.backward_segments``: one per ResNet stage, last stage 
 an optimizer graph; after each segment's replay the gradient ranges it finished are handed
 to the communication engine (``parallel/``) asynchronously on its own stream, so the
 allreduce of stage 4's gradients overlaps the backward of stages 3..1 and only the last
-segment's (small) reduction is exposed. Collectives are never captured.
+segment's (small) reduction is exposed. With the native RCCL engine (``graph_safe``) the
+collectives are captured INTO the step graph: after each backward segment the engine forks
+its comm stream off the capture stream, so the reductions are a parallel branch of one
+graph and the step is a single launch. Other reducers (torch.distributed) replay one graph
+per segment and issue their collectives from the host between the replays.
+
+roctx ranges (``utils/tracing.py``) mark the step, forward, each backward segment, the
+allreduce enqueue and the optimizer, so ``rocprofv3 --marker-trace`` timelines line up with
+the kernels. ``comm_profile`` measures allreduce time, exposed communication and overlap.
 """
 from __future__ import annotations
 
@@ -30,6 +38,7 @@ import torch
 from .ops import functional as Fn
 from .ops import _ext
 from .nn.layers import join_side_streams
+from .utils.tracing import range_
 
 
 def resnet_lr_schedule(global_batch: int, num_examples_per_epoch: int = 1281167, base_lr: float = 0.128,
@@ -102,6 +111,8 @@ class Trainer:
         self._segs = None
         self._seg_ranges = {}
         self._static = None
+        self.logits = None
+        self._skip_comm = False  # comm_profile: the same step with the collectives left out
         # overlap the allreduce with backward (segmented graphs + async reducer)
         # (force_overlap: take the segmented multi-GPU path on one rank -- tests / N=1 timing)
         self.overlap = (reducer is not None and (world_size > 1 or force_overlap) and not forward_only
@@ -115,7 +126,9 @@ class Trainer:
             ps.zero_grad()
         ps.zero_stats()
         ps.repack()
-        logits = self.model.forward(images)
+        with range_("forward"):
+            logits = self.model.forward(images)
+        self.logits = logits
         Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B,
                         self.hyper[5:6] if self.loss_scaling else None)
 
@@ -134,6 +147,10 @@ class Trainer:
         return self._seg_ranges[i]
 
     def _optimizer(self):
+        with range_("optimizer"):
+            self._optimizer_body()
+
+    def _optimizer_body(self):
         if self.forward_only:
             self.loss.copy_(self.row_loss.mean().view(1))
             return
@@ -148,15 +165,34 @@ class Trainer:
         self.loss.copy_((self.row_loss.mean() + 0.5 * self.wd * self.l2).view(1))
 
     def _reduce(self):
-        if self.reducer is not None and self.world > 1 and not self.forward_only:
-            self.reducer.allreduce_(self.ps.grad)
+        if self.reducer is not None and self.world > 1 and not self.forward_only and not self._skip_comm:
+            with range_("allreduce"):
+                self.reducer.allreduce_(self.ps.grad)
+
+    def _segments_with_comm(self):
+        """Backward segment by segment; each finished segment's gradient ranges go to the
+        communication engine (asynchronously, on its comm stream) while the next runs."""
+        gen = self.model.backward_segments(self.dlogits)
+        i = 0
+        while True:
+            with range_(f"backward.segment{i}"):
+                try:
+                    layers, _ = next(gen)
+                except StopIteration:
+                    break
+            if not self._skip_comm:
+                with range_(f"allreduce.segment{i}"):
+                    self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
+            else:
+                self._ranges(i, layers)
+            i += 1
+        if not self._skip_comm:
+            self.reducer.join()
 
     def _eager_step(self, images, labels):
         if self.overlap:
             self._forward(images, labels)
-            for i, (layers, _) in enumerate(self.model.backward_segments(self.dlogits)):
-                self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
-            self.reducer.join()
+            self._segments_with_comm()
             self._optimizer()
             return
         self._forward_backward(images, labels)
@@ -181,9 +217,7 @@ class Trainer:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                     self._forward(images, labels)
-                    for i, (layers, _) in enumerate(self.model.backward_segments(self.dlogits)):
-                        self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
-                    self.reducer.join()
+                    self._segments_with_comm()
                     self._optimizer()
                 self._g_all = g
                 self._static = (images, labels)
@@ -236,6 +270,10 @@ class Trainer:
 
     def step(self, images, labels):
         """One training step; returns the device tensor holding total_loss of this step."""
+        with range_("step"):
+            return self._step(images, labels)
+
+    def _step(self, images, labels):
         self.hyper[0:1].fill_(float(self.lr_fn(self.steps_done)))  # host write, outside the graph
         if not self.use_graph:
             self._eager_step(images, labels)
@@ -262,6 +300,83 @@ class Trainer:
                 self._g_opt.replay()
         self.steps_done += 1
         return self.loss
+
+    # ---------------------------------------------------------------- metrics
+    def accuracy(self, labels):
+        """(top-1, top-5) accuracy of the last step's logits on ``labels`` as device scalars
+        (tf_cnn_benchmarks --print_training_accuracy; the logits of a graph replay live in the
+        graph's static output buffer)."""
+        if self.logits is None:
+            return None
+        lg = self.logits[:, :self.model.num_classes].float()
+        top = lg.topk(min(5, lg.shape[1]), dim=1).indices
+        lab = labels.view(-1, 1).to(top.device)
+        top1 = (top[:, :1] == lab).any(dim=1).float().mean()
+        top5 = (top == lab).any(dim=1).float().mean()
+        return top1, top5
+
+    def comm_profile(self, images, labels, iters: int = 10):
+        """Allreduce time, exposed communication and overlap of the data-parallel step
+        (SURVEY.md §5 metrics), measured after the timed loop on the same buffers:
+
+        * ``step_ms``: the real step (as timed by the benchmark);
+        * ``compute_ms``: the same step with the collectives left out (its own graph);
+        * ``allreduce_ms``: the step's gradient reductions alone (all segment ranges, in the
+          same bucket schedule, back to back on the comm stream);
+        * ``exposed_comm_ms`` = step - compute; ``overlap_pct`` = share of the allreduce
+          time hidden under backward.
+
+        Gradients are left summed (not averaged) -- call only after the measured run."""
+        if self.reducer is None or self.forward_only or not self.overlap or self.dev.type != "cuda":
+            return None
+
+        def timed(fn):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            e1.synchronize()
+            return e0.elapsed_time(e1) / iters
+
+        step_ms = timed(lambda: self.step(images, labels))
+        self._skip_comm = True
+        try:
+            if self.use_graph:
+                g = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize()
+                with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
+                    self._forward(images, labels)
+                    self._segments_with_comm()
+                    self._optimizer()
+                compute_ms = timed(g.replay)
+                del g
+            else:
+                compute_ms = timed(lambda: self._eager_step(images, labels))
+        finally:
+            self._skip_comm = False
+        ranges = [self._seg_ranges[i] for i in sorted(self._seg_ranges)]
+
+        def reduce_all():
+            for rng in ranges:
+                self.reducer.allreduce_ranges_async_(self.ps.grad, rng)
+            self.reducer.join()
+
+        comm = getattr(self.reducer, "comm", None)
+        b0 = comm.buckets_issued() if hasattr(comm, "buckets_issued") else None
+        allreduce_ms = timed(reduce_all)
+        per_step = None
+        if b0 is not None:
+            per_step = (comm.buckets_issued() - b0) // (iters + 1)
+        exposed = max(step_ms - compute_ms, 0.0)
+        overlap = 100.0 * (1.0 - min(exposed / allreduce_ms, 1.0)) if allreduce_ms > 0 else None
+        return {"step_ms": round(step_ms, 4), "compute_ms": round(compute_ms, 4),
+                "allreduce_ms": round(allreduce_ms, 4), "exposed_comm_ms": round(exposed, 4),
+                "overlap_pct": None if overlap is None else round(overlap, 1),
+                "buckets_per_step": per_step,
+                "fusion_threshold_bytes": getattr(self.reducer, "bucket_bytes", None)}
 
 
 def synthetic_batch(model, batch_size: int, seed: int = 0):

@@ -2,14 +2,24 @@
 """Headline benchmark: ResNet-50 synchronous data-parallel training throughput,
 images/sec for the whole node, bs=64 per GPU, synthetic ImageNet, random-init weights
 (BASELINE.json metric; the reference's tf_cnn_benchmarks run of
-/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-113).
+/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-113, ``-np TOTAL_WORKERS``
+at :99-109).
 
-    python bench.py --gpus N --steps K --warmup W          (N=1)
+    python bench.py --gpus N --steps K --warmup W
+        N=1: this process trains on cuda:0.
+        N>1 without WORLD_SIZE in the environment: this process is only the launcher -- it
+             starts N worker CHILD processes (one per MI355X, launch/launcher.py: rank env,
+             NUMA pinning, fail-fast) before anything touches the GPU, waits for them and
+             exits non-zero if any of them fails.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+        each process is one rank (RANK / LOCAL_RANK / WORLD_SIZE from the environment);
+        WORLD_SIZE must equal --gpus.
 
 One process per MI355X; gradients averaged with RCCL over xGMI. W untimed warmup steps
 (the first ones also capture the HIP graph), then EXACTLY K timed steps bracketed by
-barrier + device sync; the max time over ranks is used; rank 0 prints one JSON line.
+barrier + device sync; the max time over ranks is used; rank 0 prints one JSON line that
+also carries ``world`` (torch.distributed) and ``rccl_nranks`` (read back from the native
+RCCL communicator), and every rank prints its own ``total images/sec`` line on stderr.
 """
 from __future__ import annotations
 
@@ -24,9 +34,10 @@ sys.path.insert(0, ROOT)
 import azure_hc_intel_tf_amd  # noqa: E402,F401  (HIP runtime defaults, before torch touches the GPU)
 
 BASELINE_VALUE = None  # the reference publishes no number
+METRIC = "images/sec (whole node) ResNet-50 bs=64/worker at 1/2/4/8 MI355X"
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -38,34 +49,84 @@ def main():
     ap.add_argument("--compression", default=None, choices=[None, "fp16", "bf16"])
     ap.add_argument("--engine", default="native", choices=["native", "torch"])
     ap.add_argument("--force_dp_path", action="store_true",
-                    help="N=1 only: run the multi-GPU step (segmented graphs + async RCCL engine on a 1-rank "
-                         "communicator) to time its overhead on one GPU")
+                    help="N=1 only: run the multi-GPU step (one graph with the collectives on a forked comm "
+                         "stream, async RCCL engine on a 1-rank communicator) to time its overhead on one GPU")
     ap.add_argument("--use_fp16", action="store_true",
-                    help="tf_cnn_benchmarks --use_fp16: 16-bit compute (bf16 on MI355X) with automatic loss scaling")
-    args = ap.parse_args()
+                    help="tf_cnn_benchmarks --use_fp16: 16-bit compute with automatic loss scaling")
+    ap.add_argument("--compute_dtype", default=None, choices=[None, "bf16", "fp16", "fp32"],
+                    help="activation / GEMM precision (default bf16; fp32 = the reference's precision)")
+    return ap.parse_args(argv)
 
-    import torch
-    import torch.distributed as dist
+
+def spawn_workers(args, argv) -> int:
+    """--gpus N with no rank environment: start N worker children (never exec: nothing here
+    has touched the GPU yet, and the children are separate processes)."""
+    from azure_hc_intel_tf_amd.launch.launcher import launch
+
+    one_device = os.environ.get("HCB_BENCH_ONE_DEVICE") == "1"
+    if not one_device:
+        import torch  # device_count() does not initialise the GPU
+
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"[bench] --gpus {args.gpus} but only {visible} GPU(s) visible; refusing to report a "
+                  f"{visible}-GPU run as a {args.gpus}-GPU one", file=sys.stderr)
+            return 3
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env["HCB_BENCH_SPAWNED"] = "1"
+    return launch(cmd, nproc_per_node=args.gpus, master_addr="127.0.0.1", env=env)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus < 1:
+        print("[bench] --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_workers(args, argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to run", file=sys.stderr)
+        return 3
+    if os.environ.get("HCB_BENCH_STUB_WORKER") == "1":  # CPU test of the spawn path: report the rank env
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                                                         "MASTER_ADDR", "MASTER_PORT", "HCB_BENCH_SPAWNED")}),
+              flush=True)
+        return 0
+
+    import torch
+    import torch.distributed as dist
+
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)
-        sys.exit(2)
+        return 2
     # rehearsal knobs for a one-GPU box (never used by the driver): every rank on device 0
     # and gloo instead of RCCL, which refuses two ranks on one device
     if os.environ.get("HCB_BENCH_ONE_DEVICE") == "1":
         local_rank = 0
+    if local_rank >= torch.cuda.device_count():
+        print(f"[bench] rank {rank}: LOCAL_RANK {local_rank} but {torch.cuda.device_count()} GPU(s) visible",
+              file=sys.stderr)
+        return 3
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
     from azure_hc_intel_tf_amd.models import create_model
     from azure_hc_intel_tf_amd.trainer import Trainer, resnet_lr_schedule, synthetic_batch
     from azure_hc_intel_tf_amd.ops import _ext
+    from azure_hc_intel_tf_amd.utils import tracing
 
     _ext.load()
+    dtype = args.compute_dtype or ("fp16" if args.use_fp16 else "bf16")
     reducer = None
+    backend = None
+    rccl_nranks = None
     if world > 1:
         backend = os.environ.get("HCB_BENCH_BACKEND", "nccl")
         if backend == "nccl":
@@ -87,6 +148,7 @@ def main():
                 dist.all_reduce(ok, op=dist.ReduceOp.MIN)
                 if int(ok.item()) != 1:
                     raise RuntimeError("self-test mismatch")
+                rccl_nranks = reducer.comm.size()
             except Exception as e:  # pragma: no cover - exercised only on multi-GPU nodes
                 print(f"[bench] native RCCL engine unavailable ({e}); falling back to torch.distributed",
                       file=sys.stderr)
@@ -94,12 +156,18 @@ def main():
                 reducer = make_reducer("torch", compression=args.compression)
         else:
             reducer = make_reducer("torch", compression=args.compression)
+        if rccl_nranks is None and backend == "nccl":
+            rccl_nranks = dist.get_world_size()
+        if rccl_nranks is not None and rccl_nranks != world:
+            print(f"[bench] RCCL communicator has {rccl_nranks} ranks, expected {world}", file=sys.stderr)
+            return 4
 
     if world == 1 and args.force_dp_path:
         from azure_hc_intel_tf_amd.parallel.native import NativeReducer
 
         reducer = NativeReducer(compression=args.compression, force=True)
-    model = create_model(args.model, device=dev)
+        rccl_nranks = reducer.comm.size()
+    model = create_model(args.model, device=dev, compute_dtype=dtype)
     B = args.batch_size
     from azure_hc_intel_tf_amd.ops import autotune
 
@@ -113,7 +181,7 @@ def main():
         reducer.broadcast_(model.ps.buf, 0)
     images, labels = synthetic_batch(model, B, seed=rank)
     trainer = Trainer(model, B, resnet_lr_schedule(B * world), reducer=reducer, world_size=world,
-                      use_graph=not args.no_graph, dynamic_loss_scale=args.use_fp16,
+                      use_graph=not args.no_graph, dynamic_loss_scale=(dtype == "fp16"),
                       force_overlap=args.force_dp_path)
 
     def barrier():
@@ -121,33 +189,46 @@ def main():
             dist.barrier()
 
     warmup = max(args.warmup, 0)
-    for _ in range(warmup):
-        trainer.step(images, labels)
+    with tracing.range_("bench.warmup"):
+        for _ in range(warmup):
+            trainer.step(images, labels)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     trace = torch.zeros(args.steps, device=dev) if os.environ.get("HCB_BENCH_LOSS_TRACE") == "1" else None
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        trainer.step(images, labels)
-        if trace is not None:  # device-side copy, no host sync (debug only)
-            trace[i:i + 1].copy_(trainer.loss)
+    with tracing.range_("bench.timed"):
+        for i in range(args.steps):
+            trainer.step(images, labels)
+            if trace is not None:  # device-side copy, no host sync (debug only)
+                trace[i:i + 1].copy_(trainer.loss)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
+    own = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss = float(trainer.loss.item())
+    comm = None
+    if reducer is not None:
+        if hasattr(reducer, "check_errors"):
+            reducer.check_errors()
+        if os.environ.get("HCB_BENCH_COMM_PROFILE", "1") == "1":  # after the timed region
+            comm = trainer.comm_profile(images, labels)
+    # tf_cnn_benchmarks prints "total images/sec" on every rank (run-tf-sing-ucx-openmpi.sh:99-113
+    # runs it under mpirun); stderr keeps stdout to the one JSON line
+    print(f"[rank {rank}] total images/sec: {world * B * args.steps / own:.2f} "
+          f"(own {1000.0 * own / args.steps:.3f} ms/step)", file=sys.stderr, flush=True)
     if trace is not None and rank == 0:
         print("[bench] losses " + " ".join(f"{v:.4f}" for v in trace.tolist()), file=sys.stderr)
     ips = world * B * args.steps / elapsed
     if rank == 0:
         res = {
-            "metric": "images/sec (whole node) ResNet-50 bs=64/worker at 1/2/4/8 MI355X"
-            if (args.model == "resnet50" and B == 64) else f"images/sec (whole node) {args.model} bs={B}/worker",
+            "metric": METRIC if (args.model == "resnet50" and B == 64)
+            else f"images/sec (whole node) {args.model} bs={B}/worker",
             "value": round(ips, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -157,19 +238,26 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (ips / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16",
+            "dtype": dtype,
             "data": f"synthetic (truncated-normal ImageNet {model.image_size}x{model.image_size}, random-init weights)",
+            "world": world,
+            "rccl_nranks": rccl_nranks,
+            "comm": comm,
             "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
                        "image_size": model.image_size, "parallelism": f"dp{world}",
                        "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": not args.no_graph,
-                       "engine": args.engine if (world > 1 or args.force_dp_path) else None, "compression": args.compression,
-                       "loss_scaling": "dynamic" if args.use_fp16 else None,
+                       "engine": args.engine if (world > 1 or args.force_dp_path) else None,
+                       "backend": backend, "compression": args.compression,
+                       "loss_scaling": "dynamic" if dtype == "fp16" else None,
                        "final_loss": round(loss, 4)},
         }
         print(json.dumps(res), flush=True)
+    if reducer is not None and hasattr(reducer, "close"):
+        reducer.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

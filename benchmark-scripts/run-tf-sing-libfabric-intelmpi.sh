@@ -14,7 +14,9 @@ fi
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 REPO="$(dirname "$HERE")"
 export PYTHONPATH="$REPO${PYTHONPATH:+:$PYTHONPATH}"
+# like the reference IMPI runner (run-tf-sing-libfabric-intelmpi.sh:94-105): fusion threshold
+# passed, no HOROVOD_MPI_THREADS_DISABLE, no core pinning, transport debug output on
+# (NCCL_DEBUG=INFO is set by the launcher plan as the I_MPI_DEBUG=5 analogue)
 export HOROVOD_FUSION_THRESHOLD=${HOROVOD_FUSION_THRESHOLD:-134217728}
-export HOROVOD_MPI_THREADS_DISABLE=1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 python3 -m azure_hc_intel_tf_amd.launch.run_tf_sing --flavor libfabric-intelmpi "$@"

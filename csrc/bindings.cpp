@@ -712,22 +712,30 @@ void preprocess_images(const Tensor& src, const Tensor& desc, const Tensor& desc
                                 (int)out.size(1), (int)out.size(3), sc, bi, cur_stream());
 }
 
+static int pack_mode(const Tensor& t, const char* what) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "hcb.", what, ": wire dtype must be float32, bfloat16 or float16");
+  }
+  return 0;
+}
+
 void bucket_pack(const Tensor& src, const Tensor& dst, double scale) {
   check_f32(src, "src");
   check_cuda(dst, "dst");
-  bool bf = dst.scalar_type() == at::kBFloat16;
-  TORCH_CHECK(bf || dst.scalar_type() == at::kFloat, "hcb.bucket_pack: dst dtype");
-  TORCH_CHECK(src.numel() == dst.numel(), "hcb.bucket_pack: sizes");
-  hcb::launch_bucket_pack(src.data_ptr<float>(), dst.data_ptr(), src.numel(), (float)scale, bf ? 1 : 0, cur_stream());
+  TORCH_CHECK(dst.is_contiguous() && src.numel() == dst.numel(), "hcb.bucket_pack: sizes");
+  hcb::launch_bucket_pack(src.data_ptr<float>(), dst.data_ptr(), src.numel(), (float)scale, pack_mode(dst, "bucket_pack"),
+                          cur_stream());
 }
 
 void bucket_unpack(const Tensor& src, const Tensor& dst, double scale) {
   check_cuda(src, "src");
   check_f32(dst, "dst");
-  bool bf = src.scalar_type() == at::kBFloat16;
-  TORCH_CHECK(src.numel() == dst.numel(), "hcb.bucket_unpack: sizes");
-  hcb::launch_bucket_unpack(src.data_ptr(), dst.data_ptr<float>(), src.numel(), (float)scale, bf ? 1 : 0,
-                            cur_stream());
+  TORCH_CHECK(src.is_contiguous() && src.numel() == dst.numel(), "hcb.bucket_unpack: sizes");
+  hcb::launch_bucket_unpack(src.data_ptr(), dst.data_ptr<float>(), src.numel(), (float)scale,
+                            pack_mode(src, "bucket_unpack"), cur_stream());
 }
 
 }  // namespace

@@ -43,6 +43,7 @@
 #include <thread>
 #include <vector>
 
+#include "comm/engine.h"
 #include "kernels/kernels.h"
 
 using at::Tensor;
@@ -101,6 +102,7 @@ struct Comm {
   std::ofstream tl;
   bool tl_first = true;
   int64_t cycle = 0;
+  int64_t buckets_issued = 0;  // lifetime count of bucket collectives
   // watchdog
   std::thread wd;
   std::mutex mu;
@@ -114,12 +116,14 @@ struct Comm {
   // thread only compares `done` with `enq` and the clock. Only when the caller has been
   // quiet for > 1 s (blocked on a hung collective, or idle) does the watchdog query the
   // watch event itself, under `mu`, which every enqueue also holds.
-  std::atomic<int64_t> enq{0}, done{0};
+  hcb::comm::StallWatch watch;
+  std::unique_ptr<hcb::comm::Transport> transport;  // RcclTransport, created on first use
+  std::unique_ptr<hcb::comm::BucketEngine> engine;  // lifetime bucket numbering
+  int64_t fusion_bytes = 128ll << 20;  // HOROVOD_FUSION_THRESHOLD
   bool skip_rccl = false;  // debug (HCB_COMM_SKIP_RCCL=1): stream fork/join without the collective
   hipEvent_t watch_ev = nullptr;
   int64_t watch_cycle = 0;
   std::chrono::steady_clock::time_point last_call = std::chrono::steady_clock::now();
-  double stall_warn_s = 60.0, stall_abort_s = 0.0;
   std::atomic<bool> aborted{false};
 
   hipEvent_t get_event() {
@@ -152,31 +156,23 @@ bool capturing(hipStream_t s) {
 }
 
 void watchdog_loop(Comm* c) {
-  bool warned = false;
-  int64_t seen_done = -1;
-  auto since = std::chrono::steady_clock::now();
+  using hcb::comm::StallWatch;
   while (!c->stop.load()) {
     {
       std::unique_lock<std::mutex> lk(c->mu);
       c->cv.wait_for(lk, std::chrono::milliseconds(500));
     }
     if (c->stop.load()) break;
-    if (c->stop.load()) break;
     auto now = std::chrono::steady_clock::now();
     {
       std::lock_guard<std::mutex> lk(c->mu);
-      if (c->done.load() < c->watch_cycle && std::chrono::duration<double>(now - c->last_call).count() > 1.0 &&
-          hipEventQuery(c->watch_ev) == hipSuccess)
-        c->done.store(c->watch_cycle, std::memory_order_release);
+      if (c->watch.completed() < c->watch_cycle &&
+          std::chrono::duration<double>(now - c->last_call).count() > 1.0 && hipEventQuery(c->watch_ev) == hipSuccess)
+        c->watch.complete(c->watch_cycle);
     }
-    const int64_t d = c->done.load(std::memory_order_acquire), e = c->enq.load(std::memory_order_acquire);
-    if (d >= e || d != seen_done) {  // idle, or progress since the last look
-      seen_done = d;
-      since = now;
-      warned = false;
-      continue;
-    }
-    const double waited = std::chrono::duration<double>(now - since).count();
+    double waited = 0;
+    const StallWatch::Action act = c->watch.evaluate(now, &waited);
+    if (act == StallWatch::kIdle || act == StallWatch::kProgress) continue;
     if (waited > 1.0 && c->comm) {  // stalled: only now ask RCCL whether a peer failed
       ncclResult_t ae = ncclSuccess;
       if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
@@ -189,15 +185,14 @@ void watchdog_loop(Comm* c) {
         std::_Exit(18);
       }
     }
-    if (!warned && waited > c->stall_warn_s) {
+    if (act == StallWatch::kWarn) {
       std::fprintf(stderr,
-                   "[hcb watchdog] rank %d: gradient allreduce %lld has not completed after %.0f s; "
-                   "one or more ranks may have stalled (HOROVOD_STALL_CHECK_TIME_SECONDS=%.0f)\n",
-                   c->rank, (long long)d, waited, c->stall_warn_s);
+                   "[hcb watchdog] rank %d: gradient reduction cycle %lld (buckets up to #%lld) has not completed "
+                   "after %.0f s; one or more ranks may have stalled (HOROVOD_STALL_CHECK_TIME_SECONDS=%.0f)\n",
+                   c->rank, (long long)(c->watch.completed() + 1), (long long)c->watch.last_seq(), waited,
+                   c->watch.warn_s());
       std::fflush(stderr);
-      warned = true;
-    }
-    if (c->stall_abort_s > 0 && waited > c->stall_abort_s && c->comm) {
+    } else if (act == StallWatch::kAbort && c->comm) {
       std::fprintf(stderr, "[hcb watchdog] rank %d: stalled for %.0f s > HCB_STALL_ABORT_SECONDS; aborting\n", c->rank,
                    waited);
       std::fflush(stderr);
@@ -208,6 +203,57 @@ void watchdog_loop(Comm* c) {
     }
   }
 }
+
+// RCCL transport of the bucket engine: collectives on the comm stream, forked from / joined
+// to the caller's stream with events (capturable: they become graph edges).
+struct RcclTransport final : hcb::comm::Transport {
+  Comm* c;
+  hipStream_t cur = nullptr;
+  bool cap = false, tl = false;
+  hipEvent_t e0 = nullptr;
+  explicit RcclTransport(Comm* c_) : c(c_) {}
+  void fork() override {
+    cur = c10::hip::getCurrentHIPStream().stream();
+    HCB_HIP(hipEventRecord(c->fork_ev, cur));
+    HCB_HIP(hipStreamWaitEvent(c->stream, c->fork_ev, 0));
+  }
+  void bucket_begin(const hcb::comm::Bucket&) override {
+    if (!tl) return;
+    e0 = c->get_event();
+    HCB_HIP(hipEventRecord(e0, c->stream));
+  }
+  void reduce_bucket(float* flat, const hcb::comm::Bucket& b, hcb::comm::Wire w, bool avg) override {
+    const ncclRedOp_t op = avg ? ncclAvg : ncclSum;
+    if (w != hcb::comm::Wire::F32) {
+      const int mode = (int)w;  // 1 bf16, 2 fp16
+      uint16_t* cb = reinterpret_cast<uint16_t*>(c->cbuf) + b.off;
+      hcb::launch_bucket_pack(flat + b.off, cb, b.len, 1.0f, mode, c->stream);
+      HCB_NCCL(ncclAllReduce(cb, cb, b.len, w == hcb::comm::Wire::BF16 ? ncclBfloat16 : ncclFloat16, op, c->comm,
+                             c->stream));
+      hcb::launch_bucket_unpack(cb, flat + b.off, b.len, 1.0f, mode, c->stream);
+    } else if (!c->skip_rccl) {
+      HCB_NCCL(ncclAllReduce(flat + b.off, flat + b.off, b.len, ncclFloat32, op, c->comm, c->stream));
+    }
+  }
+  void bucket_end(const hcb::comm::Bucket& b, hcb::comm::Wire w) override {
+    if (!tl) return;
+    hipEvent_t e1 = c->get_event();
+    HCB_HIP(hipEventRecord(e1, c->stream));
+    c->pending.push_back({w != hcb::comm::Wire::F32 ? "PACK_ALLREDUCE_UNPACK" : "ALLREDUCE", (int)b.seq,
+                          b.len * hcb::comm::wire_bytes(w), e0, e1});
+  }
+  void join() override {
+    HCB_HIP(hipEventRecord(c->join_ev, c->stream));
+    HCB_HIP(hipStreamWaitEvent(cur, c->join_ev, 0));
+    joined = true;
+  }
+  // the overlap form records the join event without waiting on it: join_() consumes it later
+  void mark_cycle_end(int64_t) override {
+    if (!joined) HCB_HIP(hipEventRecord(c->join_ev, c->stream));
+    joined = false;
+  }
+  bool joined = false;
+};
 
 // ------------------------------------------------------------------------- ops
 Tensor unique_id() {
@@ -247,8 +293,11 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
       c->tl << "[\n";
     }
   }
-  c->stall_warn_s = env_double("HOROVOD_STALL_CHECK_TIME_SECONDS", 60.0);
-  c->stall_abort_s = env_double("HCB_STALL_ABORT_SECONDS", 0.0);
+  c->watch.configure(env_double("HOROVOD_STALL_CHECK_TIME_SECONDS", 60.0), env_double("HCB_STALL_ABORT_SECONDS", 0.0));
+  {
+    const double fb = env_double("HOROVOD_FUSION_THRESHOLD", 128.0 * 1024 * 1024);
+    c->fusion_bytes = fb > 0 ? (int64_t)fb : 0;
+  }
   c->skip_rccl = env_double("HCB_COMM_SKIP_RCCL", 0.0) != 0.0;
   Comm* raw = c.get();
   if (env_double("HCB_COMM_WATCHDOG", 1.0) != 0.0) raw->wd = std::thread(watchdog_loop, raw);
@@ -367,19 +416,21 @@ void reduce_scatter_(int64_t h, const Tensor& in, const Tensor& out, bool averag
 }
 
 // Bucketed allreduce of the flat fp32 gradient buffer.
-// buckets: int64 CPU tensor [nb][2] of (offset, length) in elements, issued in order.
-// compress: 0 none, 1 bf16, 2 fp16 (fp16 goes through an fp32->fp16 cast kernel pair)
-// scale: multiplied in during pack (e.g. 1/world for averaging when compressing).
+// ranges: int64 CPU tensor [nr][2] of (offset, length) in elements; each range is cut into
+// buckets of at most `fusion_bytes` wire bytes (<= 0: the HOROVOD_FUSION_THRESHOLD default
+// read at create()), issued in order on the comm stream.
+// compress: 0 none (fp32), 1 bf16, 2 fp16 (IEEE half; Horovod Compression.fp16).
 void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale, bool average,
-                 bool do_join) {
+                 bool do_join, int64_t fusion_bytes) {
   Comm* c = get(h);
   TORCH_CHECK(c->comm, "hcb_comm: communicator aborted");
   TORCH_CHECK(flat.is_cuda() && flat.is_contiguous() && flat.scalar_type() == at::kFloat,
               "hcb_comm.bucket_allreduce_: flat fp32 GPU buffer");
   TORCH_CHECK(!buckets.is_cuda() && buckets.scalar_type() == at::kLong && buckets.dim() == 2 && buckets.size(1) == 2,
               "hcb_comm.bucket_allreduce_: buckets int64 [n][2] on CPU");
-  TORCH_CHECK(compress == 0 || compress == 1, "hcb_comm.bucket_allreduce_: compress must be 0 (none) or 1 (bf16)");
-  const int64_t* bk = buckets.data_ptr<int64_t>();
+  TORCH_CHECK(compress >= 0 && compress <= 2, "hcb_comm.bucket_allreduce_: compress must be 0 (none), 1 (bf16) or 2 (fp16)");
+  TORCH_CHECK(scale == 1.0, "hcb_comm.bucket_allreduce_: scale is folded into the optimizer; pass 1.0");
+  const int64_t* bk = buckets.contiguous().data_ptr<int64_t>();
   const int64_t nb = buckets.size(0);
   const int64_t n = flat.numel();
   for (int64_t i = 0; i < nb; ++i)
@@ -389,8 +440,8 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   const bool cap = capturing(cur);
   if (!cap) flush_timeline(c, false);
-  if (!cap && c->wd.joinable() && c->done.load() < c->watch_cycle && hipEventQuery(c->watch_ev) == hipSuccess)
-    c->done.store(c->watch_cycle, std::memory_order_release);
+  if (!cap && c->wd.joinable() && c->watch.completed() < c->watch_cycle && hipEventQuery(c->watch_ev) == hipSuccess)
+    c->watch.complete(c->watch_cycle);
   if (compress && c->cbuf_bytes < (size_t)n * 2) {
     TORCH_CHECK(!cap, "hcb_comm: first compressed reduction must run outside graph capture");
     HCB_HIP(hipStreamSynchronize(c->stream));
@@ -398,43 +449,27 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
     HCB_HIP(hipMalloc(&c->cbuf, (size_t)n * 2));
     c->cbuf_bytes = (size_t)n * 2;
   }
-  HCB_HIP(hipEventRecord(c->fork_ev, cur));
-  HCB_HIP(hipStreamWaitEvent(c->stream, c->fork_ev, 0));
-  const bool tl = c->tl.is_open() && !cap;
-  float* fp = flat.data_ptr<float>();
-  for (int64_t i = 0; i < nb; ++i) {
-    int64_t off = bk[2 * i], len = bk[2 * i + 1];
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (tl) {
-      e0 = c->get_event();
-      HCB_HIP(hipEventRecord(e0, c->stream));
-    }
-    if (compress) {
-      uint16_t* cb = reinterpret_cast<uint16_t*>(c->cbuf) + off;
-      hcb::launch_bucket_pack(fp + off, cb, len, (float)scale, 1, c->stream);
-      HCB_NCCL(ncclAllReduce(cb, cb, len, ncclBfloat16, average ? ncclAvg : ncclSum, c->comm, c->stream));
-      hcb::launch_bucket_unpack(cb, fp + off, len, 1.0f, 1, c->stream);
-    } else if (!c->skip_rccl) {
-      HCB_NCCL(ncclAllReduce(fp + off, fp + off, len, ncclFloat32, average ? ncclAvg : ncclSum, c->comm, c->stream));
-    }
-    if (tl) {
-      e1 = c->get_event();
-      HCB_HIP(hipEventRecord(e1, c->stream));
-      c->pending.push_back({compress ? "PACK_ALLREDUCE_UNPACK" : "ALLREDUCE", (int)i, len * (compress ? 2 : 4), e0, e1});
-    }
+  if (!c->engine) {
+    c->transport = std::make_unique<RcclTransport>(c);
+    c->engine = std::make_unique<hcb::comm::BucketEngine>(c->transport.get());
   }
-  HCB_HIP(hipEventRecord(c->join_ev, c->stream));
-  if (do_join) HCB_HIP(hipStreamWaitEvent(cur, c->join_ev, 0));
+  auto* tr = static_cast<RcclTransport*>(c->transport.get());
+  tr->cap = cap;
+  tr->tl = c->tl.is_open() && !cap;
+  std::vector<hcb::comm::Bucket> issued =
+      c->engine->submit(flat.data_ptr<float>(), n, bk, nb, (hcb::comm::Wire)compress, average,
+                 fusion_bytes > 0 ? fusion_bytes : c->fusion_bytes, do_join);
+  c->buckets_issued += (int64_t)issued.size();
   if (!cap && c->wd.joinable()) {
     HCB_HIP(hipEventRecord(c->watch_ev, c->stream));
-    c->watch_cycle = c->enq.fetch_add(1, std::memory_order_acq_rel) + 1;
+    c->watch_cycle = c->watch.enqueue(c->buckets_issued - 1);
   }
   c->cycle++;
 }
 
 void bucket_allreduce_(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale,
                        bool average) {
-  bucket_impl(h, flat, buckets, compress, scale, average, true);
+  bucket_impl(h, flat, buckets, compress, scale, average, true, 0);
 }
 
 // Overlap form: the comm stream waits for the caller's stream (everything enqueued so far,
@@ -443,8 +478,12 @@ void bucket_allreduce_(int64_t h, const Tensor& flat, const Tensor& buckets, int
 // comm stream, so one join covers them all.
 void bucket_allreduce_async_(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t compress, double scale,
                              bool average) {
-  bucket_impl(h, flat, buckets, compress, scale, average, false);
+  bucket_impl(h, flat, buckets, compress, scale, average, false, 0);
 }
+
+int64_t buckets_issued(int64_t h) { return get(h)->buckets_issued; }
+int64_t fusion_threshold(int64_t h) { return get(h)->fusion_bytes; }
+void set_fusion_threshold(int64_t h, int64_t bytes) { get(h)->fusion_bytes = bytes; }
 
 void join_(int64_t h) {
   Comm* c = get(h);
@@ -464,6 +503,7 @@ void barrier(int64_t h) {
 struct Xgmi {
   int rank = 0, world = 1, device = 0;
   int64_t cap = 0;                  // floats per slot
+  unsigned spin = 1u << 25;         // bounded-wait iterations (HCB_XGMI_SPIN)
   float* region = nullptr;          // own region: 2 slots + flags
   unsigned* err = nullptr;          // device error word (spin timeout)
   std::vector<float*> peers;        // every rank's region as mapped here (own = region)
@@ -491,7 +531,14 @@ int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, int64_t device) {
   x->cap = cap;
   HCB_HIP(hipSetDevice(x->device));
   const size_t bytes = (size_t)2 * cap * 4 + 256;
-  HCB_HIP(hipMalloc(&x->region, bytes));
+  // uncached (fine-grained) device memory: peers on OTHER GPUs spin on the ready / epoch words
+  // and read the slots over xGMI while this GPU is still running; coarse-grained memory is only
+  // coherent across devices at kernel boundaries
+  HCB_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&x->region), bytes, hipDeviceMallocUncached));
+  {
+    const double sp = env_double("HCB_XGMI_SPIN", (double)(1u << 25));
+    x->spin = sp < 1 ? 1u : (sp > 4.0e9 ? 4000000000u : (unsigned)sp);
+  }
   HCB_HIP(hipMemset(x->region, 0, bytes));
   HCB_HIP(hipMalloc(&x->err, 4));
   HCB_HIP(hipMemset(x->err, 0, 4));
@@ -540,7 +587,7 @@ void xgmi_allreduce_(int64_t h, const Tensor& t, double scale) {
   if (t.numel() == 0) return;
   std::vector<const float*> b(x->peers.begin(), x->peers.end());
   hcb::launch_xgmi_allreduce(b.data(), x->world, x->rank, t.data_ptr<float>(), t.data_ptr<float>(), t.numel(),
-                             x->cap, (float)scale, x->err, c10::hip::getCurrentHIPStream().stream());
+                             x->cap, (float)scale, x->err, x->spin, c10::hip::getCurrentHIPStream().stream());
 }
 
 int64_t xgmi_error(int64_t h) {
@@ -568,7 +615,15 @@ void xgmi_destroy(int64_t h) {
 }
 
 int64_t comm_rank(int64_t h) { return get(h)->rank; }
-int64_t comm_size(int64_t h) { return get(h)->world; }
+// rank count as the RCCL communicator reports it (not the value it was created with), so a
+// benchmark can prove how many ranks its reductions really spanned
+int64_t comm_size(int64_t h) {
+  Comm* c = get(h);
+  TORCH_CHECK(c->comm, "hcb_comm: communicator aborted");
+  int n = 0;
+  HCB_NCCL(ncclCommCount(c->comm, &n));
+  return n;
+}
 
 void abort_comm(int64_t h) {
   Comm* c = get(h);
@@ -599,6 +654,9 @@ TORCH_LIBRARY(hcb_comm, m) {
   m.def("bucket_allreduce_async_(int h, Tensor(a!) flat, Tensor buckets, int compress, float scale, bool average) -> ()",
         bucket_allreduce_async_);
   m.def("join_(int h) -> ()", join_);
+  m.def("buckets_issued(int h) -> int", buckets_issued);
+  m.def("fusion_threshold(int h) -> int", fusion_threshold);
+  m.def("set_fusion_threshold(int h, int bytes) -> ()", set_fusion_threshold);
   m.def("barrier(int h) -> ()", barrier);
   m.def("rank(int h) -> int", comm_rank);
   m.def("size(int h) -> int", comm_size);

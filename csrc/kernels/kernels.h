@@ -199,10 +199,10 @@ void launch_preprocess_images(const uint8_t* src, const int64_t* desc, int B, vo
 // One-shot xGMI allreduce (xgmi.hip): bases = every rank's IPC-mapped staging region.
 int xgmi_max_ranks();
 void launch_xgmi_allreduce(const float* const* bases, int R, int rank, const float* in, float* out, int64_t n,
-                           int64_t cap, float scale, unsigned* err, hipStream_t st);
-void launch_bucket_pack(const float* src, void* dst, int64_t n, float scale, int to_bf16,
+                           int64_t cap, float scale, unsigned* err, unsigned spin, hipStream_t st);
+void launch_bucket_pack(const float* src, void* dst, int64_t n, float scale, int mode,
                         hipStream_t st);
-void launch_bucket_unpack(const void* src, float* dst, int64_t n, float scale, int from_bf16,
+void launch_bucket_unpack(const void* src, float* dst, int64_t n, float scale, int mode,
                           hipStream_t st);
 
 }  // namespace hcb

@@ -15,15 +15,17 @@
 //           their slot e%2, read with system-scope (cache-bypassing) loads; the last
 //           workgroup advances the device epoch.
 // Ranks never write into a peer's memory; a peer's data is only read after its release.
-// Spins are bounded (HCB_XGMI_SPIN iterations of s_sleep): on timeout the kernel raises the
-// error word and completes, so a dead peer can never leave a wave running on the GPU.
+// Spins are bounded (HCB_XGMI_SPIN iterations of s_sleep(8), ~0.2 us each at 2.4 GHz; default
+// 2^25 ~ 7 s): on timeout the kernel raises the error word, POISONS its output with NaN (so a
+// reduction that did not synchronise can never pass for a good one: the loss goes NaN) and
+// completes, so a dead peer can never leave a wave running on the GPU. The host side checks
+// the error word (NativeReducer.check_errors) and raises.
 #include "common.h"
 #include "kernels.h"
 
 namespace hcb {
 
 constexpr int XGMI_MAX_RANKS = 8;
-constexpr unsigned XGMI_SPIN_LIMIT = 1u << 22;  // x s_sleep(8) ~ 64 x 2^22 cycles ~ 0.1-0.2 s
 
 struct XgmiPtrs {
   const float* base[XGMI_MAX_RANKS];  // every rank's region (own included)
@@ -34,7 +36,8 @@ __device__ __forceinline__ unsigned xg_load_flag(const unsigned* p) {
 }
 
 // thread 0 waits until every rank's ready word reaches `want`; returns false on timeout
-__device__ bool xg_wait_all(const XgmiPtrs& P, int R, size_t flag_off, unsigned want, unsigned* err) {
+__device__ bool xg_wait_all(const XgmiPtrs& P, int R, size_t flag_off, unsigned want, unsigned* err,
+                            unsigned spin) {
   __shared__ int ok;
   if (threadIdx.x == 0) {
     ok = 1;
@@ -43,7 +46,7 @@ __device__ bool xg_wait_all(const XgmiPtrs& P, int R, size_t flag_off, unsigned 
       unsigned it = 0;
       while ((int)(xg_load_flag(f) - want) < 0) {
         __builtin_amdgcn_s_sleep(8);
-        if (++it > XGMI_SPIN_LIMIT) {
+        if (++it > spin) {
           atomicOr(err, 1u);
           ok = 0;
           break;
@@ -57,12 +60,12 @@ __device__ bool xg_wait_all(const XgmiPtrs& P, int R, size_t flag_off, unsigned 
 }
 
 __global__ __launch_bounds__(256) void xgmi_push_kernel(XgmiPtrs P, int R, int rank, const float* __restrict__ in,
-                                                        int64_t n, int64_t cap, unsigned* err) {
+                                                        int64_t n, int64_t cap, unsigned* err, unsigned spin) {
   const size_t flag_off = (size_t)2 * cap;  // in floats
   float* mine = const_cast<float*>(P.base[rank]);
   unsigned* myflags = reinterpret_cast<unsigned*>(mine + flag_off);  // [0] ready [1] epoch [2] arrive
   const unsigned e = __hip_atomic_load(myflags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  if (e > 1) xg_wait_all(P, R, flag_off, e - 1, err);
+  if (e > 1) xg_wait_all(P, R, flag_off, e - 1, err, spin);
   float* slot = mine + (size_t)(e & 1) * cap;
   const int64_t n4 = n / 4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
@@ -82,13 +85,16 @@ __global__ __launch_bounds__(256) void xgmi_push_kernel(XgmiPtrs P, int R, int r
 }
 
 __global__ __launch_bounds__(256) void xgmi_reduce_kernel(XgmiPtrs P, int R, int rank, float* __restrict__ out,
-                                                          int64_t n, int64_t cap, float scale, unsigned* err) {
+                                                          int64_t n, int64_t cap, float scale, unsigned* err,
+                                                          unsigned spin) {
   const size_t flag_off = (size_t)2 * cap;
   float* mine = const_cast<float*>(P.base[rank]);
   unsigned* myflags = reinterpret_cast<unsigned*>(mine + flag_off);
   const unsigned e = __hip_atomic_load(myflags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  xg_wait_all(P, R, flag_off, e, err);
+  const bool synced = xg_wait_all(P, R, flag_off, e, err, spin) &&
+                      __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
   const size_t so = (size_t)(e & 1) * cap;
+  if (!synced) scale = __builtin_nanf("");  // poison: never return an unsynchronised sum
   const int64_t n2 = n / 2;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x) {
     float a0 = 0.f, a1 = 0.f;
@@ -124,14 +130,14 @@ __global__ __launch_bounds__(256) void xgmi_reduce_kernel(XgmiPtrs P, int R, int
 int xgmi_max_ranks() { return XGMI_MAX_RANKS; }
 
 void launch_xgmi_allreduce(const float* const* bases, int R, int rank, const float* in, float* out, int64_t n,
-                           int64_t cap, float scale, unsigned* err, hipStream_t st) {
+                           int64_t cap, float scale, unsigned* err, unsigned spin, hipStream_t st) {
   XgmiPtrs P{};
   for (int r = 0; r < R && r < XGMI_MAX_RANKS; ++r) P.base[r] = bases[r];
   // few workgroups: the push / reduce are bandwidth-light and every workgroup's thread 0 spins
   int64_t want = (n + 256 * 8 - 1) / (256 * 8);
   const int grid = (int)(want < 1 ? 1 : (want > 64 ? 64 : want));
-  hipLaunchKernelGGL(xgmi_push_kernel, dim3(grid), dim3(256), 0, st, P, R, rank, in, n, cap, err);
-  hipLaunchKernelGGL(xgmi_reduce_kernel, dim3(grid), dim3(256), 0, st, P, R, rank, out, n, cap, scale, err);
+  hipLaunchKernelGGL(xgmi_push_kernel, dim3(grid), dim3(256), 0, st, P, R, rank, in, n, cap, err, spin);
+  hipLaunchKernelGGL(xgmi_reduce_kernel, dim3(grid), dim3(256), 0, st, P, R, rank, out, n, cap, scale, err, spin);
 }
 
 }  // namespace hcb

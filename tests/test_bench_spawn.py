@@ -1,0 +1,54 @@
+"""bench.py --gpus N scaling entry: without a rank environment the process only launches N
+worker children (one per GPU) and fails loudly when the node cannot give it N GPUs
+(the reference's ``mpirun -np TOTAL_WORKERS``, run-tf-sing-ucx-openmpi.sh:99-109)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT")}
+    e.update(kw)
+    return e
+
+
+def test_gpus4_spawns_four_ranks_with_rank_env():
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--steps", "1", "--warmup", "0"],
+                         env=_env(HCB_BENCH_ONE_DEVICE="1", HCB_BENCH_STUB_WORKER="1"),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    recs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 4
+    assert sorted(int(r["RANK"]) for r in recs) == [0, 1, 2, 3]
+    assert sorted(int(r["LOCAL_RANK"]) for r in recs) == [0, 1, 2, 3]
+    assert {r["WORLD_SIZE"] for r in recs} == {"4"} and {r["LOCAL_WORLD_SIZE"] for r in recs} == {"4"}
+    assert {r["MASTER_ADDR"] for r in recs} == {"127.0.0.1"} and len({r["MASTER_PORT"] for r in recs}) == 1
+    assert {r["HCB_BENCH_SPAWNED"] for r in recs} == {"1"}
+
+
+def test_more_gpus_than_visible_fails_loudly():
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "8"], env=_env(HIP_VISIBLE_DEVICES=""),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0
+    assert "GPU(s) visible" in out.stderr
+    assert '"n_gpus"' not in out.stdout
+
+
+def test_world_size_must_match_gpus():
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2"],
+                         env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 3 and "refusing" in out.stderr
+
+
+def test_spawned_worker_failure_propagates():
+    # no stub: the children find no GPU and exit 2; the parent must exit non-zero too
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                         env=_env(HCB_BENCH_ONE_DEVICE="1", HIP_VISIBLE_DEVICES=""),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0

@@ -101,11 +101,14 @@ def test_cpu_benchmark_end_to_end(tmp_path):
     js = tmp_path / "s.json"
     cmd = [sys.executable, os.path.join(ROOT, "tf_cnn_benchmarks.py"), "--device=cpu", "--model=resnet50",
            "--batch_size=2", "--image_size=32", "--num_batches=3", "--num_warmup_batches=1", "--display_every=1",
-           "--optimizer=momentum", f"--json_summary={js}", f"--train_dir={tmp_path / 'ckpt'}"]
+           "--optimizer=momentum", f"--json_summary={js}", f"--train_dir={tmp_path / 'ckpt'}",
+           "--print_training_accuracy"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    assert "Step\tImg/sec\ttotal_loss" in out.stdout and "total images/sec:" in out.stdout
+    assert "Step\tImg/sec\ttotal_loss\ttop_1_accuracy\ttop_5_accuracy" in out.stdout
+    assert "total images/sec:" in out.stdout
     s = json.loads(js.read_text())
+    assert 0.0 <= s["top_1_accuracy"] <= s["top_5_accuracy"] <= 1.0
     assert s["workers"] == 1 and s["num_batches"] == 3 and s["total_images_per_sec"] > 0
     assert (tmp_path / "ckpt" / "model.ckpt-4.pt").exists()
     # resume continues from the saved step
@@ -159,3 +162,22 @@ def test_cpu_shares_follow_gpu_numa_nodes(tmp_path):
     assert sh[2] == list(range(8, 16)) and sh[3] == list(range(24, 32))
     # unknown topology: contiguous equal shares
     assert cpu_shares(2, list(range(8)), sysfs=str(tmp_path / "none")) == [[0, 1, 2, 3], [4, 5, 6, 7]]
+
+
+def test_flavors_differ_like_the_reference_runners():
+    """IMPI runner: no core pinning, transport debug on, no HOROVOD_MPI_THREADS_DISABLE
+    (run-tf-sing-libfabric-intelmpi.sh:94-105); OpenMPI runner: pinning + threads-disable."""
+    from azure_hc_intel_tf_amd.launch.run_tf_sing import flavor_settings
+
+    u, i = flavor_settings("ucx-openmpi"), flavor_settings("libfabric-intelmpi")
+    assert u["pin"] and not i["pin"]
+    assert u["env"]["HOROVOD_MPI_THREADS_DISABLE"] == "1" and "HOROVOD_MPI_THREADS_DISABLE" in i["unset"]
+    assert i["env"]["NCCL_DEBUG"] == "INFO" and "NCCL_DEBUG" not in u["env"]
+    env = dict(os.environ, DRY_RUN="1", DEVICE="cpu")
+    out = subprocess.run([os.path.join(ROOT, "benchmark-scripts", "run-tf-sing-libfabric-intelmpi.sh"), "1", "1", "32",
+                          "ib"], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "--no_pin" in out.stdout and "NCCL_DEBUG=INFO" in out.stdout
+    out = subprocess.run([os.path.join(ROOT, "benchmark-scripts", "run-tf-sing-ucx-openmpi.sh"), "1", "1", "32",
+                          "ib"], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "--no_pin" not in out.stdout and "HOROVOD_MPI_THREADS_DISABLE=1" in out.stdout

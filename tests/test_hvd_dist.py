@@ -1,4 +1,4 @@
-"""Horovod-compatible API and gradient reducers on CPU with gloo, world_size 2 and 4."""
+"""Horovod-compatible API and gradient reducers on CPU with gloo, world_size 2, 4 and 8."""
 import os
 import socket
 
@@ -66,7 +66,7 @@ def _collectives(hvd):
     assert torch.allclose(ts[0], torch.full((7,), (n - 1) / 2))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_hvd_collectives(world):
     run(world, _collectives)
 
@@ -91,6 +91,54 @@ def _dist_optimizer(hvd):
 
 def test_distributed_optimizer_keeps_replicas_in_sync():
     run(2, _dist_optimizer)
+
+
+def _dist_optimizer_unused_param(hvd):
+    """A parameter that receives no gradient (unused branch) must not leave its bucket
+    unreduced: the others in that bucket still get averaged (Horovod semantics: zeros)."""
+    torch.manual_seed(0)
+    used = torch.nn.Linear(4, 4)
+    unused = torch.nn.Linear(4, 4)
+    hvd.broadcast_parameters(dict(list(used.state_dict().items())), root_rank=0)
+    params = list(used.parameters()) + list(unused.parameters())
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(params, lr=1.0))
+    x = torch.full((2, 4), float(hvd.rank() + 1))
+    opt.zero_grad()
+    used(x).sum().backward()
+    opt.step()
+    w = used.weight.detach().flatten()
+    allw = hvd.allgather(w.view(1, -1))
+    assert torch.allclose(allw[0], allw[-1], atol=1e-6), "replicas diverged: a bucket was never reduced"
+    assert unused.weight.grad is not None and torch.all(unused.weight.grad == 0)
+
+
+def test_distributed_optimizer_reduces_buckets_with_unused_params(monkeypatch):
+    monkeypatch.setenv("HOROVOD_FUSION_THRESHOLD", "4096")  # one bucket holds used + unused params
+    run(2, _dist_optimizer_unused_param)
+
+
+def _engine_training_world8(hvd):
+    """world 8: overlapped, threshold-split range reductions keep every replica identical."""
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.parallel import make_reducer
+    from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+    torch.set_num_threads(1)
+    m = create_model("trivial", image_size=16, device="cpu", seed=300 + hvd.rank())
+    hvd.broadcast_global_variables(m, 0)
+    red = make_reducer("torch", bucket_bytes=64 << 10)
+    img, lab = synthetic_batch(m, 2, seed=hvd.rank())
+    img = (img - 127) / 60
+    t = Trainer(m, 2, constant_lr(0.01), reducer=red, world_size=hvd.size(), force_overlap=True)
+    for _ in range(2):
+        t.step(img, lab)
+    allw = hvd.allgather(m.ps.master.view(1, -1))
+    for r in range(1, hvd.size()):
+        assert torch.allclose(allw[0], allw[r])
+
+
+def test_reducer_training_in_sync_world8():
+    run(8, _engine_training_world8)
 
 
 def _engine_training(hvd):
