@@ -157,3 +157,61 @@ def test_xgmi_one_shot_allreduce_two_processes_one_gpu(world):
             if p.is_alive():
                 p.kill()
     assert all(ok and err == 0 for _, ok, err in res), res
+
+
+def test_fp16_wire_and_threshold_split_one_rank():
+    """IEEE fp16 wire format (Horovod Compression.fp16) through the engine, every range cut
+    into buckets of at most the fusion threshold, and the rank count read back from RCCL."""
+    from azure_hc_intel_tf_amd.parallel.native import NativeReducer
+
+    r = NativeReducer(compression="fp16", bucket_bytes=256 << 10, force=True)
+    assert r.comm.size() == 1
+    g = torch.randn(1_000_003, device="cuda")
+    g0 = g.clone()
+    b0 = r.comm.buckets_issued()
+    r.allreduce_ranges_async_(g, [(0, 600_000), (600_000, 400_003)])
+    r.join()
+    torch.cuda.synchronize()
+    assert torch.equal(g, g0.half().float())
+    issued = r.comm.buckets_issued() - b0
+    assert issued == -(-600_000 // (128 << 10)) + -(-400_003 // (128 << 10))  # 2-byte wire
+    r.close()
+
+
+def test_bucket_pack_unpack_wire_formats():
+    import azure_hc_intel_tf_amd.ops._ext as ext
+
+    hcb = ext.ops()
+    for n in (1, 3, 4, 1027, 262_147):
+        x = torch.randn(n, device="cuda") * 100
+        for dt in (torch.float32, torch.bfloat16, torch.float16):
+            w = torch.empty(n, dtype=dt, device="cuda")
+            hcb.bucket_pack(x, w, 0.5)
+            torch.cuda.synchronize()
+            assert torch.equal(w, (x * 0.5).to(dt)), (n, dt)
+            y = torch.empty(n, device="cuda")
+            hcb.bucket_unpack(w, y, 2.0)
+            torch.cuda.synchronize()
+            assert torch.equal(y, w.float() * 2.0), (n, dt)
+
+
+def test_comm_profile_on_forced_dp_path():
+    """allreduce ms / exposed ms / overlap % of the captured multi-GPU step (1-rank engine)"""
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.parallel.native import NativeReducer
+    from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+    m = create_model("resnet50", image_size=64, device="cuda")
+    img, lab = synthetic_batch(m, 8)
+    red = NativeReducer(force=True, bucket_bytes=4 << 20)
+    t = Trainer(m, 8, constant_lr(0.01), reducer=red, world_size=1, use_graph=True, force_overlap=True)
+    for _ in range(4):
+        t.step(img, lab)
+    prof = t.comm_profile(img, lab, iters=3)
+    assert prof is not None and prof["allreduce_ms"] > 0 and prof["compute_ms"] > 0
+    assert 0.0 <= prof["overlap_pct"] <= 100.0
+    # 102 MB of fp32 gradients in buckets of <= 4 MiB
+    assert prof["buckets_per_step"] >= m.num_params() * 4 // (4 << 20)
+    t1, t5 = t.accuracy(lab)
+    assert 0.0 <= float(t1) <= float(t5) <= 1.0
+    red.close()
