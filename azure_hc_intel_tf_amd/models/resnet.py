@@ -15,7 +15,7 @@ BN: decay 0.9, epsilon 1e-5, scale=True. ResNet-50 v1: 25,559,081 trainable para
 from __future__ import annotations
 
 from ..nn import layers as L
-from ..nn.layers import BNReLU, ConvBN, GlobalAvgPool, Logits, Pool, join_side_streams
+from ..nn.layers import BNReLU, ConvBN, GlobalAvgPool, Logits, Pool, StemS2D, join_side_streams
 from ..ops import functional as Fn
 from .base import CNNModel
 
@@ -77,8 +77,12 @@ class ResNet(CNNModel):
         ps = self.ps
         S = self.image_size
         v15 = self.version == "v1.5"
-        self.stem = ConvBN(ps, "conv0", (S, S, self.image_channels), 64, 7, 7, 2, 2, "SAME_RESNET",
-                           relu=True, need_dx=False, logical_cin=3)
+        if self.device.type == "cuda" and L.STEM_S2D:
+            self.stem = StemS2D(ps, "conv0", (S, S, self.image_channels), 64, relu=True, need_dx=False,
+                                logical_cin=3)
+        else:
+            self.stem = ConvBN(ps, "conv0", (S, S, self.image_channels), 64, 7, 7, 2, 2, "SAME_RESNET",
+                               relu=True, need_dx=False, logical_cin=3)
         self.pool = Pool("mpool0", self.stem.out_shape, 3, 3, 2, 2, "SAME", is_max=True)
         shape = self.pool.out_shape
         self.blocks = []

@@ -235,7 +235,7 @@ class ConvBN(Layer):
         N = x.shape[0]
         P, Q, C = self.out_shape
         z = empty_act((N, P, Q, C), x.device)
-        Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data, stats_R=STAT_R)
+        x = self._conv_fwd_stats(x, z)
         y = empty_act((N,) + tuple(pool.out_shape), x.device)
         amax = torch.empty((N,) + tuple(pool.out_shape), dtype=torch.uint8, device=x.device)
         saved = Fn.bn_relu_maxpool_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
@@ -244,6 +244,15 @@ class ConvBN(Layer):
         self._saved = (x, z, None, saved, False)
         pool._saved = (z, y, amax)  # the argmax backward reads only shapes from x / y
         return y
+
+    def _conv_fwd_stats(self, x, z):
+        """GPU conv with the BN statistics in its epilogue; returns the tensor the weight
+        gradient will read (the conv's GEMM input)."""
+        Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data, stats_R=STAT_R)
+        return x
+
+    def _wgrad(self, dz, x):
+        Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(dz.shape[-1], -1) if dz.is_cuda else self.w.grad)
 
     # ------------------------------------------------------------------ backward
     def bwd_fuse_request(self) -> Optional[Fn.BNBwdFuse]:
@@ -302,12 +311,12 @@ class ConvBN(Layer):
                 gres = dz
         if dz.is_cuda and WGRAD_STREAM:
             with torch.cuda.stream(wgrad_stream(dev)):
-                Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(C, -1))
+                self._wgrad(dz, x)
             # the allocator must not hand dz / x to the main stream before the wgrad has read them
             dz.record_stream(_SIDE[dev.index or 0])
             x.record_stream(_SIDE[dev.index or 0])
         else:
-            Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(C, -1) if dz.is_cuda else self.w.grad)
+            self._wgrad(dz, x)
         if self.need_dx:
             H, W, Cin = self.in_shape
             if dx is None:
@@ -324,6 +333,90 @@ class ConvBN(Layer):
     def clear(self):
         self._saved = None
         self._pre_reduced = False
+
+
+# GPU ResNet stem as a space-to-depth 4x4/1 GEMM (HCB_STEM_S2D=0: the direct padded 7x7/2 form)
+STEM_S2D = os.environ.get("HCB_STEM_S2D", "1") != "0"
+
+
+class StemS2D(ConvBN):
+    """The 7x7/2 'SAME_RESNET' stem conv (3 input channels, stored padded) computed on the GPU as
+    a stride-1 4x4 conv over the 2x2 space-to-depth fold of the image (csrc/kernels/stem.hip):
+    K = 256 instead of the padded direct form's 448. The fp32 master weight, its gradient, the
+    BN and the CPU path are exactly those of the 7x7 layer; only the GEMM operands are folded."""
+
+    PAD = 4  # X'(P) = x(2P + a - 4): the 3-pixel SAME_RESNET pad plus the fold's half step
+
+    def __init__(self, ps: ParamStore, name: str, in_shape, cout: int, **kw):
+        super().__init__(ps, name, in_shape, cout, 7, 7, 2, 2, "SAME_RESNET", **kw)
+        assert self.spec.pt == 3 and self.spec.pl == 3 and not self.need_dx
+        P, Q, _ = self.out_shape
+        self.fold_shape = (P + 3, Q + 3, 16)
+        self.fold_spec = ConvSpec(cin=16, cin_pad=16, cout=cout, kh=4, kw=4, sh=1, sw=1, pt=0, pl=0, pb=0, pr=0)
+        self._wfold = None
+        self._dwfold = None
+
+    def _folded_weight(self, dev):
+        if self._wfold is None or self._wfold.device != dev:
+            self._wfold = torch.empty((self.spec.cout, 256), dtype=torch.bfloat16, device=dev)
+        from ..ops import _ext
+
+        _ext.ops().stem_wfold(self.w.data, self._wfold)
+        return self._wfold
+
+    def fold_input(self, x):
+        from ..ops import _ext
+
+        xf = empty_act((x.shape[0],) + self.fold_shape, x.device)
+        _ext.ops().stem_s2d(x, xf, self.PAD)
+        return xf
+
+    def _conv_fwd_stats(self, x, z):
+        xf = self.fold_input(x)
+        Fn.conv_forward(xf, self.fold_spec, self._folded_weight(x.device), self.w.data, z, stats=self.acc_f.data,
+                        stats_R=STAT_R)
+        return xf
+
+    def _wgrad(self, dz, x):
+        if not dz.is_cuda:
+            return super()._wgrad(dz, x)
+        from ..ops import _ext
+
+        if x.shape[1:] != self.fold_shape:  # direct-form training path (forward() not forward_maxpool)
+            x = self.fold_input(x)
+        dwf = torch.zeros((self.spec.cout, 256), dtype=torch.float32, device=dz.device)
+        Fn.conv_wgrad(dz, x, self.fold_spec, dwf)
+        _ext.ops().stem_wgrad_unfold(dwf, self.w.grad)
+
+    def forward(self, x, out=None, residual=None):
+        if not x.is_cuda:
+            return super().forward(x, out, residual)
+        N = x.shape[0]
+        P, Q, C = self.out_shape
+        z = empty_act((N, P, Q, C), x.device)
+        y = out if out is not None else empty_act((N, P, Q, C), x.device)
+        if not self.training:
+            xf = self.fold_input(x)
+            Fn.conv_forward(xf, self.fold_spec, self._folded_weight(x.device), self.w.data, z)
+            Fn.bn_inference(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.eps, y,
+                            self.relu, residual=residual)
+            self._saved = None
+            return y
+        xf = self._conv_fwd_stats(x, z)
+        saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
+                                  self.eps, y, self.relu, self.acc_f.data, STAT_R, self.sv_mean.data,
+                                  self.sv_invstd.data, residual=residual)
+        self._saved = (xf, z, y, saved, residual is not None)
+        return y
+
+    def tune_view(self):
+        """The GEMM problem the autotuner must time for this layer (the folded one)."""
+        from types import SimpleNamespace
+
+        dev = self.w.data.device
+        return SimpleNamespace(spec=self.fold_spec, in_shape=self.fold_shape, out_shape=self.out_shape,
+                               need_dx=False, pack=SimpleNamespace(pack=self._folded_weight(dev), tr=None),
+                               name=self.name)
 
 
 class Pool(Layer):

@@ -22,7 +22,7 @@ from . import functional as Fn
 _DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned")
 DEFAULT_CACHE = os.path.join(_DIR, "mi355x.json")
 # bump whenever the kernel config set changes: entries of another version are re-tuned
-CACHE_VERSION = 4
+CACHE_VERSION = 5  # 5: keys carry the filter tap count
 
 
 def _key_str(k) -> str:
@@ -88,16 +88,17 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     out = []
     M = N * P * Q
     geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
-    keys = [Fn.fwd_key(M, Cout, spec.K), Fn.wgrad_key(Cout, spec.K, M)]
+    taps = spec.kh * spec.kw
+    keys = [Fn.fwd_key(M, Cout, spec.K, taps), Fn.wgrad_key(Cout, spec.K, M, taps)]
     if layer.need_dx:
-        keys.append(Fn.fwd_key(geo[0], Cin, geo[1]))
-        keys.append(Fn.dgb_key(geo[0], Cin, geo[1]))
+        keys.append(Fn.fwd_key(geo[0], Cin, geo[1], taps))
+        keys.append(Fn.dgb_key(geo[0], Cin, geo[1], taps))
     if all(k in Fn._tuned for k in keys):
         return out
     x = _bf((N, H, W, Cin), dev)
     dz = _bf((N, P, Q, Cout), dev)
     # forward
-    k = Fn.fwd_key(M, Cout, spec.K)
+    k = Fn.fwd_key(M, Cout, spec.K, taps)
     if k not in Fn._tuned:
         y = torch.empty((N, P, Q, Cout), dtype=torch.bfloat16, device=dev)
         best = None
@@ -114,7 +115,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     # data gradient
     if layer.need_dx:
         dx = torch.zeros((N, H, W, Cin), dtype=torch.bfloat16, device=dev)
-        k = Fn.fwd_key(geo[0], Cin, geo[1])
+        k = Fn.fwd_key(geo[0], Cin, geo[1], taps)
         if k not in Fn._tuned:
             best = None
             for cfg in Fn.fwd_candidates(Cin):
@@ -127,7 +128,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
             out.append((k, best))
         # the same GEMM with the fused BN-backward epilogue (ReLU mask from y, residual
         # beta-accumulate: the heaviest epilogue), used when a BN layer consumes this dx
-        k = Fn.dgb_key(geo[0], Cin, geo[1])
+        k = Fn.dgb_key(geo[0], Cin, geo[1], taps)
         if k not in Fn._tuned:
             z = _bf((N, H, W, Cin), dev)
             yv = _bf((N, H, W, Cin), dev)
@@ -144,7 +145,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
             Fn._tuned[k] = best[1]
             out.append((k, best))
     # weight gradient
-    k = Fn.wgrad_key(Cout, spec.K, M)
+    k = Fn.wgrad_key(Cout, spec.K, M, taps)
     if k not in Fn._tuned:
         dw = torch.zeros((Cout, spec.K), dtype=torch.float32, device=dev)
         best = None
@@ -168,7 +169,7 @@ def tune_model(model, batch: int, verbose=False, cache: str = DEFAULT_CACHE, sav
     n = 0
     for l in model.all_layers():
         if isinstance(l, ConvBN) and l.bn:
-            n += len(tune_conv_layer(l, batch, dev, verbose))
+            n += len(tune_conv_layer(l.tune_view() if hasattr(l, "tune_view") else l, batch, dev, verbose))
     torch.cuda.synchronize()
     if save and n and cache:
         try:

@@ -100,18 +100,20 @@ N_CU = 256
 _tuned: dict = {}
 
 
-def fwd_key(M: int, N: int, K: int):
-    return ("fwd", M, N, K)
+# Tuning keys carry the filter tap count: GEMMs of equal (M, N, K) but different geometry
+# (a 1x1 over K channels vs a 4x4 over K/16) have different im2col loaders and best tiles.
+def fwd_key(M: int, N: int, K: int, taps: int = 1):
+    return ("fwd", M, N, K, taps)
 
 
-def dgb_key(M: int, N: int, K: int):
+def dgb_key(M: int, N: int, K: int, taps: int = 1):
     """Data-grad GEMM with the fused BN-backward epilogue (its own tuning entry: the epilogue
     reads z / y / the beta source, which moves the best tile away from the plain GEMM's)."""
-    return ("dgb", M, N, K)
+    return ("dgb", M, N, K, taps)
 
 
-def wgrad_key(Nout: int, K: int, M: int):
-    return ("wgrad", Nout, K, M)
+def wgrad_key(Nout: int, K: int, M: int, taps: int = 1):
+    return ("wgrad", Nout, K, M, taps)
 
 
 def fwd_candidates(N: int):
@@ -167,16 +169,16 @@ def splitk_candidates(cfg: int, M: int, N: int, K: int):
     return out
 
 
-def conv_plan(M: int, N: int, K: int):
+def conv_plan(M: int, N: int, K: int, taps: int = 1):
     """(cfg, splits) for C[M,N] (+K)."""
-    c = conv_cfg(M, N, K)
+    c = conv_cfg(M, N, K, taps)
     return (c[0], c[1]) if isinstance(c, (tuple, list)) else (c, 1)
 
 
-def conv_cfg(M: int, N: int, K: int):
+def conv_cfg(M: int, N: int, K: int, taps: int = 1):
     """Block tile for C[M,N] (+K): the autotuned choice if known (an int cfg or a [cfg, splits]
     pair), else the biggest tile that still gives >= 2 workgroups per CU."""
-    key = fwd_key(M, N, K)
+    key = fwd_key(M, N, K, taps)
     if key in _tuned:
         return _tuned[key]
     cands = [c for c in fwd_candidates(N) if c < 4]
@@ -187,9 +189,9 @@ def conv_cfg(M: int, N: int, K: int):
     return cands[-1]
 
 
-def wgrad_cfg(Nout: int, K: int, M: int):
+def wgrad_cfg(Nout: int, K: int, M: int, taps: int = 1):
     """(tile cfg, split-K) for dW[Nout, K] reduced over M pixels."""
-    key = wgrad_key(Nout, K, M)
+    key = wgrad_key(Nout, K, M, taps)
     if key in _tuned:
         return tuple(_tuned[key])
     c = 0 if Nout >= 128 and K >= 128 else (1 if K >= 128 else 2)
@@ -223,7 +225,7 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
     P, Q = spec.out_hw(H, W)
     if x.is_cuda:
         M = N * P * Q
-        cfg, splits = _plan(cfg, M, spec.cout, spec.K, x.device)
+        cfg, splits = _plan(cfg, M, spec.cout, spec.K, x.device, spec.kh * spec.kw)
         out_f32 = out.dtype == torch.float32
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
                 spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1,
@@ -246,10 +248,10 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
     return out
 
 
-def _plan(cfg, M, N, K, device):
+def _plan(cfg, M, N, K, device, taps: int = 1):
     """Normalise a cfg argument (None = tuned / heuristic, int, or (cfg, splits))."""
     if cfg is None:
-        cfg, splits = conv_plan(M, N, K)
+        cfg, splits = conv_plan(M, N, K, taps)
     elif isinstance(cfg, (tuple, list)):
         cfg, splits = cfg
     else:
@@ -272,7 +274,7 @@ def conv_stats_slab(x_shape, spec: ConvSpec, device, cfg=None):
     P, Q = spec.out_hw(H, W)
     M = N * P * Q
     if cfg is None:
-        cfg = conv_plan(M, spec.cout, spec.K)[0]
+        cfg = conv_plan(M, spec.cout, spec.K, spec.kh * spec.kw)[0]
     bm = _CONV_TILES[cfg][0]
     T = math.ceil(M / bm)
     return torch.empty(T * 2 * spec.cout, dtype=torch.float32, device=device), T, cfg
@@ -340,9 +342,10 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
             geom = [N, P, Q, Cdz, ld(dz), H, W, spec.kh, spec.kw, 1, 1, pt, pl, spec.dh, spec.dw,
                     spec.sh, spec.sw, spec.cin_pad, K, Kpad, ld(dx), 0, H, W, 1, 1,
                     1 if accumulate else 0, 0]
+        taps = spec.kh * spec.kw
         if cfg is None and bnb is not None:
-            cfg = _tuned.get(dgb_key(M, spec.cin_pad, K))
-        cfg, splits = _plan(cfg, M, spec.cin_pad, K, dz.device)
+            cfg = _tuned.get(dgb_key(M, spec.cin_pad, K, taps))
+        cfg, splits = _plan(cfg, M, spec.cin_pad, K, dz.device, taps)
         geom = geom + [0, 0, splits]
         if bnb is not None:
             _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
@@ -373,7 +376,7 @@ def conv_wgrad(dz, x, spec: ConvSpec, dw, cfg=None):
     _, P, Q, _ = dz.shape
     if dz.is_cuda:
         M = N * P * Q
-        cfg, splits = cfg if cfg is not None else wgrad_cfg(spec.cout, spec.K, M)
+        cfg, splits = cfg if cfg is not None else wgrad_cfg(spec.cout, spec.K, M, spec.kh * spec.kw)
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
                 spec.dh, spec.dw, spec.cout, ld(dz)]
         _ext.ops().conv_wgrad(dz, x, dw, geom, cfg, splits)

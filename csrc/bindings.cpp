@@ -738,6 +738,44 @@ void bucket_unpack(const Tensor& src, const Tensor& dst, double scale) {
                             pack_mode(src, "bucket_unpack"), cur_stream());
 }
 
+// ---------------------------------------------------------------- space-to-depth stem
+void stem_s2d(const Tensor& x, const Tensor& out, int64_t pad) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.dim() == 4 && out.dim() == 4 && x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "hcb.stem_s2d: bf16 NHWC tensors");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.size(3) >= 4 && x.size(3) % 4 == 0 && out.size(3) == 16 &&
+                  out.size(0) == x.size(0),
+              "hcb.stem_s2d: x [N][H][W][>=4, multiple of 4] -> out [N][Hs][Ws][16]");
+  const int64_t H = x.size(1), W = x.size(2), Hs = out.size(1), Ws = out.size(2);
+  TORCH_CHECK(2 * Hs - 1 - pad < H + 8 && 2 * Ws - 1 - pad < W + 8 && x.numel() < (1ll << 31),
+              "hcb.stem_s2d: folded extent");
+  hcb::launch_stem_s2d(reinterpret_cast<const uint16_t*>(x.data_ptr()), (int)x.size(0), (int)H, (int)W,
+                       (int)x.size(3), reinterpret_cast<uint16_t*>(out.data_ptr()), (int)Hs, (int)Ws, (int)pad,
+                       cur_stream());
+}
+
+void stem_wfold(const Tensor& w, const Tensor& wp) {
+  check_f32(w, "w");
+  check_cuda(wp, "wp");
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == 7 && w.size(2) == 7 && w.size(3) >= 3 && w.is_contiguous(),
+              "hcb.stem_wfold: w [cout][7][7][>=3] fp32");
+  TORCH_CHECK(wp.scalar_type() == at::kBFloat16 && wp.is_contiguous() && wp.numel() == w.size(0) * 256,
+              "hcb.stem_wfold: wp bf16 [cout][256]");
+  hcb::launch_stem_wfold(w.data_ptr<float>(), (int)w.size(0), (int)w.size(3),
+                         reinterpret_cast<uint16_t*>(wp.data_ptr()), cur_stream());
+}
+
+void stem_wgrad_unfold(const Tensor& dwp, const Tensor& dw) {
+  check_f32(dwp, "dwp");
+  check_f32(dw, "dw");
+  TORCH_CHECK(dw.dim() == 4 && dw.size(1) == 7 && dw.size(2) == 7 && dw.size(3) >= 3 && dw.is_contiguous() &&
+                  dwp.is_contiguous() && dwp.numel() == dw.size(0) * 256,
+              "hcb.stem_wgrad_unfold: dwp [cout][256] -> dw [cout][7][7][>=3]");
+  hcb::launch_stem_wgrad_unfold(dwp.data_ptr<float>(), (int)dw.size(0), (int)dw.size(3), dw.data_ptr<float>(),
+                                cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(hcb, m) {
@@ -781,6 +819,9 @@ TORCH_LIBRARY(hcb, m) {
   m.def("synth_labels(Tensor(a!) out, int ncls, int seed) -> ()");
   m.def("bucket_pack(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bucket_unpack(Tensor src, Tensor(a!) dst, float scale) -> ()");
+  m.def("stem_s2d(Tensor x, Tensor(a!) out, int pad) -> ()");
+  m.def("stem_wfold(Tensor w, Tensor(a!) wp) -> ()");
+  m.def("stem_wgrad_unfold(Tensor dwp, Tensor(a!) dw) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
@@ -820,4 +861,7 @@ TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("synth_labels", synth_labels);
   m.impl("bucket_pack", bucket_pack);
   m.impl("bucket_unpack", bucket_unpack);
+  m.impl("stem_s2d", stem_s2d);
+  m.impl("stem_wfold", stem_wfold);
+  m.impl("stem_wgrad_unfold", stem_wgrad_unfold);
 }

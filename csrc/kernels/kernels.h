@@ -195,6 +195,12 @@ void launch_synth_labels(int64_t* out, int n, int ncls, uint64_t seed, hipStream
 void launch_preprocess_images(const uint8_t* src, const int64_t* desc, int B, void* out, int S, int Cpad,
                               const float* scale, const float* bias, hipStream_t st);
 
+// ---------------------------------------------------------------- space-to-depth stem (stem.hip)
+void launch_stem_s2d(const uint16_t* x, int N, int H, int W, int ldx, uint16_t* out, int Hs, int Ws, int pad,
+                     hipStream_t st);
+void launch_stem_wfold(const float* w, int cout, int cs, uint16_t* wp, hipStream_t st);
+void launch_stem_wgrad_unfold(const float* dwp, int cout, int cs, float* dw, hipStream_t st);
+
 // ---------------------------------------------------------------- gradient buckets
 // One-shot xGMI allreduce (xgmi.hip): bases = every rank's IPC-mapped staging region.
 int xgmi_max_ranks();

@@ -1,0 +1,72 @@
+"""Space-to-depth ResNet stem (csrc/kernels/stem.hip + nn/layers.StemS2D) against the plain fp32
+7x7/2 convolution: forward output, folded-weight consistency and the weight gradient mapped
+back into the 7x7 master layout."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _stem(size):
+    from azure_hc_intel_tf_amd.nn.layers import StemS2D
+    from azure_hc_intel_tf_amd.nn.params import ParamStore
+
+    ps = ParamStore(seed=3)
+    st = StemS2D(ps, "conv0", (size, size, 8), 64, relu=True, need_dx=False, logical_cin=3)
+    ps.finalize(torch.device("cuda"))
+    return st, ps
+
+
+@pytest.mark.parametrize("size", [224, 64, 30])
+def test_s2d_forward_matches_direct_conv(size):
+    import azure_hc_intel_tf_amd.ops.functional as Fn
+
+    st, ps = _stem(size)
+    torch.manual_seed(0)
+    x = torch.zeros(4, size, size, 8, device="cuda")
+    x[..., :3] = torch.randn(4, size, size, 3, device="cuda")
+    x = x.bfloat16()
+    P, Q, C = st.out_shape
+    z = torch.empty(4, P, Q, C, device="cuda", dtype=torch.bfloat16)
+    xf = st.fold_input(x)
+    Fn.conv_forward(xf, st.fold_spec, st._folded_weight(x.device), st.w.data, z)
+    w = st.w.data[..., :3].permute(0, 3, 1, 2).float().cpu()
+    ref = F.conv2d(x[..., :3].permute(0, 3, 1, 2).float().cpu(), w.bfloat16().float(), stride=2, padding=3)
+    got = z.float().permute(0, 3, 1, 2).cpu()
+    assert got.shape == ref.shape
+    err = (got - ref).abs().max() / ref.abs().max()
+    assert err < 1e-2, float(err)
+
+
+def test_s2d_weight_gradient_maps_back_to_7x7():
+    st, ps = _stem(64)
+    torch.manual_seed(1)
+    x = torch.zeros(2, 64, 64, 8, device="cuda")
+    x[..., :3] = torch.randn(2, 64, 64, 3, device="cuda")
+    x = x.bfloat16()
+    P, Q, C = st.out_shape
+    dz = torch.randn(2, P, Q, C, device="cuda").bfloat16()
+    st.w.grad.zero_()
+    st._wgrad(dz, st.fold_input(x))
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(x[..., :3].permute(0, 3, 1, 2).float().cpu(), (64, 3, 7, 7),
+                                      dz.permute(0, 3, 1, 2).float().cpu(), stride=2, padding=3)
+    got = st.w.grad[..., :3].permute(0, 3, 1, 2).cpu()
+    err = (got - ref).abs().max() / ref.abs().max()
+    assert err < 1e-2, float(err)
+    assert torch.all(st.w.grad[..., 3:] == 0), "padded input channels must get no gradient"
+
+
+def test_resnet_uses_s2d_stem_and_trains():
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.nn.layers import StemS2D
+    from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+    torch.manual_seed(0)
+    m = create_model("resnet50", image_size=96, device="cuda")
+    assert isinstance(m.stem, StemS2D)
+    img, lab = synthetic_batch(m, 16)
+    t = Trainer(m, 16, constant_lr(0.02), use_graph=True, graph_warmup=2)
+    losses = [float(t.step(img, lab)) for _ in range(16)]
+    assert all(l == l for l in losses) and min(losses[-3:]) < 0.8 * losses[2], losses

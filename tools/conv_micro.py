@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     dev = torch.device("cuda")
+    from azure_hc_intel_tf_amd.ops import autotune
+
+    autotune.load_cache()  # --cfg omitted: the autotuned config of this shape
     m = create_model(a.model, device=dev)
     m.ps.repack()
     layer = next(l for l in m.all_layers() if isinstance(l, ConvBN) and l.name == a.layer)
