@@ -98,13 +98,20 @@ class BenchmarkCNN:
         from ..models import create_model
 
         kw = {"device": self.device, "seed": p.tf_random_seed}
+        if self.on_gpu:
+            # tf_cnn_benchmarks trains fp32 unless --use_fp16 (the reference runs fp32,
+            # run-tf-sing-ucx-openmpi.sh:62-81); on MI355X the default is the bf16 HIP-kernel path
+            self.compute_dtype = p.compute_dtype or (p.half_dtype if p.use_fp16 else "bf16")
+            kw["compute_dtype"] = self.compute_dtype
+        else:
+            self.compute_dtype = "fp32"
         if p.image_size:
             kw["image_size"] = p.image_size
         self.model = create_model(p.model, **kw)
         if p.num_epochs:
             self.num_batches = int(math.ceil(p.num_epochs * 1281167 / (self.batch_size * self.size)))
         self.step_offset = 0
-        if self.on_gpu and p.autotune:
+        if self.on_gpu and p.autotune and self.model.native:
             # per-shape kernel configs (cached in tuned/mi355x.json; new shapes timed once here)
             from ..ops import autotune
 
@@ -145,9 +152,8 @@ class BenchmarkCNN:
                                weight_decay=p.weight_decay, reducer=reducer, world_size=self.size,
                                use_graph=bool(p.use_hip_graph) and self.on_gpu and p.horovod_device != "cpu",
                                forward_only=bool(p.forward_only),
-                               # --use_fp16: the GPU's 16-bit compute type is bf16 (same MFMA rate
-                               # as fp16, fp32 exponent range); the loss-scaling semantics of the
-                               # reference flags are kept (static scale or automatic scaling)
+                               # --use_fp16: loss scaling as in the reference flags (static scale or
+                               # automatic scaling), whichever 16-bit type computes
                                loss_scale=p.fp16_loss_scale if p.use_fp16 else None,
                                dynamic_loss_scale=bool(p.use_fp16 and p.fp16_enable_auto_loss_scale),
                                loss_scale_interval=p.fp16_inc_loss_scale_every_n)
@@ -172,6 +178,8 @@ class BenchmarkCNN:
         log_fn(f"Devices:     {dev}")
         log_fn(f"NUMA bind:   False")
         log_fn(f"Data format: {p.data_format} (logical; NHWC kernels)")
+        log_fn(f"Precision:   {self.compute_dtype}" + (" (HIP kernels)" if self.model.native else
+                                                       " (PyTorch reference-precision path)" if self.on_gpu else ""))
         log_fn(f"Optimizer:   {p.optimizer}")
         log_fn(f"Variables:   {p.variable_update}")
         log_fn(f"Workers:     {self.size} (one process per {'MI355X' if self.on_gpu else 'CPU worker'})")
@@ -319,7 +327,7 @@ class BenchmarkCNN:
             "step_time_ms": {"mean": 1000 * float(np.mean(step_times)) if step_times else None,
                              "p50": 1000 * float(np.percentile(step_times, 50)) if step_times else None,
                              "p90": 1000 * float(np.percentile(step_times, 90)) if step_times else None},
-            "dtype": "bf16" if self.on_gpu else "fp32", "data": "imagenet-tfrecord" if loader else "synthetic",
+            "dtype": self.compute_dtype, "data": "imagenet-tfrecord" if loader else "synthetic",
             "input_decode_s": loader.decode_s if loader else None,
             "variable_update": p.variable_update, "comm_engine": p.comm_engine if self.size > 1 else None,
             "gradient_compression": p.gradient_compression, "hip_graph": self.trainer.use_graph,

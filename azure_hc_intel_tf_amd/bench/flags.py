@@ -67,7 +67,12 @@ FLAGS: List[Flag] = [
     Flag("num_decode_threads", None, int, "JPEG decode threads per worker (real data)"),
     # --- tf_cnn_benchmarks flags used by the BASELINE configs / common runs
     Flag("num_gpus", 1, int, "GPUs per process (horovod: 1)"),
-    Flag("use_fp16", False, parse_bool, "fp16 compute (bf16 is the default GPU compute type)"),
+    Flag("use_fp16", False, parse_bool, "16-bit compute with loss scaling: IEEE fp16 (--half_dtype=fp16, the "
+         "PyTorch reference-precision path) or bf16 (--half_dtype=bf16, the HIP kernels)"),
+    Flag("half_dtype", "fp16", str, "the 16-bit type --use_fp16 selects", choices=["fp16", "bf16"]),
+    Flag("compute_dtype", None, str, "activation / GEMM precision on the GPU: bf16 (HIP kernels, default) | "
+         "fp32 (the reference's precision) | fp16; overrides --use_fp16's choice",
+         choices=["bf16", "fp32", "fp16"]),
     Flag("fp16_loss_scale", 128.0, float, "static loss scale for --use_fp16"),
     Flag("fp16_enable_auto_loss_scale", False, parse_bool, "dynamic loss scaling for --use_fp16"),
     Flag("fp16_inc_loss_scale_every_n", 1000, int, "double the auto loss scale after N clean steps"),

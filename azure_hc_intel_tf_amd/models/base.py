@@ -11,7 +11,8 @@ from ..nn.params import ParamStore
 
 
 # activation / GEMM-operand precisions the GPU path implements (the CPU path is fp32/fp64)
-GPU_COMPUTE_DTYPES = ("bf16",)
+GPU_COMPUTE_DTYPES = ("bf16", "fp32", "fp16")
+TORCH_DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}
 
 
 def check_compute_dtype(compute_dtype, device) -> str:
@@ -46,14 +47,18 @@ class CNNModel:
         self.compute_dtype = check_compute_dtype(compute_dtype, device)
         self.image_size = image_size or self.default_image_size
         self.device = torch.device(device)
+        # native: the hand-written bf16 HIP kernels; otherwise (CPU, or a GPU in the fp32 /
+        # IEEE-fp16 reference-precision mode) the PyTorch path of ops/functional.py
+        self.native = self.device.type == "cuda" and self.compute_dtype == "bf16"
         if image_channels is None:
-            image_channels = 8 if self.device.type == "cuda" else 3
-        assert image_channels in (3, 8) and (self.device.type != "cuda" or image_channels == 8)
+            image_channels = 8 if self.native else 3
+        assert image_channels in (3, 8) and (not self.native or image_channels == 8)
         self.image_channels = image_channels
+        self.activate()
         self.ps = ParamStore(seed=seed)
         self.layers: List = []
         self.build()
-        self.ps.finalize(self.device)
+        self.ps.finalize(self.device, pack=self.native)
 
     # -- to implement
     def build(self):
@@ -101,9 +106,18 @@ class CNNModel:
         join_side_streams()
         yield seg + list(tail), True
 
+    def activate(self) -> None:
+        """Make this model's activation dtype current for the layer helpers (GPU models of
+        different compute dtypes can coexist in one process)."""
+        if self.device.type == "cuda":
+            from ..nn.layers import set_gpu_compute_dtype
+
+            set_gpu_compute_dtype(TORCH_DTYPES[self.compute_dtype])
+
     # -- helpers
     @property
     def act_dtype(self):
+        self.activate()
         return act_dtype(self.device)
 
     def input_shape(self, batch: int):

@@ -77,7 +77,7 @@ class ResNet(CNNModel):
         ps = self.ps
         S = self.image_size
         v15 = self.version == "v1.5"
-        if self.device.type == "cuda" and L.STEM_S2D:
+        if self.native and L.STEM_S2D:
             self.stem = StemS2D(ps, "conv0", (S, S, self.image_channels), 64, relu=True, need_dx=False,
                                 logical_cin=3)
         else:
@@ -99,7 +99,7 @@ class ResNet(CNNModel):
         self.layers = [self.stem, self.pool] + [l for b in self.blocks for l in b.layers()] + [self.gap, self.fc]
 
     def _stem_pool(self, images):
-        if images.is_cuda and L.FUSE_STEM_POOL and self.stem.training:
+        if Fn.native(images) and L.FUSE_STEM_POOL and self.stem.training:
             return self.stem.forward_maxpool(images, self.pool)
         return self.pool.forward(self.stem.forward(images))
 

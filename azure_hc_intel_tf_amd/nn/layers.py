@@ -26,10 +26,20 @@ from ..ops.functional import ConvSpec, same_pads
 from .params import ParamStore
 
 
+_GPU_ACT_DTYPE = [torch.bfloat16]
+
+
+def set_gpu_compute_dtype(dt: torch.dtype) -> None:
+    """Activation dtype of GPU models built / stepped from now on: bf16 (the hand-written HIP
+    kernels) or fp32 / fp16 (the reference-precision PyTorch path, --compute_dtype)."""
+    _GPU_ACT_DTYPE[0] = dt
+
+
 def act_dtype(device) -> torch.dtype:
-    """bf16 activations on the GPU; fp32 on the CPU (HCB_CPU_DTYPE=float64 for exact tests)."""
+    """bf16 activations on the GPU (or the reference-precision dtype); fp32 on the CPU
+    (HCB_CPU_DTYPE=float64 for exact tests)."""
     if torch.device(device).type == "cuda":
-        return torch.bfloat16
+        return _GPU_ACT_DTYPE[0]
     return torch.float64 if os.environ.get("HCB_CPU_DTYPE") == "float64" else torch.float32
 
 
@@ -192,7 +202,7 @@ class ConvBN(Layer):
         if self.bn and not self.training:
             z = empty_act((N, P, Q, C), dev)
             y = out if out is not None else empty_act((N, P, Q, C), dev)
-            Fn.conv_forward(x, self.spec, self.pack.pack if x.is_cuda else None, self.w.data, z)
+            Fn.conv_forward(x, self.spec, self.pack.pack if Fn.native(x) else None, self.w.data, z)
             Fn.bn_inference(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.eps, y,
                             self.relu, residual=residual)
             self._saved = None
@@ -200,7 +210,7 @@ class ConvBN(Layer):
         if self.bn:
             z = empty_act((N, P, Q, C), dev)
             y = out if out is not None else empty_act((N, P, Q, C), dev)
-            if x.is_cuda:
+            if Fn.native(x):
                 # conv epilogue accumulates the batch statistics; the apply kernel finalizes them
                 Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data,
                                 stats_R=STAT_R)
@@ -221,7 +231,7 @@ class ConvBN(Layer):
             return y
         assert residual is None or not self.relu, "conv without BN: residual add only without ReLU"
         y = out if out is not None else empty_act((N, P, Q, C), dev)
-        Fn.conv_forward(x, self.spec, self.pack.pack if x.is_cuda else None, self.w.data, y,
+        Fn.conv_forward(x, self.spec, self.pack.pack if Fn.native(x) else None, self.w.data, y,
                         bias=self.bias.data if self.bias is not None else None, relu=self.relu, residual=residual)
         self._saved = (x, None, y, None, False)
         return y
@@ -231,7 +241,7 @@ class ConvBN(Layer):
         launches: the conv (BN statistics in its epilogue) and one BN+ReLU+pool kernel. The
         full-size BN+ReLU activation is never written; ``pool`` keeps the argmax for its
         backward and this layer recomputes the ReLU mask from z."""
-        assert self.bn and self.relu and x.is_cuda and pool.is_max and self.training
+        assert self.bn and self.relu and Fn.native(x) and pool.is_max and self.training
         N = x.shape[0]
         P, Q, C = self.out_shape
         z = empty_act((N, P, Q, C), x.device)
@@ -252,7 +262,7 @@ class ConvBN(Layer):
         return x
 
     def _wgrad(self, dz, x):
-        Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(dz.shape[-1], -1) if dz.is_cuda else self.w.grad)
+        Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(dz.shape[-1], -1) if Fn.native(dz) else self.w.grad)
 
     # ------------------------------------------------------------------ backward
     def bwd_fuse_request(self) -> Optional[Fn.BNBwdFuse]:
@@ -279,7 +289,7 @@ class ConvBN(Layer):
             # dy is already g = dy * mask and (GPU) acc_b holds sum(g), sum(g*xhat)
             self._pre_reduced = False
             dz = empty_act((N, P, Q, C), dev)
-            if dy.is_cuda:
+            if Fn.native(dy):
                 Fn.bn_backward_acc(dy, None, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
                                    self.beta.grad, dz, self.acc_b.data, STAT_R, None, pre_reduced=True)
             else:
@@ -292,7 +302,7 @@ class ConvBN(Layer):
             if want_gres:
                 gres = empty_act((N, P, Q, C), dev)
             relu_mode = (1 if had_res else 2) if self.relu else 0
-            if dy.is_cuda:
+            if Fn.native(dy):
                 Fn.bn_backward_acc(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
                                    self.beta.grad, dz, self.acc_b.data, STAT_R, gres)
             else:
@@ -300,7 +310,7 @@ class ConvBN(Layer):
                                self.beta.grad, dz, gres)
         else:
             if self.relu:
-                if dy.is_cuda and not (dy.is_contiguous() and y.is_contiguous()):
+                if Fn.native(dy) and not (dy.is_contiguous() and y.is_contiguous()):
                     dy, y = dy.contiguous(), y.contiguous()  # concat-window views (GoogLeNet)
                 dz = Fn.relu_backward(dy, y, empty_act((N, P, Q, C), dev))
             else:
@@ -309,7 +319,7 @@ class ConvBN(Layer):
                 Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
                 gres = dz
-        if dz.is_cuda and WGRAD_STREAM:
+        if Fn.native(dz) and WGRAD_STREAM:
             with torch.cuda.stream(wgrad_stream(dev)):
                 self._wgrad(dz, x)
             # the allocator must not hand dz / x to the main stream before the wgrad has read them
@@ -321,7 +331,7 @@ class ConvBN(Layer):
             H, W, Cin = self.in_shape
             if dx is None:
                 strided_1x1 = (self.spec.sh > 1 or self.spec.sw > 1) and self.spec.kh == 1 and self.spec.kw == 1
-                dx = empty_act((N, H, W, Cin), dev, zero=strided_1x1 and dev.type == "cuda")
+                dx = empty_act((N, H, W, Cin), dev, zero=strided_1x1 and Fn.native(dz))
                 accumulate = False
             fuse = dx_bn is not None and self.spec.cout * self.spec.kh * self.spec.kw >= FUSE_BN_BWD_MIN_K
             bnb = dx_bn.bwd_fuse_request() if fuse else None
@@ -367,7 +377,7 @@ class StemS2D(ConvBN):
     def fold_input(self, x):
         from ..ops import _ext
 
-        xf = empty_act((x.shape[0],) + self.fold_shape, x.device)
+        xf = torch.empty((x.shape[0],) + self.fold_shape, dtype=x.dtype, device=x.device)
         _ext.ops().stem_s2d(x, xf, self.PAD)
         return xf
 
@@ -378,7 +388,7 @@ class StemS2D(ConvBN):
         return xf
 
     def _wgrad(self, dz, x):
-        if not dz.is_cuda:
+        if not Fn.native(dz):
             return super()._wgrad(dz, x)
         from ..ops import _ext
 
@@ -389,7 +399,7 @@ class StemS2D(ConvBN):
         _ext.ops().stem_wgrad_unfold(dwf, self.w.grad)
 
     def forward(self, x, out=None, residual=None):
-        if not x.is_cuda:
+        if not Fn.native(x):
             return super().forward(x, out, residual)
         N = x.shape[0]
         P, Q, C = self.out_shape
@@ -439,7 +449,7 @@ class Pool(Layer):
         N = x.shape[0]
         y = out if out is not None else empty_act((N,) + self.out_shape, x.device)
         amax = None
-        if self.is_max and x.is_cuda:
+        if self.is_max and Fn.native(x):
             amax = torch.empty((N,) + self.out_shape, dtype=torch.uint8, device=x.device)
         Fn.pool_forward(x, y, *self.k, *self.s, self.pads, self.is_max, self.incl_pad, argmax=amax)
         self._saved = (x, y, amax)
@@ -527,10 +537,10 @@ class Dropout(Layer):
         if self._step is None or self._step.device != x.device:
             self._step = torch.zeros(1, dtype=torch.int64, device=x.device)
         y = torch.empty_like(x)
-        if x.is_cuda:
+        if Fn.native(x):
             mask = torch.empty((x.numel() + 7) // 8, dtype=torch.uint8, device=x.device)
         else:
-            mask = torch.empty(x.shape, dtype=torch.bool)
+            mask = torch.empty(x.shape, dtype=torch.bool, device=x.device)
         Fn.dropout_forward(x, y, mask, self.keep, self.seed, self._step)
         self._step.add_(1)  # device-side: a replayed graph advances it too
         self._mask = mask
@@ -587,7 +597,7 @@ class Logits(Layer):
         B = x.shape[0]
         x4 = x.view(B, 1, 1, self.cin)
         logits = torch.empty((B, self.ld), dtype=torch.float32, device=x.device)
-        if x.is_cuda:
+        if Fn.native(x):
             Fn.conv_forward(x4, self.spec, self.pack.pack, None, logits.view(B, 1, 1, self.ld)[..., :self.ld],
                             bias=self.b.data)
         else:
@@ -602,7 +612,7 @@ class Logits(Layer):
         x = self._x
         B = x.shape[0]
         Fn.colsum(dlogits, B, self.ncls, self.b.grad)
-        if x.is_cuda:
+        if Fn.native(x):
             hcb = Fn._ext.ops()
             geom = [B, 1, 1, self.cin, self.cin, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, self.ncls, self.ld]
             cfg, splits = 2, 1

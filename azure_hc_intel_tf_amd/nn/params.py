@@ -161,7 +161,9 @@ class ParamStore:
         return lambda t: t.fill_(v)
 
     # ------------------------------------------------------------------ finalize
-    def finalize(self, device, dtype_pack=torch.bfloat16):
+    def finalize(self, device, dtype_pack=torch.bfloat16, pack: bool = True):
+        """Allocate the flat buffers on ``device``; ``pack``: also the bf16 GEMM operands of the
+        HIP kernels (GPU; not in the reference-precision PyTorch mode)."""
         order = [p for p in self.params if p.decay] + [p for p in self.params if not p.decay]
         off = 0
         self.n_decay = 0
@@ -213,7 +215,7 @@ class ParamStore:
             self.pack_max_work = max(self.pack_max_work, work)
         self.pack_total = poff
         self.device = torch.device(device)
-        if self.device.type == "cuda" and self.packs:
+        if self.device.type == "cuda" and self.packs and pack:
             # the pack kernel moves 8-channel vectors (fp32 float4 pairs -> one 16-byte bf16 store)
             for pk in self.packs:
                 assert pk.C % 8 == 0 and pk.Kpad % 64 == 0, f"pack of {pk.param.name}: C % 8, Kpad % 64"

@@ -38,6 +38,13 @@ def _round_up(x: int, m: int) -> int:
 
 
 # --------------------------------------------------------------------------- conv
+def native(t) -> bool:
+    """True when ``t`` goes through the hand-written HIP kernels: a bf16 activation on the GPU.
+    Other GPU tensors (the fp32 / IEEE-fp16 reference-precision mode, --compute_dtype) take
+    the PyTorch path below (MIOpen / rocBLAS), the same code as the CPU path."""
+    return t.is_cuda and t.dtype == torch.bfloat16
+
+
 @dataclass
 class ConvSpec:
     """Geometry of one convolution (NHWC activations, KRSC weights)."""
@@ -223,7 +230,7 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
     statistics: per-tile slab (stats_R=0) or fp32 atomics into stats_R replicas of [2][cout]."""
     N, H, W, _ = x.shape
     P, Q = spec.out_hw(H, W)
-    if x.is_cuda:
+    if native(x):
         M = N * P * Q
         cfg, splits = _plan(cfg, M, spec.cout, spec.K, x.device, spec.kh * spec.kw)
         out_f32 = out.dtype == torch.float32
@@ -262,7 +269,7 @@ def _plan(cfg, M, N, K, device, taps: int = 1):
 
 
 def relu_backward(dy, y, dz):
-    if dy.is_cuda:
+    if native(dy):
         _ext.ops().relu_bwd(dy, y, dz)
         return dz
     dz.copy_(dy * (y > 0).to(dy.dtype))
@@ -324,7 +331,7 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
     result is gated by the consuming BN layer's ReLU mask and its backward sums are fused."""
     N, P, Q, _ = dz.shape
     _, H, W, _ = dx.shape
-    if dz.is_cuda:
+    if native(dz):
         Cdz = spec.cout if spec.cout % 8 == 0 else _round_up(spec.cout, 8)
         K = spec.kh * spec.kw * Cdz
         Kpad = spec.Kpad_t
@@ -374,7 +381,7 @@ def conv_wgrad(dz, x, spec: ConvSpec, dw, cfg=None):
     """dw[cout, kh, kw, cin_pad] (fp32) += sum over pixels of dz (x) im2col(x)."""
     N, H, W, _ = x.shape
     _, P, Q, _ = dz.shape
-    if dz.is_cuda:
+    if native(dz):
         M = N * P * Q
         cfg, splits = cfg if cfg is not None else wgrad_cfg(spec.cout, spec.K, M, spec.kh * spec.kw)
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
@@ -404,7 +411,7 @@ def bn_inference(z, gamma, beta, running_mean, running_var, eps, out, relu: bool
     phase_train=False): out = act(gamma*(z-moving_mean)/sqrt(moving_var+eps) + beta [+ res])."""
     invstd = torch.rsqrt(running_var + eps)
     N, H, W, C = z.shape
-    if z.is_cuda:
+    if native(z):
         _ext.ops().bn_apply(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0,
                             N * H * W, C, running_mean, invstd, gamma, beta, 1 if relu else 0)
         return out
@@ -421,7 +428,7 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
     out = act(gamma*xhat + beta [+ residual])."""
     N, H, W, C = z.shape
     M = N * H * W
-    if z.is_cuda:
+    if native(z):
         hcb = _ext.ops()
         if stats is None:
             stats_T = hcb.bn_partials(M, C)
@@ -434,6 +441,8 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
                      mean, invstd, gamma, beta, 1 if relu else 0)
         return BNSaved(mean, invstd)
     zf = z.reshape(M, C) if z.is_contiguous() else z.contiguous().reshape(M, C)
+    if zf.dtype == torch.float16:  # fused batch norm keeps its statistics in fp32 (TF semantics)
+        zf = zf.float()
     mean = zf.mean(0)
     var = zf.var(0, unbiased=False)
     invstd = torch.rsqrt(var + eps)
@@ -442,7 +451,7 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
             unb = var * M / max(M - 1, 1)
             running_mean.mul_(momentum).add_((1 - momentum) * mean)
             running_var.mul_(momentum).add_((1 - momentum) * unb)
-    y = (z - mean) * (invstd * gamma) + beta
+    y = (z.to(mean.dtype) - mean) * (invstd * gamma) + beta
     if residual is not None:
         y = y + residual
     if relu:
@@ -506,7 +515,7 @@ def bn_backward(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, d
     masked upstream gradient gres (the residual branch's gradient)."""
     N, H, W, C = z.shape
     M = N * H * W
-    if z.is_cuda:
+    if native(z):
         hcb = _ext.ops()
         T = hcb.bn_partials(M, C)
         slab = torch.empty(T * 2 * C, dtype=torch.float32, device=z.device)
@@ -517,6 +526,9 @@ def bn_backward(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, d
         hcb.bn_bwd_apply(dy, ld(dy), y if relu_mode == 1 else None, ld(y) if relu_mode == 1 else 0, z, ld(z),
                          dz, ld(dz), M, C, saved.mean, saved.invstd, gamma, beta, dgamma, dbeta, relu_mode)
         return dz
+    if z.dtype == torch.float16:  # backward reductions in fp32 as well
+        z, dy = z.float(), dy.float()
+        y = y.float() if y is not None else None
     xhat = (z - saved.mean) * saved.invstd
     g = dy
     if relu_mode == 1:
@@ -529,7 +541,7 @@ def bn_backward(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, d
     dg = (gf * xf).sum(0)
     dbeta.copy_(db)
     dgamma.copy_(dg)
-    dz.copy_(gamma.to(dz.dtype) * saved.invstd * (g - db / M - xhat * dg / M))
+    dz.copy_(gamma.to(g.dtype) * saved.invstd * (g - db / M - xhat * dg / M))
     if gres is not None:
         gres.copy_(g)
     return dz
@@ -546,7 +558,7 @@ def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False, argmax=No
     """argmax (GPU, max pool): uint8 [N,P,Q,C] window position of the first maximum, which
     makes the backward a cheap gather."""
     pt, pb, pl, pr = pads
-    if x.is_cuda:
+    if native(x):
         _ext.ops().pool_fwd(x, out, argmax, pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad))
         return out
     xt = x.permute(0, 3, 1, 2)
@@ -567,7 +579,7 @@ def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False, argmax=No
 
 def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, accumulate=False, argmax=None):
     pt, pb, pl, pr = pads
-    if x.is_cuda:
+    if native(x):
         # the kernel walks x / dx with one pixel stride and y / dy with another: align views
         if ld(y) != ld(dy):
             y = y.contiguous() if ld(dy) == y.shape[3] else y
@@ -606,7 +618,7 @@ def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, ac
 
 def gap_forward(x, out):
     N, H, W, C = x.shape
-    if x.is_cuda:
+    if native(x):
         assert x.is_contiguous()
         _ext.ops().gap_fwd(x, out, N, H * W, C)
         return out
@@ -616,7 +628,7 @@ def gap_forward(x, out):
 
 def gap_backward(dy, dx):
     N, H, W, C = dx.shape
-    if dy.is_cuda:
+    if native(dy):
         _ext.ops().gap_bwd(dy, dx, N, H * W, C)
         return dx
     dx.copy_((dy / (H * W)).view(N, 1, 1, C).expand(N, H, W, C))
@@ -628,7 +640,7 @@ def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None)
     """Per-row cross entropy (into row_loss) and dlogits = (softmax - onehot) * scale
     (* scale_dev[0], a device-resident loss scale, when given)."""
     B = labels.numel()
-    if logits.is_cuda:
+    if logits.is_cuda and dlogits.dtype == torch.bfloat16:
         _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale, scale_dev)
         return
     if scale_dev is not None:
@@ -645,7 +657,7 @@ def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None)
 def add(a, b, out=None):
     """out = a + b on activations (bf16 HIP kernel on the GPU)."""
     out = torch.empty_like(a) if out is None else out
-    if a.is_cuda:
+    if native(a):
         a, b = a.contiguous(), b.contiguous()
         _ext.ops().add_bf16(a, b, out)
         return out
@@ -658,18 +670,18 @@ def dropout_forward(x, y, mask, keep: float, seed: int, step):
     (seed, step[0], index), one bit per element in ``mask`` (uint8, numel/8); ``step`` is a
     device int64 counter so captured-graph replays draw fresh masks. CPU: ``mask`` is a bool
     tensor of x's shape drawn from a generator seeded with (seed, step)."""
-    if x.is_cuda:
+    if native(x):
         _ext.ops().dropout_fwd(x, y, mask, float(keep), int(seed), step)
         return y
     g = torch.Generator().manual_seed(int(seed) * 1000003 + int(step[0]))
-    m = torch.rand(x.shape, generator=g) < keep
+    m = (torch.rand(x.shape, generator=g) < keep).to(x.device)
     mask.copy_(m)
     y.copy_(x * m.to(x.dtype) / keep)
     return y
 
 
 def dropout_backward(dy, mask, dx, keep: float):
-    if dy.is_cuda:
+    if native(dy):
         _ext.ops().dropout_bwd(dy, mask, dx, float(keep))
         return dx
     dx.copy_(dy * mask.to(dy.dtype) / keep)
@@ -677,7 +689,7 @@ def dropout_backward(dy, mask, dx, keep: float):
 
 
 def colsum(g, M, N, out):
-    if g.is_cuda:
+    if native(g):
         _ext.ops().colsum(g, ld(g), M, N, out)
         return out
     out.copy_(g[:M, :N].float().sum(0))
@@ -687,7 +699,7 @@ def colsum(g, M, N, out):
 # -------------------------------------------------------------------- optimizer
 def nonfinite(g, flag):
     """flag[0] = 1 if g holds an Inf/NaN (flag must be zeroed by the caller)."""
-    if g.is_cuda:
+    if g.is_cuda:  # the fp32 flat gradient buffer: same kernel in every compute mode
         _ext.ops().nonfinite(g, flag)
         return
     if not bool(torch.isfinite(g).all()):

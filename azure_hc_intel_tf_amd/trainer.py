@@ -85,7 +85,9 @@ class Trainer:
         self.forward_only = forward_only
         if forward_only and hasattr(model, "set_training"):
             model.set_training(False)  # inference BN / no dropout (tf_cnn_benchmarks phase_train=False)
-        self.use_graph = use_graph and self.dev.type == "cuda"
+        # graphs for the HIP-kernel path; the reference-precision PyTorch path (fp32 / fp16
+        # --compute_dtype) runs eagerly (MIOpen's first-call searches are not capturable)
+        self.use_graph = use_graph and self.dev.type == "cuda" and getattr(model, "native", True)
         self.graph_warmup = graph_warmup
         ld = model.fc.ld if hasattr(model, "fc") else (model.num_classes + 7) // 8 * 8
         self.ld = ld
@@ -121,6 +123,8 @@ class Trainer:
 
     # ---------------------------------------------------------------- pieces
     def _forward(self, images, labels):
+        if hasattr(self.model, "activate"):
+            self.model.activate()
         ps = self.ps
         if not self.forward_only:
             ps.zero_grad()
@@ -384,7 +388,7 @@ def synthetic_batch(model, batch_size: int, seed: int = 0):
     uniform labels in [0, num_classes-1), created once and reused every step."""
     shape = model.input_shape(batch_size)
     dev = model.device
-    if dev.type == "cuda":
+    if dev.type == "cuda" and getattr(model, "native", True):
         img = torch.empty(shape, dtype=torch.bfloat16, device=dev)
         lab = torch.empty(batch_size, dtype=torch.int64, device=dev)
         hcb = _ext.ops()
@@ -398,4 +402,4 @@ def synthetic_batch(model, batch_size: int, seed: int = 0):
     if shape[3] > 3:
         img[..., 3:] = 0
     lab = torch.randint(0, model.num_classes - 1, (batch_size,), generator=g, dtype=torch.int64)
-    return img.to(dev), lab.to(dev)
+    return img.to(dev, model.act_dtype), lab.to(dev)

@@ -52,7 +52,8 @@ def parse_args(argv=None):
                     help="N=1 only: run the multi-GPU step (one graph with the collectives on a forked comm "
                          "stream, async RCCL engine on a 1-rank communicator) to time its overhead on one GPU")
     ap.add_argument("--use_fp16", action="store_true",
-                    help="tf_cnn_benchmarks --use_fp16: 16-bit compute with automatic loss scaling")
+                    help="tf_cnn_benchmarks --use_fp16: IEEE fp16 compute (PyTorch reference path) with automatic "
+                         "loss scaling; with --compute_dtype bf16: the HIP kernels plus loss scaling")
     ap.add_argument("--compute_dtype", default=None, choices=[None, "bf16", "fp16", "fp32"],
                     help="activation / GEMM precision (default bf16; fp32 = the reference's precision)")
     return ap.parse_args(argv)
@@ -172,7 +173,7 @@ def main(argv=None):
     from azure_hc_intel_tf_amd.ops import autotune
 
     autotune.load_cache()
-    if not args.no_tune:
+    if not args.no_tune and model.native:
         n = autotune.tune_model(model, B, save=(rank == 0))
         if n and rank == 0:
             print(f"[bench] autotuned {n} conv problems", file=sys.stderr)
@@ -181,7 +182,7 @@ def main(argv=None):
         reducer.broadcast_(model.ps.buf, 0)
     images, labels = synthetic_batch(model, B, seed=rank)
     trainer = Trainer(model, B, resnet_lr_schedule(B * world), reducer=reducer, world_size=world,
-                      use_graph=not args.no_graph, dynamic_loss_scale=(dtype == "fp16"),
+                      use_graph=not args.no_graph, dynamic_loss_scale=(args.use_fp16 or dtype == "fp16"),
                       force_overlap=args.force_dp_path)
 
     def barrier():
@@ -245,10 +246,11 @@ def main(argv=None):
             "comm": comm,
             "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
                        "image_size": model.image_size, "parallelism": f"dp{world}",
-                       "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": not args.no_graph,
+                       "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": trainer.use_graph,
                        "engine": args.engine if (world > 1 or args.force_dp_path) else None,
                        "backend": backend, "compression": args.compression,
-                       "loss_scaling": "dynamic" if dtype == "fp16" else None,
+                       "loss_scaling": "dynamic" if (args.use_fp16 or dtype == "fp16") else None,
+                       "kernels": "hip" if model.native else "pytorch-reference (MIOpen/rocBLAS)",
                        "final_loss": round(loss, 4)},
         }
         print(json.dumps(res), flush=True)

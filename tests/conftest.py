@@ -13,6 +13,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running test")
 
 
+@pytest.fixture(autouse=True)
+def _default_gpu_compute_dtype():
+    """Every test starts with the default (bf16 HIP-kernel) GPU activation dtype; models of the
+    reference-precision mode switch it while they step."""
+    import torch
+
+    from azure_hc_intel_tf_amd.nn.layers import set_gpu_compute_dtype
+
+    set_gpu_compute_dtype(torch.bfloat16)
+    yield
+
+
 def gpu_available():
     try:
         import torch

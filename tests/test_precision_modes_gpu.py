@@ -1,0 +1,54 @@
+"""Reference-precision compute modes on the GPU (--compute_dtype fp32 / fp16): the PyTorch
+path (MIOpen / rocBLAS) of ops/functional.py, the same code the CPU path runs. fp32 is the
+reference's precision (run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16)."""
+import pytest
+import torch
+
+from azure_hc_intel_tf_amd.models import create_model
+from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fp32_gpu_matches_fp32_cpu_step():
+    """One fp32 training step on the GPU equals the fp32 CPU step: the loss to fp32 tolerance,
+    the gradient as a whole (direction and norm)."""
+    kw = dict(image_size=64, seed=7)
+    mg = create_model("resnet50", device="cuda", compute_dtype="fp32", **kw)
+    mc = create_model("resnet50", device="cpu", **kw)
+    assert not mg.native and mg.image_channels == 3
+    assert torch.equal(mg.ps.master.cpu(), mc.ps.master)
+    img_c, lab_c = synthetic_batch(mc, 4, seed=3)
+    img_c = (img_c - 127.0) / 60.0
+    tg = Trainer(mg, 4, constant_lr(0.05))
+    tc = Trainer(mc, 4, constant_lr(0.05))
+    lg = float(tg.step(img_c.cuda(), lab_c.cuda()))
+    lc = float(tc.step(img_c, lab_c))
+    torch.cuda.synchronize()
+    assert abs(lg - lc) <= 1e-4 * abs(lc), (lg, lc)
+    # whole-network gradients of a random-init BN net are chaotic in the rounding order
+    # (MIOpen vs oneDNN accumulation): compared as a whole, not elementwise
+    gg, gc = mg.ps.grad.cpu(), mc.ps.grad
+    assert (gg - gc).norm() / gc.norm() < 5e-2
+    assert float(gg @ gc / (gg.norm() * gc.norm())) > 0.999
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp16"])
+def test_reference_precision_training_learns(dtype):
+    torch.manual_seed(0)
+    m = create_model("resnet50", image_size=64, device="cuda", compute_dtype=dtype)
+    img, lab = synthetic_batch(m, 8)
+    assert img.dtype == {"fp32": torch.float32, "fp16": torch.float16}[dtype]
+    img = (img.float() - 127.0).div(60.0).to(img.dtype)
+    t = Trainer(m, 8, constant_lr(0.02), dynamic_loss_scale=(dtype == "fp16"))
+    losses = [float(t.step(img, lab)) for _ in range(12)]
+    assert all(l == l for l in losses)
+    assert min(losses[-3:]) < 0.8 * losses[0], losses
+
+
+def test_bf16_and_fp32_models_coexist():
+    """A bf16 (HIP) and an fp32 (reference) GPU model in one process keep their own
+    activation dtypes."""
+    a = create_model("resnet50", image_size=64, device="cuda", compute_dtype="fp32")
+    b = create_model("resnet50", image_size=64, device="cuda")
+    assert b.native and b.act_dtype == torch.bfloat16 and a.act_dtype == torch.float32
