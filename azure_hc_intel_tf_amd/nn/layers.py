@@ -178,12 +178,26 @@ class ConvBN(Layer):
             self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0)) if bias else None
         self._saved = None
         self._mask = None
+        self._acc = None  # (fwd acc, bwd acc, replicas) of the current step
         self._pre_reduced = False
         self.training = True  # False: inference BN from the moving statistics (forward-only)
 
     def flops(self, batch: int) -> int:
         P, Q, C = self.out_shape
         return 2 * batch * P * Q * C * self.spec.kh * self.spec.kw * self.spec.cin
+
+    def _stat_bufs(self, N: int, dev):
+        """(forward acc, backward acc, replicas) of this step's BN statistics: the persistent
+        STAT_R-replica buffers, or in deterministic mode fresh ones with a replica per 64 rows
+        (each fp32 slot then receives a single add)."""
+        if not Fn.deterministic():
+            self._acc = (self.acc_f.data, self.acc_b.data, STAT_R)
+        else:
+            P, Q, C = self.out_shape
+            R = Fn.det_replicas(N * P * Q)
+            self._acc = (torch.zeros((R, 2, C), dtype=torch.float32, device=dev),
+                         torch.zeros((R, 2, C), dtype=torch.float32, device=dev), R)
+        return self._acc
 
     def params(self):
         """Trainable ParamRefs of this layer (gradient slots in the flat buffer)."""
@@ -212,15 +226,15 @@ class ConvBN(Layer):
             y = out if out is not None else empty_act((N, P, Q, C), dev)
             if Fn.native(x):
                 # conv epilogue accumulates the batch statistics; the apply kernel finalizes them
-                Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data,
-                                stats_R=STAT_R)
+                acc_f, _, R = self._stat_bufs(N, dev)
+                Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=acc_f, stats_R=R)
                 # residual + ReLU outputs keep a bit mask for the fused backward (mode 3)
                 mask = None
                 if (RELU_BITMASK and self.relu and residual is not None and FUSE_BN_BWD
                         and Fn.ld(z) == C and Fn.ld(y) == C):
                     mask = torch.empty((N * P * Q, C // 8), dtype=torch.uint8, device=dev)
                 saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
-                                          self.decay, self.eps, y, self.relu, self.acc_f.data, STAT_R,
+                                          self.decay, self.eps, y, self.relu, acc_f, R,
                                           self.sv_mean.data, self.sv_invstd.data, residual=residual, mask=mask)
                 self._mask = mask
             else:
@@ -248,8 +262,9 @@ class ConvBN(Layer):
         x = self._conv_fwd_stats(x, z)
         y = empty_act((N,) + tuple(pool.out_shape), x.device)
         amax = torch.empty((N,) + tuple(pool.out_shape), dtype=torch.uint8, device=x.device)
+        acc_f, _, R = self._acc
         saved = Fn.bn_relu_maxpool_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
-                                       self.eps, self.acc_f.data, STAT_R, self.sv_mean.data, self.sv_invstd.data, y,
+                                       self.eps, acc_f, R, self.sv_mean.data, self.sv_invstd.data, y,
                                        amax, *pool.k, *pool.s, pool.pads)
         self._saved = (x, z, None, saved, False)
         pool._saved = (z, y, amax)  # the argmax backward reads only shapes from x / y
@@ -258,7 +273,8 @@ class ConvBN(Layer):
     def _conv_fwd_stats(self, x, z):
         """GPU conv with the BN statistics in its epilogue; returns the tensor the weight
         gradient will read (the conv's GEMM input)."""
-        Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=self.acc_f.data, stats_R=STAT_R)
+        acc_f, _, R = self._stat_bufs(x.shape[0], x.device)
+        Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=acc_f, stats_R=R)
         return x
 
     def _wgrad(self, dz, x):
@@ -272,9 +288,10 @@ class ConvBN(Layer):
         x, z, y, saved, had_res = self._saved
         mode = (1 if had_res else 2) if self.relu else 0
         self._pre_reduced = True
+        _, acc_b, R = self._acc if self._acc is not None else (None, self.acc_b.data, STAT_R)
         if mode == 1 and self._mask is not None:
-            return Fn.BNBwdFuse(z, self._mask, saved, self.gamma.data, self.beta.data, 3, self.acc_b.data, STAT_R)
-        return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, self.acc_b.data, STAT_R)
+            return Fn.BNBwdFuse(z, self._mask, saved, self.gamma.data, self.beta.data, 3, acc_b, R)
+        return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, acc_b, R)
 
     def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False, dx_bn=None):
         """Returns (dx or None, gres or None). gres = gradient w.r.t. the residual input.
@@ -290,8 +307,9 @@ class ConvBN(Layer):
             self._pre_reduced = False
             dz = empty_act((N, P, Q, C), dev)
             if Fn.native(dy):
+                _, acc_b, R = self._acc
                 Fn.bn_backward_acc(dy, None, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
-                                   self.beta.grad, dz, self.acc_b.data, STAT_R, None, pre_reduced=True)
+                                   self.beta.grad, dz, acc_b, R, None, pre_reduced=True)
             else:
                 Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
                                self.beta.grad, dz, None)
@@ -303,8 +321,9 @@ class ConvBN(Layer):
                 gres = empty_act((N, P, Q, C), dev)
             relu_mode = (1 if had_res else 2) if self.relu else 0
             if Fn.native(dy):
+                _, acc_b, R = self._acc
                 Fn.bn_backward_acc(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
-                                   self.beta.grad, dz, self.acc_b.data, STAT_R, gres)
+                                   self.beta.grad, dz, acc_b, R, gres)
             else:
                 Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
                                self.beta.grad, dz, gres)
@@ -383,8 +402,8 @@ class StemS2D(ConvBN):
 
     def _conv_fwd_stats(self, x, z):
         xf = self.fold_input(x)
-        Fn.conv_forward(xf, self.fold_spec, self._folded_weight(x.device), self.w.data, z, stats=self.acc_f.data,
-                        stats_R=STAT_R)
+        acc_f, _, R = self._stat_bufs(x.shape[0], x.device)
+        Fn.conv_forward(xf, self.fold_spec, self._folded_weight(x.device), self.w.data, z, stats=acc_f, stats_R=R)
         return xf
 
     def _wgrad(self, dz, x):
@@ -413,8 +432,9 @@ class StemS2D(ConvBN):
             self._saved = None
             return y
         xf = self._conv_fwd_stats(x, z)
+        acc_f, _, R = self._acc
         saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
-                                  self.eps, y, self.relu, self.acc_f.data, STAT_R, self.sv_mean.data,
+                                  self.eps, y, self.relu, acc_f, R, self.sv_mean.data,
                                   self.sv_invstd.data, residual=residual)
         self._saved = (xf, z, y, saved, residual is not None)
         return y

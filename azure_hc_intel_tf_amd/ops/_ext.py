@@ -1,7 +1,8 @@
 """Loader for the in-tree gfx950 kernel library (``_hcb_kernels.so``).
 
-GPU tensors ALWAYS go through the hand-written HIP kernels: if the library is missing on a
-machine with a GPU this raises instead of silently falling back to PyTorch/MIOpen.
+bf16 GPU activations ALWAYS go through the hand-written HIP kernels: if the library is missing
+on a machine with a GPU this raises instead of silently falling back to PyTorch/MIOpen (the
+PyTorch path on the GPU is only the explicitly requested fp32 / fp16 reference-precision mode).
 CPU tensors use the PyTorch reference implementations in ``functional.py`` (the
 reference's ``--device=cpu`` path, BASELINE config 1).
 """
@@ -34,6 +35,10 @@ def load(build_if_missing: bool = True) -> bool:
             _build.build_kernels()
         torch.ops.load_library(KERNELS_SO)
         _LOADED = True
+        from . import functional
+
+        if functional.deterministic():
+            torch.ops.hcb.set_deterministic(True)
         return True
 
 

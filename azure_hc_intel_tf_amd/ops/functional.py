@@ -16,6 +16,7 @@ their channel window of the concat buffer (no concat kernel).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -38,6 +39,30 @@ def _round_up(x: int, m: int) -> int:
 
 
 # --------------------------------------------------------------------------- conv
+_DET = [os.environ.get("HCB_DETERMINISTIC", "0") == "1"]
+
+
+def set_deterministic(on: bool = True) -> None:
+    """Opt-in bitwise-reproducible GPU training (HCB_DETERMINISTIC=1): no split-K (conv and
+    weight-gradient tiles have a single writer), BN statistic / backward accumulators with one
+    replica per contributing tile or block (every fp32 slot receives exactly one add, summed
+    later in a fixed order), single-block bias column sums. Slower; for debugging and the
+    determinism test."""
+    _DET[0] = bool(on)
+    if _ext.loaded():
+        _ext.ops().set_deterministic(bool(on))
+
+
+def deterministic() -> bool:
+    return _DET[0]
+
+
+def det_replicas(M: int) -> int:
+    """Accumulator replicas for an M-row BN layer in deterministic mode: one per 64 rows covers
+    every GEMM row tile (tiles are >= 64 rows) and every BN-backward row block."""
+    return max(1, (M + 63) // 64)
+
+
 def native(t) -> bool:
     """True when ``t`` goes through the hand-written HIP kernels: a bf16 activation on the GPU.
     Other GPU tensors (the fp32 / IEEE-fp16 reference-precision mode, --compute_dtype) take
@@ -263,6 +288,8 @@ def _plan(cfg, M, N, K, device, taps: int = 1):
         cfg, splits = cfg
     else:
         splits = 1
+    if _DET[0]:
+        splits = 1
     if splits > 1:
         ensure_splitk_workspace(device)
     return int(cfg), int(splits)
@@ -384,6 +411,8 @@ def conv_wgrad(dz, x, spec: ConvSpec, dw, cfg=None):
     if native(dz):
         M = N * P * Q
         cfg, splits = cfg if cfg is not None else wgrad_cfg(spec.cout, spec.K, M, spec.kh * spec.kw)
+        if _DET[0]:
+            splits = 1  # sole writer per dW tile: no float atomics
         geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
                 spec.dh, spec.dw, spec.cout, ld(dz)]
         _ext.ops().conv_wgrad(dz, x, dw, geom, cfg, splits)

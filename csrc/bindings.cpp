@@ -776,6 +776,8 @@ void stem_wgrad_unfold(const Tensor& dwp, const Tensor& dw) {
                                 cur_stream());
 }
 
+void set_deterministic(bool on) { hcb::set_deterministic(on); }
+
 }  // namespace
 
 TORCH_LIBRARY(hcb, m) {
@@ -820,6 +822,7 @@ TORCH_LIBRARY(hcb, m) {
   m.def("bucket_pack(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("bucket_unpack(Tensor src, Tensor(a!) dst, float scale) -> ()");
   m.def("stem_s2d(Tensor x, Tensor(a!) out, int pad) -> ()");
+  m.def("set_deterministic(bool on) -> ()", set_deterministic);
   m.def("stem_wfold(Tensor w, Tensor(a!) wp) -> ()");
   m.def("stem_wgrad_unfold(Tensor dwp, Tensor(a!) dw) -> ()");
 }

@@ -895,6 +895,9 @@ void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv,
                               int relu, float* acc, int R, void* gout, int ldg, hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
+  // every block adds into replica blockIdx.x % R; deterministic mode: at most R row blocks, so
+  // each replica slot gets one add (the kernel strides over the rows with any grid)
+  if (deterministic() && (int)grid.x > R) grid.x = R;
   size_t lds = (size_t)2 * (256 / cvb) * cvb * 8 * 4;
   hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
                      (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu,

@@ -68,6 +68,10 @@ struct ConvParams {
   unsigned* cnt;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
+// deterministic reductions (misc.hip): colsum / BN-backward reduce grids limited so that
+// every fp32 accumulator slot receives a single add
+void set_deterministic(bool on);
+bool deterministic();
 int conv_tile_m(int cfg);
 int conv_tile_n(int cfg);
 

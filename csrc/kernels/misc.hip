@@ -478,9 +478,15 @@ void launch_nonfinite(const float* g, int64_t n, float* flag, hipStream_t st) {
 void launch_loss_scale_update(float* hyper, float world, int dynamic, hipStream_t st) {
   hipLaunchKernelGGL(loss_scale_update_kernel, dim3(1), dim3(1), 0, st, hyper, world, dynamic);
 }
+// Deterministic mode (hcb.set_deterministic): reductions whose float atomics would add in a
+// run-dependent order are launched so that every accumulator slot receives exactly one add.
+static bool g_deterministic = false;
+void set_deterministic(bool on) { g_deterministic = on; }
+bool deterministic() { return g_deterministic; }
+
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st) {
   const int gy = (N + 255) / 256;
-  int gx = (M + 63) / 64;  // >= 8 rows per thread
+  int gx = g_deterministic ? 1 : (M + 63) / 64;  // >= 8 rows per thread
   const int cap = (2048 + gy - 1) / gy;
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
