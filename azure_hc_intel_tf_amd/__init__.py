@@ -10,6 +10,10 @@ touched (the HIP runtime reads them once, at initialisation):
   (corrupted gradients within a few steps; reproduced with ``tools/dp_variants.sh`` even with
   the collective itself removed). With it off the same graphs are exact and the step time is
   unchanged (7.80 vs 7.81 ms/step, ResNet-50 bs=64). Set it explicitly to override.
+  Investigation (profiles/r2f_graph_packet_capture.txt): only graphs with SEVERAL fork/join
+  pairs between backward segments diverge (also with empty comm branches and with a distinct
+  event per edge); no-fork and single-fork step graphs, and the standalone fork/join repro
+  ``tools/graph_fork_repro.hip`` (same API sequence), are exact with packet capture on.
 """
 import os as _os
 

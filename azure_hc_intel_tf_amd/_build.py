@@ -65,6 +65,13 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
 
 
+# No packed-fp32 VALU code (v_pk_{add,mul,fma,mov}_f32): with it, the BN-statistics epilogue of
+# the 64x64 conv tile summed its squares non-deterministically wrong on MI355X (relative errors
+# up to 3x the variance, other sums exact; tools/diag_bn_stats.py, profiles/r2e_bn_shift_and_pkf32.txt)
+# while the same source built without it is exact -- and the whole step is ~1.7% faster without.
+NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+
+
 def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(BUILD, exist_ok=True)
     hdrs = _headers()
@@ -77,7 +84,7 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
         objs.append(obj)
         if _newer(obj, [src] + hdrs):
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                              "-munsafe-fp-atomics", "-Wno-unused-result",
+                              "-munsafe-fp-atomics", "-Wno-unused-result", *NO_PACKED_FP32,
                               "-I" + os.path.join(CSRC, "kernels"), "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(BUILD, "bindings.o")

@@ -71,6 +71,10 @@ FUSE_STEM_POOL = os.environ.get("HCB_FUSE_STEM_POOL", "1") != "0"
 STAT_R = max(1, int(os.environ.get("HCB_STAT_R", "8")))
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
 FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
+# shifted single-pass BN statistics: the conv epilogue sums (v - K), (v - K)^2 with K = the
+# layer's previous batch mean, so E[x^2] - E[x]^2 does not cancel in fp32 when |mean| >> std
+# (HCB_BN_SHIFT=0: K = 0, the plain single-pass form)
+BN_SHIFT = os.environ.get("HCB_BN_SHIFT", "1") != "0"
 # ...only when the data-grad GEMM's reduction depth (cout * kh * kw of the producing conv) is at
 # least this: a shallow GEMM (stage-1 1x1, K=64) is all epilogue, and the fused gating +
 # reductions there cost more than a separate BN-backward reduce pass
@@ -173,6 +177,9 @@ class ConvBN(Layer):
             self.acc_b = ps.add_stat(f"{name}/bn_acc_bwd", (STAT_R, 2, cout))
             self.sv_mean = ps.add_stat(f"{name}/bn_mean", (cout,))
             self.sv_invstd = ps.add_stat(f"{name}/bn_invstd", (cout,))
+            # statistics shift K: the previous step's batch mean (written by the BN backward); the
+            # epilogue accumulates (v - K) so the single-pass variance does not cancel (|mean| >> std)
+            self.shift = ps.add_persist(f"{name}/bn_shift", (cout,)) if BN_SHIFT else None
         else:
             # ResNet-v2's un-normalised convs (shortcut, conv3) have no bias in tf_cnn_benchmarks
             self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0)) if bias else None
@@ -226,8 +233,8 @@ class ConvBN(Layer):
             y = out if out is not None else empty_act((N, P, Q, C), dev)
             if Fn.native(x):
                 # conv epilogue accumulates the batch statistics; the apply kernel finalizes them
-                acc_f, _, R = self._stat_bufs(N, dev)
-                Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=acc_f, stats_R=R)
+                x = self._conv_fwd_stats(x, z)
+                acc_f, _, R = self._acc
                 # residual + ReLU outputs keep a bit mask for the fused backward (mode 3)
                 mask = None
                 if (RELU_BITMASK and self.relu and residual is not None and FUSE_BN_BWD
@@ -235,7 +242,8 @@ class ConvBN(Layer):
                     mask = torch.empty((N * P * Q, C // 8), dtype=torch.uint8, device=dev)
                 saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
                                           self.decay, self.eps, y, self.relu, acc_f, R,
-                                          self.sv_mean.data, self.sv_invstd.data, residual=residual, mask=mask)
+                                          self.sv_mean.data, self.sv_invstd.data, residual=residual, mask=mask,
+                                          shift=self._shift())
                 self._mask = mask
             else:
                 Fn.conv_forward(x, self.spec, None, self.w.data, z)
@@ -265,7 +273,7 @@ class ConvBN(Layer):
         acc_f, _, R = self._acc
         saved = Fn.bn_relu_maxpool_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
                                        self.eps, acc_f, R, self.sv_mean.data, self.sv_invstd.data, y,
-                                       amax, *pool.k, *pool.s, pool.pads)
+                                       amax, *pool.k, *pool.s, pool.pads, shift=self._shift())
         self._saved = (x, z, None, saved, False)
         pool._saved = (z, y, amax)  # the argmax backward reads only shapes from x / y
         return y
@@ -274,8 +282,12 @@ class ConvBN(Layer):
         """GPU conv with the BN statistics in its epilogue; returns the tensor the weight
         gradient will read (the conv's GEMM input)."""
         acc_f, _, R = self._stat_bufs(x.shape[0], x.device)
-        Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=acc_f, stats_R=R)
+        Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=acc_f, stats_R=R,
+                        stats_shift=self._shift())
         return x
+
+    def _shift(self):
+        return self.shift.data if self.shift is not None else None
 
     def _wgrad(self, dz, x):
         Fn.conv_wgrad(dz, x, self.spec, self.w.grad.view(dz.shape[-1], -1) if Fn.native(dz) else self.w.grad)
@@ -309,7 +321,7 @@ class ConvBN(Layer):
             if Fn.native(dy):
                 _, acc_b, R = self._acc
                 Fn.bn_backward_acc(dy, None, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
-                                   self.beta.grad, dz, acc_b, R, None, pre_reduced=True)
+                                   self.beta.grad, dz, acc_b, R, None, pre_reduced=True, shift_out=self._shift())
             else:
                 Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
                                self.beta.grad, dz, None)
@@ -323,7 +335,7 @@ class ConvBN(Layer):
             if Fn.native(dy):
                 _, acc_b, R = self._acc
                 Fn.bn_backward_acc(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
-                                   self.beta.grad, dz, acc_b, R, gres)
+                                   self.beta.grad, dz, acc_b, R, gres, shift_out=self._shift())
             else:
                 Fn.bn_backward(dy, y, z, saved, self.gamma.data, self.beta.data, relu_mode, self.gamma.grad,
                                self.beta.grad, dz, gres)
@@ -403,7 +415,8 @@ class StemS2D(ConvBN):
     def _conv_fwd_stats(self, x, z):
         xf = self.fold_input(x)
         acc_f, _, R = self._stat_bufs(x.shape[0], x.device)
-        Fn.conv_forward(xf, self.fold_spec, self._folded_weight(x.device), self.w.data, z, stats=acc_f, stats_R=R)
+        Fn.conv_forward(xf, self.fold_spec, self._folded_weight(x.device), self.w.data, z, stats=acc_f, stats_R=R,
+                        stats_shift=self._shift())
         return xf
 
     def _wgrad(self, dz, x):
@@ -435,7 +448,7 @@ class StemS2D(ConvBN):
         acc_f, _, R = self._acc
         saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
                                   self.eps, y, self.relu, acc_f, R, self.sv_mean.data,
-                                  self.sv_invstd.data, residual=residual)
+                                  self.sv_invstd.data, residual=residual, shift=self._shift())
         self._saved = (xf, z, y, saved, residual is not None)
         return y
 

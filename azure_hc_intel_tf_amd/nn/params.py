@@ -82,6 +82,7 @@ class ParamStore:
         self.params: List[ParamRef] = []
         self.buffers: List[BufferRef] = []
         self.stats: List[BufferRef] = []
+        self.persist: List[BufferRef] = []
         self.packs: List[PackRef] = []
         self.gen = torch.Generator().manual_seed(seed)
         self.finalized = False
@@ -103,6 +104,13 @@ class ParamStore:
         buffer, zeroed once per step together with the gradients."""
         b = BufferRef(name, tuple(shape), 0.0)
         self.stats.append(b)
+        return b
+
+    def add_persist(self, name, shape) -> BufferRef:
+        """Cross-step scratch (the BN statistic shifts): zero at finalize, never zeroed per step
+        and not part of the checkpoint state (any value is numerically valid)."""
+        b = BufferRef(name, tuple(shape), 0.0)
+        self.persist.append(b)
         return b
 
     def add_pack(self, p: ParamRef, Nout, R, S, C, Kpad, Kpad_t, want_tr=True) -> PackRef:
@@ -200,6 +208,13 @@ class ParamStore:
         self.statbuf = torch.zeros(max(soff, ALIGN), dtype=torch.float32, device=device)
         for b in self.stats:
             b.data = self.statbuf[b.offset:b.offset + b.numel].view(b.shape)
+        poff = 0
+        for b in self.persist:
+            b.offset = poff
+            poff += _align(b.numel)
+        self.persistbuf = torch.zeros(max(poff, ALIGN), dtype=torch.float32, device=device)
+        for b in self.persist:
+            b.data = self.persistbuf[b.offset:b.offset + b.numel].view(b.shape)
         # bf16 GEMM operands (GPU only)
         poff = 0
         rows = []

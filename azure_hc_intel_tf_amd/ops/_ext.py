@@ -16,7 +16,8 @@ import torch
 _LOCK = threading.Lock()
 _LOADED = False
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS_SO = os.path.join(_PKG, "_hcb_kernels.so")
+# HCB_KERNELS_SO: load another build of the library (kernel-variant A/B runs, tools/build_variant.py)
+KERNELS_SO = os.environ.get("HCB_KERNELS_SO") or os.path.join(_PKG, "_hcb_kernels.so")
 
 
 def load(build_if_missing: bool = True) -> bool:

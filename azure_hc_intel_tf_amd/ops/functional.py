@@ -250,9 +250,11 @@ def set_tuned(table: dict) -> None:
 
 # ---------------------------------------------------------------- conv forward
 def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None, relu=False,
-                 stats_R: int = 0, residual=None):
+                 stats_R: int = 0, residual=None, stats_shift=None):
     """out[N,P,Q,cout] = conv(x, W) (+bias) [ReLU]. GPU: fp32 acc, bf16 (or fp32) out + fused BN
-    statistics: per-tile slab (stats_R=0) or fp32 atomics into stats_R replicas of [2][cout]."""
+    statistics: per-tile slab (stats_R=0) or fp32 atomics into stats_R replicas of [2][cout].
+    ``stats_shift`` (fp32 [cout]): the statistics are sums of (v - shift) and (v - shift)^2, which
+    keeps the single-pass variance exact when |mean| >> std; the BN apply gets the same shift."""
     N, H, W, _ = x.shape
     P, Q = spec.out_hw(H, W)
     if native(x):
@@ -264,7 +266,7 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
                 1 if residual is not None else 0, 1 if out_f32 else 0, 1 if relu else 0, int(stats_R), splits]
         if residual is not None:  # beta-accumulate epilogue: out = conv(x) + residual (same layout)
             assert ld(residual) == ld(out) and residual.shape == out.shape
-        _ext.ops().conv_igemm(x, wpack, out, residual, bias, stats, geom, cfg)
+        _ext.ops().conv_igemm(x, wpack, out, residual, bias, stats, geom, cfg, stats_shift)
         return out
     xt = x.permute(0, 3, 1, 2)
     if spec.pt or spec.pb or spec.pl or spec.pr:
@@ -490,51 +492,53 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
 
 
 def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out, relu: bool, acc, R: int,
-                   saved_mean, saved_invstd, residual=None, mask=None):
+                   saved_mean, saved_invstd, residual=None, mask=None, shift=None):
     """GPU BN forward whose batch statistics were accumulated by the producing conv's epilogue
     into ``acc`` (R replicas of [2][C]); mean/invstd are derived inside the apply kernel (no
     finalize launch) and written to saved_mean / saved_invstd for the backward. ``mask``
     (uint8 [M, C/8]): also store the output's ReLU bit mask, which the mode-3 fused
-    BN-backward epilogue reads instead of the full bf16 output (1/16 of the bytes)."""
+    BN-backward epilogue reads instead of the full bf16 output (1/16 of the bytes). ``shift``:
+    the per-channel offset the producing conv subtracted before accumulating (conv_forward)."""
     N, H, W, C = z.shape
     M = N * H * W
     _ext.ops().bn_apply_acc(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0, M, C,
                             acc, R, eps, momentum, gamma, beta, 1 if relu else 0, saved_mean, saved_invstd,
-                            running_mean, running_var, mask)
+                            running_mean, running_var, mask, shift)
     return BNSaved(saved_mean, saved_invstd)
 
 
 def bn_relu_maxpool_acc(z, gamma, beta, running_mean, running_var, momentum, eps, acc, R: int, saved_mean,
-                        saved_invstd, out, argmax, kh, kw, sh, sw, pads):
+                        saved_invstd, out, argmax, kh, kw, sh, sw, pads, shift=None):
     """GPU: BN (conv-epilogue statistics in ``acc``) + ReLU + max pool in one kernel; writes the
     pooled ``out`` and the uint8 window ``argmax`` only (the BN+ReLU activation is not stored)."""
     N, H, W, C = z.shape
     _, P, Q, _ = out.shape
     pt, pb, pl, pr = pads
     _ext.ops().bn_relu_maxpool_acc(z, out, argmax, [N, H, W, C, P, Q, ld(out), kh, kw, sh, sw, pt, pl], acc, R, eps,
-                                   momentum, gamma, beta, saved_mean, saved_invstd, running_mean, running_var)
+                                   momentum, gamma, beta, saved_mean, saved_invstd, running_mean, running_var, shift)
     return BNSaved(saved_mean, saved_invstd)
 
 
 def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, acc, R: int,
-                    gres=None, pre_reduced: bool = False):
+                    gres=None, pre_reduced: bool = False, shift_out=None):
     """GPU BN(+ReLU) backward with the dgamma/dbeta reduction accumulated in ``acc`` replicas
     (zeroed per step) and consumed directly by the apply kernel. ``pre_reduced``: dy is already
     the gated g and ``acc`` already holds its sums (a BNBwdFuse data-grad epilogue produced it),
-    so only the apply pass runs."""
+    so only the apply pass runs. ``shift_out``: receives this step's batch mean, the statistics
+    shift of the layer's next forward."""
     N, H, W, C = z.shape
     M = N * H * W
     hcb = _ext.ops()
     if pre_reduced:
         assert gres is None, "pre-reduced dy is itself the residual gradient"
         hcb.bn_bwd_apply_acc(dy, ld(dy), None, 0, z, ld(z), dz, ld(dz), M, C, saved.mean, saved.invstd, gamma,
-                             beta, acc, R, dgamma, dbeta, 0)
+                             beta, acc, R, dgamma, dbeta, 0, shift_out)
         return dz
     ym = y if relu_mode == 1 else None
     hcb.bn_bwd_reduce_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), M, C, saved.mean, saved.invstd,
                           gamma, beta, relu_mode, acc, R, gres, ld(gres) if gres is not None else 0)
     hcb.bn_bwd_apply_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), dz, ld(dz), M, C, saved.mean,
-                         saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode)
+                         saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode, shift_out)
     return dz
 
 

@@ -141,10 +141,19 @@ void set_splitk_workspace(const Tensor& ws, const Tensor& cnt) {
   g_splitk_cnt_n = cnt.numel();
 }
 
+const float* opt_f32(const c10::optional<Tensor>& t, int64_t n, const char* what) {
+  if (!t.has_value()) return nullptr;
+  check_f32(*t, what);
+  TORCH_CHECK(t->numel() >= n, "hcb: ", what, " too small");
+  return t->data_ptr<float>();
+}
+
 void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                 const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
-                at::IntArrayRef g, int64_t cfg) {
+                at::IntArrayRef g, int64_t cfg, const c10::optional<Tensor>& stats_shift) {
   hcb::ConvParams p = conv_params(x, w, y, yres, bias, stats, g, cfg);
+  TORCH_CHECK(!stats_shift.has_value() || p.stats != nullptr, "hcb.conv_igemm: stats_shift without stats");
+  p.stats_shift = opt_f32(stats_shift, p.Nout, "stats_shift");
   hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
 }
 
@@ -366,7 +375,7 @@ void bn_bwd_apply(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y
 void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, at::IntArrayRef g, const Tensor& acc,
                          int64_t R, double eps, double momentum, const Tensor& gamma, const Tensor& beta,
                          const Tensor& saved_mean, const Tensor& saved_invstd, const Tensor& run_mean,
-                         const Tensor& run_var) {
+                         const Tensor& run_var, const c10::optional<Tensor>& shift) {
   TORCH_CHECK(g.size() == 13, "hcb.bn_relu_maxpool_acc: geom");
   check_bf16(z, "z");
   check_bf16(y, "y");
@@ -387,7 +396,7 @@ void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, a
                                   g[10], g[11], g[12], acc.data_ptr<float>(), R, (float)eps, (float)momentum,
                                   gamma.data_ptr<float>(), beta.data_ptr<float>(), saved_mean.data_ptr<float>(),
                                   saved_invstd.data_ptr<float>(), run_mean.data_ptr<float>(),
-                                  run_var.data_ptr<float>(), cur_stream());
+                                  run_var.data_ptr<float>(), opt_f32(shift, C, "shift"), cur_stream());
 }
 
 // geom = [N,H,W,C,ldx,P,Q,ldy,kh,kw,sh,sw,ph,pw,is_max,incl_pad]
@@ -538,7 +547,7 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                   int64_t ldr, int64_t M, int64_t C, const Tensor& acc, int64_t R, double eps, double momentum,
                   const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& saved_mean,
                   const Tensor& saved_invstd, const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv,
-                  const c10::optional<Tensor>& mask) {
+                  const c10::optional<Tensor>& mask, const c10::optional<Tensor>& shift) {
   check_bf16(x, "x");
   check_bf16(y, "y");
   check_f32(acc, "acc");
@@ -564,7 +573,8 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                            acc.data_ptr<float>(), (int)R, (float)eps, (float)momentum, gamma.data_ptr<float>(),
                            beta.data_ptr<float>(), (int)relu, saved_mean.data_ptr<float>(),
                            saved_invstd.data_ptr<float>(), rm.has_value() ? rm->data_ptr<float>() : nullptr,
-                           rv.has_value() ? rv->data_ptr<float>() : nullptr, mp, cur_stream());
+                           rv.has_value() ? rv->data_ptr<float>() : nullptr, mp, opt_f32(shift, C, "shift"),
+                           cur_stream());
 }
 
 void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
@@ -598,7 +608,8 @@ void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tenso
 void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
                       const Tensor& x, int64_t ldx, const Tensor& dx, int64_t lddx, int64_t M, int64_t C,
                       const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
-                      const Tensor& acc, int64_t R, const Tensor& dgamma, const Tensor& dbeta, int64_t relu) {
+                      const Tensor& acc, int64_t R, const Tensor& dgamma, const Tensor& dbeta, int64_t relu,
+                      const c10::optional<Tensor>& shift_out) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   check_bf16(dx, "dx");
@@ -616,7 +627,8 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
   hcb::launch_bn_bwd_apply_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, dx.data_ptr(),
                                (int)lddx, (int)M, (int)C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                gamma.data_ptr<float>(), beta.data_ptr<float>(), acc.data_ptr<float>(), (int)R,
-                               dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu, cur_stream());
+                               dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu,
+                               const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream());
 }
 
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
@@ -781,7 +793,7 @@ void set_deterministic(bool on) { hcb::set_deterministic(on); }
 }  // namespace
 
 TORCH_LIBRARY(hcb, m) {
-  m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg) -> ()");
+  m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
   m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
@@ -807,14 +819,14 @@ TORCH_LIBRARY(hcb, m) {
   m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");
   m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
-  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor(f!)? mask=None) -> ()");
+  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor(f!)? mask=None, Tensor? shift=None) -> ()");
   m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg) -> ()");
-  m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu) -> ()");
+  m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu, Tensor(d!)? shift_out=None) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
   m.def("preprocess_images(Tensor src, Tensor desc, Tensor desc_host, Tensor(a!) out, float[] scale, float[] bias) -> ()");
   m.def("bn_relu_maxpool_acc(Tensor z, Tensor(a!) y, Tensor(b!) amax, int[] geom, Tensor acc, int R, float eps, "
         "float momentum, Tensor gamma, Tensor beta, Tensor(c!) saved_mean, Tensor(d!) saved_invstd, "
-        "Tensor(e!) run_mean, Tensor(f!) run_var) -> ()");
+        "Tensor(e!) run_mean, Tensor(f!) run_var, Tensor? shift=None) -> ()");
   m.def("dropout_fwd(Tensor x, Tensor(a!) y, Tensor(b!) mask, float keep, int seed, Tensor step) -> ()");
   m.def("dropout_bwd(Tensor dy, Tensor mask, Tensor(a!) dx, float keep) -> ()");
   m.def("synth_images(Tensor(a!) out, int C, int Cpad, float mean, float std, int seed) -> ()");

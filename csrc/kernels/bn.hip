@@ -551,7 +551,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ y, int ldy, const uint16_t* __restrict__ res,
     int ldr, int M, int C, int CVB, const float* __restrict__ acc, int R, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
-    float* saved_invstd, float* run_mean, float* run_var, uint8_t* __restrict__ mask) {
+    float* saved_invstd, float* run_mean, float* run_var, uint8_t* __restrict__ mask, const float* shift) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
@@ -584,8 +584,9 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
       const int c = gm.c0 + i;
-      float mu = sums[i] * inv_n;
-      float var = fmaxf(sums[gm.CB + i] * inv_n - mu * mu, 0.f);
+      const float d = sums[i] * inv_n;  // E[v - K]
+      float mu = d + (shift != nullptr ? shift[c] : 0.f);
+      float var = fmaxf(sums[gm.CB + i] * inv_n - d * d, 0.f);
       saved_mean[c] = mu;
       saved_invstd[c] = rsqrtf(var + eps);
       if (run_mean != nullptr) {
@@ -599,8 +600,9 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
   float sc[8], sh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    float mu = sums[cl + e] * inv_n;
-    float var = fmaxf(sums[gm.CB + cl + e] * inv_n - mu * mu, 0.f);
+    const float d = sums[cl + e] * inv_n;
+    float mu = d + (shift != nullptr ? shift[gm.c0 + cl + e] : 0.f);
+    float var = fmaxf(sums[gm.CB + cl + e] * inv_n - d * d, 0.f);
     float s = gam[e] * rsqrtf(var + eps);
     sc[e] = s;
     sh[e] = bet[e] - mu * s;
@@ -706,7 +708,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
     const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ dx, int lddx, int M, int C, int CVB,
     const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
-    int R, float* dgamma, float* dbeta, int relu) {
+    int R, float* dgamma, float* dbeta, int relu, float* shift_out) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]: dbeta, dgamma
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
@@ -734,6 +736,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
       dbeta[gm.c0 + i] = sums[i];
       dgamma[gm.c0 + i] = sums[gm.CB + i];
+      // this step's batch mean becomes the next step's statistic shift (the forward readers of
+      // the shift have all run: no block of this launch reads it)
+      if (shift_out != nullptr) shift_out[gm.c0 + i] = mean[gm.c0 + i];
     }
   }
   if (!active) return;
@@ -772,7 +777,8 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
     const uint16_t* __restrict__ z, int H, int W, int C, int CVB, uint16_t* __restrict__ y, int P, int Q, int ldy,
     uint8_t* __restrict__ amax, int kh, int kw, int sh, int sw, int ph, int pw, int Nimg, int M,
     const float* __restrict__ acc, int R, float eps, float momentum, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var) {
+    const float* __restrict__ beta, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
+    const float* shift) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
   const GroupMap gm = groupmap(CVB);
   reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
@@ -780,8 +786,9 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
       const int c = gm.c0 + i;
-      const float mu = sums[i] * inv_n;
-      const float var = fmaxf(sums[gm.CB + i] * inv_n - mu * mu, 0.f);
+      const float d = sums[i] * inv_n;
+      const float mu = d + (shift != nullptr ? shift[c] : 0.f);
+      const float var = fmaxf(sums[gm.CB + i] * inv_n - d * d, 0.f);
       saved_mean[c] = mu;
       saved_invstd[c] = rsqrtf(var + eps);
       if (run_mean != nullptr) {
@@ -796,8 +803,9 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
   const int cl = (threadIdx.x % CVB) * 8;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const float mu = sums[cl + e] * inv_n;
-    const float var = fmaxf(sums[gm.CB + cl + e] * inv_n - mu * mu, 0.f);
+    const float d = sums[cl + e] * inv_n;
+    const float mu = d + (shift != nullptr ? shift[gm.c0 + cl + e] : 0.f);
+    const float var = fmaxf(sums[gm.CB + cl + e] * inv_n - d * d, 0.f);
     const float s = gamma[gm.c0 + cl + e] * rsqrtf(var + eps);
     sc[e] = s;
     sft[e] = beta[gm.c0 + cl + e] - mu * s;
@@ -871,23 +879,24 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         void* mask, hipStream_t st) {
+                         void* mask, const float* shift, hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   hipLaunchKernelGGL(bn_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x, ldx,
                      (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta,
-                     relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask);
+                     relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask, shift);
 }
 
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
                                 int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
                                 float momentum, const float* gamma, const float* beta, float* saved_mean,
-                                float* saved_invstd, float* run_mean, float* run_var, hipStream_t st) {
+                                float* saved_invstd, float* run_mean, float* run_var, const float* shift,
+                                hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(N * P * Q, C, &cvb);
   hipLaunchKernelGGL(bn_relu_maxpool_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W,
                      C, cvb, (uint16_t*)y, P, Q, ldy, (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps,
-                     momentum, gamma, beta, saved_mean, saved_invstd, run_mean, run_var);
+                     momentum, gamma, beta, saved_mean, saved_invstd, run_mean, run_var, shift);
 }
 
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
@@ -907,12 +916,12 @@ void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv,
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
-                             hipStream_t st) {
+                             float* shift_out, hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   hipLaunchKernelGGL(bn_bwd_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)dy,
                      lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, (uint16_t*)dx, lddx, M, C, cvb, mean,
-                     invstd, gamma, beta, acc, R, dgamma, dbeta, relu);
+                     invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out);
 }
 
 }  // namespace hcb

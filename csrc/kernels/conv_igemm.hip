@@ -225,6 +225,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 
   const int nk = p.Kpad / BK;
   EpiPrefetch<WM, WN, TM, TN, BNB> pre;
+  pre.load_shift(p, n0, wn, lane);
   const bool early = BNB && nk <= EARLY_EPI_KSTEPS;
   if (early) pre.load(p, 0, m0, n0, tid);
   gload(0);
@@ -305,6 +306,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
   const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's k-steps
   if (kb > 0) al.seek(p, kb);
   EpiPrefetch<WM, WN, TM, TN, BNB> pre;
+  pre.load_shift(p, n0, wn, lane);
   const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS;
   if (early) pre.load(p, 0, m0, n0, tid);
 #pragma unroll

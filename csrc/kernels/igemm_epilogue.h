@@ -39,6 +39,17 @@ struct EpiPrefetch {
   static constexpr int CH = BNB ? (ITER < 4 ? ITER : 4) : 1;
   u32x4 pr[CH], pz[CH], py[CH];
   uint32_t pm[CH];  // mode 3: ReLU bit mask byte of the segment
+  // forward GEMMs: the BN statistic shift of each of the lane's accumulator columns, loaded
+  // before the main loop so the epilogue does not wait on it
+  static constexpr int NKC = BNB ? 1 : TN / 16;
+  float kc[NKC];
+  __device__ __forceinline__ void load_shift(const ConvParams& p, int n0, int wn, int lane) {
+#pragma unroll
+    for (int j = 0; j < NKC; ++j) {
+      const int gcol = n0 + wn * TN + j * 16 + (lane & 15);
+      kc[j] = (!BNB && p.stats != nullptr && p.stats_shift != nullptr && gcol < p.Nout) ? p.stats_shift[gcol] : 0.f;
+    }
+  }
   __device__ __forceinline__ void load(const ConvParams& p, int it0, int m0, int n0, int tid) {
     const int col = n0 + (tid % SEGS) * 8;
     if (col >= p.Nout) return;
@@ -73,20 +84,35 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   float* Cs = reinterpret_cast<float*>(smem);
   float* red = Cs + BM * LDC;  // [WM][2][BN] per-wave column partial sums
   if (p.stats != nullptr) {
-    // per-column partial BN statistics straight from the accumulators (rows beyond M are
-    // exact zeros): sum the wave's row quads in registers, then across the 4 lane groups
-    // that share a column with two xor-shuffles.
+    // per-column partial BN statistics straight from the accumulators, shifted by the
+    // column's K: sum the wave's row quads in registers, then across the 4 lane groups that
+    // share a column with two xor-shuffles. Rows at or beyond M (only in the last row tile)
+    // are skipped: their zero accumulators would otherwise add (-K)^2.
+    const int wrows = p.M - (m0 + wm * TM);
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       float s1 = 0.f, s2 = 0.f;
+      float kc = 0.f;
+      if constexpr (!BNB) kc = pre.kc[j];
+      if (wrows >= TM) {
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[i][j][e];
-          s1 += v;
-          s2 += v * v;
-        }
+          for (int e = 0; e < 4; ++e) {
+            const float v = acc[i][j][e] - kc;
+            s1 += v;
+            s2 += v * v;
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = i * 16 + fq * 4 + e < wrows ? acc[i][j][e] - kc : 0.f;
+            s1 += v;
+            s2 += v * v;
+          }
+      }
       s1 += __shfl_xor(s1, 16, 64);
       s2 += __shfl_xor(s2, 16, 64);
       s1 += __shfl_xor(s1, 32, 64);

@@ -38,6 +38,10 @@ struct ConvParams {
   const void* yres;  // beta-accumulate source (same layout as y)
   const float* bias;  // [Nout] or null
   float* stats;       // [tiles_m][2][Nout] or null
+  // per-column shift K of the BN statistics (null = 0): the epilogue accumulates sum(v - K) and
+  // sum((v - K)^2), so var = E[(v-K)^2] - E[v-K]^2 stays well conditioned when |mean| >> std
+  // (K = the layer's batch mean of the previous step, written by its BN backward)
+  const float* stats_shift;
   int N, H, W, C, ldx;
   int P, Q, R, S;
   int stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, idil_h, idil_w;
@@ -131,20 +135,19 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         void* mask, hipStream_t st);
+                         void* mask, const float* shift, hipStream_t st);
 // BN(acc statistics) + ReLU + max pool (NHWC, C contiguous): pooled y [N,P,Q] (row stride ldy) and
 // the uint8 window argmax [N,P,Q,C]; the BN+ReLU activation itself is not materialised
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
                                 int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
                                 float momentum, const float* gamma, const float* beta, float* saved_mean,
-                                float* saved_invstd, float* run_mean, float* run_var, hipStream_t st);
+                                float* saved_invstd, float* run_mean, float* run_var, const float* shift, hipStream_t st);
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
                               int relu, float* acc, int R, void* gout, int ldg, hipStream_t st);
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
-                             const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
-                             hipStream_t st);
+                             const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu, float* shift_out, hipStream_t st);
 
 // ---------------------------------------------------------------- pooling
 void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,

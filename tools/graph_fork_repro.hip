@@ -1,0 +1,133 @@
+// Minimal fork/join HIP-graph ordering checks, shaped like the training step's graph.
+//
+//   hipcc --offload-arch=gfx950 -O2 tools/graph_fork_repro.hip -o tools/graph_fork_repro
+//   DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 tools/graph_fork_repro <replays> <mode>
+//
+// mode 0 "fork": k_seed bumps a device epoch e and fills x = e; a forked branch computes
+//   y = x + 1 through a dependent chain, the main branch computes z = 2x meanwhile; after the
+//   join k_check counts elements with y != e + 1 or z != 2e.
+// mode 1 "segments": the data-parallel step's pattern -- a long chain of dependent kernels on
+//   the main stream (a = a + 1, 256 launches) with, every 32 launches, a fork of the comm stream
+//   off the main stream (ONE fork event and ONE join event, re-recorded per segment, as in
+//   csrc/comm/comm.cpp), a kernel on the comm stream over a separate buffer, the join event
+//   recorded without a wait; the main stream waits on the last join at the end.
+// mode 2: mode 1 with an EMPTY comm branch (the HCB_COMM_SKIP_RCCL=1 shape).
+// mode 3 / 4: modes 1 / 2 with a highest-priority comm stream (as the engine creates it).
+// Any ordering violation (a kernel started before its predecessor finished) shows up as a
+// nonzero error count.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                                     \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) {                                                                       \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));     \
+      std::exit(2);                                                                               \
+    }                                                                                             \
+  } while (0)
+
+__global__ void k_seed(const unsigned* epoch, float* x, int n) {
+  const float e = (float)((*epoch + 1) & 0xffff);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = e;
+}
+__global__ void k_bump(unsigned* epoch) { *epoch += 1; }
+__global__ void k_copy_add(const float* a, float* b, int n, float add) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b[i] = a[i] + add;
+}
+__global__ void k_scale(const float* a, float* b, int n, float s) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b[i] = a[i] * s;
+}
+__global__ void k_check(const unsigned* epoch, const float* y, float yadd, const float* z, float zmul, int n,
+                        unsigned* errors) {
+  const float e = (float)(*epoch & 0xffff);
+  unsigned bad = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    bad += (y[i] != e + yadd) + (z != nullptr && z[i] != zmul * e);
+  if (bad) atomicAdd(errors, bad);
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 1000;
+  const int mode = argc > 2 ? std::atoi(argv[2]) : 0;
+  const int n = mode == 0 ? 1 << 22 : 1 << 18;
+  float *x, *t0, *t1, *y, *z;
+  unsigned *epoch, *errors;
+  CK(hipMalloc(&x, n * 4));
+  CK(hipMalloc(&t0, n * 4));
+  CK(hipMalloc(&t1, n * 4));
+  CK(hipMalloc(&y, n * 4));
+  CK(hipMalloc(&z, n * 4));
+  CK(hipMalloc(&epoch, 4));
+  CK(hipMalloc(&errors, 4));
+  CK(hipMemset(epoch, 0, 4));
+  CK(hipMemset(errors, 0, 4));
+  CK(hipMemset(z, 0, n * 4));
+  hipStream_t s, c;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  if (mode >= 3) {  // the engine's comm stream: highest priority
+    int lo = 0, hi = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    CK(hipStreamCreateWithPriority(&c, hipStreamNonBlocking, hi));
+  } else {
+    CK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+  }
+  hipEvent_t fork, join;
+  CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+
+  const dim3 g(mode == 0 ? 1024 : 256), b(256);
+  const int chain = 256, seg = 32;
+  hipGraph_t graph;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  hipLaunchKernelGGL(k_seed, g, b, 0, s, epoch, x, n);
+  hipLaunchKernelGGL(k_bump, dim3(1), dim3(1), 0, s, epoch);
+  if (mode == 0) {
+    CK(hipEventRecord(fork, s));
+    CK(hipStreamWaitEvent(c, fork, 0));
+    hipLaunchKernelGGL(k_copy_add, g, b, 0, c, x, t0, n, 0.25f);
+    hipLaunchKernelGGL(k_copy_add, g, b, 0, c, t0, t1, n, 0.25f);
+    hipLaunchKernelGGL(k_copy_add, g, b, 0, c, t1, y, n, 0.5f);
+    CK(hipEventRecord(join, c));
+    hipLaunchKernelGGL(k_scale, g, b, 0, s, x, z, n, 2.f);
+    CK(hipStreamWaitEvent(s, join, 0));
+    hipLaunchKernelGGL(k_check, g, b, 0, s, epoch, y, 1.f, z, 2.f, n, errors);
+  } else {
+    float* a = x;
+    float* o = t0;
+    for (int k = 0; k < chain; ++k) {
+      hipLaunchKernelGGL(k_copy_add, g, b, 0, s, a, o, n, 1.f);
+      float* t = a;
+      a = o;
+      o = t;
+      if ((k + 1) % seg == 0) {
+        CK(hipEventRecord(fork, s));
+        CK(hipStreamWaitEvent(c, fork, 0));
+        // comm branch: reads the segment's result into a side buffer (like a bucket pack)
+        if (mode == 1 || mode == 3) hipLaunchKernelGGL(k_scale, g, b, 0, c, a, z, n, 1.f);
+        CK(hipEventRecord(join, c));
+      }
+    }
+    CK(hipStreamWaitEvent(s, join, 0));
+    hipLaunchKernelGGL(k_check, g, b, 0, s, epoch, a, (float)chain, nullptr, 0.f, n, errors);
+    // z holds the LAST segment's value (e + chain) when the comm branch ran in order
+    if (mode == 1 || mode == 3) hipLaunchKernelGGL(k_check, g, b, 0, s, epoch, z, (float)chain, nullptr, 0.f, n, errors);
+  }
+  CK(hipStreamEndCapture(s, &graph));
+  hipGraphExec_t exec;
+  CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+
+  for (int it = 0; it < iters; ++it) CK(hipGraphLaunch(exec, s));
+  CK(hipStreamSynchronize(s));
+  unsigned host_err = 0, host_epoch = 0;
+  CK(hipMemcpy(&host_err, errors, 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(&host_epoch, epoch, 4, hipMemcpyDeviceToHost));
+  const char* pc = std::getenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE");
+  std::printf("graph_fork_repro: mode=%d DEBUG_CLR_GRAPH_PACKET_CAPTURE=%s replays=%d epoch=%u errors=%u\n", mode,
+              pc ? pc : "(unset)", iters, host_epoch, host_err);
+  CK(hipGraphExecDestroy(exec));
+  CK(hipGraphDestroy(graph));
+  return host_err == 0 && host_epoch == (unsigned)iters ? 0 : 1;
+}
