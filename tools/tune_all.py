@@ -25,7 +25,7 @@ def main():
             continue
         t0 = time.time()
         m = create_model(name, device="cuda")
-        n = autotune.tune_model(m, b, save=True)
+        n = autotune.tune_model(m, b, verbose=True, save=True)  # per-layer lines: progress for gpurun
         del m
         torch.cuda.empty_cache()
         print(f"{name} bs{b}: tuned {n} problems in {time.time() - t0:.0f} s", flush=True)
