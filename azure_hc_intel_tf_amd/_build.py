@@ -6,6 +6,8 @@ box with the repo snapshot):
 * ``_hcb_kernels.so`` -- the hand-written CDNA4 kernels (``csrc/kernels/*.hip``, compiled
   with ``hipcc --offload-arch=gfx950``) plus their ``torch.library`` registrations
   (``csrc/bindings.cpp``), loaded with ``torch.ops.load_library``.
+* ``_hcb_kernels_f16.so`` -- the same kernel sources built for IEEE-fp16 activations
+  (``-DHCB_F16``, C++ and torch.library namespace ``hcb16``): the native ``--use_fp16`` path.
 * ``_hcb_data*.so`` -- the native real-data pipeline core (TFRecord / tf.Example / crop
   windows / prefetch threads; ``csrc/data/*.cpp``).
 * ``_hcb_engine_cpu*.so`` -- the bucket engine core on an in-process fake fabric (CPU tests).
@@ -32,6 +34,10 @@ BUILD = os.path.join(REPO, "build", "obj")
 ARCH = os.environ.get("HCB_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 KERNELS_SO = os.path.join(PKG_DIR, "_hcb_kernels.so")
+KERNELS_F16_SO = os.path.join(PKG_DIR, "_hcb_kernels_f16.so")
+# IEEE-fp16 build: the activation-type switch of csrc/kernels/common.h plus a renamed namespace
+# (C++ symbols and torch.library ops), so both libraries load into one process side by side
+F16_FLAGS = ["-DHCB_F16", "-Dhcb=hcb16"]
 COMM_SO = os.path.join(PKG_DIR, "_hcb_comm.so")
 
 
@@ -72,36 +78,39 @@ def _headers():
 NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
-def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build_kernels(verbose: bool = False, jobs: int = 8, f16: bool = False) -> str:
+    build = os.path.join(BUILD, "f16") if f16 else BUILD
+    so = KERNELS_F16_SO if f16 else KERNELS_SO
+    extra = F16_FLAGS if f16 else []
+    os.makedirs(build, exist_ok=True)
     hdrs = _headers()
     hips = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     inc, tlib, abi = _torch_paths()
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     objs, jobs_list = [], []
     for src in hips:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(build, os.path.basename(src) + ".o")
         objs.append(obj)
         if _newer(obj, [src] + hdrs):
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                              "-munsafe-fp-atomics", "-Wno-unused-result", *NO_PACKED_FP32,
+                              "-munsafe-fp-atomics", "-Wno-unused-result", *NO_PACKED_FP32, *extra,
                               "-I" + os.path.join(CSRC, "kernels"), "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.o")
+    bobj = os.path.join(build, "bindings.o")
     objs.append(bobj)
     if _newer(bobj, [bsrc] + hdrs):
-        jobs_list.append(["g++", "-std=c++17", "-O2", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+        jobs_list.append(["g++", "-std=c++17", "-O2", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM", *extra,
                           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I" + os.path.join(ROCM, "include"),
                           *["-I" + i for i in inc], "-I" + CSRC, "-c", bsrc, "-o", bobj])
     if jobs_list:
         with _cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
-    if _newer(KERNELS_SO, objs):
-        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", KERNELS_SO, *objs,
-              "-Wl,-soname,_hcb_kernels.so",
+    if _newer(so, objs):
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so, *objs,
+              "-Wl,-soname," + os.path.basename(so),
               "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip",
               "-Wl,-rpath," + tlib], verbose)
-    return KERNELS_SO
+    return so
 
 
 def build_comm(verbose: bool = False, jobs: int = 8) -> str:
@@ -198,6 +207,7 @@ def build_tools(verbose: bool = False) -> str:
 
 def build_all(verbose: bool = False) -> None:
     build_kernels(verbose)
+    build_kernels(verbose, f16=True)
     build_comm(verbose)
     build_data(verbose)
     build_engine_cpu(verbose)

@@ -47,9 +47,12 @@ class CNNModel:
         self.compute_dtype = check_compute_dtype(compute_dtype, device)
         self.image_size = image_size or self.default_image_size
         self.device = torch.device(device)
-        # native: the hand-written bf16 HIP kernels; otherwise (CPU, or a GPU in the fp32 /
-        # IEEE-fp16 reference-precision mode) the PyTorch path of ops/functional.py
-        self.native = self.device.type == "cuda" and self.compute_dtype == "bf16"
+        # native: the hand-written HIP kernels (bf16, or the IEEE-fp16 build); otherwise (CPU, or
+        # a GPU in the fp32 reference-precision mode) the PyTorch path of ops/functional.py
+        from ..ops import functional as Fn
+
+        self.native = self.device.type == "cuda" and (
+            self.compute_dtype == "bf16" or (self.compute_dtype == "fp16" and Fn.F16_NATIVE))
         if image_channels is None:
             image_channels = 8 if self.native else 3
         assert image_channels in (3, 8) and (not self.native or image_channels == 8)
@@ -58,7 +61,8 @@ class CNNModel:
         self.ps = ParamStore(seed=seed)
         self.layers: List = []
         self.build()
-        self.ps.finalize(self.device, pack=self.native)
+        self.ps.finalize(self.device, dtype_pack=TORCH_DTYPES[self.compute_dtype] if self.native else torch.bfloat16,
+                         pack=self.native)
 
     # -- to implement
     def build(self):

@@ -30,9 +30,13 @@ _GPU_ACT_DTYPE = [torch.bfloat16]
 
 
 def set_gpu_compute_dtype(dt: torch.dtype) -> None:
-    """Activation dtype of GPU models built / stepped from now on: bf16 (the hand-written HIP
-    kernels) or fp32 / fp16 (the reference-precision PyTorch path, --compute_dtype)."""
+    """Activation dtype of GPU models built / stepped from now on: bf16 or IEEE fp16 (the
+    hand-written HIP kernels, bf16 / fp16 builds) or fp32 (the reference-precision PyTorch
+    path, --compute_dtype)."""
+    from ..ops import _ext
+
     _GPU_ACT_DTYPE[0] = dt
+    _ext.set_act("fp16" if dt == torch.float16 else "bf16")
 
 
 def act_dtype(device) -> torch.dtype:
@@ -399,7 +403,7 @@ class StemS2D(ConvBN):
 
     def _folded_weight(self, dev):
         if self._wfold is None or self._wfold.device != dev:
-            self._wfold = torch.empty((self.spec.cout, 256), dtype=torch.bfloat16, device=dev)
+            self._wfold = torch.empty((self.spec.cout, 256), dtype=act_dtype(dev), device=dev)
         from ..ops import _ext
 
         _ext.ops().stem_wfold(self.w.data, self._wfold)

@@ -74,8 +74,15 @@ def _time(fn, reps=5) -> float:
     return s.elapsed_time(e) / reps
 
 
+def _act():
+    """16-bit activation dtype of the kernel library being tuned (bf16 / IEEE-fp16 build)."""
+    from ..nn.layers import act_dtype
+
+    return act_dtype("cuda")
+
+
 def _bf(shape, dev):
-    return torch.randn(shape, device=dev).to(torch.bfloat16)
+    return torch.randn(shape, device=dev).to(_act())
 
 
 def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
@@ -100,7 +107,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     # forward
     k = Fn.fwd_key(M, Cout, spec.K, taps)
     if k not in Fn._tuned:
-        y = torch.empty((N, P, Q, Cout), dtype=torch.bfloat16, device=dev)
+        y = torch.empty((N, P, Q, Cout), dtype=_act(), device=dev)
         best = None
         acc = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
         for cfg in Fn.fwd_candidates(Cout):
@@ -114,7 +121,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
         out.append((k, best))
     # data gradient
     if layer.need_dx:
-        dx = torch.zeros((N, H, W, Cin), dtype=torch.bfloat16, device=dev)
+        dx = torch.zeros((N, H, W, Cin), dtype=_act(), device=dev)
         k = Fn.fwd_key(geo[0], Cin, geo[1], taps)
         if k not in Fn._tuned:
             best = None

@@ -49,8 +49,8 @@ def set_deterministic(on: bool = True) -> None:
     later in a fixed order), single-block bias column sums. Slower; for debugging and the
     determinism test."""
     _DET[0] = bool(on)
-    if _ext.loaded():
-        _ext.ops().set_deterministic(bool(on))
+    for ns in _ext.loaded_namespaces():
+        ns.set_deterministic(bool(on))
 
 
 def deterministic() -> bool:
@@ -63,11 +63,17 @@ def det_replicas(M: int) -> int:
     return max(1, (M + 63) // 64)
 
 
+# IEEE-fp16 activations through the fp16 build of the HIP kernels (HCB_F16_NATIVE=0: through
+# the PyTorch / MIOpen path instead, the round-2 reference-precision form)
+F16_NATIVE = os.environ.get("HCB_F16_NATIVE", "1") != "0"
+
+
 def native(t) -> bool:
-    """True when ``t`` goes through the hand-written HIP kernels: a bf16 activation on the GPU.
-    Other GPU tensors (the fp32 / IEEE-fp16 reference-precision mode, --compute_dtype) take
-    the PyTorch path below (MIOpen / rocBLAS), the same code as the CPU path."""
-    return t.is_cuda and t.dtype == torch.bfloat16
+    """True when ``t`` goes through the hand-written HIP kernels: a bf16 (or, with the fp16
+    build, IEEE-fp16) activation on the GPU. Other GPU tensors (the fp32 reference-precision
+    mode, --compute_dtype fp32) take the PyTorch path below (MIOpen / rocBLAS), the same code
+    as the CPU path."""
+    return t.is_cuda and (t.dtype == torch.bfloat16 or (t.dtype == torch.float16 and F16_NATIVE))
 
 
 @dataclass
@@ -176,13 +182,18 @@ _splitk = {}
 
 
 def ensure_splitk_workspace(device) -> None:
+    """One workspace per device, registered with each kernel library (bf16 / fp16 build) that
+    launches convs; the libraries never run concurrently on one stream."""
     dev = torch.device(device)
-    if _splitk.get("dev") == dev:
+    key = _ext._ACT[0]
+    if _splitk.get("dev") != dev:
+        _splitk.clear()
+        _splitk.update(dev=dev, ws=torch.empty(SPLITK_WS_FLOATS, dtype=torch.float32, device=dev),
+                       cnt=torch.zeros(SPLITK_MAX_TILES, dtype=torch.int32, device=dev), libs=set())
+    if key in _splitk["libs"]:
         return
-    ws = torch.empty(SPLITK_WS_FLOATS, dtype=torch.float32, device=dev)
-    cnt = torch.zeros(SPLITK_MAX_TILES, dtype=torch.int32, device=dev)
-    _ext.ops().set_splitk_workspace(ws, cnt)
-    _splitk.update(dev=dev, ws=ws, cnt=cnt)
+    _ext.ops().set_splitk_workspace(_splitk["ws"], _splitk["cnt"])
+    _splitk["libs"].add(key)
 
 
 def splitk_candidates(cfg: int, M: int, N: int, K: int):
@@ -673,7 +684,7 @@ def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None)
     """Per-row cross entropy (into row_loss) and dlogits = (softmax - onehot) * scale
     (* scale_dev[0], a device-resident loss scale, when given)."""
     B = labels.numel()
-    if logits.is_cuda and dlogits.dtype == torch.bfloat16:
+    if native(dlogits):
         _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale, scale_dev)
         return
     if scale_dev is not None:

@@ -36,7 +36,7 @@ def load():
         if not _loaded:
             from ..ops import _ext
 
-            _ext.load()  # the comm library links against the kernel library
+            _ext.load(act="bf16")  # the comm library links against the (bf16) kernel library
             if not os.path.exists(COMM_SO):
                 from .. import _build
 

@@ -389,7 +389,7 @@ def synthetic_batch(model, batch_size: int, seed: int = 0):
     shape = model.input_shape(batch_size)
     dev = model.device
     if dev.type == "cuda" and getattr(model, "native", True):
-        img = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+        img = torch.empty(shape, dtype=model.act_dtype, device=dev)  # (makes the model current)
         lab = torch.empty(batch_size, dtype=torch.int64, device=dev)
         hcb = _ext.ops()
         hcb.synth_images(img, 3, shape[3], 127.0, 60.0, seed + 1)

@@ -1,4 +1,5 @@
-// torch.library registrations (namespace `hcb`) for the hand-written gfx950 kernels.
+// torch.library registrations (namespace `hcb`; `hcb16` for the IEEE-fp16 build of the same
+// sources, -DHCB_F16 -Dhcb=hcb16) for the hand-written gfx950 kernels.
 //
 // Every op is a thin, allocation-free launcher: Python pre-allocates outputs with the
 // caching allocator (so the whole training step can be captured in a HIP graph) and
@@ -15,6 +16,17 @@
 
 using at::Tensor;
 
+#ifdef HCB_F16
+constexpr at::ScalarType kAct = at::kHalf;  // 16-bit activation / GEMM operand type of this build
+#define HCB_ACT_NAME "float16"
+#else
+constexpr at::ScalarType kAct = at::kBFloat16;
+#define HCB_ACT_NAME "bfloat16"
+#endif
+// library name through one macro level, so -Dhcb=hcb16 also renames the torch.library namespace
+#define HCB_TORCH_LIBRARY(ns, m) TORCH_LIBRARY(ns, m)
+#define HCB_TORCH_LIBRARY_IMPL(ns, k, m) TORCH_LIBRARY_IMPL(ns, k, m)
+
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -28,9 +40,9 @@ int64_t g_splitk_cnt_n = 0;
 void check_cuda(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), "hcb: ", name, " must be a GPU tensor");
 }
-void check_bf16(const Tensor& t, const char* name) {
+void check_act(const Tensor& t, const char* name) {
   check_cuda(t, name);
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "hcb: ", name, " must be bfloat16");
+  TORCH_CHECK(t.scalar_type() == kAct, "hcb: ", name, " must be " HCB_ACT_NAME " (the activation dtype of this build)");
 }
 void check_f32(const Tensor& t, const char* name) {
   check_cuda(t, name);
@@ -54,8 +66,8 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
                             const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
                             at::IntArrayRef g, int64_t cfg) {
   TORCH_CHECK(g.size() >= 28 && g.size() <= 31, "hcb.conv_igemm: geom must have 28 (+relu, +stats_R, +splits) entries");
-  check_bf16(x, "x");
-  check_bf16(w, "w");
+  check_act(x, "x");
+  check_act(w, "w");
   check_cuda(y, "y");
   hcb::ConvParams p{};
   p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];
@@ -84,7 +96,7 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   if (p.remap)
     TORCH_CHECK((p.P - 1) * p.osh < p.OH && (p.Q - 1) * p.osw < p.OW, "hcb.conv_igemm: remap out of range");
   int64_t esz = p.out_f32 ? 4 : 2;
-  TORCH_CHECK(y.scalar_type() == (p.out_f32 ? at::kFloat : at::kBFloat16), "hcb.conv_igemm: y dtype");
+  TORCH_CHECK(y.scalar_type() == (p.out_f32 ? at::kFloat : kAct), "hcb.conv_igemm: y dtype");
   check_range(y, rows * p.ldy * esz - (p.ldy - ((p.Nout + 7) / 8) * 8) * esz, "y");
   check_align16(x.data_ptr(), "x");
   check_align16(w.data_ptr(), "w");
@@ -170,13 +182,13 @@ void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10
   TORCH_CHECK(ld % 8 == 0 && ld >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm_bnb: bad ld");
   int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
   int64_t need = (rows - 1) * ld * 2 + ((p.Nout + 7) / 8) * 8 * 2;
-  check_bf16(z, "z");
+  check_act(z, "z");
   check_range(z, need, "z");
   check_align16(z.data_ptr(), "z");
   p.bnb_y = nullptr;
   if (mode == 1) {
     TORCH_CHECK(yact.has_value(), "hcb.conv_igemm_bnb: mode 1 needs y");
-    check_bf16(*yact, "y");
+    check_act(*yact, "y");
     check_range(*yact, need, "y");
     check_align16(yact->data_ptr(), "y");
     p.bnb_y = yact->data_ptr();
@@ -214,8 +226,8 @@ int64_t conv_tiles_m(int64_t M, int64_t cfg) {
 void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArrayRef g, int64_t cfg,
                 int64_t splits) {
   TORCH_CHECK(g.size() == 17, "hcb.conv_wgrad: geom must have 17 entries");
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
+  check_act(dy, "dy");
+  check_act(x, "x");
   check_f32(dw, "dw");
   hcb::WgradParams p{};
   p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];
@@ -253,7 +265,7 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArra
 }
 
 void bn_stats(const Tensor& x, int64_t M, int64_t C, int64_t ldx, const Tensor& slab) {
-  check_bf16(x, "x");
+  check_act(x, "x");
   check_f32(slab, "slab");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0, "hcb.bn_stats: C % 8 == 0, C <= 2048");
   check_range(x, ((M - 1) * ldx + C) * 2, "x");
@@ -290,14 +302,14 @@ void bn_finalize(const Tensor& slab, int64_t T, int64_t C, double count, double 
 void bn_apply(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, const c10::optional<Tensor>& res,
               int64_t ldr, int64_t M, int64_t C, const Tensor& mean, const Tensor& invstd,
               const Tensor& gamma, const Tensor& beta, int64_t relu) {
-  check_bf16(x, "x");
-  check_bf16(y, "y");
+  check_act(x, "x");
+  check_act(y, "y");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldy % 8 == 0, "hcb.bn_apply: C/ld");
   check_range(x, ((M - 1) * ldx + C) * 2, "x");
   check_range(y, ((M - 1) * ldy + C) * 2, "y");
   const void* rp = nullptr;
   if (res.has_value()) {
-    check_bf16(*res, "res");
+    check_act(*res, "res");
     TORCH_CHECK(ldr % 8 == 0, "hcb.bn_apply: ldr");
     check_range(*res, ((M - 1) * ldr + C) * 2, "res");
     rp = res->data_ptr();
@@ -311,8 +323,8 @@ void bn_bwd_reduce(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& 
                    const Tensor& x, int64_t ldx, int64_t M, int64_t C, const Tensor& mean,
                    const Tensor& invstd, const Tensor& gamma, const Tensor& beta, int64_t relu,
                    const Tensor& slab, const c10::optional<Tensor>& gout, int64_t ldg) {
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
+  check_act(dy, "dy");
+  check_act(x, "x");
   check_f32(slab, "slab");
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "hcb.bn_bwd_reduce: C");
   check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
@@ -325,7 +337,7 @@ void bn_bwd_reduce(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& 
   }
   void* gp = nullptr;
   if (gout.has_value()) {
-    check_bf16(*gout, "gout");
+    check_act(*gout, "gout");
     check_range(*gout, ((M - 1) * ldg + C) * 2, "gout");
     gp = gout->data_ptr();
   }
@@ -353,9 +365,9 @@ void bn_bwd_apply(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y
                   const Tensor& x, int64_t ldx, const Tensor& dx, int64_t lddx, int64_t M, int64_t C,
                   const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
                   const Tensor& dgamma, const Tensor& dbeta, int64_t relu) {
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
-  check_bf16(dx, "dx");
+  check_act(dy, "dy");
+  check_act(x, "x");
+  check_act(dx, "dx");
   check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
   check_range(x, ((M - 1) * ldx + C) * 2, "x");
   check_range(dx, ((M - 1) * lddx + C) * 2, "dx");
@@ -377,8 +389,8 @@ void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, a
                          const Tensor& saved_mean, const Tensor& saved_invstd, const Tensor& run_mean,
                          const Tensor& run_var, const c10::optional<Tensor>& shift) {
   TORCH_CHECK(g.size() == 13, "hcb.bn_relu_maxpool_acc: geom");
-  check_bf16(z, "z");
-  check_bf16(y, "y");
+  check_act(z, "z");
+  check_act(y, "y");
   check_cuda(amax, "amax");
   const int64_t N = g[0], H = g[1], W = g[2], C = g[3], P = g[4], Q = g[5], ldy = g[6];
   TORCH_CHECK(z.is_contiguous() && z.numel() == N * H * W * C, "hcb.bn_relu_maxpool_acc: z contiguous [N,H,W,C]");
@@ -402,8 +414,8 @@ void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, a
 // geom = [N,H,W,C,ldx,P,Q,ldy,kh,kw,sh,sw,ph,pw,is_max,incl_pad]
 void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx, at::IntArrayRef g) {
   TORCH_CHECK(g.size() == 16, "hcb.pool_fwd: geom");
-  check_bf16(x, "x");
-  check_bf16(y, "y");
+  check_act(x, "x");
+  check_act(y, "y");
   TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_fwd: C/ld % 8");
   TORCH_CHECK(g[0] * g[5] * g[6] * (g[3] / 8) < (1ll << 31), "hcb.pool_fwd: 32-bit index range");
   check_range(x, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "x");
@@ -421,10 +433,10 @@ void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx
 void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx,
               const Tensor& dx, at::IntArrayRef g, bool accumulate) {
   TORCH_CHECK(g.size() == 16, "hcb.pool_bwd: geom");
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
-  check_bf16(y, "y");
-  check_bf16(dx, "dx");
+  check_act(dy, "dy");
+  check_act(x, "x");
+  check_act(y, "y");
+  check_act(dx, "dx");
   check_range(x, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "x");
   check_range(dx, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "dx");
   check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "y");
@@ -440,8 +452,8 @@ void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::opt
 }
 
 void gap_fwd(const Tensor& x, const Tensor& y, int64_t N, int64_t HW, int64_t C) {
-  check_bf16(x, "x");
-  check_bf16(y, "y");
+  check_act(x, "x");
+  check_act(y, "y");
   TORCH_CHECK(C % 8 == 0, "hcb.gap_fwd: C % 8");
   check_range(x, N * HW * C * 2, "x");
   check_range(y, N * C * 2, "y");
@@ -449,8 +461,8 @@ void gap_fwd(const Tensor& x, const Tensor& y, int64_t N, int64_t HW, int64_t C)
 }
 
 void gap_bwd(const Tensor& dy, const Tensor& dx, int64_t N, int64_t HW, int64_t C) {
-  check_bf16(dy, "dy");
-  check_bf16(dx, "dx");
+  check_act(dy, "dy");
+  check_act(dx, "dx");
   check_range(dy, N * C * 2, "dy");
   check_range(dx, N * HW * C * 2, "dx");
   hcb::launch_gap_bwd(dy.data_ptr(), dx.data_ptr(), (int)N, (int)HW, (int)C, cur_stream());
@@ -462,7 +474,7 @@ void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_
   check_f32(logits, "logits");
   check_cuda(labels, "labels");
   TORCH_CHECK(labels.scalar_type() == at::kLong, "hcb.softmax_xent: labels int64");
-  check_bf16(dlogits, "dlogits");
+  check_act(dlogits, "dlogits");
   int64_t B = labels.numel();
   check_range(logits, B * ld * 4, "logits");
   check_range(dlogits, B * lddl * 2, "dlogits");
@@ -490,7 +502,7 @@ void colsum(const Tensor& g, int64_t ld, int64_t M, int64_t N, const Tensor& out
   check_cuda(g, "g");
   check_f32(out, "out");
   bool f32 = g.scalar_type() == at::kFloat;
-  TORCH_CHECK(f32 || g.scalar_type() == at::kBFloat16, "hcb.colsum: dtype");
+  TORCH_CHECK(f32 || g.scalar_type() == kAct, "hcb.colsum: dtype");
   // the kernel reads whole 8-column vectors: rows padded to 8 columns, 16-byte aligned
   TORCH_CHECK(ld % 8 == 0 && ld >= ((N + 7) / 8) * 8, "hcb.colsum: ld must be a multiple of 8 covering N");
   check_range(g, ((M - 1) * ld + ((N + 7) / 8) * 8) * (f32 ? 4 : 2), "g");
@@ -517,7 +529,7 @@ void sgd_momentum(const Tensor& w, const Tensor& mom, const Tensor& g, int64_t n
 
 void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, int64_t max_work) {
   check_f32(master, "master");
-  check_bf16(pack, "pack");
+  check_act(pack, "pack");
   check_cuda(table, "table");
   TORCH_CHECK(table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 9, "hcb.weight_pack: table [n][9] int64");
   TORCH_CHECK(table.is_contiguous(), "hcb.weight_pack: table contiguous");
@@ -528,15 +540,15 @@ void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, 
 
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {
   check_f32(x, "x");
-  check_bf16(y, "y");
+  check_act(y, "y");
   TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "hcb.cast: shape");
   hcb::launch_cast_f32_bf16(x.data_ptr<float>(), (uint16_t*)y.data_ptr(), x.numel(), cur_stream());
 }
 
 void add_bf16(const Tensor& a, const Tensor& b, const Tensor& y) {
-  check_bf16(a, "a");
-  check_bf16(b, "b");
-  check_bf16(y, "y");
+  check_act(a, "a");
+  check_act(b, "b");
+  check_act(y, "y");
   TORCH_CHECK(a.numel() == b.numel() && a.numel() == y.numel() && a.numel() % 8 == 0, "hcb.add_bf16: sizes");
   TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && y.is_contiguous(), "hcb.add_bf16: contiguous");
   hcb::launch_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream());
@@ -548,8 +560,8 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                   const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& saved_mean,
                   const Tensor& saved_invstd, const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv,
                   const c10::optional<Tensor>& mask, const c10::optional<Tensor>& shift) {
-  check_bf16(x, "x");
-  check_bf16(y, "y");
+  check_act(x, "x");
+  check_act(y, "y");
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldy % 8 == 0 && R >= 1, "hcb.bn_apply_acc: C/ld/R");
   TORCH_CHECK(acc.numel() >= R * 2 * C && saved_mean.numel() >= C && saved_invstd.numel() >= C, "hcb.bn_apply_acc: sizes");
@@ -557,7 +569,7 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
   check_range(y, ((M - 1) * ldy + C) * 2, "y");
   const void* rp = nullptr;
   if (res.has_value()) {
-    check_bf16(*res, "res");
+    check_act(*res, "res");
     TORCH_CHECK(ldr % 8 == 0, "hcb.bn_apply_acc: ldr");
     check_range(*res, ((M - 1) * ldr + C) * 2, "res");
     rp = res->data_ptr();
@@ -581,8 +593,8 @@ void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tenso
                        const Tensor& x, int64_t ldx, int64_t M, int64_t C, const Tensor& mean, const Tensor& invstd,
                        const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& acc, int64_t R,
                        const c10::optional<Tensor>& gout, int64_t ldg) {
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
+  check_act(dy, "dy");
+  check_act(x, "x");
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_reduce_acc: C/R");
   check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
@@ -595,7 +607,7 @@ void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tenso
   }
   void* gp = nullptr;
   if (gout.has_value()) {
-    check_bf16(*gout, "gout");
+    check_act(*gout, "gout");
     check_range(*gout, ((M - 1) * ldg + C) * 2, "gout");
     gp = gout->data_ptr();
   }
@@ -610,9 +622,9 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
                       const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
                       const Tensor& acc, int64_t R, const Tensor& dgamma, const Tensor& dbeta, int64_t relu,
                       const c10::optional<Tensor>& shift_out) {
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
-  check_bf16(dx, "dx");
+  check_act(dy, "dy");
+  check_act(x, "x");
+  check_act(dx, "dx");
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_apply_acc: C/R");
   check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
@@ -632,17 +644,17 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
 }
 
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
-  check_bf16(dy, "dy");
-  check_bf16(y, "y");
-  check_bf16(dz, "dz");
+  check_act(dy, "dy");
+  check_act(y, "y");
+  check_act(dz, "dz");
   TORCH_CHECK(dy.numel() == y.numel() && dy.numel() == dz.numel() && dy.numel() % 8 == 0, "hcb.relu_bwd: sizes");
   TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dz.is_contiguous(), "hcb.relu_bwd: contiguous");
   hcb::launch_relu_bwd(dy.data_ptr(), y.data_ptr(), dz.data_ptr(), dy.numel(), cur_stream());
 }
 
 void dropout_fwd(const Tensor& x, const Tensor& y, const Tensor& mask, double keep, int64_t seed, const Tensor& step) {
-  check_bf16(x, "x");
-  check_bf16(y, "y");
+  check_act(x, "x");
+  check_act(y, "y");
   check_cuda(mask, "mask");
   check_cuda(step, "step");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && mask.is_contiguous(), "hcb.dropout_fwd: contiguous");
@@ -656,8 +668,8 @@ void dropout_fwd(const Tensor& x, const Tensor& y, const Tensor& mask, double ke
 }
 
 void dropout_bwd(const Tensor& dy, const Tensor& mask, const Tensor& dx, double keep) {
-  check_bf16(dy, "dy");
-  check_bf16(dx, "dx");
+  check_act(dy, "dy");
+  check_act(dx, "dx");
   check_cuda(mask, "mask");
   TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous() && mask.is_contiguous(), "hcb.dropout_bwd: contiguous");
   TORCH_CHECK(dy.numel() == dx.numel() && dy.numel() % 8 == 0 && mask.scalar_type() == at::kByte &&
@@ -680,7 +692,7 @@ void l2norm_sq(const Tensor& x, const Tensor& out) {
 }
 
 void synth_images(const Tensor& out, int64_t C, int64_t Cpad, double mean, double std, int64_t seed) {
-  check_bf16(out, "out");
+  check_act(out, "out");
   TORCH_CHECK(out.numel() % Cpad == 0, "hcb.synth_images: numel % Cpad");
   hcb::launch_synth_images(out.data_ptr(), out.numel() / Cpad, (int)C, (int)Cpad, (float)mean, (float)std,
                            (uint64_t)seed, cur_stream());
@@ -697,7 +709,7 @@ void preprocess_images(const Tensor& src, const Tensor& desc, const Tensor& desc
                        at::ArrayRef<double> scale, at::ArrayRef<double> bias) {
   check_cuda(src, "src");
   check_cuda(desc, "desc");
-  check_bf16(out, "out");
+  check_act(out, "out");
   TORCH_CHECK(src.scalar_type() == at::kByte && src.is_contiguous(), "hcb.preprocess_images: src uint8 contiguous");
   TORCH_CHECK(desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 4 && desc.is_contiguous(),
               "hcb.preprocess_images: desc int64 [B][4]");
@@ -754,8 +766,8 @@ void bucket_unpack(const Tensor& src, const Tensor& dst, double scale) {
 void stem_s2d(const Tensor& x, const Tensor& out, int64_t pad) {
   check_cuda(x, "x");
   check_cuda(out, "out");
-  TORCH_CHECK(x.dim() == 4 && out.dim() == 4 && x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
-              "hcb.stem_s2d: bf16 NHWC tensors");
+  TORCH_CHECK(x.dim() == 4 && out.dim() == 4 && x.scalar_type() == kAct && out.scalar_type() == kAct,
+              "hcb.stem_s2d: 16-bit NHWC tensors");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.size(3) >= 4 && x.size(3) % 4 == 0 && out.size(3) == 16 &&
                   out.size(0) == x.size(0),
               "hcb.stem_s2d: x [N][H][W][>=4, multiple of 4] -> out [N][Hs][Ws][16]");
@@ -772,7 +784,7 @@ void stem_wfold(const Tensor& w, const Tensor& wp) {
   check_cuda(wp, "wp");
   TORCH_CHECK(w.dim() == 4 && w.size(1) == 7 && w.size(2) == 7 && w.size(3) >= 3 && w.is_contiguous(),
               "hcb.stem_wfold: w [cout][7][7][>=3] fp32");
-  TORCH_CHECK(wp.scalar_type() == at::kBFloat16 && wp.is_contiguous() && wp.numel() == w.size(0) * 256,
+  TORCH_CHECK(wp.scalar_type() == kAct && wp.is_contiguous() && wp.numel() == w.size(0) * 256,
               "hcb.stem_wfold: wp bf16 [cout][256]");
   hcb::launch_stem_wfold(w.data_ptr<float>(), (int)w.size(0), (int)w.size(3),
                          reinterpret_cast<uint16_t*>(wp.data_ptr()), cur_stream());
@@ -792,7 +804,7 @@ void set_deterministic(bool on) { hcb::set_deterministic(on); }
 
 }  // namespace
 
-TORCH_LIBRARY(hcb, m) {
+HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
   m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
@@ -839,7 +851,7 @@ TORCH_LIBRARY(hcb, m) {
   m.def("stem_wgrad_unfold(Tensor dwp, Tensor(a!) dw) -> ()");
 }
 
-TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
+HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("conv_igemm", conv_igemm);
   m.impl("conv_igemm_bnb", conv_igemm_bnb);
   m.impl("nonfinite", nonfinite);

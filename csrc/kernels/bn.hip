@@ -634,7 +634,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const uint32_t h = (o[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-            bits |= ((h - 1u) < 0x7f80u ? 1u : 0u) << e;  // 0 < bf16 <= +inf
+            bits |= ((h - 1u) < HCB_ACT_POS_INF ? 1u : 0u) << e;  // 0 < y <= +inf
           }
           mask[(size_t)m * (C >> 3) + gm.cv] = (uint8_t)bits;
         }

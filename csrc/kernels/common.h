@@ -7,8 +7,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -21,6 +19,19 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // Offset used to force a buffer load out of range (returns 0).
 #define HCB_OOB 0x80000000u
 
+// 16-bit activation type of this build of the library: bf16 (default) or, with -DHCB_F16, IEEE
+// fp16 (the reference's --use_fp16 precision; the same sources are compiled a second time into
+// _hcb_kernels_f16.so with the namespace renamed to hcb16). Activations, GEMM operands and
+// 16-bit gradients use act2f / f2act / pack8 / unpack8 / mfma16; explicitly-bf16 data (the
+// bf16 wire format of the gradient buckets) keeps bf2f / f2bf.
+#ifdef HCB_F16
+typedef _Float16 act16x8 __attribute__((ext_vector_type(8)));
+#define HCB_ACT_POS_INF 0x7c00u  // bit pattern of +inf: 0 < x <= +inf  <=>  bits - 1 < this
+#else
+typedef __bf16 act16x8 __attribute__((ext_vector_type(8)));
+#define HCB_ACT_POS_INF 0x7f80u
+#endif
+
 namespace hcb {
 
 __device__ __forceinline__ float bf2f(uint16_t v) {
@@ -31,14 +42,32 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return *reinterpret_cast<uint16_t*>(&b);
 }
+#ifdef HCB_F16
+__device__ __forceinline__ float act2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ uint16_t f2act(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ __forceinline__ f32x4 mfma16(const act16x8& a, const act16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+#else
+__device__ __forceinline__ float act2f(uint16_t v) { return bf2f(v); }
+__device__ __forceinline__ uint16_t f2act(float f) { return f2bf(f); }
+__device__ __forceinline__ f32x4 mfma16(const act16x8& a, const act16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+#endif
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return (uint32_t)f2act(lo) | ((uint32_t)f2act(hi) << 16);
 }
 __device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+#ifdef HCB_F16
+    f[2 * i] = act2f((uint16_t)(v[i] & 0xffffu));
+    f[2 * i + 1] = act2f((uint16_t)(v[i] >> 16));
+#else
     f[2 * i] = __uint_as_float(v[i] << 16);
     f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+#endif
   }
 }
 __device__ __forceinline__ u32x4 pack8(const float* f) {

@@ -143,24 +143,24 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
   const int frow = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    bf16x8 af[MI], bfr[NI];
+    act16x8 af[MI], bfr[NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       int row = wm * TM + i * 16 + frow;
       int ch = ks * 4 + fq;
-      af[i] = __builtin_bit_cast(bf16x8, Ab[row * 8 + (ch ^ ((row >> 1) & 7))]);
+      af[i] = __builtin_bit_cast(act16x8, Ab[row * 8 + (ch ^ ((row >> 1) & 7))]);
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       int row = wn * TN + j * 16 + frow;
       int ch = ks * 4 + fq;
-      bfr[j] = __builtin_bit_cast(bf16x8, Bb[row * 8 + (ch ^ ((row >> 1) & 7))]);
+      bfr[j] = __builtin_bit_cast(act16x8, Bb[row * 8 + (ch ^ ((row >> 1) & 7))]);
     }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
   }
 }
 

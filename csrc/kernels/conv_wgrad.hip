@@ -170,14 +170,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     const char* Bb = Bs + cur * BK * BN * 2;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[MI], bfr[NI];
+      act16x8 af[MI], bfr[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         int col = wm * TM + i * 16;
         short4v lo = tr_read_a(Ab, ks * 32 + 8 * g, col);
         short4v hi = tr_read_a(Ab, ks * 32 + 8 * g + 4, col);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, t);
+        af[i] = __builtin_bit_cast(act16x8, t);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -185,13 +185,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
         short4v lo = tr_read_b(Bb, ks * 32 + 8 * g, col);
         short4v hi = tr_read_b(Bb, ks * 32 + 8 * g + 4, col);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, t);
+        bfr[j] = __builtin_bit_cast(act16x8, t);
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
     if (kt + 1 < kt_end) lstore(cur ^ 1);
     __syncthreads();
@@ -360,14 +360,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradPara
     const char* Bb = Ab + BK * BM * 2;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[MI], bfr[NI];
+      act16x8 af[MI], bfr[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int col = wm * TM + i * 16;
         short4v lo = tr_read_a(Ab, ks * 32 + 8 * g, col);
         short4v hi = tr_read_a(Ab, ks * 32 + 8 * g + 4, col);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, t);
+        af[i] = __builtin_bit_cast(act16x8, t);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -375,13 +375,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradPara
         short4v lo = tr_read_b(Bb, ks * 32 + 8 * g, col);
         short4v hi = tr_read_b(Bb, ks * 32 + 8 * g + 4, col);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, t);
+        bfr[j] = __builtin_bit_cast(act16x8, t);
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
   }
   __syncthreads();  // every wave is done with the ring before the epilogue reuses LDS
@@ -519,26 +519,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
 #pragma unroll
     for (int ks = 0; ks < KW / 32; ++ks) {
       const int krow = wk * KW + ks * 32;
-      bf16x8 af[4], bfr[4];
+      act16x8 af[4], bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         short4v lo = tr_read_a(Ab, krow + 8 * g, wm * 64 + i * 16);
         short4v hi = tr_read_a(Ab, krow + 8 * g + 4, wm * 64 + i * 16);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, t);
+        af[i] = __builtin_bit_cast(act16x8, t);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         short4v lo = tr_read_b(Bb, krow + 8 * g, wn * 64 + j * 16);
         short4v hi = tr_read_b(Bb, krow + 8 * g + 4, wn * 64 + j * 16);
         short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, t);
+        bfr[j] = __builtin_bit_cast(act16x8, t);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();

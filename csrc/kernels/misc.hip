@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   for (int c = tid; c < lddl; c += 256) {
     float g = 0.f;
     if (c < ncls) g = (__expf(lr[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * scale;
-    dl[(size_t)row * lddl + c] = f2bf(g);
+    dl[(size_t)row * lddl + c] = f2act(g);
   }
 }
 
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
           reinterpret_cast<u32x4*>(pack + o)[0] = v0;
           reinterpret_cast<u32x4*>(pack + o)[1] = v1;
         } else {
-          for (int q = 0; q < 16 && kk0 + k16 + q < Nout; ++q) pack[o + q] = f2bf(tile[k16 + q][c]);
+          for (int q = 0; q < 16 && kk0 + k16 + q < Nout; ++q) pack[o + q] = f2act(tile[k16 + q][c]);
         }
       }
     }
@@ -284,12 +284,12 @@ __global__ __launch_bounds__(256) void dropout_bwd_kernel(const uint16_t* __rest
 __global__ void cast_f32_bf16_kernel(const float* x, uint16_t* y, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
-    y[i] = f2bf(x[i]);
+    y[i] = f2act(x[i]);
 }
 __global__ void cast_bf16_f32_kernel(const uint16_t* x, float* y, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
-    y[i] = bf2f(x[i]);
+    y[i] = act2f(x[i]);
 }
 __global__ void add_bf16_kernel(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n8) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
@@ -353,7 +353,7 @@ __global__ void synth_images_kernel(uint16_t* out, int64_t n_pix, int C, int Cpa
       }
       v = mean + std * z;
     }
-    out[i] = f2bf(v);
+    out[i] = f2act(v);
   }
 }
 

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void stem_wfold_kernel(const float* __restrict
   const int r = 2 * i + a - 1, s = 2 * j + b - 1;
   float v = 0.f;
   if ((unsigned)r < 7u && (unsigned)s < 7u && c < 3) v = w[((k * 7 + r) * 7 + s) * cs + c];
-  wp[t] = f2bf(v);
+  wp[t] = f2act(v);
 }
 
 // dw[cout][7][7][cs] += dW'[cout][256] mapped back (each real weight has exactly one folded slot)

@@ -11,11 +11,11 @@ from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 pytestmark = pytest.mark.gpu
 
 
-def _run(steps=4, size=96, batch=16):
+def _run(steps=4, size=96, batch=16, lr=0.05):
     torch.manual_seed(0)
     m = create_model("resnet50", image_size=size, device="cuda", seed=21)
     img, lab = synthetic_batch(m, batch, seed=3)
-    t = Trainer(m, batch, constant_lr(0.05), use_graph=True, graph_warmup=1)
+    t = Trainer(m, batch, constant_lr(lr), use_graph=True, graph_warmup=1)
     tr = torch.zeros(steps, device="cuda")
     for i in range(steps):
         tr[i:i + 1].copy_(t.step(img, lab))
@@ -38,11 +38,13 @@ def test_deterministic_mode_is_bitwise_reproducible():
 def test_deterministic_mode_trains_like_default():
     Fn.set_deterministic(True)
     try:
-        _, _, trd = _run(steps=6)
+        _, _, trd = _run(steps=6, lr=0.01)
     finally:
         Fn.set_deterministic(False)
-    _, _, trn = _run(steps=6)
-    assert torch.allclose(trd[:3], trn[:3], rtol=3e-2, atol=3e-2), (trd.tolist(), trn.tolist())
+    _, _, trn = _run(steps=6, lr=0.01)
+    # (a stable learning rate: at 0.05 this tiny-batch run diverges and amplifies the
+    # rounding-order difference chaotically)
+    assert torch.allclose(trd, trn, rtol=3e-2, atol=3e-2), (trd.tolist(), trn.tolist())
 
 
 def _shallow(device, **kw):

@@ -62,10 +62,11 @@ def test_graph_training_step_runs_and_learns():
     m = create_model("resnet50", image_size=96, device="cuda")
     img, lab = synthetic_batch(m, 16)
     t = Trainer(m, 16, constant_lr(0.02), use_graph=True, graph_warmup=2)
-    losses = [float(t.step(img, lab)) for _ in range(16)]
+    losses = [float(t.step(img, lab)) for _ in range(28)]
     assert all(torch.isfinite(torch.tensor(losses)))
     assert t._g_all is not None
-    assert min(losses[-3:]) < 0.8 * losses[2]
+    # (the plateau's length varies with the rounding of the run: 28 steps clear it)
+    assert min(losses[-3:]) < 0.8 * losses[2], losses
 
 
 def test_full_size_resnet50_step_bs64():

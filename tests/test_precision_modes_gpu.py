@@ -1,6 +1,7 @@
-"""Reference-precision compute modes on the GPU (--compute_dtype fp32 / fp16): the PyTorch
-path (MIOpen / rocBLAS) of ops/functional.py, the same code the CPU path runs. fp32 is the
-reference's precision (run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16)."""
+"""Reference-precision compute modes on the GPU: --compute_dtype fp32 (and IEEE fp16 with
+HCB_F16_NATIVE=0) through the PyTorch path (MIOpen / rocBLAS) of ops/functional.py, the same
+code the CPU path runs. fp32 is the reference's precision (run-tf-sing-ucx-openmpi.sh:62-81
+passes no --use_fp16). The default fp16 mode runs the HIP kernels: test_fp16_native_gpu.py."""
 import pytest
 import torch
 
@@ -34,9 +35,13 @@ def test_fp32_gpu_matches_fp32_cpu_step():
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
-def test_reference_precision_training_learns(dtype):
+def test_reference_precision_training_learns(dtype, monkeypatch):
+    from azure_hc_intel_tf_amd.ops import functional as Fn
+
+    monkeypatch.setattr(Fn, "F16_NATIVE", False)  # fp16 through MIOpen, not the fp16 kernel build
     torch.manual_seed(0)
     m = create_model("resnet50", image_size=64, device="cuda", compute_dtype=dtype)
+    assert not m.native
     img, lab = synthetic_batch(m, 8)
     assert img.dtype == {"fp32": torch.float32, "fp16": torch.float16}[dtype]
     img = (img.float() - 127.0).div(60.0).to(img.dtype)
