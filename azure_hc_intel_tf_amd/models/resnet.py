@@ -42,6 +42,12 @@ class Bottleneck:
         return [l for l in (self.sc, self.c1, self.c2, self.c3) if l is not None]
 
     def forward(self, x):
+        if self.proj and L.FUSE_RES_BN and self.sc.training and Fn.native(x):
+            # the shortcut's BN is applied inside conv3's BN pass (its output never stored)
+            z_sc = self.sc.forward_deferred(x)
+            a = self.c1.forward(x)
+            b = self.c2.forward(a)
+            return self.c3.forward(b, residual=z_sc, residual_bn=self.sc)
         sc = self.sc.forward(x) if self.proj else x
         a = self.c1.forward(x)
         b = self.c2.forward(a)

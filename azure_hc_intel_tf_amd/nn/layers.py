@@ -75,6 +75,9 @@ FUSE_STEM_POOL = os.environ.get("HCB_FUSE_STEM_POOL", "1") != "0"
 STAT_R = max(1, int(os.environ.get("HCB_STAT_R", "8")))
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
 FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
+# projection blocks: the shortcut's BN is applied inside the block output's BN pass
+# (act(BN3(z3) + BN_sc(z_sc)) in one kernel), so the shortcut's normalised tensor is never written
+FUSE_RES_BN = os.environ.get("HCB_FUSE_RES_BN", "1") != "0"
 # shifted single-pass BN statistics: the conv epilogue sums (v - K), (v - K)^2 with K = the
 # layer's previous batch mean, so E[x^2] - E[x]^2 does not cancel in fp32 when |mean| >> std
 # (HCB_BN_SHIFT=0: K = 0, the plain single-pass form)
@@ -220,7 +223,26 @@ class ConvBN(Layer):
         return out
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x, out=None, residual=None):
+    def forward_deferred(self, x):
+        """GPU training forward of a conv + BN whose BN apply is left to the consumer (a
+        projection shortcut: the block output's BN pass normalises z_sc on the fly, see
+        ``forward(residual_bn=)``). Returns z; the saved batch moments are written by that pass."""
+        assert self.bn and not self.relu and self.training and Fn.native(x)
+        P, Q, C = self.out_shape
+        z = empty_act((x.shape[0], P, Q, C), x.device)
+        x = self._conv_fwd_stats(x, z)
+        self._saved = (x, z, None, Fn.BNSaved(self.sv_mean.data, self.sv_invstd.data), False)
+        return z
+
+    def res_bn_args(self):
+        """The residual-BN operands of a deferred BN (bn_forward_acc res_bn)."""
+        acc_f, _, _ = self._acc
+        return (acc_f, self.gamma.data, self.beta.data, self.sv_mean.data, self.sv_invstd.data, self.rmean.data,
+                self.rvar.data, self._shift())
+
+    def forward(self, x, out=None, residual=None, residual_bn=None):
+        """``residual_bn``: the ConvBN (run with forward_deferred) whose raw output ``residual``
+        is BN-normalised inside this layer's BN pass before the add."""
         N = x.shape[0]
         P, Q, C = self.out_shape
         dev = x.device
@@ -244,10 +266,13 @@ class ConvBN(Layer):
                 if (RELU_BITMASK and self.relu and residual is not None and FUSE_BN_BWD
                         and Fn.ld(z) == C and Fn.ld(y) == C):
                     mask = torch.empty((N * P * Q, C // 8), dtype=torch.uint8, device=dev)
+                if residual_bn is not None:
+                    assert residual_bn._acc[2] == R, "residual BN accumulators must match the replica count"
                 saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
                                           self.decay, self.eps, y, self.relu, acc_f, R,
                                           self.sv_mean.data, self.sv_invstd.data, residual=residual, mask=mask,
-                                          shift=self._shift())
+                                          shift=self._shift(),
+                                          res_bn=residual_bn.res_bn_args() if residual_bn is not None else None)
                 self._mask = mask
             else:
                 Fn.conv_forward(x, self.spec, None, self.w.data, z)

@@ -503,18 +503,21 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
 
 
 def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out, relu: bool, acc, R: int,
-                   saved_mean, saved_invstd, residual=None, mask=None, shift=None):
+                   saved_mean, saved_invstd, residual=None, mask=None, shift=None, res_bn=None):
     """GPU BN forward whose batch statistics were accumulated by the producing conv's epilogue
     into ``acc`` (R replicas of [2][C]); mean/invstd are derived inside the apply kernel (no
     finalize launch) and written to saved_mean / saved_invstd for the backward. ``mask``
     (uint8 [M, C/8]): also store the output's ReLU bit mask, which the mode-3 fused
     BN-backward epilogue reads instead of the full bf16 output (1/16 of the bytes). ``shift``:
-    the per-channel offset the producing conv subtracted before accumulating (conv_forward)."""
+    the per-channel offset the producing conv subtracted before accumulating (conv_forward).
+    ``res_bn`` = (acc, gamma, beta, saved_mean, saved_invstd, running_mean, running_var, shift) of a
+    second BN applied to ``residual`` in the same pass (a projection shortcut's raw conv output:
+    its normalised tensor is never written); same M, C and replica count R."""
     N, H, W, C = z.shape
     M = N * H * W
     _ext.ops().bn_apply_acc(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0, M, C,
                             acc, R, eps, momentum, gamma, beta, 1 if relu else 0, saved_mean, saved_invstd,
-                            running_mean, running_var, mask, shift)
+                            running_mean, running_var, mask, shift, *(res_bn or ()))
     return BNSaved(saved_mean, saved_invstd)
 
 

@@ -559,7 +559,11 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                   int64_t ldr, int64_t M, int64_t C, const Tensor& acc, int64_t R, double eps, double momentum,
                   const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& saved_mean,
                   const Tensor& saved_invstd, const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv,
-                  const c10::optional<Tensor>& mask, const c10::optional<Tensor>& shift) {
+                  const c10::optional<Tensor>& mask, const c10::optional<Tensor>& shift,
+                  const c10::optional<Tensor>& res_acc, const c10::optional<Tensor>& res_gamma,
+                  const c10::optional<Tensor>& res_beta, const c10::optional<Tensor>& res_saved_mean,
+                  const c10::optional<Tensor>& res_saved_invstd, const c10::optional<Tensor>& res_rm,
+                  const c10::optional<Tensor>& res_rv, const c10::optional<Tensor>& res_shift) {
   check_act(x, "x");
   check_act(y, "y");
   check_f32(acc, "acc");
@@ -581,12 +585,27 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
     TORCH_CHECK(mask->numel() >= M * (C / 8), "hcb.bn_apply_acc: mask too small");
     mp = mask->data_ptr();
   }
+  // residual BN (projection shortcut): the residual is that BN's raw input z_sc
+  hcb::ResBN rb{};
+  if (res_acc.has_value()) {
+    TORCH_CHECK(rp != nullptr && res_gamma && res_beta && res_saved_mean && res_saved_invstd,
+                "hcb.bn_apply_acc: a residual BN needs res plus its acc / gamma / beta / saved stats");
+    rb.acc = opt_f32(res_acc, R * 2 * C, "res_acc");
+    rb.gamma = opt_f32(res_gamma, C, "res_gamma");
+    rb.beta = opt_f32(res_beta, C, "res_beta");
+    rb.saved_mean = const_cast<float*>(opt_f32(res_saved_mean, C, "res_saved_mean"));
+    rb.saved_invstd = const_cast<float*>(opt_f32(res_saved_invstd, C, "res_saved_invstd"));
+    rb.run_mean = const_cast<float*>(opt_f32(res_rm, C, "res_running_mean"));
+    rb.run_var = const_cast<float*>(opt_f32(res_rv, C, "res_running_var"));
+    TORCH_CHECK((rb.run_mean == nullptr) == (rb.run_var == nullptr), "hcb.bn_apply_acc: residual running stats");
+    rb.shift = opt_f32(res_shift, C, "res_shift");
+  }
   hcb::launch_bn_apply_acc(x.data_ptr(), (int)ldx, y.data_ptr(), (int)ldy, rp, (int)ldr, (int)M, (int)C,
                            acc.data_ptr<float>(), (int)R, (float)eps, (float)momentum, gamma.data_ptr<float>(),
                            beta.data_ptr<float>(), (int)relu, saved_mean.data_ptr<float>(),
                            saved_invstd.data_ptr<float>(), rm.has_value() ? rm->data_ptr<float>() : nullptr,
                            rv.has_value() ? rv->data_ptr<float>() : nullptr, mp, opt_f32(shift, C, "shift"),
-                           cur_stream());
+                           res_acc.has_value() ? &rb : nullptr, cur_stream());
 }
 
 void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
@@ -831,7 +850,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");
   m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
-  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor(f!)? mask=None, Tensor? shift=None) -> ()");
+  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor(f!)? mask=None, Tensor? shift=None, Tensor? res_acc=None, Tensor? res_gamma=None, Tensor? res_beta=None, Tensor(g!)? res_saved_mean=None, Tensor(h!)? res_saved_invstd=None, Tensor(i!)? res_running_mean=None, Tensor(j!)? res_running_var=None, Tensor? res_shift=None) -> ()");
   m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg) -> ()");
   m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu, Tensor(d!)? shift_out=None) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");

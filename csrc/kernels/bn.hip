@@ -547,12 +547,17 @@ __device__ __forceinline__ void reduce_group_replicas(const float* acc, int R, i
   __syncthreads();
 }
 
+// RBN: the residual operand is a projection shortcut's raw conv output normalised here (ResBN);
+// its own instantiation, so the common kernel keeps its register budget
+template <bool RBN>
 __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ y, int ldy, const uint16_t* __restrict__ res,
     int ldr, int M, int C, int CVB, const float* __restrict__ acc, int R, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
-    float* saved_invstd, float* run_mean, float* run_var, uint8_t* __restrict__ mask, const float* shift) {
-  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
+    float* saved_invstd, float* run_mean, float* run_var, uint8_t* __restrict__ mask, const float* shift,
+    ResBN rb) {
+  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB] (+ [2][CB] of the residual BN)
+  constexpr bool rbn = RBN;
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
   const int cl = (threadIdx.x % CVB) * 8;
@@ -570,43 +575,59 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     }
   };
   // First rows and the affine parameters are in flight while the statistics are reduced.
-  float gam[8], bet[8];
+  float gam[8], bet[8], gam2[RBN ? 8 : 1], bet2[RBN ? 8 : 1];
   if (active) {
     load_rows(m0);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       gam[e] = gamma[gm.c0 + cl + e];
       bet[e] = beta[gm.c0 + cl + e];
-    }
-  }
-  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
-  const float inv_n = 1.f / (float)M;
-  if (blockIdx.x == 0) {
-    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
-      const int c = gm.c0 + i;
-      const float d = sums[i] * inv_n;  // E[v - K]
-      float mu = d + (shift != nullptr ? shift[c] : 0.f);
-      float var = fmaxf(sums[gm.CB + i] * inv_n - d * d, 0.f);
-      saved_mean[c] = mu;
-      saved_invstd[c] = rsqrtf(var + eps);
-      if (run_mean != nullptr) {
-        float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-        run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * mu;
-        run_var[c] = momentum * run_var[c] + (1.f - momentum) * unb;
+      if constexpr (RBN) {
+        gam2[e] = rb.gamma[gm.c0 + cl + e];
+        bet2[e] = rb.beta[gm.c0 + cl + e];
       }
     }
   }
-  if (!active) return;
-  float sc[8], sh[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float d = sums[cl + e] * inv_n;
-    float mu = d + (shift != nullptr ? shift[gm.c0 + cl + e] : 0.f);
-    float var = fmaxf(sums[gm.CB + cl + e] * inv_n - d * d, 0.f);
-    float s = gam[e] * rsqrtf(var + eps);
-    sc[e] = s;
-    sh[e] = bet[e] - mu * s;
+  if constexpr (RBN) {  // both reductions, one barrier each
+    reduce_group_replicas(rb.acc, R, C, gm.c0, gm.CB, sums + 2 * gm.CB);
   }
+  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
+  const float inv_n = 1.f / (float)M;
+  // mean / invstd of channel group sums s[0..CB) / s[CB..2CB) (shifted by K), block 0 publishes
+  auto finalize = [&](const float* s, const float* K, float* smean, float* sinv, float* rmean, float* rvar) {
+    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
+      const int c = gm.c0 + i;
+      const float d = s[i] * inv_n;  // E[v - K]
+      float mu = d + (K != nullptr ? K[c] : 0.f);
+      float var = fmaxf(s[gm.CB + i] * inv_n - d * d, 0.f);
+      smean[c] = mu;
+      sinv[c] = rsqrtf(var + eps);
+      if (rmean != nullptr) {
+        float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        rmean[c] = momentum * rmean[c] + (1.f - momentum) * mu;
+        rvar[c] = momentum * rvar[c] + (1.f - momentum) * unb;
+      }
+    }
+  };
+  if (blockIdx.x == 0) {
+    finalize(sums, shift, saved_mean, saved_invstd, run_mean, run_var);
+    if constexpr (RBN) finalize(sums + 2 * gm.CB, rb.shift, rb.saved_mean, rb.saved_invstd, rb.run_mean, rb.run_var);
+  }
+  if (!active) return;
+  float sc[8], sh[8], sc2[RBN ? 8 : 1], sh2[RBN ? 8 : 1];
+  auto affine = [&](const float* s, const float* K, const float* g, const float* b, float* a, float* o) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = s[cl + e] * inv_n;
+      float mu = d + (K != nullptr ? K[gm.c0 + cl + e] : 0.f);
+      float var = fmaxf(s[gm.CB + cl + e] * inv_n - d * d, 0.f);
+      float v = g[e] * rsqrtf(var + eps);
+      a[e] = v;
+      o[e] = b[e] - mu * v;
+    }
+  };
+  affine(sums, shift, gam, bet, sc, sh);
+  if constexpr (RBN) affine(sums + 2 * gm.CB, rb.shift, gam2, bet2, sc2, sh2);
   for (; m0 < M; m0 += BN_U * stride) {
     if (m0 != blockIdx.x * gm.rows + gm.r0) load_rows(m0);
 #pragma unroll
@@ -619,8 +640,13 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
       if (res != nullptr) {
         float r[8];
         unpack8(rv[u], r);
+        if constexpr (RBN) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += r[e];
+          for (int e = 0; e < 8; ++e) f[e] += r[e] * sc2[e] + sh2[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] += r[e];
+        }
       }
       if (relu) {
 #pragma unroll
@@ -879,12 +905,18 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         void* mask, const float* shift, hipStream_t st) {
+                         void* mask, const float* shift, const ResBN* res_bn, hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
-  hipLaunchKernelGGL(bn_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x, ldx,
-                     (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta,
-                     relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask, shift);
+  const ResBN rb = res_bn != nullptr ? *res_bn : ResBN{};
+  if (res_bn != nullptr)
+    hipLaunchKernelGGL(bn_apply_acc_kernel<true>, grid, dim3(256), (size_t)4 * cvb * 8 * 4, st, (const uint16_t*)x,
+                       ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma,
+                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask, shift, rb);
+  else
+    hipLaunchKernelGGL(bn_apply_acc_kernel<false>, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x,
+                       ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma,
+                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask, shift, rb);
 }
 
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,

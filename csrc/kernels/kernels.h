@@ -132,10 +132,23 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
 // Blocks tile (row split) x (channel group) so each block only reduces its group's replicas.
 // mask (optional): uint8 [M][C/8] ReLU mask of the output (bit e of byte c/8 = y[m][c+e] > 0),
 // read back by the mode-3 fused BN-backward epilogue instead of the full bf16 output
+// A second BatchNorm applied to the residual operand inside the same pass (a projection
+// shortcut's conv output z_sc, whose statistics its conv epilogue accumulated): the block output
+// is act(BN(x) + BN_sc(res)) and BN_sc's normalised tensor is never written. Same M, C, R.
+struct ResBN {
+  const float* acc;
+  const float* gamma;
+  const float* beta;
+  float* saved_mean;
+  float* saved_invstd;
+  float* run_mean;
+  float* run_var;
+  const float* shift;
+};
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         void* mask, const float* shift, hipStream_t st);
+                         void* mask, const float* shift, const ResBN* res_bn, hipStream_t st);
 // BN(acc statistics) + ReLU + max pool (NHWC, C contiguous): pooled y [N,P,Q] (row stride ldy) and
 // the uint8 window argmax [N,P,Q,C]; the BN+ReLU activation itself is not materialised
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
