@@ -1,0 +1,11 @@
+# round-2 closing run: smoke, the whole GPU suite, bench (N=1), kernel stats; summaries -> gpurun_out/
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/final_smoke.log 2>&1 || { tail -20 gpurun_out/final_smoke.log; exit 1; }
+tail -1 gpurun_out/final_smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/final_pytest_gpu.log 2>&1 || { tail -30 gpurun_out/final_pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/final_pytest_gpu.log
+timeout -k 10 300 python bench.py > gpurun_out/final_bench_default.json 2> gpurun_out/final_bench_default.err || { tail -20 gpurun_out/final_bench_default.err; exit 1; }
+cut -c1-200 gpurun_out/final_bench_default.json
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/final_prof" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 > "$GRAFT_REPO_ROOT/gpurun_out/final_prof.log" 2>&1 || { echo "rocprof failed"; exit 1; }
+echo final done
