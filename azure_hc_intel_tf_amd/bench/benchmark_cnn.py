@@ -156,7 +156,8 @@ class BenchmarkCNN:
                                # automatic scaling), whichever 16-bit type computes
                                loss_scale=p.fp16_loss_scale if p.use_fp16 else None,
                                dynamic_loss_scale=bool(p.use_fp16 and p.fp16_enable_auto_loss_scale),
-                               loss_scale_interval=p.fp16_inc_loss_scale_every_n)
+                               loss_scale_interval=p.fp16_inc_loss_scale_every_n,
+                               comm_check=True if p.comm_check else None)
         if p.horovod_device == "cpu" and self.size > 1 and self.on_gpu:
             self.trainer.reducer = _HostStagedReducer(reducer)
 

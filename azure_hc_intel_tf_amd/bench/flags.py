@@ -84,6 +84,8 @@ FLAGS: List[Flag] = [
     Flag("save_model_steps", None, int, "checkpoint every N steps"),
     Flag("save_model_secs", 0, int, "checkpoint every N seconds"),
     Flag("trace_file", "", str, "Chrome trace of one profiled step (torch.profiler / roctracer)"),
+    Flag("comm_check", False, parse_bool, "race detector: re-do every overlapped gradient reduction with a blocking "
+         "reference allreduce and fail on a mismatch (eager steps; HCB_COMM_CHECK=1)"),
     Flag("benchmark_log_dir", None, str, "directory for the machine-readable JSON summary"),
     Flag("tf_random_seed", 1234, int, "random seed"),
     Flag("print_training_accuracy", False, parse_bool, "log top-1/top-5 of the training batch"),

@@ -71,7 +71,7 @@ class Trainer:
                  weight_decay: float = 4e-5, reducer=None, world_size: int = 1, use_graph: bool = True,
                  nesterov: bool = False, graph_warmup: int = 2, forward_only: bool = False,
                  loss_scale: Optional[float] = None, dynamic_loss_scale: bool = False,
-                 loss_scale_interval: int = 1000, force_overlap: bool = False):
+                 loss_scale_interval: int = 1000, force_overlap: bool = False, comm_check: Optional[bool] = None):
         self.model = model
         self.ps = model.ps
         self.B = batch_size
@@ -87,7 +87,16 @@ class Trainer:
             model.set_training(False)  # inference BN / no dropout (tf_cnn_benchmarks phase_train=False)
         # graphs for the HIP-kernel path; the reference-precision PyTorch path (fp32 / fp16
         # --compute_dtype) runs eagerly (MIOpen's first-call searches are not capturable)
-        self.use_graph = use_graph and self.dev.type == "cuda" and getattr(model, "native", True)
+        # comm_check (HCB_COMM_CHECK=1 / --comm_check): the race detector of the overlapped
+        # allreduce -- every async segment reduction is re-done by a blocking reference
+        # allreduce of a snapshot taken before it was issued and the two must agree (a missing
+        # stream dependency between backward and the comm stream shows up as a mismatch).
+        # Eager steps only (host comparison).
+        self.comm_check = (os.environ.get("HCB_COMM_CHECK", "0") == "1") if comm_check is None else comm_check
+        self.comm_check_errs = []
+        self._check = None
+        self.use_graph = (use_graph and self.dev.type == "cuda" and getattr(model, "native", True)
+                          and not self.comm_check)
         self.graph_warmup = graph_warmup
         ld = model.fc.ld if hasattr(model, "fc") else (model.num_classes + 7) // 8 * 8
         self.ld = ld
@@ -185,6 +194,8 @@ class Trainer:
                 except StopIteration:
                     break
             if not self._skip_comm:
+                if self.comm_check:
+                    self._check_snapshot(self._ranges(i, layers))
                 with range_(f"allreduce.segment{i}"):
                     self.reducer.allreduce_ranges_async_(self.ps.grad, self._ranges(i, layers))
             else:
@@ -192,6 +203,36 @@ class Trainer:
             i += 1
         if not self._skip_comm:
             self.reducer.join()
+            if self.comm_check:
+                self._check_verify()
+
+    def _check_snapshot(self, ranges):
+        """comm_check: copy the segment's local gradient ranges (stream-ordered before the fork)."""
+        if self._check is None:
+            self._check = torch.zeros_like(self.ps.grad)
+            self._check_ranges = []
+        g = self.ps.grad
+        for off, n in ranges:
+            self._check[off:off + n].copy_(g[off:off + n])
+            self._check_ranges.append((off, n))
+
+    def _check_verify(self):
+        """comm_check: blocking reference allreduce of the snapshots vs the engine's result."""
+        ref = self._check
+        self.reducer.allreduce_(ref)
+        g = self.ps.grad
+        worst = 0.0
+        for off, n in self._check_ranges:
+            a, b = g[off:off + n], ref[off:off + n]
+            scale = float(b.abs().max()) if n else 0.0
+            err = float((a - b).abs().max()) if n else 0.0
+            worst = max(worst, err / (scale + 1e-30))
+            if err > 1e-5 * scale + 1e-20:
+                raise RuntimeError(f"comm check: reduced gradient range [{off}, {off + n}) differs from the blocking "
+                                   f"reference allreduce by {err:.3e} (max |ref| {scale:.3e}): the overlapped "
+                                   "reduction read the gradients before backward had finished writing them")
+        self.comm_check_errs.append(worst)
+        self._check_ranges = []
 
     def _eager_step(self, images, labels):
         if self.overlap:

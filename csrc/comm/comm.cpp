@@ -88,6 +88,14 @@ struct TimelineRec {
 };
 
 struct Comm {
+  // process exit without destroy() (static destruction of g_comms): stop and join the
+  // watchdog thread -- a joinable std::thread would std::terminate -- and touch nothing else
+  // (HIP / RCCL may already be torn down)
+  ~Comm() {
+    stop = true;
+    cv.notify_all();
+    if (wd.joinable()) wd.join();
+  }
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1, device = 0;
   hipStream_t stream = nullptr;  // comm stream

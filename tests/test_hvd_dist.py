@@ -311,3 +311,40 @@ def test_segmented_backward_equals_plain_backward(name, size, monkeypatch):
     if name != "alexnet":
         assert nseg >= 2
     assert torch.allclose(m.ps.grad, g_plain, rtol=1e-4, atol=1e-6)
+
+
+def _comm_check(hvd):
+    """The overlapped-allreduce race detector (Trainer comm_check) passes on a correct engine and
+    fails loudly when a reduction reads gradients that are not final."""
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.parallel import make_reducer
+    from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+    m = create_model("resnet50", image_size=32, device="cpu", seed=3 + hvd.rank())
+    hvd.broadcast_global_variables(m, 0)
+    img, lab = synthetic_batch(m, 2, seed=hvd.rank())
+    img = (img - 127) / 60
+    red = make_reducer("torch", bucket_bytes=1 << 20)
+    t = Trainer(m, 2, constant_lr(0.01), reducer=red, world_size=hvd.size(), comm_check=True)
+    assert t.overlap and not t.use_graph
+    t.step(img, lab)
+    assert len(t.comm_check_errs) == 1 and t.comm_check_errs[0] < 1e-6
+    # a broken engine: every async range reduction sees this rank's gradients scaled by 2
+    real = red.allreduce_ranges_async_
+
+    def stale(flat, ranges):
+        for off, n in ranges:
+            flat[off:off + n].mul_(2.0)
+        return real(flat, ranges)
+
+    red.allreduce_ranges_async_ = stale
+    try:
+        t.step(img, lab)
+    except RuntimeError as e:
+        assert "comm check" in str(e)
+    else:
+        raise AssertionError("comm check missed a corrupted reduction")
+
+
+def test_comm_check_race_detector():
+    run(2, _comm_check)

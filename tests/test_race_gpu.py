@@ -1,0 +1,68 @@
+"""Race detection on the GPU: the same deterministic-mode training run with every kernel and copy
+serialised by the HIP runtime (AMD_SERIALIZE_KERNEL=3, AMD_SERIALIZE_COPY=3, HIP_LAUNCH_BLOCKING=1)
+must be bitwise equal to the normal asynchronous run -- graph replays, the forked comm-stream
+branches of the multi-GPU step (1-rank RCCL communicator) and the weight-gradient side work
+included. A missing stream / event dependency makes the asynchronous run read data early and
+diverge. (race detection.)"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import hashlib, json, sys
+sys.path.insert(0, sys.argv[1])
+import torch
+from azure_hc_intel_tf_amd.models import create_model
+from azure_hc_intel_tf_amd.ops import functional as Fn
+from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
+
+Fn.set_deterministic(True)
+dp = sys.argv[2] == "dp"
+m = create_model("resnet50", image_size=64, device="cuda", seed=5)
+img, lab = synthetic_batch(m, 8, seed=3)
+red = None
+if dp:
+    from azure_hc_intel_tf_amd.parallel.native import NativeReducer
+    red = NativeReducer(force=True)
+t = Trainer(m, 8, constant_lr(0.02), use_graph=True, graph_warmup=1, reducer=red, force_overlap=dp)
+rows = []
+for _ in range(4):
+    t.step(img, lab)
+    rows.append(t.row_loss.clone())
+torch.cuda.synchronize()
+# per-row cross entropies (the reported total adds an atomically accumulated L2 term)
+losses = [hashlib.sha256(r.cpu().numpy().tobytes()).hexdigest() for r in rows]
+print(json.dumps({"losses": losses, "graph": t._g_all is not None or t._g_fb is not None,
+                  "overlap": t.overlap,
+                  "master": hashlib.sha256(m.ps.master.cpu().numpy().tobytes()).hexdigest()}))
+if red is not None:
+    red.close()
+"""
+
+
+def _run(mode, serialize):
+    env = dict(os.environ)
+    if serialize:
+        env.update(AMD_SERIALIZE_KERNEL="3", AMD_SERIALIZE_COPY="3", HIP_LAUNCH_BLOCKING="1")
+    if mode == "dp":
+        env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29650 + int(serialize)), RANK="0", WORLD_SIZE="1",
+                   LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
+    out = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, mode], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("mode", ["single", "dp"])
+def test_serialised_run_equals_async_run(mode):
+    a = _run(mode, serialize=False)
+    s = _run(mode, serialize=True)
+    assert a["graph"] and a["overlap"] == (mode == "dp")
+    assert a["losses"] == s["losses"], (a["losses"], s["losses"])
+    assert a["master"] == s["master"], "weights differ between the asynchronous and the serialised run"
