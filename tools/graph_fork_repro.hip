@@ -13,6 +13,9 @@
 //   recorded without a wait; the main stream waits on the last join at the end.
 // mode 2: mode 1 with an EMPTY comm branch (the HCB_COMM_SKIP_RCCL=1 shape).
 // mode 3 / 4: modes 1 / 2 with a highest-priority comm stream (as the engine creates it).
+// mode 5: mode 2 plus, in every link of the chain, a hipMemsetAsync node zeroing an accumulator
+//   that the next kernel adds into (the training step's zero-initialised BN accumulators /
+//   split-K dx buffers: torch.zeros inside the capture); mode 6: the same without the forks.
 // Any ordering violation (a kernel started before its predecessor finished) shows up as a
 // nonzero error count.
 #include <hip/hip_runtime.h>
@@ -39,6 +42,9 @@ __global__ void k_copy_add(const float* a, float* b, int n, float add) {
 }
 __global__ void k_scale(const float* a, float* b, int n, float s) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b[i] = a[i] * s;
+}
+__global__ void k_accum(const float* a, float* acc, int n) {  // acc = 0 (memset) + a + 1
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) acc[i] += a[i] + 1.f;
 }
 __global__ void k_check(const unsigned* epoch, const float* y, float yadd, const float* z, float zmul, int n,
                         unsigned* errors) {
@@ -97,12 +103,18 @@ int main(int argc, char** argv) {
   } else {
     float* a = x;
     float* o = t0;
+    const bool memset_mode = mode >= 5;
     for (int k = 0; k < chain; ++k) {
-      hipLaunchKernelGGL(k_copy_add, g, b, 0, s, a, o, n, 1.f);
+      if (memset_mode) {  // o = 0 by a memset node, then o += a + 1
+        CK(hipMemsetAsync(o, 0, n * 4, s));
+        hipLaunchKernelGGL(k_accum, g, b, 0, s, a, o, n);
+      } else {
+        hipLaunchKernelGGL(k_copy_add, g, b, 0, s, a, o, n, 1.f);
+      }
       float* t = a;
       a = o;
       o = t;
-      if ((k + 1) % seg == 0) {
+      if ((k + 1) % seg == 0 && mode != 6) {
         CK(hipEventRecord(fork, s));
         CK(hipStreamWaitEvent(c, fork, 0));
         // comm branch: reads the segment's result into a side buffer (like a bucket pack)
