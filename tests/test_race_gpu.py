@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SCRIPT = r"""
-import hashlib, json, sys
+import hashlib, json, os, sys
 sys.path.insert(0, sys.argv[1])
 import torch
 from azure_hc_intel_tf_amd.models import create_model
@@ -24,15 +24,19 @@ from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 
 Fn.set_deterministic(True)
 dp = sys.argv[2] == "dp"
-m = create_model("resnet50", image_size=64, device="cuda", seed=5)
-img, lab = synthetic_batch(m, 8, seed=3)
+size, batch = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (64, 8)
+if len(sys.argv) > 5 and sys.argv[5] == "tuned":  # the autotuned kernel configs bench.py runs
+    from azure_hc_intel_tf_amd.ops import autotune
+    autotune.load_cache()
+m = create_model("resnet50", image_size=size, device="cuda", seed=5)
+img, lab = synthetic_batch(m, batch, seed=3)
 red = None
 if dp:
     from azure_hc_intel_tf_amd.parallel.native import NativeReducer
     red = NativeReducer(force=True)
-t = Trainer(m, 8, constant_lr(0.02), use_graph=True, graph_warmup=1, reducer=red, force_overlap=dp)
+t = Trainer(m, batch, constant_lr(0.02), use_graph=True, graph_warmup=1, reducer=red, force_overlap=dp)
 rows = []
-for _ in range(4):
+for _ in range(int(os.environ.get("RACE_STEPS", "4"))):
     t.step(img, lab)
     rows.append(t.row_loss.clone())
 torch.cuda.synchronize()
