@@ -97,9 +97,13 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
     taps = spec.kh * spec.kw
     keys = [Fn.fwd_key(M, Cout, spec.K, taps), Fn.wgrad_key(Cout, spec.K, M, taps)]
+    phases = Fn.dgrad_phases(spec, H, W) if layer.need_dx and Fn.uses_dgrad_phases(spec, H, W) else []
     if layer.need_dx:
         keys.append(Fn.fwd_key(geo[0], Cin, geo[1], taps))
         keys.append(Fn.dgb_key(geo[0], Cin, geo[1], taps))
+    for ph in phases:  # the stride-phase GEMMs of a strided k x k data gradient
+        pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
+        keys += [Fn.fwd_key(pm, Cin, pk, pt), Fn.dgb_key(pm, Cin, pk, pt)]
     if all(k in Fn._tuned for k in keys):
         return out
     x = _bf((N, H, W, Cin), dev)
@@ -151,6 +155,28 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
                         best = (t, plan)
             Fn._tuned[k] = best[1]
             out.append((k, best))
+        for ph in phases:
+            pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
+            for fused in (False, True):
+                k = (Fn.dgb_key if fused else Fn.fwd_key)(pm, Cin, pk, pt)
+                if k in Fn._tuned:
+                    continue
+                bnbp = None
+                if fused:
+                    z = _bf((N, H, W, Cin), dev)
+                    yv = _bf((N, H, W, Cin), dev)
+                    st = [torch.rand(Cin, device=dev) + 0.5 for _ in range(4)]
+                    bnbp = Fn.BNBwdFuse(z, yv, Fn.BNSaved(st[0], st[1]), st[2], st[3], 1,
+                                        torch.zeros(8 * 2 * Cin, dtype=torch.float32, device=dev), 8)
+                best = None
+                for cfg in Fn.fwd_candidates(Cin):
+                    for sp in Fn.splitk_candidates(cfg, pm, Cin, pk):
+                        plan = cfg if sp == 1 else [cfg, sp]
+                        t = _time(lambda: Fn.dgrad_phase(dz, spec, layer.pack.tr, dx, fused, ph, cfg=plan, bnb=bnbp))
+                        if best is None or t < best[0]:
+                            best = (t, plan)
+                Fn._tuned[k] = best[1]
+                out.append((k, best))
     # weight gradient
     k = Fn.wgrad_key(Cout, spec.K, M, taps)
     if k not in Fn._tuned:

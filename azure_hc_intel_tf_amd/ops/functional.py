@@ -365,6 +365,86 @@ def unpack_relu_mask(mask, shape):
     return m.reshape(shape)
 
 
+# strided k x k data gradients as sh*sw stride-phase GEMMs (HCB_DGRAD_PHASES=0: one GEMM over the
+# zero-dilated dz, which spends (sh*sw - 1)/(sh*sw) of its MFMA work on the inserted zeros)
+DGRAD_PHASES = os.environ.get("HCB_DGRAD_PHASES", "1") != "0"
+_phase_packs = {}
+
+
+def dgrad_phases(spec: ConvSpec, H: int, W: int):
+    """Stride phases of a strided conv's data gradient: for every output parity (ph, pw) the
+    forward taps r = r0 + sh*j that reach rows h = sh*i + ph, as a stride-1 correlation of dz
+    with the flipped sub-kernel. Yields (ph, pw, Hph, Wph, (r taps), (s taps), pad_t, pad_l);
+    taps in the sub-kernel's order (flipped), None when a phase has no tap."""
+    out = []
+    for ph in range(spec.sh):
+        for pw in range(spec.sw):
+            Hph, Wph = -(-(H - ph) // spec.sh), -(-(W - pw) // spec.sw)
+            r0, c0 = (ph + spec.pt) % spec.sh, (pw + spec.pl) % spec.sw
+            rs = list(range(r0, spec.kh, spec.sh))
+            ss = list(range(c0, spec.kw, spec.sw))
+            if not rs or not ss or Hph <= 0 or Wph <= 0:
+                out.append(None)
+                continue
+            a, b = (ph + spec.pt - r0) // spec.sh, (pw + spec.pl - c0) // spec.sw
+            out.append((ph, pw, Hph, Wph, rs[::-1], ss[::-1], len(rs) - 1 - a, len(ss) - 1 - b))
+    return out
+
+
+def _phase_pack(wtr, spec: ConvSpec, Cdz: int, rs, ss):
+    """[cin_pad][Kpad] operand of one phase: the columns of the transposed-flipped data-grad pack
+    (column block (kh-1-r)*kw + (kw-1-s) holds forward tap (r, s)) for the phase's taps, in the
+    sub-kernel's order; refreshed from the current pack on every call."""
+    C = spec.cin_pad
+    K = len(rs) * len(ss) * Cdz
+    key = (wtr.data_ptr(), tuple(rs), tuple(ss))
+    ent = _phase_packs.get(key)
+    if ent is None:
+        Kp = _round_up(K, 64)
+        taps = [(spec.kh - 1 - r) * spec.kw + (spec.kw - 1 - s) for r in rs for s in ss]
+        ent = (torch.zeros((C, Kp), dtype=wtr.dtype, device=wtr.device),
+               torch.tensor(taps, dtype=torch.int64, device=wtr.device))
+        _phase_packs[key] = ent
+    sub, idx = ent
+    trv = wtr.view(C, -1)[:, :spec.kh * spec.kw * Cdz].view(C, spec.kh * spec.kw, Cdz)
+    sub[:, :K].view(C, len(rs) * len(ss), Cdz).copy_(trv.index_select(1, idx))
+    return sub, K
+
+
+def dgrad_phase_problem(spec: ConvSpec, N: int, phase):
+    """(M, K, taps) of one stride-phase data-grad GEMM (its tuning key)."""
+    _, _, Hph, Wph, rs, ss, _, _ = phase
+    Cdz = spec.cout if spec.cout % 8 == 0 else _round_up(spec.cout, 8)
+    return N * Hph * Wph, len(rs) * len(ss) * Cdz, len(rs) * len(ss)
+
+
+def dgrad_phase(dz, spec: ConvSpec, wtr, dx, accumulate: bool, phase, cfg=None, bnb: "BNBwdFuse" = None):
+    """One stride-phase GEMM of a strided k x k data gradient (see dgrad_phases)."""
+    N, P, Q, _ = dz.shape
+    _, H, W, _ = dx.shape
+    ph, pw, Hph, Wph, rs, ss, pad_t, pad_l = phase
+    Cdz = spec.cout if spec.cout % 8 == 0 else _round_up(spec.cout, 8)
+    sub, Kph = _phase_pack(wtr, spec, Cdz, rs, ss)
+    M, _, taps = dgrad_phase_problem(spec, N, phase)
+    geom = [N, P, Q, Cdz, ld(dz), Hph, Wph, len(rs), len(ss), 1, 1, pad_t, pad_l, 1, 1, 1, 1,
+            spec.cin_pad, Kph, sub.shape[1], ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, 0]
+    if cfg is None and bnb is not None:
+        cfg = _tuned.get(dgb_key(M, spec.cin_pad, Kph, taps))
+    cfg, splits = _plan(cfg, M, spec.cin_pad, Kph, dz.device, taps)
+    geom = geom + [0, 0, splits, ph, pw]
+    if bnb is not None:
+        _ext.ops().conv_igemm_bnb(dz, sub, dx, dx if accumulate else None, geom, cfg, bnb.z,
+                                  bnb.y if bnb.mode in (1, 3) else None, ld(bnb.z), bnb.saved.mean,
+                                  bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
+    else:
+        _ext.ops().conv_igemm(dz, sub, dx, dx if accumulate else None, None, None, geom, cfg)
+
+
+def uses_dgrad_phases(spec: ConvSpec, H: int, W: int) -> bool:
+    return ((spec.sh > 1 or spec.sw > 1) and DGRAD_PHASES and not (spec.kh == 1 and spec.kw == 1)
+            and spec.dh == 1 and spec.dw == 1 and all(ph is not None for ph in dgrad_phases(spec, H, W)))
+
+
 def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None, bnb: "BNBwdFuse" = None):
     """dx[N,H,W,cin] (+)= conv_transpose(dz, W). dx must be zero-filled by the caller when
     not accumulating and the conv is a strided 1x1 (remap path leaves gaps). With ``bnb`` the
@@ -377,6 +457,11 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
         Kpad = spec.Kpad_t
         assert K <= Kpad
         strided = spec.sh > 1 or spec.sw > 1
+        if cfg is None and uses_dgrad_phases(spec, H, W):
+            # one stride-1 GEMM per output parity over dz, rows scattered to (sh*i + ph, sw*j + pw)
+            for phase in dgrad_phases(spec, H, W):
+                dgrad_phase(dz, spec, wtr, dx, accumulate, phase, None, bnb)
+            return dx
         if strided and spec.kh == 1 and spec.kw == 1 and spec.pt == 0 and spec.pl == 0:
             # 1x1 strided: dense GEMM over dz pixels, scatter rows to (p*sh, q*sw)
             M = N * P * Q

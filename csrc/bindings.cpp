@@ -65,7 +65,8 @@ void check_align16(const void* p, const char* name) {
 hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                             const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
                             at::IntArrayRef g, int64_t cfg) {
-  TORCH_CHECK(g.size() >= 28 && g.size() <= 31, "hcb.conv_igemm: geom must have 28 (+relu, +stats_R, +splits) entries");
+  TORCH_CHECK(g.size() >= 28 && g.size() <= 33,
+              "hcb.conv_igemm: geom must have 28 (+relu, +stats_R, +splits, +remap origin h, w) entries");
   check_act(x, "x");
   check_act(w, "w");
   check_cuda(y, "y");
@@ -80,6 +81,8 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   p.relu = g.size() > 28 ? (int)g[28] : 0;
   p.stats_R = g.size() > 29 ? (int)g[29] : 0;
   p.splits = g.size() > 30 ? (int)g[30] : 1;
+  p.oh0 = g.size() > 31 ? (int)g[31] : 0;
+  p.ow0 = g.size() > 32 ? (int)g[32] : 0;
   p.M = p.N * p.P * p.Q;
   TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0 && p.ldx >= p.C, "hcb.conv_igemm: C, ldx must be multiples of 8");
   TORCH_CHECK(p.Kpad % 64 == 0 && p.Kpad >= p.K && p.K == p.R * p.S * p.C,
@@ -93,8 +96,12 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   check_range(x, xb, "x");
   check_range(w, wb, "w");
   int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
-  if (p.remap)
-    TORCH_CHECK((p.P - 1) * p.osh < p.OH && (p.Q - 1) * p.osw < p.OW, "hcb.conv_igemm: remap out of range");
+  if (p.remap) {
+    TORCH_CHECK(p.oh0 >= 0 && p.ow0 >= 0 && (p.P - 1) * p.osh + p.oh0 < p.OH && (p.Q - 1) * p.osw + p.ow0 < p.OW,
+                "hcb.conv_igemm: remap out of range");
+  } else {
+    TORCH_CHECK(p.oh0 == 0 && p.ow0 == 0, "hcb.conv_igemm: a remap origin needs remap");
+  }
   int64_t esz = p.out_f32 ? 4 : 2;
   TORCH_CHECK(y.scalar_type() == (p.out_f32 ? at::kFloat : kAct), "hcb.conv_igemm: y dtype");
   check_range(y, rows * p.ldy * esz - (p.ldy - ((p.Nout + 7) / 8) * 8) * esz, "y");

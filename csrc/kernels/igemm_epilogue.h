@@ -18,13 +18,14 @@ constexpr size_t igemm_epilogue_lds(int BM, int BN, int WM) {
   return (size_t)BM * (BN + 4) * 4 + (size_t)WM * 2 * BN * 4;
 }
 
-// Output row of GEMM row m (strided-output remap for strided 1x1 data gradients).
+// Output row of GEMM row m (strided-output remap: strided 1x1 data gradients, and the stride
+// phases of a strided k x k data gradient, each phase one GEMM with its own origin).
 __device__ __forceinline__ size_t epi_out_row(const ConvParams& p, int m) {
   if (!p.remap) return (size_t)m;
   const int PQ = p.P * p.Q;
   int n = m / PQ, r = m - n * PQ;
   int pp = r / p.Q, qq = r - pp * p.Q;
-  return ((size_t)n * p.OH + (size_t)pp * p.osh) * p.OW + (size_t)qq * p.osw;
+  return ((size_t)n * p.OH + (size_t)pp * p.osh + p.oh0) * p.OW + (size_t)qq * p.osw + p.ow0;
 }
 
 // Register prefetch of the fused BN-backward epilogue operands (z, y and the beta source) for

@@ -48,6 +48,7 @@ struct ConvParams {
   int Nout, K, Kpad, ldy;
   int M;
   int remap, OH, OW, osh, osw;
+  int oh0, ow0;  // remap origin: GEMM pixel (p, q) -> output pixel (p*osh + oh0, q*osw + ow0)
   int beta, out_f32;
   int relu;     // fused ReLU in the epilogue (affine layers without BN)
   int stats_R;  // 0: per-tile slab [tiles][2][Nout]; R>0: atomics into [R][2][Nout] replicas
