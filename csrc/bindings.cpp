@@ -830,12 +830,15 @@ void set_deterministic(bool on) { hcb::set_deterministic(on); }
 
 }  // namespace
 
+static void set_wgrad_ri_op(int64_t on) { hcb::set_wgrad_ri((int)on); }
+
 HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
   m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
+  m.def("set_wgrad_ri(int on) -> ()", set_wgrad_ri_op);
   m.def("bn_stats(Tensor x, int M, int C, int ldx, Tensor(a!) slab) -> ()");
   m.def("bn_partials(int M, int C) -> int", bn_partials);
   m.def("bn_finalize(Tensor slab, int T, int C, float count, float eps, float momentum, Tensor(a!) mean, Tensor(b!) invstd, Tensor(c!)? running_mean, Tensor(d!)? running_var) -> ()");

@@ -17,6 +17,10 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdlib.h>
+
+#include <type_traits>
+
 namespace hcb {
 
 // 32-byte-slot XOR swizzle for an LDS row of NSLOT slots (NSLOT = tile cols / 16): the 8 rows
@@ -46,8 +50,228 @@ __device__ __forceinline__ void wgrad_store_tile(const WgradParams& p, const flo
   }
 }
 
-template <int WM, int WN, int TM, int TN, bool CBIG>
+// ---- incremental row addressing for the register-staged loaders (RI = "row-incremental").
+// Both operands' rows are pixels m = (n, p, q) that advance by BK per k-step. Re-deriving
+// (n, p, q) and the im2col source address of every row with magic-number divides and 32-bit
+// multiplies made these k-loops VALU-bound: 40 quarter-rate integer multiplies and ~90 other
+// VALU ops against 16 MFMAs per k-step in the 64x64 k-split kernel. Instead each thread keeps
+// (h, w, byte offset) of its rows and adds a precomputed mixed-radix step of BK pixels
+// (dn, dp, dq) with at most one carry per digit (dq < Q and dp < P): adds, two compares and
+// selects. The thread -> (row, 16-byte vector) map is the original one (a vector's column, so
+// its filter tap, is fixed per thread); the original loaders remain as the HCB_WGRAD_RI=0
+// A/B baseline.
+// HCB_WGRAD_RI=0 (or set_wgrad_ri(0)) selects the original loaders everywhere (A/B knob)
+static int g_wgrad_ri = -1;
+void set_wgrad_ri(int on) { g_wgrad_ri = on; }  // 0 off, 1 on, 2 on without shared rows
+bool riv_enabled() {
+  if (g_wgrad_ri < 0) {
+    const char* e = getenv("HCB_WGRAD_RI");
+    g_wgrad_ri = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return g_wgrad_ri >= 1;
+}
+static bool shared_rows_enabled() { return g_wgrad_ri == 1; }
+
+struct WgAdvance {  // wave-uniform per-k-step increments (bytes / input rows / input cols)
+  int dqw, dqo, qs, qco, dph, dpo, ps, pco, dno;
+};
+__device__ __forceinline__ WgAdvance wg_advance(const WgradParams& p, int rows) {
+  const int PQ = p.P * p.Q;
+  const int dn = rows / PQ, rem = rows - dn * PQ, dp = rem / p.Q, dq = rem - dp * p.Q;
+  const int pix = p.ldx * 2, rowb = p.W * pix;
+  WgAdvance a;
+  a.dqw = dq * p.stride_w;
+  a.dqo = dq * p.stride_w * pix;
+  a.qs = p.Q * p.stride_w;
+  a.qco = p.stride_h * rowb - p.Q * p.stride_w * pix;  // carry into the next output row
+  a.dph = dp * p.stride_h;
+  a.dpo = dp * p.stride_h * rowb;
+  a.ps = p.P * p.stride_h;
+  a.pco = (p.H - p.P * p.stride_h) * rowb;  // carry into the next image
+  a.dno = dn * p.H * rowb;
+  return a;
+}
+
+template <int ROWS, int COLS, int NT>
+struct WgSeg {
+  static constexpr int VPR = COLS / 8;            // 16-byte vectors per LDS row
+  static constexpr int V = ROWS * VPR / NT;       // vectors per thread per k-step
+  // one vector of a row per thread: each load instruction then covers whole 128-byte lines
+  // (VPR lanes per row) and each LDS store whole rows (conflict free). Measured: 4-vector row
+  // segments per thread (a quarter of the address updates) were 10-20% SLOWER on the k-split
+  // kernel -- 4x the L1 line requests per instruction and 2x LDS store conflicts.
+  static constexpr int SEGV = 1;
+  static constexpr int TPR = VPR / SEGV;          // threads per row
+  static constexpr int RPT = V / SEGV;            // rows per thread
+  static constexpr int RSTEP = NT / TPR;          // row distance between a thread's rows
+  static_assert(SEGV >= 1 && SEGV <= VPR && RPT * SEGV == V && RSTEP * RPT == ROWS, "segment mapping");
+  // LDS image [ROWS][COLS] bf16, 32-byte slots XOR-swizzled (wg_swz): byte offset of vector s
+  // of this thread's row i (loop-invariant, hoisted by the compiler)
+  __device__ __forceinline__ static int lds_off(int tid, int i, int s) {
+    const int row = tid / TPR + RSTEP * i, cv = (tid % TPR) * SEGV + s;
+    return row * COLS * 2 + (((cv >> 1) ^ wg_swz<COLS / 16>(row)) * 32) + (cv & 1) * 16;
+  }
+};
+
+// dY operand: rows m, columns = output channels [i0, i0 + COLS)
+template <int ROWS, int COLS, int NT>
+struct WgALoad {
+  using G = WgSeg<ROWS, COLS, NT>;
+  uint32_t off[G::RPT];
+  int m[G::RPT];
+  bool colok[G::SEGV];
+  __device__ __forceinline__ void init(const WgradParams& p, int mbeg, int i0, int tid) {
+    const int col = i0 + (tid % G::TPR) * G::SEGV * 8;
+#pragma unroll
+    for (int s = 0; s < G::SEGV; ++s) colok[s] = col + 8 * s < p.Nout;
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      m[i] = mbeg + tid / G::TPR + G::RSTEP * i;
+      off[i] = (uint32_t)(m[i] * p.ldy + col) * 2u;
+    }
+  }
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int mend, u32x4 (&d)[G::V]) const {
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      const uint32_t base = m[i] < mend ? off[i] : HCB_OOB;
+#pragma unroll
+      for (int s = 0; s < G::SEGV; ++s) d[i * G::SEGV + s] = buf_load16(r, colok[s] ? base + 16u * s : HCB_OOB);
+    }
+  }
+  __device__ __forceinline__ void advance(uint32_t step_bytes) {
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      off[i] += step_bytes;
+      m[i] += ROWS;
+    }
+  }
+};
+
+// X operand (implicit im2col): rows m, columns j = (r, s, c) in [j0, j0 + COLS); the thread's
+// segment lies in one tap, so its (dh, dw, c) are constant over the k-loop
+template <int ROWS, int COLS, int NT>
+struct WgBLoad {
+  using G = WgSeg<ROWS, COLS, NT>;
+  int hh[G::RPT], ww[G::RPT], m[G::RPT];
+  int off[G::RPT];  // byte offset of (n, hh, ww, c); meaningful only while in range
+  int dh, dw;
+  bool colok[G::SEGV];
+  __device__ __forceinline__ void init(const WgradParams& p, int mbeg, int j0, int tid) {
+    const int col = j0 + (tid % G::TPR) * G::SEGV * 8;
+#pragma unroll
+    for (int s = 0; s < G::SEGV; ++s) colok[s] = col + 8 * s < p.K;
+    const int tap = col / p.C, c = col - tap * p.C;
+    const int r = tap / p.S, s = tap - r * p.S;
+    dh = r * p.dil_h - p.pad_h;
+    dw = s * p.dil_w - p.pad_w;
+    const int PQ = p.P * p.Q;
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      m[i] = mbeg + tid / G::TPR + G::RSTEP * i;
+      const int n = m[i] / PQ, rem = m[i] - n * PQ, pp = rem / p.Q, qq = rem - pp * p.Q;
+      hh[i] = pp * p.stride_h + dh;
+      ww[i] = qq * p.stride_w + dw;
+      off[i] = (((n * p.H + hh[i]) * p.W + ww[i]) * p.ldx + c) * 2;
+    }
+  }
+  __device__ __forceinline__ void load(const WgradParams& p, __amdgpu_buffer_rsrc_t r, int mend,
+                                       u32x4 (&d)[G::V]) const {
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      const bool ok = m[i] < mend && (unsigned)hh[i] < (unsigned)p.H && (unsigned)ww[i] < (unsigned)p.W;
+      const uint32_t base = ok ? (uint32_t)off[i] : HCB_OOB;
+#pragma unroll
+      for (int s = 0; s < G::SEGV; ++s) d[i * G::SEGV + s] = buf_load16(r, colok[s] ? base + 16u * s : HCB_OOB);
+    }
+  }
+  __device__ __forceinline__ void advance(const WgAdvance& a, int sh) {
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      int w = ww[i] + a.dqw, h = hh[i], o = off[i] + a.dqo;
+      const bool cq = w >= a.qs + dw;  // q wrapped: next output row
+      w = cq ? w - a.qs : w;
+      h = cq ? h + sh : h;
+      o = cq ? o + a.qco : o;
+      h += a.dph;
+      o += a.dpo;
+      const bool cp = h >= a.ps + dh;  // p wrapped: next image
+      h = cp ? h - a.ps : h;
+      o = cp ? o + a.pco : o;
+      ww[i] = w;
+      hh[i] = h;
+      off[i] = o + a.dno;
+      m[i] += ROWS;
+    }
+  }
+};
+
+// Shared-row variant of the X loader, for tiles whose columns all lie in ONE filter tap
+// (1x1 convs, or C % tile cols == 0): every lane of a pixel row then needs the same source
+// pixel, so instead of each lane stepping all RPT of its rows (VPR lanes redundantly per row),
+// lane t of a wave steps just wave row t and the loads fetch their row's byte offset from the
+// owning lane with one ds_bpermute (__shfl) + the lane's channel offset.
+template <int ROWS, int COLS, int NT>
+struct WgBLoadShared {
+  using G = WgSeg<ROWS, COLS, NT>;
+  static constexpr int RW = 64 / G::TPR;   // rows per load instruction per wave
+  static constexpr int TRK = RW * G::RPT;  // rows a wave loads per k-step
+  static_assert(64 % G::TPR == 0 && TRK <= 64, "one tracked row per lane");
+  int th, tw, tm, toff;  // tracked row: input row / col (tap applied), pixel index, byte offset
+  int dh, dw;
+  int src[G::RPT];       // lane owning row (lane / TPR) + RW * i of this wave
+  uint32_t lane_c;       // this lane's byte offset within the row segment
+  bool colok;
+  __device__ __forceinline__ void init(const WgradParams& p, int mbeg, int j0, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    const int col = j0 + (tid % G::TPR) * 8;
+    colok = col < p.K;
+    lane_c = (uint32_t)((tid % G::TPR) * 16);
+    const int tap = j0 / p.C, c0 = j0 - tap * p.C;  // the tile's tap (uniform)
+    const int r = tap / p.S, s = tap - r * p.S;
+    dh = r * p.dil_h - p.pad_h;
+    dw = s * p.dil_w - p.pad_w;
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) src[i] = lane / G::TPR + RW * i;
+    const int t = lane < TRK ? lane : TRK - 1;
+    const int row = w * RW + t % RW + G::RSTEP * (t / RW);
+    tm = mbeg + row;
+    const int PQ = p.P * p.Q;
+    const int n = tm / PQ, rem = tm - n * PQ, pp = rem / p.Q, qq = rem - pp * p.Q;
+    th = pp * p.stride_h + dh;
+    tw = qq * p.stride_w + dw;
+    toff = (((n * p.H + th) * p.W + tw) * p.ldx + c0) * 2;
+  }
+  __device__ __forceinline__ void load(const WgradParams& p, __amdgpu_buffer_rsrc_t r, int mend,
+                                       u32x4 (&d)[G::V]) const {
+    const bool ok = tm < mend && (unsigned)th < (unsigned)p.H && (unsigned)tw < (unsigned)p.W;
+    const int val = ok ? toff : (int)HCB_OOB;
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      const uint32_t o = (uint32_t)__shfl(val, src[i], 64);  // OOB + lane_c stays out of range
+      d[i] = buf_load16(r, colok ? o + lane_c : HCB_OOB);
+    }
+  }
+  __device__ __forceinline__ void advance(const WgAdvance& a, int sh) {
+    int w = tw + a.dqw, h = th, o = toff + a.dqo;
+    const bool cq = w >= a.qs + dw;
+    w = cq ? w - a.qs : w;
+    h = cq ? h + sh : h;
+    o = cq ? o + a.qco : o;
+    h += a.dph;
+    o += a.dpo;
+    const bool cp = h >= a.ps + dh;
+    th = cp ? h - a.ps : h;
+    tw = w;
+    toff = (cp ? o + a.pco : o) + a.dno;
+    tm += ROWS;
+  }
+};
+
+// LD: 0 generic im2col columns, 1 whole tile in one tap (C % BN == 0), 2 row-incremental (RI)
+// per-lane rows, 3 RI with shared rows (one tap per tile)
+template <int WM, int WN, int TM, int TN, int LD>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
+  constexpr bool CBIG = LD == 1, RI = LD >= 2, RIS = LD == 3;
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AVR = BM / 8, BVR = BN / 8;        // 16-byte vectors per LDS row
@@ -108,7 +332,27 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  using GA = WgSeg<BK, BM, 256>;
+  using GB = WgSeg<BK, BN, 256>;
+  static_assert(!RI || (GA::V == AV && GB::V == BV), "RI mapping");
+  WgALoad<BK, BM, 256> ald;
+  std::conditional_t<RIS, WgBLoadShared<BK, BN, 256>, WgBLoad<BK, BN, 256>> bld;
+  WgAdvance adv;
+  const uint32_t a_step = (uint32_t)(BK * p.ldy * 2);
+  if constexpr (RI) {
+    ald.init(p, kt_begin * BK, i0, tid);
+    bld.init(p, kt_begin * BK, j0, tid);
+    adv = wg_advance(p, BK);
+  }
   auto gload = [&](int kt) {
+    if constexpr (RI) {
+      // k-steps are issued strictly in order: the loaders hold k-step kt's rows
+      ald.load(dyr, p.M, ra);
+      bld.load(p, xr, p.M, rb);
+      ald.advance(a_step);
+      bld.advance(adv, p.stride_h);
+      return;
+    }
     const int mb = kt * BK;
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
@@ -133,6 +377,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     }
   };
   auto lstore = [&](int buf) {
+    if constexpr (RI) {
+#pragma unroll
+      for (int v = 0; v < AV; ++v)
+        *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = ra[v];
+#pragma unroll
+      for (int v = 0; v < BV; ++v)
+        *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = rb[v];
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       int row = a_r0 + A_RSTEP * v;
@@ -409,8 +662,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradPara
 // tile over a 32-deep quarter -- against the 2x2 arrangement of 32x32 wave tiles this halves
 // the transposed LDS fragment bytes per MFMA (16 reads feed 16 MFMAs per wave, not 8 reads 4
 // MFMAs), and that kernel is LDS-read bound. <2,1,2> / <1,2,2>: 128x64 / 64x128 blocks.
-template <int WMt, int WNt, int KS>
+// RIM: 0 original loaders, 1 row-incremental per-lane rows, 2 row-incremental shared rows
+template <int WMt, int WNt, int KS, int RIM>
 __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
+  constexpr bool RI = RIM >= 1;
   static_assert(WMt * WNt * KS == 4, "4 waves");
   constexpr int BM = 64 * WMt, BN = 64 * WNt, BK = 128, KW = BK / KS;  // KW: k rows per wave
   constexpr int AVR = BM / 8, BVR = BN / 8;                // 16-byte vectors per LDS row
@@ -452,7 +707,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
   const int b_dh = b_r * p.dil_h - p.pad_h, b_dw = b_s * p.dil_w - p.pad_w;
 
   u32x4 ra[AV], rb[BV];
+  using GA = WgSeg<BK, BM, 256>;
+  using GB = WgSeg<BK, BN, 256>;
+  static_assert(!RI || (GA::V == AV && GB::V == BV), "RI mapping");
+  WgALoad<BK, BM, 256> ald;
+  std::conditional_t<RIM == 2, WgBLoadShared<BK, BN, 256>, WgBLoad<BK, BN, 256>> bld;
+  WgAdvance adv;
+  const uint32_t a_step = (uint32_t)(BK * p.ldy * 2);
+  if constexpr (RI) {
+    ald.init(p, mbeg, i0, tid);
+    bld.init(p, mbeg, j0, tid);
+    adv = wg_advance(p, BK);
+  }
   auto gload = [&](int kt) {
+    if constexpr (RI) {  // k-steps in order: the loaders hold k-step kt's rows
+      ald.load(dyr, mend, ra);
+      bld.load(p, xr, mend, rb);
+      ald.advance(a_step);
+      bld.advance(adv, p.stride_h);
+      return;
+    }
     const int mb = mbeg + kt * BK;
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
@@ -476,6 +750,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
     }
   };
   auto lstore = [&](int buf) {
+    if constexpr (RI) {
+#pragma unroll
+      for (int v = 0; v < AV; ++v)
+        *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = ra[v];
+#pragma unroll
+      for (int v = 0; v < BV; ++v)
+        *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = rb[v];
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       const int row = a_r0 + A_RSTEP * v;
@@ -568,6 +851,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
   wgrad_store_tile(p, Cs, LDC, BM, BN, i0, j0, tid, 256, gridDim.x == ntiles);
 }
 
+// the row-incremental loaders need a thread's 16-byte vector inside one filter tap
+static bool wgrad_ri_ok(const WgradParams& p) { return (p.C % 8) == 0 && riv_enabled(); }
+// every column tile of width BN lies in one filter tap (shared-row X loader)
+static bool wgrad_one_tap(const WgradParams& p, int BN) {
+  return (p.R * p.S == 1 || (p.C % BN) == 0) && shared_rows_enabled();
+}
+
 template <int WMt, int WNt, int KS>
 static void wlaunch_kq(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = 64 * WMt, BN = 64 * WNt;
@@ -577,11 +867,21 @@ static void wlaunch_kq(const WgradParams& p, int splits, hipStream_t st) {
   const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS>,
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, 0>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, 2>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
-  hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS>), dim3(tiles * splits), dim3(256), lds, st, p);
+  const dim3 grid(tiles * splits);
+  if (!wgrad_ri_ok(p))
+    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, 0>), grid, dim3(256), lds, st, p);
+  else if (wgrad_one_tap(p, BN))
+    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, 2>), grid, dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, 1>), grid, dim3(256), lds, st, p);
 }
 
 template <int WM, int WN, int TM, int TN, int NST>
@@ -613,25 +913,28 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
   size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2;
   size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-  bool cbig = (p.C % BN) == 0;
+  const int ld = wgrad_ri_ok(p) ? (wgrad_one_tap(p, BN) ? 3 : 2) : ((p.C % BN) == 0 ? 1 : 0);
   dim3 grid(tiles * splits);
-  if (cbig) {
-    static bool once = false;
-    if (!once) {
-      (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      once = true;
-    }
-    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true>), grid, dim3(256), lds, st, p);
-  } else {
-    static bool once = false;
-    if (!once) {
-      (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      once = true;
-    }
-    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false>), grid, dim3(256), lds, st, p);
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 0>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 3>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    once = true;
   }
+  if (ld == 3)
+    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 3>), grid, dim3(256), lds, st, p);
+  else if (ld == 2)
+    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 2>), grid, dim3(256), lds, st, p);
+  else if (ld == 1)
+    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 1>), grid, dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 0>), grid, dim3(256), lds, st, p);
 }
 
 // cfg 0..2: register-staged {128x128, 64x128, 64x64}; 3..9: LDS-DMA ring {128x128 (4 waves of

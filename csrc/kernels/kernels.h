@@ -94,6 +94,9 @@ struct WgradParams {
   uint32_t dy_bytes, x_bytes;
 };
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st);
+// row-incremental weight-grad loaders on (default) / off, for A/B runs
+void set_wgrad_ri(int on);
+bool riv_enabled();
 int wgrad_tile_m(int cfg);
 int wgrad_tile_n(int cfg);
 

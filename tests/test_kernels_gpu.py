@@ -261,6 +261,41 @@ def test_conv_wgrad_all_configs(cfg):
         assert rel_err(dw, ref.view(cout, -1)) < 1e-2, (cfg, cin, cout, k)
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 10, 11, 12])
+def test_conv_wgrad_row_incremental_loaders(cfg):
+    """The row-incremental register-staged loaders (mixed-radix pixel stepping; per-lane rows,
+    and rows shared through ds_bpermute when a column tile lies in one filter tap) against the
+    original divide-per-row loaders: with one split (no atomics) all run the
+    same MFMA sequence, so dW must be bitwise equal; plus the fp32 CPU reference. Geometries
+    cover a k-step spanning images (7x7 output: dn > 0), output-row carries, stride 2 with
+    padding, partial Nout / pixel tiles."""
+    hcb = _ext.ops()
+    torch.manual_seed(8)
+    try:
+        for cin, cout, k, s, pads, H, N in [(64, 64, 3, 1, (1, 1, 1, 1), 14, 3),
+                                            (128, 72, 3, 1, (1, 1, 1, 1), 7, 5),
+                                            (96, 128, 3, 2, (1, 1, 1, 1), 15, 2),
+                                            (256, 192, 1, 1, (0, 0, 0, 0), 9, 4),
+                                            (64, 256, 1, 2, (0, 0, 0, 0), 13, 3)]:
+            spec, p, pk = make_conv(cin, cout, k, k, s, s, pads)
+            P, Q = spec.out_hw(H, H)
+            x = bf(torch.randn(N, H, H, cin, device=DEV))
+            dz = bf(torch.randn(N, P, Q, cout, device=DEV))
+            out = []
+            for ri in (0, 2, 1):  # original, row-incremental per-lane rows, shared rows (one tap per tile)
+                hcb.set_wgrad_ri(ri)
+                dw = torch.zeros(cout, spec.K, dtype=torch.float32, device=DEV)
+                Fn.conv_wgrad(dz, x, spec, dw, cfg=(cfg, 1))
+                out.append(dw)
+            assert torch.equal(out[0], out[1]), (cfg, cin, cout, k, s)
+            assert torch.equal(out[0], out[2]), (cfg, cin, cout, k, s)
+            ref = torch.zeros(cout, k, k, cin)
+            Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
+            assert rel_err(out[2], ref.view(cout, -1)) < 1e-2, (cfg, cin, cout, k)
+    finally:
+        hcb.set_wgrad_ri(1)
+
+
 def test_conv_wgrad_split_k_large_reduction():
     torch.manual_seed(5)
     spec, p, pk = make_conv(64, 64, 3, 3, 1, 1, (1, 1, 1, 1))

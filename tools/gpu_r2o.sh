@@ -1,0 +1,11 @@
+# restored-tree check (smoke, GPU suite, default bench) + hipBLASLt same-shape ceiling per conv GEMM
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/o_smoke.log 2>&1 || { tail -20 gpurun_out/o_smoke.log; exit 1; }
+tail -1 gpurun_out/o_smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/o_pytest_gpu.log 2>&1 || { tail -30 gpurun_out/o_pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/o_pytest_gpu.log
+timeout -k 10 300 python bench.py > gpurun_out/o_bench.json 2> gpurun_out/o_bench.err || { tail -20 gpurun_out/o_bench.err; exit 1; }
+cut -c1-220 gpurun_out/o_bench.json
+timeout -k 10 300 python -u tools/gemm_equiv.py > gpurun_out/o_gemm_equiv.txt 2>&1 || { tail -20 gpurun_out/o_gemm_equiv.txt; exit 1; }
+cat gpurun_out/o_gemm_equiv.txt
