@@ -799,6 +799,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
 // of one pooled pixel x 8 channels, keeps the max and the first-max window position (the
 // argmax the pool backward gathers with), and stores only the pooled tensor. The backward
 // recomputes the ReLU mask from z (mode 2), so nothing else needs the full-size activation.
+// K3: the 3x3 window unrolled, its 9 loads in flight together (buffer loads, out-of-image taps
+// excluded by a select) instead of one dependent loop trip per tap.
+template <bool K3>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
     const uint16_t* __restrict__ z, int H, int W, int C, int CVB, uint16_t* __restrict__ y, int P, int Q, int ldy,
     uint8_t* __restrict__ amax, int kh, int kw, int sh, int sw, int ph, int pw, int Nimg, int M,
@@ -849,6 +852,32 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
       best[e] = -INFINITY;
       arg[e] = 255;
     }
+    if constexpr (K3) {
+      const __amdgpu_buffer_rsrc_t zr = make_rsrc(z, (uint32_t)M * (uint32_t)C * 2u);
+      const int base = ((n * H + h0) * W + w0) * C + gm.cv * 8;  // element offset of tap (0, 0)
+      u32x4 v[9];
+      bool okt[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          okt[r * 3 + t] = (unsigned)(h0 + r) < (unsigned)H && (unsigned)(w0 + t) < (unsigned)W;
+          v[r * 3 + t] = buf_load16(zr, okt[r * 3 + t] ? (uint32_t)(base + (r * W + t) * C) * 2u : HCB_OOB);
+        }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        float f[8];
+        unpack8(v[k], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float val = okt[k] ? fmaxf(f[e] * sc[e] + sft[e], 0.f) : -INFINITY;
+          if (val > best[e]) {  // strict: the FIRST maximal element keeps the gradient
+            best[e] = val;
+            arg[e] = k;
+          }
+        }
+      }
+    } else
     for (int r = 0; r < kh; ++r) {
       const int h = h0 + r;
       if ((unsigned)h >= (unsigned)H) continue;
@@ -926,9 +955,11 @@ void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void*
                                 hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(N * P * Q, C, &cvb);
-  hipLaunchKernelGGL(bn_relu_maxpool_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W,
-                     C, cvb, (uint16_t*)y, P, Q, ldy, (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps,
-                     momentum, gamma, beta, saved_mean, saved_invstd, run_mean, run_var, shift);
+  const bool k3 = kh == 3 && kw == 3 && (long)N * H * W * C < (1l << 30);
+  hipLaunchKernelGGL(k3 ? bn_relu_maxpool_acc_kernel<true> : bn_relu_maxpool_acc_kernel<false>, grid, dim3(256),
+                     (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W, C, cvb, (uint16_t*)y, P, Q, ldy,
+                     (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps, momentum, gamma, beta,
+                     saved_mean, saved_invstd, run_mean, run_var, shift);
 }
 
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,

@@ -297,61 +297,64 @@ __global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const uint16_t* __r
 
 // Max-pool backward from the recorded argmax when at most NPW x NPW windows cover a pixel
 // (ceil(k/s) <= NPW; ResNet's 3x3/2: 2x2): the candidate windows are unrolled so all their dy /
-// argmax loads are in flight together instead of one loop trip at a time.
+// argmax loads are in flight together instead of one loop trip at a time. Grid: x over the
+// (w, channel vector) pairs of one input row, y = n * H + h, so the row / image indices are
+// wave-uniform (no per-thread divisions: the earlier flat index cost four runtime-divisor
+// divides per 8-channel item) and offsets are 32-bit.
 template <int NPW>
 __global__ __launch_bounds__(256) void maxpool_bwd_amax_kernel(
     const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N, int H, int W, int C, int ldx, int P, int Q,
-    int ldy, int kw, int sh, int sw, int ph, int pw, int accum, const uint8_t* __restrict__ amax) {
-  const unsigned CV = (unsigned)C >> 3;
-  const unsigned total = (unsigned)N * H * W * CV;
-  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-    const int cv = (int)(idx % CV);
-    const unsigned pix = idx / CV;
-    const int w = (int)(pix % (unsigned)W);
-    const unsigned t = pix / (unsigned)W;
-    const int h = (int)(t % (unsigned)H);
-    const int n = (int)(t / (unsigned)H);
-    // windows p with p*sh - ph <= h, i.e. p <= (h+ph)/sh, and h < p*sh - ph + kh
-    const int p_hi = (h + ph) / sh, q_hi = (w + pw) / sw;
-    u32x4 d[NPW][NPW];
-    u32x2 a[NPW][NPW];
-    bool ok[NPW][NPW];
+    int ldy, int kw, int sh, int sw, int ph, int pw, int accum, const uint8_t* __restrict__ amax, int cv_shift) {
+  const int CV = C >> 3;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= W * CV) return;
+  const int w = cv_shift >= 0 ? idx >> cv_shift : idx / CV;
+  const int cv = idx - w * CV;
+  const int t = blockIdx.y;  // n * H + h (uniform)
+  const int n = t / H, h = t - n * H;
+  // windows p with p*sh - ph <= h, i.e. p <= (h+ph)/sh, and h < p*sh - ph + kh
+  const int p_hi = (h + ph) / sh, q_hi = (w + pw) / sw;
+  u32x4 d[NPW][NPW];
+  u32x2 a[NPW][NPW];
+  bool ok[NPW][NPW];
 #pragma unroll
-    for (int i = 0; i < NPW; ++i)
+  for (int i = 0; i < NPW; ++i) {
+    const int p = p_hi - i;
+    const bool pok = p >= 0 && p < P && h - (p * sh - ph) < kw;  // uniform
+    const uint32_t prow = (uint32_t)(n * P + (pok ? p : 0)) * (uint32_t)Q;
 #pragma unroll
-      for (int j = 0; j < NPW; ++j) {
-        const int p = p_hi - i, q = q_hi - j;
-        const int h0 = p * sh - ph, w0 = q * sw - pw;
-        ok[i][j] = p >= 0 && q >= 0 && p < P && q < Q && h - h0 < kw && w - w0 < kw;  // kh == kw
-        const size_t o = ((size_t)(n * P + (ok[i][j] ? p : 0)) * Q + (ok[i][j] ? q : 0));
-        d[i][j] = *reinterpret_cast<const u32x4*>(dy + o * ldy + cv * 8);
-        a[i][j] = *reinterpret_cast<const u32x2*>(amax + o * C + cv * 8);
-      }
-    float g[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = 0.f;
-#pragma unroll
-    for (int i = 0; i < NPW; ++i)
-#pragma unroll
-      for (int j = 0; j < NPW; ++j) {
-        const int p = p_hi - i, q = q_hi - j;
-        const int mine = (h - (p * sh - ph)) * kw + (w - (q * sw - pw));
-        if (!ok[i][j]) continue;
-        float f[8];
-        unpack8(d[i][j], f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if ((int)((a[i][j][e >> 2] >> (8 * (e & 3))) & 0xff) == mine) g[e] += f[e];
-      }
-    uint16_t* dp = dx + ((size_t)(n * H + h) * W + w) * ldx + cv * 8;
-    if (accum) {
-      float o[8];
-      unpack8(*reinterpret_cast<const u32x4*>(dp), o);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] += o[e];
+    for (int j = 0; j < NPW; ++j) {
+      const int q = q_hi - j;
+      ok[i][j] = pok && q >= 0 && q < Q && w - (q * sw - pw) < kw;  // kh == kw
+      const uint32_t o = prow + (uint32_t)(ok[i][j] ? q : 0);
+      d[i][j] = *reinterpret_cast<const u32x4*>(dy + o * (uint32_t)ldy + cv * 8);
+      a[i][j] = *reinterpret_cast<const u32x2*>(amax + o * (uint32_t)C + cv * 8);
     }
-    *reinterpret_cast<u32x4*>(dp) = pack8(g);
   }
+  float g[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPW; ++i)
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) {
+      const int p = p_hi - i, q = q_hi - j;
+      const int mine = (h - (p * sh - ph)) * kw + (w - (q * sw - pw));
+      if (!ok[i][j]) continue;
+      float f[8];
+      unpack8(d[i][j], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if ((int)((a[i][j][e >> 2] >> (8 * (e & 3))) & 0xff) == mine) g[e] += f[e];
+    }
+  uint16_t* dp = dx + ((uint32_t)t * (uint32_t)W + (uint32_t)w) * (uint32_t)ldx + cv * 8;
+  if (accum) {
+    float o[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dp), o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] += o[e];
+  }
+  *reinterpret_cast<u32x4*>(dp) = pack8(g);
 }
 
 // global average pool [N][HW][C] -> [N][C]
@@ -426,14 +429,20 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
                      int pw, int is_max, int count_include_pad, int accum, const void* idx,
                      hipStream_t st) {
   long total = (long)N * H * W * (C / 8);
-  if (is_max && idx != nullptr && (kh + sh - 1) / sh <= 2 && (kw + sw - 1) / sw <= 2 && kh == kw && sh == sw) {
-    hipLaunchKernelGGL(maxpool_bwd_amax_kernel<2>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
-                       (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx);
+  // argmax gather: 2-D grid (input row, w x channel vector); 32-bit offsets
+  const bool amax_ok = is_max && idx != nullptr && kh == kw && sh == sw && (long)N * H <= 65535 &&
+                       (long)N * H * W * ldx < (1l << 31) && (long)N * P * Q * (ldy > C ? ldy : C) < (1l << 31);
+  const int cvn = C / 8;
+  const int cv_shift = (cvn & (cvn - 1)) == 0 ? __builtin_ctz((unsigned)cvn) : -1;
+  const dim3 agrid((unsigned)((W * cvn + 255) / 256), (unsigned)(N * H));
+  if (amax_ok && (kh + sh - 1) / sh <= 2) {
+    hipLaunchKernelGGL(maxpool_bwd_amax_kernel<2>, agrid, dim3(256), 0, st, (const uint16_t*)dy, (uint16_t*)dx, N, H,
+                       W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx, cv_shift);
     return;
   }
-  if (is_max && idx != nullptr && (kh + sh - 1) / sh <= 3 && (kw + sw - 1) / sw <= 3 && kh == kw && sh == sw) {
-    hipLaunchKernelGGL(maxpool_bwd_amax_kernel<3>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
-                       (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx);
+  if (amax_ok && (kh + sh - 1) / sh <= 3) {
+    hipLaunchKernelGGL(maxpool_bwd_amax_kernel<3>, agrid, dim3(256), 0, st, (const uint16_t*)dy, (uint16_t*)dx, N, H,
+                       W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx, cv_shift);
     return;
   }
   const long dybytes = (long)N * P * Q * ldy * 2;
