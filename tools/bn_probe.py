@@ -45,7 +45,7 @@ def main():
         t_b = tm(lambda: Fn.bn_backward_acc(g, None, z, saved, gamma, beta, 0, dg, db, y, acc, R, pre_reduced=True))
         t_c = tm(lambda: y.copy_(z))
         t_a = tm(lambda: torch.add(z, r, out=y))
-        bw = lambda n, t: n * mb / t / 1e3
+        bw = lambda n, t: n * mb / t  # MB/us = TB/s
         print(f"{M:7d} x {C:4d} {mb:6.1f} | {t_f:6.1f} {bw(2, t_f):4.2f} | {t_r:6.1f} {bw(3, t_r):4.2f} | {t_b:6.1f} "
               f"{bw(3, t_b):4.2f} | {t_c:6.1f} {bw(2, t_c):4.2f} {t_a:6.1f} {bw(3, t_a):4.2f}", flush=True)
 
