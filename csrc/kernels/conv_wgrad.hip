@@ -416,8 +416,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   gload(kt_begin);
   lstore(0);
   __syncthreads();
-  for (int kt = kt_begin; kt < kt_end; ++kt) {
-    const int cur = (kt - kt_begin) & 1;
+  // the k-loop is unrolled by two so the LDS buffer of each half is a compile-time constant: the
+  // fragment-read addresses become loop-invariant registers + immediate offsets (no per-k-step
+  // address VALU)
+  auto kstep = [&](auto cur_c, int kt) {
+    constexpr int cur = decltype(cur_c)::value;
     if (kt + 1 < kt_end) gload(kt + 1);
     const char* Ab = As + cur * BK * BM * 2;
     const char* Bb = Bs + cur * BK * BN * 2;
@@ -448,6 +451,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     }
     if (kt + 1 < kt_end) lstore(cur ^ 1);
     __syncthreads();
+  };
+  for (int kt = kt_begin; kt < kt_end; kt += 2) {
+    kstep(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < kt_end) kstep(std::integral_constant<int, 1>{}, kt + 1);
   }
 
   // epilogue: stage fp32 tile in LDS, then 256-byte contiguous atomic rows
