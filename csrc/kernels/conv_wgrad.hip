@@ -413,17 +413,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * BN * 2 + slot * 32 + (cb & 31)));
   };
 
-  gload(kt_begin);
-  lstore(0);
-  __syncthreads();
-  // the k-loop is unrolled by two so the LDS buffer of each half is a compile-time constant: the
-  // fragment-read addresses become loop-invariant registers + immediate offsets (no per-k-step
-  // address VALU)
-  auto kstep = [&](auto cur_c, int kt) {
-    constexpr int cur = decltype(cur_c)::value;
-    if (kt + 1 < kt_end) gload(kt + 1);
-    const char* Ab = As + cur * BK * BM * 2;
-    const char* Bb = Bs + cur * BK * BN * 2;
+  auto mfma_kstep = [&](const char* Ab, const char* Bb) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       act16x8 af[MI], bfr[NI];
@@ -449,12 +439,70 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
         for (int j = 0; j < NI; ++j)
           acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (kt + 1 < kt_end) lstore(cur ^ 1);
-    __syncthreads();
   };
-  for (int kt = kt_begin; kt < kt_end; kt += 2) {
-    kstep(std::integral_constant<int, 0>{}, kt);
-    if (kt + 1 < kt_end) kstep(std::integral_constant<int, 1>{}, kt + 1);
+
+  if constexpr (RI) {
+    // Two register sets: the loads of k-step k+2 are issued while k-step k is multiplied and
+    // k+1 is stored to LDS, so a load has two k-steps (not one) of MFMA time to land -- the
+    // 64x64 tile's 8 MFMAs per wave and k-step are far shorter than an L2 round trip.
+    u32x4 sa[2][AV], sb[2][BV];
+    // rows past this split's range come back as zeros without memory traffic, so the loads
+    // and stores of the pipeline tail need no conditions (straight-line k-loop)
+    const int mend = min(kt_end * BK, p.M);
+    auto ld = [&](auto set_c) {
+      constexpr int S = decltype(set_c)::value;
+      ald.load(dyr, mend, sa[S]);
+      bld.load(p, xr, mend, sb[S]);
+      ald.advance(a_step);
+      bld.advance(adv, p.stride_h);
+    };
+    auto st = [&](auto set_c, int buf) {
+      constexpr int S = decltype(set_c)::value;
+#pragma unroll
+      for (int v = 0; v < AV; ++v)
+        *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = sa[S][v];
+#pragma unroll
+      for (int v = 0; v < BV; ++v)
+        *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = sb[S][v];
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    const int nks = kt_end - kt_begin;
+    ld(I0{});
+    ld(I1{});
+    st(I0{}, 0);
+    __syncthreads();
+    auto kstep = [&](auto cur_c, int k) {
+      constexpr int cur = decltype(cur_c)::value;
+      ld(cur_c);  // k-step k + 2 into set `cur` (stored to LDS one k-step ago)
+      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
+      st(std::integral_constant<int, cur ^ 1>{}, cur ^ 1);  // k-step k + 1
+      __syncthreads();
+    };
+    // an odd count runs one extra k-step over all-zero tiles (both operands out of range: adds
+    // exactly 0) instead of a conditional second half, which made the compiler copy the
+    // accumulators between register files every iteration
+    for (int k = 0; k < nks; k += 2) {
+      kstep(I0{}, k);
+      kstep(I1{}, k + 1);
+    }
+  } else {
+    gload(kt_begin);
+    lstore(0);
+    __syncthreads();
+    // the k-loop is unrolled by two so the LDS buffer of each half is a compile-time constant:
+    // the fragment-read addresses become loop-invariant registers + immediate offsets
+    auto kstep = [&](auto cur_c, int kt) {
+      constexpr int cur = decltype(cur_c)::value;
+      if (kt + 1 < kt_end) gload(kt + 1);
+      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
+      if (kt + 1 < kt_end) lstore(cur ^ 1);
+      __syncthreads();
+    };
+    for (int kt = kt_begin; kt < kt_end; kt += 2) {
+      kstep(std::integral_constant<int, 0>{}, kt);
+      if (kt + 1 < kt_end) kstep(std::integral_constant<int, 1>{}, kt + 1);
+    }
   }
 
   // epilogue: stage fp32 tile in LDS, then 256-byte contiguous atomic rows

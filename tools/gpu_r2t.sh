@@ -1,4 +1,4 @@
-# weight-grad k-loop unrolled by two (constant LDS buffers): tests, per-layer A/B, bench
+# weight-grad two-set register prefetch: tests, per-layer A/B, bench
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "wgrad" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_test.log 2>&1 || { tail -30 gpurun_out/t_test.log; exit 1; }
