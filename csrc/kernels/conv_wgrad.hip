@@ -846,14 +846,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
-    const char* Ab = As + cur * BK * BM * 2;
-    const char* Bb = Bs + cur * BK * BN * 2;
+  auto mfma_kstep = [&](const char* Ab, const char* Bb) {
 #pragma unroll
     for (int ks = 0; ks < KW / 32; ++ks) {
       const int krow = wk * KW + ks * 32;
@@ -878,8 +871,58 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+  };
+
+  // the 64x64 (1,1,4) variant keeps the single-set loop: with two sets the compiler copies its 64
+  // accumulators between register files every k-step (56 extra VALU per two k-steps)
+  constexpr bool PIPE2 = RI && !(WMt == 1 && WNt == 1);
+  if constexpr (PIPE2) {
+    // two register sets, k-step k + 2 in flight while k is multiplied (see conv_wgrad_kernel)
+    u32x4 sa[2][AV], sb[2][BV];
+    auto ld = [&](auto set_c) {
+      constexpr int S = decltype(set_c)::value;
+      ald.load(dyr, mend, sa[S]);
+      bld.load(p, xr, mend, sb[S]);
+      ald.advance(a_step);
+      bld.advance(adv, p.stride_h);
+    };
+    auto st = [&](auto set_c, int buf) {
+      constexpr int S = decltype(set_c)::value;
+#pragma unroll
+      for (int v = 0; v < AV; ++v)
+        *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = sa[S][v];
+#pragma unroll
+      for (int v = 0; v < BV; ++v)
+        *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = sb[S][v];
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    ld(I0{});
+    ld(I1{});
+    st(I0{}, 0);
     __syncthreads();
+    auto kstep = [&](auto cur_c) {
+      constexpr int cur = decltype(cur_c)::value;
+      ld(cur_c);
+      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
+      st(std::integral_constant<int, cur ^ 1>{}, cur ^ 1);
+      __syncthreads();
+    };
+    for (int k = 0; k < nk; k += 2) {  // odd counts: one extra all-zero k-step (adds 0)
+      kstep(I0{});
+      kstep(I1{});
+    }
+  } else {
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) gload(kt + 1);
+      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
+      if (kt + 1 < nk) lstore(cur ^ 1);
+      __syncthreads();
+    }
   }
 
   // the KS k-shares' partial tiles -> LDS, summed, then stored / atomically added
