@@ -412,7 +412,11 @@ template <int WM, int WN, int TM, int TN, int NST, bool BNB>
 static void launch_glds(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
-  size_t lds_main = (size_t)NST * (BM + BN) * 128;
+  // a block never touches more ring stages than it has k-steps: short-K layers (1x1 over 64-256
+  // channels: 1-4 k-steps) get the LDS of the stages they use, so more workgroups fit per CU
+  const int ksteps = (p.Kpad / 64 + p.splits - 1) / p.splits;
+  const int stages = ksteps < NST ? (ksteps > 0 ? ksteps : 1) : NST;
+  size_t lds_main = (size_t)stages * (BM + BN) * 128;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   bool cbig = (p.C % 64) == 0;
