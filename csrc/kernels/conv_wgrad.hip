@@ -1039,13 +1039,15 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
 // 64x64, NST 4), 128x128 (8 waves of 64x32), 256x128 (8 waves of 64x64), 128x256 (8 waves of
 // 64x64), 64x128 (8 waves of 32x32, NST 4), 64x64 (4 waves, NST 4), 64x128 (4 waves of 64x32,
 // NST 4)}
-constexpr int N_WGRAD_CFG = 13;  // 10-12: intra-workgroup k-split 64x64, 128x64, 64x128
+// 10-12: intra-workgroup k-split 64x64, 128x64, 64x128; 13-14: register-staged 128x64 / 64x128 with
+// 64x32 / 32x64 wave tiles (twice the MFMAs per loaded row of the 64x64 tile)
+constexpr int N_WGRAD_CFG = 15;
 int wgrad_tile_m(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64, 64, 128, 64};
+  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64, 64, 128, 64, 128, 64};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 int wgrad_tile_n(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128, 64, 64, 128};
+  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128, 64, 64, 128, 64, 128};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 
@@ -1063,6 +1065,8 @@ void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st
     case 10: wlaunch_kq<1, 1, 4>(p, splits, st); break;
     case 11: wlaunch_kq<2, 1, 2>(p, splits, st); break;
     case 12: wlaunch_kq<1, 2, 2>(p, splits, st); break;
+    case 13: wlaunch<2, 2, 64, 32>(p, splits, st); break;  // 128 x 64
+    case 14: wlaunch<2, 2, 32, 64>(p, splits, st); break;  // 64 x 128
     default: wlaunch<2, 2, 32, 32>(p, splits, st); break; // 64 x 64
   }
 }

@@ -239,10 +239,10 @@ def test_conv_wgrad(case):
     assert rel_err(dw, ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(13)))
+@pytest.mark.parametrize("cfg", list(range(15)))
 def test_conv_wgrad_all_configs(cfg):
-    """Every weight-grad tile config (register-staged 0-2, LDS-DMA ring 3-9, intra-workgroup
-    k-split 10-12) with split-K on
+    """Every weight-grad tile config (register-staged 0-2 and 13-14, LDS-DMA ring 3-9,
+    intra-workgroup k-split 10-12) with split-K on
     1x1 / 3x3 / strided / odd-channel geometries (partial tiles in Nout, K and pixels)."""
     torch.manual_seed(6)
     for cin, cout, k, s, pads, H, splits in [(64, 256, 1, 1, (0, 0, 0, 0), 14, 3),
@@ -261,7 +261,7 @@ def test_conv_wgrad_all_configs(cfg):
         assert rel_err(dw, ref.view(cout, -1)) < 1e-2, (cfg, cin, cout, k)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 10, 11, 12])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 10, 11, 12, 13, 14])
 def test_conv_wgrad_row_incremental_loaders(cfg):
     """The row-incremental register-staged loaders (mixed-radix pixel stepping; per-lane rows,
     and rows shared through ds_bpermute when a column tile lies in one filter tap) against the
