@@ -386,7 +386,7 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
   size_t lds_main = (size_t)2 * (BM + BN) * 8 * 16;
-  size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
+  size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
@@ -417,7 +417,7 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
   const int ksteps = (p.Kpad / 64 + p.splits - 1) / p.splits;
   const int stages = ksteps < NST ? (ksteps > 0 ? ksteps : 1) : NST;
   size_t lds_main = (size_t)stages * (BM + BN) * 128;
-  size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
+  size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;

@@ -13,9 +13,15 @@
 
 namespace hcb {
 
-// Bytes of LDS the epilogue needs for a BM x BN tile computed by WM x WN waves.
-constexpr size_t igemm_epilogue_lds(int BM, int BN, int WM) {
-  return (size_t)BM * (BN + 4) * 4 + (size_t)WM * 2 * BN * 4;
+// Bytes of LDS the epilogue needs for a BM x BN tile computed by WM x WN waves. s16: the plain
+// bf16-output epilogue without beta / bias stages the tile as 16-bit values (rounded once, the
+// same values the fp32 staging would store), half the LDS -- more workgroups per CU on the
+// memory-bound short-K layers whose occupancy the staging buffer sets.
+constexpr size_t igemm_epilogue_lds(int BM, int BN, int WM, bool s16 = false) {
+  return (s16 ? (size_t)BM * (BN + 8) * 2 : (size_t)BM * (BN + 4) * 4) + (size_t)WM * 2 * BN * 4;
+}
+__host__ __device__ inline bool igemm_stage16(const ConvParams& p) {
+  return !p.beta && !p.out_f32 && p.bias == nullptr && p.bnb_acc == nullptr;
 }
 
 // Output row of GEMM row m (strided-output remap: strided 1x1 data gradients, and the stride
@@ -83,7 +89,11 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   static_assert(NT % SEGS == 0 && ITER >= 1, "a thread keeps one column segment across the store pass");
   const int frow = lane & 15, fq = lane >> 4;
   float* Cs = reinterpret_cast<float*>(smem);
-  float* red = Cs + BM * LDC;  // [WM][2][BN] per-wave column partial sums
+  constexpr int LDC16 = BN + 8;  // 16-bit staging row (16-byte aligned rows)
+  const bool s16 = !BNB && igemm_stage16(p);
+  uint16_t* Cs16 = reinterpret_cast<uint16_t*>(smem);
+  float* red = s16 ? reinterpret_cast<float*>(smem + (size_t)BM * LDC16 * 2)
+                   : Cs + BM * LDC;  // [WM][2][BN] per-wave column partial sums
   if (p.stats != nullptr) {
     // per-column partial BN statistics straight from the accumulators, shifted by the
     // column's K: sum the wave's row quads in registers, then across the 4 lane groups that
@@ -124,16 +134,29 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       }
     }
   }
+  if (s16) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int row = wm * TM + i * 16 + fq * 4 + e;
-        int col = wn * TN + j * 16 + frow;
-        Cs[row * LDC + col] = acc[i][j][e];
-      }
+        for (int e = 0; e < 4; ++e) {
+          int row = wm * TM + i * 16 + fq * 4 + e;
+          int col = wn * TN + j * 16 + frow;
+          Cs16[row * LDC16 + col] = f2act(acc[i][j][e]);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int row = wm * TM + i * 16 + fq * 4 + e;
+          int col = wn * TN + j * 16 + frow;
+          Cs[row * LDC + col] = acc[i][j][e];
+        }
+  }
 
   const int cs = tid % SEGS;
   const int col = n0 + cs * 8;
@@ -186,6 +209,23 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   };
 
   if constexpr (!BNB) {
+    if (s16) {  // bf16 output, no beta / bias: rows of 8 staged 16-bit values, optional ReLU
+      for (int it = 0; it < ITER; ++it) {
+        const int row = (tid + it * NT) / SEGS;
+        const int m = m0 + row;
+        if (!col_ok || m >= p.M) continue;
+        u32x4 v = *reinterpret_cast<const u32x4*>(Cs16 + row * LDC16 + cs * 8);
+        if (p.relu) {
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+          v = pack8(f);
+        }
+        *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + out_row(m) * p.ldy + col) = v;
+      }
+      return;
+    }
     for (int it = 0; it < ITER; ++it) {
       const int row = (tid + it * NT) / SEGS;
       const int m = m0 + row;
