@@ -172,8 +172,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   constexpr int AV = BM / 32, BV = BN / 32;  // 16-byte vectors per thread per k-step
   static_assert(WM * WN == 4, "4 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  u32x4* As = reinterpret_cast<u32x4*>(smem);  // [2][BM*8]
-  u32x4* Bs = As + 2 * BM * 8;                 // [2][BN*8]
+  u32x4* As = reinterpret_cast<u32x4*>(smem);  // [2][BM*8] ([1][..] for a single k-step)
+  u32x4* Bs = As + (p.Kpad > 64 ? 2 : 1) * BM * 8;  // [2][BN*8]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -385,7 +385,8 @@ template <int WM, int WN, int TM, int TN, bool BNB>
 static void launch_reg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
-  size_t lds_main = (size_t)2 * (BM + BN) * 8 * 16;
+  // a single k-step (1x1 over <= 64 channels) uses one buffer pair
+  size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   bool cbig = (p.C % 64) == 0;
