@@ -62,7 +62,9 @@ def save_cache(path: str = DEFAULT_CACHE) -> None:
         json.dump({"arch": "gfx950", "version": CACHE_VERSION, "entries": old}, f, indent=0, sort_keys=True)
 
 
-def _time(fn, reps=5) -> float:
+def _time(fn, reps=None) -> float:
+    # HCB_TUNE_REPS: timed launches per candidate (default 5; more = less noise, slower tuning)
+    reps = reps or int(os.environ.get("HCB_TUNE_REPS", "5"))
     fn()
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
