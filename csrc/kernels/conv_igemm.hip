@@ -41,6 +41,17 @@ namespace hcb {
 // epilogue loads before the main loop (EpiPrefetch)
 constexpr int EARLY_EPI_KSTEPS = 2;
 
+// LDS offset of the fused BN-backward parameters: above the main-loop buffers and the epilogue
+// staging (full ring for the LDS-DMA kernels)
+constexpr size_t reg_param_off(int BM, int BN, int WM) {
+  const size_t a = (size_t)2 * (BM + BN) * 8 * 16, b = igemm_epilogue_lds(BM, BN, WM);
+  return a > b ? a : b;
+}
+constexpr size_t glds_param_off(int BM, int BN, int WM, int NST) {
+  const size_t a = (size_t)NST * (BM + BN) * 128, b = igemm_epilogue_lds(BM, BN, WM);
+  return a > b ? a : b;
+}
+
 // ---- per-thread implicit-im2col address generation, shared by both main loops.
 // k-steps are issued strictly in order (kt = 0, 1, 2, ...), so the loader keeps the current
 // filter tap / channel offset as wave-uniform state and advances it without divisions. In
@@ -226,6 +237,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   const int nk = p.Kpad / BK;
   EpiPrefetch<WM, WN, TM, TN, BNB> pre;
   pre.load_shift(p, n0, wn, lane);
+  constexpr size_t PARAM_OFF = reg_param_off(BM, BN, WM);
+  if constexpr (BNB) stage_bnb_params<BN, 256>(p, n0, smem + PARAM_OFF);  // published by the first barrier
   const bool early = BNB && nk <= EARLY_EPI_KSTEPS;
   if (early) pre.load(p, 0, m0, n0, tid);
   gload(0);
@@ -238,7 +251,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
-  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early);
+  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early, smem + PARAM_OFF);
 }
 
 // ============================================================== LDS-DMA multi-stage main loop
@@ -307,6 +320,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
   if (kb > 0) al.seek(p, kb);
   EpiPrefetch<WM, WN, TM, TN, BNB> pre;
   pre.load_shift(p, n0, wn, lane);
+  constexpr size_t PARAM_OFF = glds_param_off(BM, BN, WM, NST);
+  constexpr bool PARAM_LDS = PARAM_OFF + bnb_param_lds(BN) <= 160 * 1024;
+  if constexpr (BNB && PARAM_LDS) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
   const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS;
   if (early) pre.load(p, 0, m0, n0, tid);
 #pragma unroll
@@ -370,7 +386,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
         for (int j = 0; j < NI; ++j) acc[i][j] += slab[((size_t)s2 * FR + i * NI + j) * NT + tid];
     }
   }
-  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early);
+  igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early,
+                                      PARAM_LDS ? smem + PARAM_OFF : nullptr);
 }
 
 // ============================================================== launch
@@ -389,6 +406,7 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
   size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+  if (BNB) lds = reg_param_off(BM, BN, WM) + bnb_param_lds(BN);
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
@@ -420,6 +438,8 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
   size_t lds_main = (size_t)stages * (BM + BN) * 128;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+  if (BNB && glds_param_off(BM, BN, WM, NST) + bnb_param_lds(BN) <= 160 * 1024)
+    lds = glds_param_off(BM, BN, WM, NST) + bnb_param_lds(BN);
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;

@@ -80,10 +80,26 @@ struct EpiPrefetch {
   }
 };
 
+// Fused BN-backward: the tile's per-column (mean, invstd, gamma, beta) staged in LDS at kernel
+// start (one float4 per column, above every other use of the workgroup's LDS), so the epilogue
+// reads them with LDS latency instead of issuing 32 dependent global loads per thread after the
+// MFMAs (a full memory round trip exposed per workgroup).
+constexpr size_t bnb_param_lds(int BN) { return (size_t)BN * 16; }
+template <int BN, int NT>
+__device__ __forceinline__ void stage_bnb_params(const ConvParams& p, int n0, char* base) {
+  float4* bp = reinterpret_cast<float4*>(base);
+  for (int c = threadIdx.x; c < BN; c += NT) {
+    const int gc = n0 + c;
+    bp[c] = gc < p.Nout ? make_float4(p.bnb_mean[gc], p.bnb_invstd[gc], p.bnb_gamma[gc], p.bnb_beta[gc])
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 template <int WM, int WN, int TM, int TN, bool BNB>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)[TM / 16][TN / 16], char* smem,
                                                int tm, int m0, int n0, int wm, int wn, int lane, int tid,
-                                               EpiPrefetch<WM, WN, TM, TN, BNB>& pre, bool prefetched) {
+                                               EpiPrefetch<WM, WN, TM, TN, BNB>& pre, bool prefetched,
+                                               const char* bnb_params = nullptr) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN + 4;
@@ -271,10 +287,18 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const bool okc = col + e < p.Nout;
-      bmu[e] = okc ? p.bnb_mean[col + e] : 0.f;
-      bis[e] = okc ? p.bnb_invstd[col + e] : 0.f;
-      bsc[e] = okc ? p.bnb_gamma[col + e] * bis[e] : 0.f;
-      bsh[e] = okc ? p.bnb_beta[col + e] - bmu[e] * bsc[e] : 0.f;
+      if (bnb_params != nullptr) {
+        const float4 q = reinterpret_cast<const float4*>(bnb_params)[cs * 8 + e];  // zeros past Nout
+        bmu[e] = q.x;
+        bis[e] = q.y;
+        bsc[e] = q.z * q.y;
+        bsh[e] = q.w - q.x * bsc[e];
+      } else {  // the LDS budget had no room (deepest rings): global loads
+        bmu[e] = okc ? p.bnb_mean[col + e] : 0.f;
+        bis[e] = okc ? p.bnb_invstd[col + e] : 0.f;
+        bsc[e] = okc ? p.bnb_gamma[col + e] * bis[e] : 0.f;
+        bsh[e] = okc ? p.bnb_beta[col + e] - bmu[e] * bsc[e] : 0.f;
+      }
       bs1[e] = 0.f;
       bs2[e] = 0.f;
     }
