@@ -301,16 +301,24 @@ class BenchmarkCNN:
         images_per_sec = self.size * self.batch_size * self.num_batches / elapsed_max
         own_images_per_sec = self.size * self.batch_size * self.num_batches / elapsed
         final_loss = float(self.trainer.loss.item())
-        comm = None
-        if self.size > 1 and self.on_gpu and p.comm_profile:
-            comm = self.trainer.comm_profile(images, labels)
         if self.reducer is not None and hasattr(self.reducer, "check_errors"):
             self.reducer.check_errors()
         if loader is not None:
             loader.close()
+        # final state first (checkpoint, accuracy of the last timed step), THEN the comm profile,
+        # which runs extra steps (it restores the training state afterwards, and a failure in it
+        # cannot lose the measured result)
         if p.train_dir and self.rank == 0:
             checkpoint.save(p.train_dir, self.step_offset + self.num_warmup_batches + self.num_batches,
                             self.model.ps)
+        accs = self.trainer.accuracy(labels) if acc else None
+        comm = None
+        if self.size > 1 and self.on_gpu and p.comm_profile:
+            try:
+                comm = self.trainer.comm_profile(images, labels)
+            except Exception as e:  # noqa: BLE001 -- a profile failure must not lose the timed result
+                comm = {"error": f"{type(e).__name__}: {e}"}
+                log_fn(f"[rank {self.rank}] comm profile failed: {e}")
         # every worker prints its own total, as tf_cnn_benchmarks does under mpirun
         # (run-tf-sing-ucx-openmpi.sh:99-113); rank 0 reports the job figure (slowest rank)
         if self.rank == 0:
@@ -341,8 +349,8 @@ class BenchmarkCNN:
             allr = [torch.zeros_like(per_rank) for _ in range(self.size)]
             torch.distributed.all_gather(allr, per_rank)
             summary["per_rank_images_per_sec"] = [round(float(x.item()), 2) for x in allr]
-        if acc:
-            t1, t5 = self.trainer.accuracy(labels)
+        if accs is not None:
+            t1, t5 = accs
             summary["top_1_accuracy"], summary["top_5_accuracy"] = float(t1), float(t5)
         self.summary = summary
         if self.rank == 0:

@@ -80,6 +80,25 @@ def gpu_numa_nodes(sysfs: str = "/sys") -> List[int]:
     return out
 
 
+def visible_gpu_count(sysfs: str = "/sys") -> int:
+    """GPUs this process would see, counted WITHOUT any GPU runtime: the KFD topology's GPU
+    agents, filtered by HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (set but
+    empty = none). A launcher parent uses this so that neither torch nor HIP is ever loaded in the
+    process that forks the workers (torch.cuda.device_count() falls back to hipGetDeviceCount,
+    which initialises HIP, whenever its amdsmi query fails)."""
+    n = len(gpu_numa_nodes(sysfs))
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None:
+            continue
+        ids = [i.strip() for i in v.split(",") if i.strip() != ""]
+        try:
+            n = len([i for i in ids if 0 <= int(i) < n])
+        except ValueError:  # UUID-style ids: trust their count
+            n = min(n, len(ids))
+    return n
+
+
 def cpu_shares(n_workers: int, cpus: Optional[List[int]] = None, sysfs: str = "/sys") -> List[List[int]]:
     """CPU set per local worker: the cores of its GPU's NUMA node, split evenly between the
     workers whose GPUs share that node (the reference's ``--map-by ppr:W:socket,pe=C``,

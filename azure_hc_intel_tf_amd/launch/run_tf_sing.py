@@ -48,12 +48,9 @@ def gpus_per_node_default() -> int:
     v = os.environ.get("GPUS_PER_NODE")
     if v:
         return int(v)
-    try:
-        import torch
+    from .launcher import visible_gpu_count
 
-        return torch.cuda.device_count()  # counting devices does not initialise the GPU
-    except Exception:
-        return 0
+    return visible_gpu_count()  # KFD topology: this launcher process never loads torch / HIP
 
 
 @dataclass

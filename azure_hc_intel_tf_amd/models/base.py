@@ -78,10 +78,7 @@ class CNNModel:
         """Backward in segments, for overlapping the gradient allreduce with the rest of the
         backward pass: yields ``(layers, last)`` after each segment, where every parameter
         gradient of ``layers`` is final. Default: one segment (the whole backward)."""
-        from ..nn.layers import join_side_streams
-
         self.backward(dlogits)
-        join_side_streams()
         yield None, True  # None: every gradient
 
     @staticmethod
@@ -95,8 +92,6 @@ class CNNModel:
         parameter-free layers that are never back-propagated through. A segment is closed
         (yielded) once it owns >= HCB_SEGMENT_PARAMS parameters (default 2M = 8 MB fp32), so
         the first reductions start while most of the backward is still ahead."""
-        from ..nn.layers import join_side_streams
-
         thr = int(os.environ.get("HCB_SEGMENT_PARAMS", 2_000_000))
         seg, n = list(head), self._param_count(head)
         for i, (fn, layers) in enumerate(units):
@@ -104,10 +99,8 @@ class CNNModel:
             seg += list(layers)
             n += self._param_count(layers)
             if i < len(units) - 1 and n >= thr:
-                join_side_streams()  # the segment's weight gradients are final
                 yield seg, False
                 seg, n = [], 0
-        join_side_streams()
         yield seg + list(tail), True
 
     def activate(self) -> None:

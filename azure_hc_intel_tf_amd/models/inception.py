@@ -18,7 +18,7 @@ from typing import List
 
 import torch
 
-from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_act, join_side_streams
+from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_act
 from .base import CNNModel
 
 BN_KW = dict(eps=1e-3, decay=0.999, scale=False)
@@ -229,7 +229,6 @@ class InceptionV3(CNNModel):
                 dx, _ = l.backward(dx, dx_bn=self._stem_bn_below(i))
             else:
                 dx = l.backward(dx)
-        join_side_streams()
 
     def _stem_bn_below(self, i):
         """The conv+BN feeding stem layer i directly (its BN-backward reduction is fused into

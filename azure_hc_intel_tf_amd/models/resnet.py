@@ -15,7 +15,7 @@ BN: decay 0.9, epsilon 1e-5, scale=True. ResNet-50 v1: 25,559,081 trainable para
 from __future__ import annotations
 
 from ..nn import layers as L
-from ..nn.layers import BNReLU, ConvBN, GlobalAvgPool, Logits, Pool, StemS2D, join_side_streams
+from ..nn.layers import BNReLU, ConvBN, GlobalAvgPool, Logits, Pool, StemS2D
 from ..ops import functional as Fn
 from .base import CNNModel
 
@@ -131,13 +131,11 @@ class ResNet(CNNModel):
             dx = self.blocks[i].backward(dx, self.blocks[i - 1].c3 if i > 0 else None)
             seg += self.blocks[i].layers()
             if i > 0 and self.blocks[i].stage != self.blocks[i - 1].stage:
-                join_side_streams()  # the segment's weight gradients are final
                 yield seg, False
                 seg = []
         dx = self.pool.backward(dx)
         self.stem.backward(dx)
         self._last = None
-        join_side_streams()
         yield seg + [self.pool, self.stem], True
 
 
@@ -234,4 +232,3 @@ class ResNetV2(CNNModel):
         for b in reversed(self.blocks):
             dx = b.backward(dx)
         self.stem.backward(self.pool.backward(dx))
-        join_side_streams()

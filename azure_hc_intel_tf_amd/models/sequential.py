@@ -16,7 +16,7 @@ from __future__ import annotations
 
 from typing import List, Tuple
 
-from ..nn.layers import ConvBN, Dropout, GlobalAvgPool, Layer, Logits, Pool, join_side_streams
+from ..nn.layers import ConvBN, Dropout, GlobalAvgPool, Layer, Logits, Pool
 from .base import CNNModel
 from .inception import InceptionModule
 
@@ -125,7 +125,6 @@ class SequentialCNN(CNNModel):
                     break
             else:
                 dx = l.backward(dx)
-        join_side_streams()
 
 
 

@@ -5,7 +5,7 @@ framework overhead rather than compute. On the GPU the 1-unit layer is stored 8 
 the image's 3 channels are padded to 8 the same way as for the CNNs."""
 from __future__ import annotations
 
-from ..nn.layers import ConvBN, Logits, join_side_streams
+from ..nn.layers import ConvBN, Logits
 from ..nn.params import ParamStore
 from .base import CNNModel
 
@@ -50,4 +50,3 @@ class Trivial(CNNModel):
         dh, _ = self.a2.backward(dh)
         self.a1.need_dx = False
         self.a1.backward(dh)
-        join_side_streams()

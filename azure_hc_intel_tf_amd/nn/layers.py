@@ -82,43 +82,6 @@ FUSE_RES_BN = os.environ.get("HCB_FUSE_RES_BN", "1") != "0"
 # layer's previous batch mean, so E[x^2] - E[x]^2 does not cancel in fp32 when |mean| >> std
 # (HCB_BN_SHIFT=0: K = 0, the plain single-pass form)
 BN_SHIFT = os.environ.get("HCB_BN_SHIFT", "1") != "0"
-# ...only when the data-grad GEMM's reduction depth (cout * kh * kw of the producing conv) is at
-# least this: a shallow GEMM (stage-1 1x1, K=64) is all epilogue, and the fused gating +
-# reductions there cost more than a separate BN-backward reduce pass
-FUSE_BN_BWD_MIN_K = int(os.environ.get("HCB_FUSE_BN_BWD_MIN_K", "0"))
-# HCB_RELU_BITMASK=1: residual+ReLU BN outputs also store a 1-bit ReLU mask and the fused
-# backward epilogue reads it instead of the bf16 output (bnb mode 3, 1/16 of the bytes).
-# Off by default: measured on MI355X (ResNet-50 bs=64) 8385 vs 8394 img/s -- the stage-1
-# data-grad epilogues are not bound by that read (profiles/relu_bitmask_ab_r1.txt).
-RELU_BITMASK = os.environ.get("HCB_RELU_BITMASK", "0") == "1"
-# HCB_WGRAD_STREAM=1: run weight-gradient GEMMs on a second HIP stream, concurrent with the
-# data-grad chain (the critical path of backward), captured as parallel graph branches.
-# Off by default: measured on MI355X (ResNet-50 bs=64) the split-K-tuned GEMMs already fill
-# the 256 CUs, and the concurrent pairs contend (7594 vs 7699 img/s).
-WGRAD_STREAM = os.environ.get("HCB_WGRAD_STREAM", "0") == "1"
-_SIDE = {}
-_SIDE_USED = set()
-
-
-def wgrad_stream(dev) -> "torch.cuda.Stream":
-    """The side stream of ``dev``, forked from the current stream (waits for all work so far)."""
-    idx = torch.device(dev).index or 0
-    s = _SIDE.get(idx)
-    if s is None:
-        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
-    s.wait_stream(torch.cuda.current_stream(idx))
-    _SIDE_USED.add(idx)
-    return s
-
-
-def join_side_streams():
-    """Make the current stream wait for every forked weight-gradient stream (before the
-    gradients are reduced / applied, and before a graph capture ends)."""
-    for idx in list(_SIDE_USED):
-        torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
-    _SIDE_USED.clear()
-
-
 class _FixedParam:
     """A non-trainable per-channel constant with a scratch gradient sink (BN scale=False)."""
 
@@ -191,7 +154,6 @@ class ConvBN(Layer):
             # ResNet-v2's un-normalised convs (shortcut, conv3) have no bias in tf_cnn_benchmarks
             self.bias = ps.add(f"{name}/conv2d/bias", (cout,), True, ParamStore.const(0.0)) if bias else None
         self._saved = None
-        self._mask = None
         self._acc = None  # (fwd acc, bwd acc, replicas) of the current step
         self._pre_reduced = False
         self.training = True  # False: inference BN from the moving statistics (forward-only)
@@ -261,19 +223,13 @@ class ConvBN(Layer):
                 # conv epilogue accumulates the batch statistics; the apply kernel finalizes them
                 x = self._conv_fwd_stats(x, z)
                 acc_f, _, R = self._acc
-                # residual + ReLU outputs keep a bit mask for the fused backward (mode 3)
-                mask = None
-                if (RELU_BITMASK and self.relu and residual is not None and FUSE_BN_BWD
-                        and Fn.ld(z) == C and Fn.ld(y) == C):
-                    mask = torch.empty((N * P * Q, C // 8), dtype=torch.uint8, device=dev)
                 if residual_bn is not None:
                     assert residual_bn._acc[2] == R, "residual BN accumulators must match the replica count"
                 saved = Fn.bn_forward_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
                                           self.decay, self.eps, y, self.relu, acc_f, R,
-                                          self.sv_mean.data, self.sv_invstd.data, residual=residual, mask=mask,
+                                          self.sv_mean.data, self.sv_invstd.data, residual=residual,
                                           shift=self._shift(),
                                           res_bn=residual_bn.res_bn_args() if residual_bn is not None else None)
-                self._mask = mask
             else:
                 Fn.conv_forward(x, self.spec, None, self.w.data, z)
                 saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
@@ -330,8 +286,6 @@ class ConvBN(Layer):
         mode = (1 if had_res else 2) if self.relu else 0
         self._pre_reduced = True
         _, acc_b, R = self._acc if self._acc is not None else (None, self.acc_b.data, STAT_R)
-        if mode == 1 and self._mask is not None:
-            return Fn.BNBwdFuse(z, self._mask, saved, self.gamma.data, self.beta.data, 3, acc_b, R)
         return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, acc_b, R)
 
     def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False, dx_bn=None):
@@ -379,25 +333,16 @@ class ConvBN(Layer):
                 Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
                 gres = dz
-        if Fn.native(dz) and WGRAD_STREAM:
-            with torch.cuda.stream(wgrad_stream(dev)):
-                self._wgrad(dz, x)
-            # the allocator must not hand dz / x to the main stream before the wgrad has read them
-            dz.record_stream(_SIDE[dev.index or 0])
-            x.record_stream(_SIDE[dev.index or 0])
-        else:
-            self._wgrad(dz, x)
+        self._wgrad(dz, x)
         if self.need_dx:
             H, W, Cin = self.in_shape
             if dx is None:
                 strided_1x1 = (self.spec.sh > 1 or self.spec.sw > 1) and self.spec.kh == 1 and self.spec.kw == 1
                 dx = empty_act((N, H, W, Cin), dev, zero=strided_1x1 and Fn.native(dz))
                 accumulate = False
-            fuse = dx_bn is not None and self.spec.cout * self.spec.kh * self.spec.kw >= FUSE_BN_BWD_MIN_K
-            bnb = dx_bn.bwd_fuse_request() if fuse else None
+            bnb = dx_bn.bwd_fuse_request() if dx_bn is not None else None
             Fn.conv_dgrad(dz, self.spec, self.pack.tr, self.w.data, dx, accumulate, bnb=bnb)
         self._saved = None
-        self._mask = None
         return dx, gres
 
     def clear(self):

@@ -63,9 +63,9 @@ def det_replicas(M: int) -> int:
     return max(1, (M + 63) // 64)
 
 
-# IEEE-fp16 activations through the fp16 build of the HIP kernels (HCB_F16_NATIVE=0: through
-# the PyTorch / MIOpen path instead, the round-2 reference-precision form)
-F16_NATIVE = os.environ.get("HCB_F16_NATIVE", "1") != "0"
+# IEEE-fp16 activations through the fp16 build of the HIP kernels (a module switch: tests set it
+# False to run fp16 through the PyTorch / MIOpen path, the round-2 reference-precision form)
+F16_NATIVE = True
 
 
 def native(t) -> bool:
@@ -342,32 +342,15 @@ class BNBwdFuse:
         """CPU semantics of the fused epilogue's gating (the reductions stay in bn_backward)."""
         if self.mode == 1:
             g.mul_((self.y > 0).to(g.dtype))
-        elif self.mode == 3:
-            g.mul_(unpack_relu_mask(self.y, g.shape).to(g.dtype))
         elif self.mode == 2:
             xhat = (self.z - self.saved.mean) * self.saved.invstd
             g.mul_(((xhat * self.gamma + self.beta) > 0).to(g.dtype))
         return g
 
 
-def pack_relu_mask(y):
-    """Reference packer of the bn_apply_acc ReLU bit mask: y[..., C] -> uint8 [M, C/8]."""
-    C = y.shape[-1]
-    b = (y.reshape(-1, C // 8, 8).float() > 0).to(torch.int32)
-    w = (1 << torch.arange(8, dtype=torch.int32, device=y.device))
-    return (b * w).sum(-1).to(torch.uint8)
-
-
-def unpack_relu_mask(mask, shape):
-    """uint8 [M, C/8] ReLU bit mask (bit e of byte j = channel 8j+e) -> bool tensor ``shape``."""
-    bits = torch.arange(8, dtype=torch.int32, device=mask.device)
-    m = ((mask.to(torch.int32).unsqueeze(-1) >> bits) & 1).bool()
-    return m.reshape(shape)
-
-
-# strided k x k data gradients as sh*sw stride-phase GEMMs (HCB_DGRAD_PHASES=0: one GEMM over the
+# strided k x k data gradients as sh*sw stride-phase GEMMs (module switch, False: one GEMM over the
 # zero-dilated dz, which spends (sh*sw - 1)/(sh*sw) of its MFMA work on the inserted zeros)
-DGRAD_PHASES = os.environ.get("HCB_DGRAD_PHASES", "1") != "0"
+DGRAD_PHASES = True
 _phase_packs = {}
 
 
@@ -588,12 +571,10 @@ def bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, out, re
 
 
 def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out, relu: bool, acc, R: int,
-                   saved_mean, saved_invstd, residual=None, mask=None, shift=None, res_bn=None):
+                   saved_mean, saved_invstd, residual=None, shift=None, res_bn=None):
     """GPU BN forward whose batch statistics were accumulated by the producing conv's epilogue
     into ``acc`` (R replicas of [2][C]); mean/invstd are derived inside the apply kernel (no
-    finalize launch) and written to saved_mean / saved_invstd for the backward. ``mask``
-    (uint8 [M, C/8]): also store the output's ReLU bit mask, which the mode-3 fused
-    BN-backward epilogue reads instead of the full bf16 output (1/16 of the bytes). ``shift``:
+    finalize launch) and written to saved_mean / saved_invstd for the backward. ``shift``:
     the per-channel offset the producing conv subtracted before accumulating (conv_forward).
     ``res_bn`` = (acc, gamma, beta, saved_mean, saved_invstd, running_mean, running_var, shift) of a
     second BN applied to ``residual`` in the same pass (a projection shortcut's raw conv output:
@@ -602,7 +583,7 @@ def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out
     M = N * H * W
     _ext.ops().bn_apply_acc(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0, M, C,
                             acc, R, eps, momentum, gamma, beta, 1 if relu else 0, saved_mean, saved_invstd,
-                            running_mean, running_var, mask, shift, *(res_bn or ()))
+                            running_mean, running_var, shift, *(res_bn or ()))
     return BNSaved(saved_mean, saved_invstd)
 
 

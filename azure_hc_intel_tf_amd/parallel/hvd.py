@@ -272,6 +272,7 @@ class DistributedOptimizer(torch.optim.Optimizer):
         self._buckets: List[List[torch.Tensor]] = []
         self._pending: Dict[int, int] = {}
         self._launched = set()
+        self._next = 0  # next bucket to launch (buckets go out strictly in order)
         limit = fusion_threshold_bytes()
         cur, cur_bytes = [], 0
         for p in reversed(params):  # backward produces the last layers' grads first
@@ -306,8 +307,13 @@ class DistributedOptimizer(torch.optim.Optimizer):
             return
         bi = self._bucket_of[p]
         self._pending[bi] = self._pending.get(bi, 0) + 1
-        if self._pending[bi] == len(self._buckets[bi]):
-            self._launch(bi)
+        # launch strictly in bucket order: a ready bucket waits for every earlier one, so all
+        # ranks issue their collectives in the same order even when a data-dependent branch
+        # leaves a bucket incomplete on some ranks only (it is then launched by synchronize(),
+        # together with everything behind it -- no negotiation round needed)
+        while self._next < len(self._buckets) and self._pending.get(self._next, 0) == len(self._buckets[self._next]):
+            self._launch(self._next)
+            self._next += 1
 
     def _launch(self, bi):
         ps = self._buckets[bi]
@@ -322,12 +328,12 @@ class DistributedOptimizer(torch.optim.Optimizer):
         self._launched.add(bi)
 
     def synchronize(self):
-        # buckets whose parameters did not all receive a gradient (unused branch, frozen layer)
-        # were never launched from the hooks: reduce them now, in bucket order -- the same on
-        # every rank -- instead of silently stepping with local gradients
-        for bi in range(len(self._buckets)):
-            if bi not in self._launched:
-                self._launch(bi)
+        # buckets whose parameters did not all receive a gradient (unused branch, frozen layer),
+        # and every bucket behind the first such one, were not launched from the hooks: reduce
+        # them now, continuing the same bucket order -- identical on every rank
+        while self._next < len(self._buckets):
+            self._launch(self._next)
+            self._next += 1
         for work, c, ctx, flat, grads in self._handles:
             work.wait()
             out = self._compression.decompress(c, ctx)
@@ -340,6 +346,7 @@ class DistributedOptimizer(torch.optim.Optimizer):
         self._handles.clear()
         self._pending.clear()
         self._launched.clear()
+        self._next = 0
 
     def step(self, closure=None):
         self._counter += 1

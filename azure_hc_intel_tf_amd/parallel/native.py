@@ -107,6 +107,13 @@ class Communicator:
     def buckets_issued(self) -> int:
         return int(self._cc.buckets_issued(self.h))
 
+    def step_mark(self):
+        """Stall-watchdog heartbeat after a replayed step graph (its collectives make no host call)."""
+        self._cc.step_mark(self.h)
+
+    def steps_marked(self) -> int:
+        return int(self._cc.steps_marked(self.h))
+
     def join_(self):
         self._cc.join_(self.h)
 
@@ -176,8 +183,6 @@ class NativeReducer:
     def allreduce_ranges_async_(self, flat, ranges):
         if self.comm.world == 1 and not self.compress and not self.force:
             return
-        if os.environ.get("HCB_COMM_NOOP") == "1":  # debug: segmented step without collectives
-            return
         if self.xgmi is not None:  # small ranges: one hop over xGMI on the caller's stream
             small = [r for r in ranges if r[1] * 4 <= self.xgmi_bytes]
             for off, n in small:
@@ -191,11 +196,16 @@ class NativeReducer:
     def join(self):
         self.comm.join_()
 
+    def step_mark(self):
+        """Per-step stall-watchdog heartbeat of the graph-replayed step (trainer.py calls it after
+        every replay): the captured collectives make no host call the watchdog could see."""
+        self.comm.step_mark()
+
     def check_errors(self):
         """Raise if the one-shot xGMI path timed out waiting for a peer (its output was
         poisoned with NaN on the device). Synchronises; call outside the timed loop."""
         if self.xgmi is not None and self.xgmi.error():
-            raise RuntimeError("xGMI allreduce: a peer did not publish within HCB_XGMI_SPIN; gradients of "
+            raise RuntimeError("xGMI allreduce: a peer did not publish within the bounded wait; gradients of "
                                "that step were poisoned (NaN) instead of being reduced unsynchronised")
 
     def broadcast_(self, t, root=0):

@@ -62,13 +62,13 @@ def parse_args(argv=None):
 def spawn_workers(args, argv) -> int:
     """--gpus N with no rank environment: start N worker children (never exec: nothing here
     has touched the GPU yet, and the children are separate processes)."""
-    from azure_hc_intel_tf_amd.launch.launcher import launch
+    from azure_hc_intel_tf_amd.launch.launcher import launch, visible_gpu_count
 
     one_device = os.environ.get("HCB_BENCH_ONE_DEVICE") == "1"
+    if os.environ.get("HCB_BENCH_REPORT_PARENT") == "1":  # tests: the parent never loads torch / HIP
+        print(f"[bench] launcher parent: torch loaded = {'torch' in sys.modules}", file=sys.stderr, flush=True)
     if not one_device:
-        import torch  # device_count() does not initialise the GPU
-
-        visible = torch.cuda.device_count()
+        visible = visible_gpu_count()  # KFD topology: no torch, no HIP runtime in this process
         if visible < args.gpus:
             print(f"[bench] --gpus {args.gpus} but only {visible} GPU(s) visible; refusing to report a "
                   f"{visible}-GPU run as a {args.gpus}-GPU one", file=sys.stderr)
@@ -218,7 +218,11 @@ def main(argv=None):
         if hasattr(reducer, "check_errors"):
             reducer.check_errors()
         if os.environ.get("HCB_BENCH_COMM_PROFILE", "1") == "1":  # after the timed region
-            comm = trainer.comm_profile(images, labels)
+            try:  # restores the training state itself; a failure must not lose the timed result
+                comm = trainer.comm_profile(images, labels)
+            except Exception as e:  # noqa: BLE001
+                comm = {"error": f"{type(e).__name__}: {e}"}
+                print(f"[bench] comm profile failed: {e}", file=sys.stderr)
     # tf_cnn_benchmarks prints "total images/sec" on every rank (run-tf-sing-ucx-openmpi.sh:99-113
     # runs it under mpirun); stderr keeps stdout to the one JSON line
     print(f"[rank {rank}] total images/sec: {world * B * args.steps / own:.2f} "

@@ -185,7 +185,7 @@ void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10
                     const Tensor& acc, int64_t R, int64_t mode) {
   hcb::ConvParams p = conv_params(x, w, y, yres, c10::nullopt, c10::nullopt, g, cfg);
   TORCH_CHECK(!p.out_f32 && !p.relu && p.bias == nullptr, "hcb.conv_igemm_bnb: bf16 output without bias/relu");
-  TORCH_CHECK(mode >= 0 && mode <= 3 && R >= 1, "hcb.conv_igemm_bnb: bad mode / R");
+  TORCH_CHECK(mode >= 0 && mode <= 2 && R >= 1, "hcb.conv_igemm_bnb: bad mode / R");
   TORCH_CHECK(ld % 8 == 0 && ld >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm_bnb: bad ld");
   int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
   int64_t need = (rows - 1) * ld * 2 + ((p.Nout + 7) / 8) * 8 * 2;
@@ -198,12 +198,6 @@ void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10
     check_act(*yact, "y");
     check_range(*yact, need, "y");
     check_align16(yact->data_ptr(), "y");
-    p.bnb_y = yact->data_ptr();
-  } else if (mode == 3) {
-    TORCH_CHECK(yact.has_value(), "hcb.conv_igemm_bnb: mode 3 needs the ReLU bit mask");
-    TORCH_CHECK(yact->scalar_type() == at::kByte && yact->is_cuda() && yact->is_contiguous(),
-                "hcb.conv_igemm_bnb: mask must be a contiguous uint8 GPU tensor");
-    TORCH_CHECK(yact->numel() >= rows * (ld / 8), "hcb.conv_igemm_bnb: mask too small");
     p.bnb_y = yact->data_ptr();
   }
   for (const Tensor* t : {&mean, &invstd, &gamma, &beta}) {
@@ -566,8 +560,7 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                   int64_t ldr, int64_t M, int64_t C, const Tensor& acc, int64_t R, double eps, double momentum,
                   const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& saved_mean,
                   const Tensor& saved_invstd, const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv,
-                  const c10::optional<Tensor>& mask, const c10::optional<Tensor>& shift,
-                  const c10::optional<Tensor>& res_acc, const c10::optional<Tensor>& res_gamma,
+                  const c10::optional<Tensor>& shift, const c10::optional<Tensor>& res_acc, const c10::optional<Tensor>& res_gamma,
                   const c10::optional<Tensor>& res_beta, const c10::optional<Tensor>& res_saved_mean,
                   const c10::optional<Tensor>& res_saved_invstd, const c10::optional<Tensor>& res_rm,
                   const c10::optional<Tensor>& res_rv, const c10::optional<Tensor>& res_shift) {
@@ -584,13 +577,6 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
     TORCH_CHECK(ldr % 8 == 0, "hcb.bn_apply_acc: ldr");
     check_range(*res, ((M - 1) * ldr + C) * 2, "res");
     rp = res->data_ptr();
-  }
-  void* mp = nullptr;
-  if (mask.has_value()) {
-    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_cuda() && mask->is_contiguous(),
-                "hcb.bn_apply_acc: mask must be a contiguous uint8 GPU tensor");
-    TORCH_CHECK(mask->numel() >= M * (C / 8), "hcb.bn_apply_acc: mask too small");
-    mp = mask->data_ptr();
   }
   // residual BN (projection shortcut): the residual is that BN's raw input z_sc
   hcb::ResBN rb{};
@@ -611,7 +597,7 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                            acc.data_ptr<float>(), (int)R, (float)eps, (float)momentum, gamma.data_ptr<float>(),
                            beta.data_ptr<float>(), (int)relu, saved_mean.data_ptr<float>(),
                            saved_invstd.data_ptr<float>(), rm.has_value() ? rm->data_ptr<float>() : nullptr,
-                           rv.has_value() ? rv->data_ptr<float>() : nullptr, mp, opt_f32(shift, C, "shift"),
+                           rv.has_value() ? rv->data_ptr<float>() : nullptr, opt_f32(shift, C, "shift"),
                            res_acc.has_value() ? &rb : nullptr, cur_stream());
 }
 
@@ -830,7 +816,6 @@ void set_deterministic(bool on) { hcb::set_deterministic(on); }
 
 }  // namespace
 
-static void set_wgrad_ri_op(int64_t on) { hcb::set_wgrad_ri((int)on); }
 
 HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
@@ -838,7 +823,6 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
-  m.def("set_wgrad_ri(int on) -> ()", set_wgrad_ri_op);
   m.def("bn_stats(Tensor x, int M, int C, int ldx, Tensor(a!) slab) -> ()");
   m.def("bn_partials(int M, int C) -> int", bn_partials);
   m.def("bn_finalize(Tensor slab, int T, int C, float count, float eps, float momentum, Tensor(a!) mean, Tensor(b!) invstd, Tensor(c!)? running_mean, Tensor(d!)? running_var) -> ()");
@@ -860,7 +844,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");
   m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
-  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor(f!)? mask=None, Tensor? shift=None, Tensor? res_acc=None, Tensor? res_gamma=None, Tensor? res_beta=None, Tensor(g!)? res_saved_mean=None, Tensor(h!)? res_saved_invstd=None, Tensor(i!)? res_running_mean=None, Tensor(j!)? res_running_var=None, Tensor? res_shift=None) -> ()");
+  m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor? shift=None, Tensor? res_acc=None, Tensor? res_gamma=None, Tensor? res_beta=None, Tensor(g!)? res_saved_mean=None, Tensor(h!)? res_saved_invstd=None, Tensor(i!)? res_running_mean=None, Tensor(j!)? res_running_var=None, Tensor? res_shift=None) -> ()");
   m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg) -> ()");
   m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu, Tensor(d!)? shift_out=None) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");

@@ -19,6 +19,10 @@
 //   * watchdog thread: warns when a launched reduction has not completed within
 //     HOROVOD_STALL_CHECK_TIME_SECONDS, polls ncclCommGetAsyncError, optionally aborts
 //     the communicator (HCB_STALL_ABORT_SECONDS) so a dead rank cannot hang the job.
+//     Eager reductions are watched per call; on the default multi-GPU path the collectives
+//     live inside the replayed step graph (no host call per reduction), so the trainer calls
+//     step_mark() after every replay: one watch cycle per step, completed by an event recorded
+//     on the caller's stream behind the graph (whose comm branch joins before its end).
 #include <torch/library.h>
 #include <ATen/core/Tensor.h>
 #include <ATen/ops/empty.h>
@@ -28,6 +32,7 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -129,6 +134,11 @@ struct Comm {
   std::unique_ptr<hcb::comm::BucketEngine> engine;  // lifetime bucket numbering
   int64_t fusion_bytes = 128ll << 20;  // HOROVOD_FUSION_THRESHOLD
   bool skip_rccl = false;  // debug (HCB_COMM_SKIP_RCCL=1): stream fork/join without the collective
+  // debug (HCB_COMM_DEBUG_SLEEP_MS): a bounded device sleep on the comm stream at every fork, so a
+  // stalled collective can be staged on one GPU (it is captured into the step graph like the rest)
+  int debug_sleep_ms = 0;
+  int64_t steps_marked = 0;  // step_mark() heartbeats (graph-replayed steps)
+  std::atomic<int64_t> first_mark_cycle{-1};  // first watch cycle enqueued by step_mark()
   hipEvent_t watch_ev = nullptr;
   int64_t watch_cycle = 0;
   std::chrono::steady_clock::time_point last_call = std::chrono::steady_clock::now();
@@ -194,11 +204,12 @@ void watchdog_loop(Comm* c) {
       }
     }
     if (act == StallWatch::kWarn) {
+      const int64_t cyc = c->watch.completed() + 1, fm = c->first_mark_cycle.load();
       std::fprintf(stderr,
-                   "[hcb watchdog] rank %d: gradient reduction cycle %lld (buckets up to #%lld) has not completed "
+                   "[hcb watchdog] rank %d: gradient reduction cycle %lld%s (buckets up to #%lld) has not completed "
                    "after %.0f s; one or more ranks may have stalled (HOROVOD_STALL_CHECK_TIME_SECONDS=%.0f)\n",
-                   c->rank, (long long)(c->watch.completed() + 1), (long long)c->watch.last_seq(), waited,
-                   c->watch.warn_s());
+                   c->rank, (long long)cyc, fm >= 0 && cyc >= fm ? " (graph-replayed step)" : "",
+                   (long long)c->watch.last_seq(), waited, c->watch.warn_s());
       std::fflush(stderr);
     } else if (act == StallWatch::kAbort && c->comm) {
       std::fprintf(stderr, "[hcb watchdog] rank %d: stalled for %.0f s > HCB_STALL_ABORT_SECONDS; aborting\n", c->rank,
@@ -224,6 +235,7 @@ struct RcclTransport final : hcb::comm::Transport {
     cur = c10::hip::getCurrentHIPStream().stream();
     HCB_HIP(hipEventRecord(c->fork_ev, cur));
     HCB_HIP(hipStreamWaitEvent(c->stream, c->fork_ev, 0));
+    if (cap && c->debug_sleep_ms > 0) hcb::launch_debug_sleep(c->debug_sleep_ms, c->stream);
   }
   void bucket_begin(const hcb::comm::Bucket&) override {
     if (!tl) return;
@@ -307,6 +319,7 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
     c->fusion_bytes = fb > 0 ? (int64_t)fb : 0;
   }
   c->skip_rccl = env_double("HCB_COMM_SKIP_RCCL", 0.0) != 0.0;
+  c->debug_sleep_ms = (int)std::min(10000.0, std::max(0.0, env_double("HCB_COMM_DEBUG_SLEEP_MS", 0.0)));
   Comm* raw = c.get();
   if (env_double("HCB_COMM_WATCHDOG", 1.0) != 0.0) raw->wd = std::thread(watchdog_loop, raw);
   std::lock_guard<std::mutex> lk(g_mu);
@@ -438,7 +451,8 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
               "hcb_comm.bucket_allreduce_: buckets int64 [n][2] on CPU");
   TORCH_CHECK(compress >= 0 && compress <= 2, "hcb_comm.bucket_allreduce_: compress must be 0 (none), 1 (bf16) or 2 (fp16)");
   TORCH_CHECK(scale == 1.0, "hcb_comm.bucket_allreduce_: scale is folded into the optimizer; pass 1.0");
-  const int64_t* bk = buckets.contiguous().data_ptr<int64_t>();
+  const at::Tensor bc = buckets.contiguous();  // keep the (possibly copied) table alive while it is read
+  const int64_t* bk = bc.data_ptr<int64_t>();
   const int64_t nb = buckets.size(0);
   const int64_t n = flat.numel();
   for (int64_t i = 0; i < nb; ++i)
@@ -489,6 +503,30 @@ void bucket_allreduce_async_(int64_t h, const Tensor& flat, const Tensor& bucket
   bucket_impl(h, flat, buckets, compress, scale, average, false, 0);
 }
 
+// Per-step heartbeat of the graph-replayed data-parallel step (call right after the replay, on
+// the stream it was launched on, never inside a capture). The collectives of a captured step
+// make no host call when replayed, so without this the watchdog would never learn about them:
+// record the watch event behind the step (the graph's comm branch joins the capture stream
+// before the graph ends, so the event completes only once every reduction of the step has)
+// and enqueue one watch cycle. As for eager reductions, completion is observed without
+// blocking on the CALLER's thread (the previous mark's event) or, once the caller has been
+// quiet for > 1 s (blocked on a hung step), by the watchdog thread itself.
+void step_mark(int64_t h) {
+  Comm* c = get(h);
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  TORCH_CHECK(!capturing(cur), "hcb_comm.step_mark: call after a replay, not inside a capture");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->last_call = std::chrono::steady_clock::now();
+  c->steps_marked++;
+  if (!c->wd.joinable()) return;
+  if (c->watch.completed() < c->watch_cycle && hipEventQuery(c->watch_ev) == hipSuccess)
+    c->watch.complete(c->watch_cycle);
+  HCB_HIP(hipEventRecord(c->watch_ev, cur));
+  c->watch_cycle = c->watch.enqueue(c->buckets_issued - 1);
+  if (c->first_mark_cycle.load() < 0) c->first_mark_cycle = c->watch_cycle;
+}
+int64_t steps_marked(int64_t h) { return get(h)->steps_marked; }
+
 int64_t buckets_issued(int64_t h) { return get(h)->buckets_issued; }
 int64_t fusion_threshold(int64_t h) { return get(h)->fusion_bytes; }
 void set_fusion_threshold(int64_t h, int64_t bytes) { get(h)->fusion_bytes = bytes; }
@@ -511,7 +549,7 @@ void barrier(int64_t h) {
 struct Xgmi {
   int rank = 0, world = 1, device = 0;
   int64_t cap = 0;                  // floats per slot
-  unsigned spin = 1u << 25;         // bounded-wait iterations (HCB_XGMI_SPIN)
+  unsigned spin = 1u << 25;         // bounded-wait iterations
   float* region = nullptr;          // own region: 2 slots + flags
   unsigned* err = nullptr;          // device error word (spin timeout)
   std::vector<float*> peers;        // every rank's region as mapped here (own = region)
@@ -543,10 +581,7 @@ int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, int64_t device) {
   // and read the slots over xGMI while this GPU is still running; coarse-grained memory is only
   // coherent across devices at kernel boundaries
   HCB_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&x->region), bytes, hipDeviceMallocUncached));
-  {
-    const double sp = env_double("HCB_XGMI_SPIN", (double)(1u << 25));
-    x->spin = sp < 1 ? 1u : (sp > 4.0e9 ? 4000000000u : (unsigned)sp);
-  }
+  x->spin = 1u << 25;  // bounded waits: ~7 s of s_sleep(8) before a dead peer is reported
   HCB_HIP(hipMemset(x->region, 0, bytes));
   HCB_HIP(hipMalloc(&x->err, 4));
   HCB_HIP(hipMemset(x->err, 0, 4));
@@ -663,6 +698,8 @@ TORCH_LIBRARY(hcb_comm, m) {
         bucket_allreduce_async_);
   m.def("join_(int h) -> ()", join_);
   m.def("buckets_issued(int h) -> int", buckets_issued);
+  m.def("step_mark(int h) -> ()", step_mark);
+  m.def("steps_marked(int h) -> int", steps_marked);
   m.def("fusion_threshold(int h) -> int", fusion_threshold);
   m.def("set_fusion_threshold(int h, int bytes) -> ()", set_fusion_threshold);
   m.def("barrier(int h) -> ()", barrier);

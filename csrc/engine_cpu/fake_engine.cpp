@@ -202,6 +202,26 @@ void FakeRank::mark_cycle_end(int64_t cycle) {
   push([this, cycle] { watch_.complete(cycle); });
 }
 
+void FakeRank::replay(float* flat, const std::vector<comm::Bucket>& plan, comm::Wire w, bool avg, int step) {
+  const bool stall = rank_ == cfg_.stall_rank && step == cfg_.stall_step && cfg_.stall_ms > 0;
+  for (size_t i = 0; i < plan.size(); ++i) {
+    const comm::Bucket b = plan[i];
+    // a fresh rendezvous key per replay (the fabric slot of step k is freed once all departed)
+    const int64_t key = (int64_t)step * 1000000 + b.seq;
+    const bool sleep = stall && i == 0;
+    push([this, flat, b, w, avg, key, sleep] {
+      if (sleep) std::this_thread::sleep_for(std::chrono::milliseconds(cfg_.stall_ms));
+      fab_->allreduce(rank_, key, flat + b.off, b.len, w, avg);
+    });
+  }
+}
+
+void FakeRank::step_mark() {
+  const int64_t cycle = watch_.enqueue(engine_.next_seq() - 1);
+  last_cycle_ = cycle;
+  push([this, cycle] { watch_.complete(cycle); });
+}
+
 std::vector<comm::Bucket> FakeRank::submit(float* flat, int64_t numel, const std::vector<int64_t>& ranges,
                                            comm::Wire w, bool avg, int64_t threshold, bool do_join) {
   return engine_.submit(flat, numel, ranges.data(), (int64_t)ranges.size() / 2, w, avg, threshold, do_join);
@@ -223,9 +243,27 @@ RunResult run(const RunConfig& cfg, const std::vector<std::vector<float>>& init,
       try {
         float* flat = res.buffers[r].data();
         const int64_t numel = (int64_t)res.buffers[r].size();
-        for (size_t c = 0; c < cycles.size(); ++c) {
-          const bool last = c + 1 == cycles.size();
-          ranks[r]->submit(flat, numel, cycles[c], cfg.wire, cfg.average, cfg.threshold_bytes, last);
+        if (cfg.replay_steps > 0) {
+          // capture: the step's bucket schedule, planned exactly as submit() plans it
+          std::vector<comm::Bucket> plan;
+          for (const auto& c : cycles) {
+            auto bs = comm::plan_buckets(c.data(), (int64_t)c.size() / 2,
+                                         comm::bucket_elems_for(cfg.threshold_bytes, cfg.wire));
+            for (auto& b : bs) {
+              if (b.off < 0 || b.off + b.len > numel) throw std::out_of_range("bucket out of range");
+              b.seq = (int64_t)plan.size();
+              plan.push_back(b);
+            }
+          }
+          for (int s = 0; s < cfg.replay_steps; ++s) {
+            ranks[r]->replay(flat, plan, cfg.wire, cfg.average, s);
+            if (cfg.heartbeat) ranks[r]->step_mark();
+          }
+        } else {
+          for (size_t c = 0; c < cycles.size(); ++c) {
+            const bool last = c + 1 == cycles.size();
+            ranks[r]->submit(flat, numel, cycles[c], cfg.wire, cfg.average, cfg.threshold_bytes, last);
+          }
         }
         ranks[r]->drain();
       } catch (const std::exception& e) {

@@ -30,6 +30,12 @@ struct RunConfig {
   int64_t stall_seq = -1;
   int stall_ms = 0;
   double warn_s = 0.0;       // > 0: run a watchdog per rank with this warn threshold
+  // graph-replay emulation (the default multi-GPU path): the cycles are "captured" once (bucket
+  // plan, no watch cycles), then replayed `replay_steps` times with no engine call per bucket;
+  // with `heartbeat` each replay is followed by step_mark() -- the only thing the watchdog sees
+  int replay_steps = 0;
+  bool heartbeat = true;
+  int stall_step = -1;       // replay mode: stall_rank's comm thread sleeps stall_ms in this step
 };
 
 struct Warning {
@@ -69,6 +75,10 @@ class FakeRank final : public comm::Transport {
   ~FakeRank() override;
   std::vector<comm::Bucket> submit(float* flat, int64_t numel, const std::vector<int64_t>& ranges, comm::Wire w,
                                    bool avg, int64_t threshold, bool do_join);
+  // graph-replay emulation: enqueue a captured bucket schedule again (no watch cycle), and the
+  // per-step heartbeat (one watch cycle completed behind the step's buckets)
+  void replay(float* flat, const std::vector<comm::Bucket>& plan, comm::Wire w, bool avg, int step);
+  void step_mark();
   void drain();
   std::vector<comm::Bucket> log() {
     std::lock_guard<std::mutex> lk(wmu_);

@@ -9,7 +9,8 @@ using namespace hcb;
 
 static py::dict run_py(int world, const std::vector<std::vector<float>>& init,
                        const std::vector<std::vector<int64_t>>& cycles, int wire, bool average, int64_t threshold_bytes,
-                       int stall_rank, int64_t stall_seq, int stall_ms, double warn_s) {
+                       int stall_rank, int64_t stall_seq, int stall_ms, double warn_s, int replay_steps,
+                       bool heartbeat, int stall_step) {
   if (world < 1 || (int)init.size() != world) throw std::invalid_argument("init must hold one buffer per rank");
   if (wire < 0 || wire > 2) throw std::invalid_argument("wire: 0 fp32, 1 bf16, 2 fp16");
   fake::RunConfig cfg;
@@ -21,6 +22,9 @@ static py::dict run_py(int world, const std::vector<std::vector<float>>& init,
   cfg.stall_seq = stall_seq;
   cfg.stall_ms = stall_ms;
   cfg.warn_s = warn_s;
+  cfg.replay_steps = replay_steps;
+  cfg.heartbeat = heartbeat;
+  cfg.stall_step = stall_step;
   fake::RunResult r;
   {
     py::gil_scoped_release nogil;
@@ -71,7 +75,8 @@ PYBIND11_MODULE(_hcb_engine_cpu, m) {
   m.doc() = "CPU fake backend of the hcb gradient bucket engine (tests)";
   m.def("run", &run_py, py::arg("world"), py::arg("init"), py::arg("cycles"), py::arg("wire") = 0,
         py::arg("average") = false, py::arg("threshold_bytes") = 128ll << 20, py::arg("stall_rank") = -1,
-        py::arg("stall_seq") = -1, py::arg("stall_ms") = 0, py::arg("warn_s") = 0.0);
+        py::arg("stall_seq") = -1, py::arg("stall_ms") = 0, py::arg("warn_s") = 0.0, py::arg("replay_steps") = 0,
+        py::arg("heartbeat") = true, py::arg("stall_step") = -1);
   m.def("plan", &plan_py, py::arg("ranges"), py::arg("threshold_bytes"), py::arg("wire") = 0);
   m.def("stall_decisions", &stall_decisions);
   m.def("f32_to_f16_bits", &fake::f32_to_f16);

@@ -554,8 +554,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ y, int ldy, const uint16_t* __restrict__ res,
     int ldr, int M, int C, int CVB, const float* __restrict__ acc, int R, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
-    float* saved_invstd, float* run_mean, float* run_var, uint8_t* __restrict__ mask, const float* shift,
-    ResBN rb) {
+    float* saved_invstd, float* run_mean, float* run_var, const float* shift, ResBN rb) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB] (+ [2][CB] of the residual BN)
   constexpr bool rbn = RBN;
   const GroupMap gm = groupmap(CVB);
@@ -652,19 +651,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
       }
-      if (m < M) {
-        const u32x4 o = pack8(f);
-        *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + gm.cv * 8) = o;
-        if (mask != nullptr) {  // bit e: the STORED bf16 value is > 0 (same test as mode 1)
-          uint32_t bits = 0;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const uint32_t h = (o[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-            bits |= ((h - 1u) < HCB_ACT_POS_INF ? 1u : 0u) << e;  // 0 < y <= +inf
-          }
-          mask[(size_t)m * (C >> 3) + gm.cv] = (uint8_t)bits;
-        }
-      }
+      if (m < M) *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + gm.cv * 8) = pack8(f);
     }
   }
 }
@@ -916,12 +903,8 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
   if (target < 1) target = 1;
   // Small tensors: give every thread up to BN_U rows (all loads in flight at once) rather than
   // one row per thread -- fewer workgroups to dispatch and one memory round trip, while the
-  // grid still covers every CU. HCB_BN_ROWS_PER_THREAD=1 restores one row per thread.
-  static const int rpt = [] {
-    const char* e = std::getenv("HCB_BN_ROWS_PER_THREAD");
-    const int v = e ? std::atoi(e) : BN_U;
-    return v < 1 ? 1 : (v > BN_U ? BN_U : v);
-  }();
+  // grid still covers every CU.
+  constexpr int rpt = BN_U;
   int floor_s = (256 + groups - 1) / groups;
   int want = (need + rpt - 1) / rpt;
   if (want < floor_s) want = floor_s < need ? floor_s : need;
@@ -934,18 +917,18 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         void* mask, const float* shift, const ResBN* res_bn, hipStream_t st) {
+                         const float* shift, const ResBN* res_bn, hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   const ResBN rb = res_bn != nullptr ? *res_bn : ResBN{};
   if (res_bn != nullptr)
     hipLaunchKernelGGL(bn_apply_acc_kernel<true>, grid, dim3(256), (size_t)4 * cvb * 8 * 4, st, (const uint16_t*)x,
                        ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma,
-                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask, shift, rb);
+                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, shift, rb);
   else
     hipLaunchKernelGGL(bn_apply_acc_kernel<false>, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x,
                        ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma,
-                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, (uint8_t*)mask, shift, rb);
+                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, shift, rb);
 }
 
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,

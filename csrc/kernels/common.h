@@ -26,10 +26,8 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // bf16 wire format of the gradient buckets) keeps bf2f / f2bf.
 #ifdef HCB_F16
 typedef _Float16 act16x8 __attribute__((ext_vector_type(8)));
-#define HCB_ACT_POS_INF 0x7c00u  // bit pattern of +inf: 0 < x <= +inf  <=>  bits - 1 < this
 #else
 typedef __bf16 act16x8 __attribute__((ext_vector_type(8)));
-#define HCB_ACT_POS_INF 0x7f80u
 #endif
 
 namespace hcb {

@@ -57,21 +57,9 @@ __device__ __forceinline__ void wgrad_store_tile(const WgradParams& p, const flo
 // VALU ops against 16 MFMAs per k-step in the 64x64 k-split kernel. Instead each thread keeps
 // (h, w, byte offset) of its rows and adds a precomputed mixed-radix step of BK pixels
 // (dn, dp, dq) with at most one carry per digit (dq < Q and dp < P): adds, two compares and
-// selects. The thread -> (row, 16-byte vector) map is the original one (a vector's column, so
-// its filter tap, is fixed per thread); the original loaders remain as the HCB_WGRAD_RI=0
-// A/B baseline.
-// HCB_WGRAD_RI=0 (or set_wgrad_ri(0)) selects the original loaders everywhere (A/B knob)
-static int g_wgrad_ri = -1;
-void set_wgrad_ri(int on) { g_wgrad_ri = on; }  // 0 off, 1 on, 2 on without shared rows
-bool riv_enabled() {
-  if (g_wgrad_ri < 0) {
-    const char* e = getenv("HCB_WGRAD_RI");
-    g_wgrad_ri = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  return g_wgrad_ri >= 1;
-}
-static bool shared_rows_enabled() { return g_wgrad_ri == 1; }
-
+// selects. The thread -> (row, 16-byte vector) map keeps a vector's column, so its filter tap,
+// fixed per thread. (The original divide-per-row loaders were measured 10-30% slower on every
+// ResNet-50 layer and removed: profiles/r2p_wgrad_row_incremental.txt.)
 struct WgAdvance {  // wave-uniform per-k-step increments (bytes / input rows / input cols)
   int dqw, dqo, qs, qco, dph, dpo, ps, pco, dno;
 };
@@ -267,11 +255,10 @@ struct WgBLoadShared {
   }
 };
 
-// LD: 0 generic im2col columns, 1 whole tile in one tap (C % BN == 0), 2 row-incremental (RI)
-// per-lane rows, 3 RI with shared rows (one tap per tile)
-template <int WM, int WN, int TM, int TN, int LD>
+// RIS: the X loader shares rows across lanes (every column of a tile in one filter tap), else
+// per-lane rows
+template <int WM, int WN, int TM, int TN, bool RIS>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
-  constexpr bool CBIG = LD == 1, RI = LD >= 2, RIS = LD == 3;
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AVR = BM / 8, BVR = BN / 8;        // 16-byte vectors per LDS row
@@ -300,32 +287,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(p.dy, p.dy_bytes);
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
 
-  // A (dY) thread mapping: column vector fixed, rows vary
-  const int a_cv = tid % AVR, a_r0 = tid / AVR;
-  constexpr int A_RSTEP = 256 / AVR;
-  const int a_col = i0 + a_cv * 8;
-  const bool a_colok = a_col < p.Nout;
-  // B (im2col X) thread mapping
-  const int b_cv = tid % BVR, b_r0 = tid / BVR;
-  constexpr int B_RSTEP = 256 / BVR;
-  const int b_col = j0 + b_cv * 8;
-  bool b_colok = b_col < p.K;
-  int b_r = 0, b_s = 0, b_c = 0;
-  if constexpr (CBIG) {
-    // whole tile in one tap: computed from j0 (C % BN == 0)
-    int tap = j0 / p.C;
-    b_c = j0 - tap * p.C + b_cv * 8;
-    b_r = tap / p.S;
-    b_s = tap - b_r * p.S;
-  } else {
-    int tap = (int)fdiv((uint32_t)b_col, p.fd_c);
-    b_c = b_col - tap * p.C;
-    b_r = (int)fdiv((uint32_t)tap, p.fd_s);
-    b_s = tap - b_r * p.S;
-  }
-  const int b_dh = b_r * p.dil_h - p.pad_h, b_dw = b_s * p.dil_w - p.pad_w;
-
-  u32x4 ra[AV], rb[BV];
   f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -334,71 +295,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 
   using GA = WgSeg<BK, BM, 256>;
   using GB = WgSeg<BK, BN, 256>;
-  static_assert(!RI || (GA::V == AV && GB::V == BV), "RI mapping");
+  static_assert(GA::V == AV && GB::V == BV, "loader mapping");
   WgALoad<BK, BM, 256> ald;
   std::conditional_t<RIS, WgBLoadShared<BK, BN, 256>, WgBLoad<BK, BN, 256>> bld;
-  WgAdvance adv;
   const uint32_t a_step = (uint32_t)(BK * p.ldy * 2);
-  if constexpr (RI) {
-    ald.init(p, kt_begin * BK, i0, tid);
-    bld.init(p, kt_begin * BK, j0, tid);
-    adv = wg_advance(p, BK);
-  }
-  auto gload = [&](int kt) {
-    if constexpr (RI) {
-      // k-steps are issued strictly in order: the loaders hold k-step kt's rows
-      ald.load(dyr, p.M, ra);
-      bld.load(p, xr, p.M, rb);
-      ald.advance(a_step);
-      bld.advance(adv, p.stride_h);
-      return;
-    }
-    const int mb = kt * BK;
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      int m = mb + a_r0 + A_RSTEP * v;
-      uint32_t off = (a_colok && m < p.M) ? (uint32_t)(m * p.ldy + a_col) * 2u : HCB_OOB;
-      ra[v] = buf_load16(dyr, off);
-    }
-#pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      int m = mb + b_r0 + B_RSTEP * v;
-      uint32_t off = HCB_OOB;
-      if (b_colok && m < p.M) {
-        int n = (int)fdiv((uint32_t)m, p.fd_pq);
-        int rem = m - n * p.P * p.Q;
-        int pp = (int)fdiv((uint32_t)rem, p.fd_q);
-        int qq = rem - pp * p.Q;
-        int h = pp * p.stride_h + b_dh, w = qq * p.stride_w + b_dw;
-        if (h >= 0 && h < p.H && w >= 0 && w < p.W)
-          off = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c) * 2u;
-      }
-      rb[v] = buf_load16(xr, off);
-    }
-  };
-  auto lstore = [&](int buf) {
-    if constexpr (RI) {
-#pragma unroll
-      for (int v = 0; v < AV; ++v)
-        *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = ra[v];
-#pragma unroll
-      for (int v = 0; v < BV; ++v)
-        *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = rb[v];
-      return;
-    }
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      int row = a_r0 + A_RSTEP * v;
-      int slot = (a_cv >> 1) ^ wg_swz<BM / 16>(row);
-      *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + row * BM * 2 + slot * 32 + (a_cv & 1) * 16) = ra[v];
-    }
-#pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      int row = b_r0 + B_RSTEP * v;
-      int slot = (b_cv >> 1) ^ wg_swz<BN / 16>(row);
-      *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + row * BN * 2 + slot * 32 + (b_cv & 1) * 16) = rb[v];
-    }
-  };
+  ald.init(p, kt_begin * BK, i0, tid);
+  bld.init(p, kt_begin * BK, j0, tid);
+  const WgAdvance adv = wg_advance(p, BK);
 
   const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
   // lane supplies row (row + q4), columns col + 4*p4 (col a multiple of 16); rows are NSLOT*32 B
@@ -441,68 +344,49 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     }
   };
 
-  if constexpr (RI) {
-    // Two register sets: the loads of k-step k+2 are issued while k-step k is multiplied and
-    // k+1 is stored to LDS, so a load has two k-steps (not one) of MFMA time to land -- the
-    // 64x64 tile's 8 MFMAs per wave and k-step are far shorter than an L2 round trip.
-    u32x4 sa[2][AV], sb[2][BV];
-    // rows past this split's range come back as zeros without memory traffic, so the loads
-    // and stores of the pipeline tail need no conditions (straight-line k-loop)
-    const int mend = min(kt_end * BK, p.M);
-    auto ld = [&](auto set_c) {
-      constexpr int S = decltype(set_c)::value;
-      ald.load(dyr, mend, sa[S]);
-      bld.load(p, xr, mend, sb[S]);
-      ald.advance(a_step);
-      bld.advance(adv, p.stride_h);
-    };
-    auto st = [&](auto set_c, int buf) {
-      constexpr int S = decltype(set_c)::value;
+  // Two register sets: the loads of k-step k+2 are issued while k-step k is multiplied and
+  // k+1 is stored to LDS, so a load has two k-steps (not one) of MFMA time to land -- the
+  // 64x64 tile's 8 MFMAs per wave and k-step are far shorter than an L2 round trip.
+  u32x4 sa[2][AV], sb[2][BV];
+  // rows past this split's range come back as zeros without memory traffic, so the loads
+  // and stores of the pipeline tail need no conditions (straight-line k-loop)
+  const int mend = min(kt_end * BK, p.M);
+  auto ld = [&](auto set_c) {
+    constexpr int S = decltype(set_c)::value;
+    ald.load(dyr, mend, sa[S]);
+    bld.load(p, xr, mend, sb[S]);
+    ald.advance(a_step);
+    bld.advance(adv, p.stride_h);
+  };
+  auto st = [&](auto set_c, int buf) {
+    constexpr int S = decltype(set_c)::value;
 #pragma unroll
-      for (int v = 0; v < AV; ++v)
-        *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = sa[S][v];
+    for (int v = 0; v < AV; ++v)
+      *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = sa[S][v];
 #pragma unroll
-      for (int v = 0; v < BV; ++v)
-        *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = sb[S][v];
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    const int nks = kt_end - kt_begin;
-    ld(I0{});
-    ld(I1{});
-    st(I0{}, 0);
+    for (int v = 0; v < BV; ++v)
+      *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = sb[S][v];
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  const int nks = kt_end - kt_begin;
+  ld(I0{});
+  ld(I1{});
+  st(I0{}, 0);
+  __syncthreads();
+  auto kstep = [&](auto cur_c, int k) {
+    constexpr int cur = decltype(cur_c)::value;
+    ld(cur_c);  // k-step k + 2 into set `cur` (stored to LDS one k-step ago)
+    mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
+    st(std::integral_constant<int, cur ^ 1>{}, cur ^ 1);  // k-step k + 1
     __syncthreads();
-    auto kstep = [&](auto cur_c, int k) {
-      constexpr int cur = decltype(cur_c)::value;
-      ld(cur_c);  // k-step k + 2 into set `cur` (stored to LDS one k-step ago)
-      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
-      st(std::integral_constant<int, cur ^ 1>{}, cur ^ 1);  // k-step k + 1
-      __syncthreads();
-    };
-    // an odd count runs one extra k-step over all-zero tiles (both operands out of range: adds
-    // exactly 0) instead of a conditional second half, which made the compiler copy the
-    // accumulators between register files every iteration
-    for (int k = 0; k < nks; k += 2) {
-      kstep(I0{}, k);
-      kstep(I1{}, k + 1);
-    }
-  } else {
-    gload(kt_begin);
-    lstore(0);
-    __syncthreads();
-    // the k-loop is unrolled by two so the LDS buffer of each half is a compile-time constant:
-    // the fragment-read addresses become loop-invariant registers + immediate offsets
-    auto kstep = [&](auto cur_c, int kt) {
-      constexpr int cur = decltype(cur_c)::value;
-      if (kt + 1 < kt_end) gload(kt + 1);
-      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
-      if (kt + 1 < kt_end) lstore(cur ^ 1);
-      __syncthreads();
-    };
-    for (int kt = kt_begin; kt < kt_end; kt += 2) {
-      kstep(std::integral_constant<int, 0>{}, kt);
-      if (kt + 1 < kt_end) kstep(std::integral_constant<int, 1>{}, kt + 1);
-    }
+  };
+  // an odd count runs one extra k-step over all-zero tiles (both operands out of range: adds
+  // exactly 0) instead of a conditional second half, which made the compiler copy the
+  // accumulators between register files every iteration
+  for (int k = 0; k < nks; k += 2) {
+    kstep(I0{}, k);
+    kstep(I1{}, k + 1);
   }
 
   // epilogue: stage fp32 tile in LDS, then 256-byte contiguous atomic rows
@@ -717,10 +601,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_wgrad_glds_kernel(WgradPara
 // tile over a 32-deep quarter -- against the 2x2 arrangement of 32x32 wave tiles this halves
 // the transposed LDS fragment bytes per MFMA (16 reads feed 16 MFMAs per wave, not 8 reads 4
 // MFMAs), and that kernel is LDS-read bound. <2,1,2> / <1,2,2>: 128x64 / 64x128 blocks.
-// RIM: 0 original loaders, 1 row-incremental per-lane rows, 2 row-incremental shared rows
-template <int WMt, int WNt, int KS, int RIM>
+// RIS: X loader with rows shared across lanes (one filter tap per tile), else per-lane rows
+template <int WMt, int WNt, int KS, bool RIS>
 __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
-  constexpr bool RI = RIM >= 1;
   static_assert(WMt * WNt * KS == 4, "4 waves");
   constexpr int BM = 64 * WMt, BN = 64 * WNt, BK = 128, KW = BK / KS;  // KW: k rows per wave
   constexpr int AVR = BM / 8, BVR = BN / 8;                // 16-byte vectors per LDS row
@@ -748,84 +631,29 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
 
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(p.dy, p.dy_bytes);
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
-  const int a_cv = tid % AVR, a_r0 = tid / AVR;
-  constexpr int A_RSTEP = 256 / AVR;
-  const int a_col = i0 + a_cv * 8;
-  const bool a_colok = a_col < p.Nout;
-  const int b_cv = tid % BVR, b_r0 = tid / BVR;
-  constexpr int B_RSTEP = 256 / BVR;
-  const int b_col = j0 + b_cv * 8;
-  const bool b_colok = b_col < p.K;
-  int tap = (int)fdiv((uint32_t)b_col, p.fd_c);
-  const int b_c = b_col - tap * p.C;
-  const int b_r = (int)fdiv((uint32_t)tap, p.fd_s), b_s = tap - b_r * p.S;
-  const int b_dh = b_r * p.dil_h - p.pad_h, b_dw = b_s * p.dil_w - p.pad_w;
-
   u32x4 ra[AV], rb[BV];
   using GA = WgSeg<BK, BM, 256>;
   using GB = WgSeg<BK, BN, 256>;
-  static_assert(!RI || (GA::V == AV && GB::V == BV), "RI mapping");
+  static_assert(GA::V == AV && GB::V == BV, "loader mapping");
   WgALoad<BK, BM, 256> ald;
-  std::conditional_t<RIM == 2, WgBLoadShared<BK, BN, 256>, WgBLoad<BK, BN, 256>> bld;
-  WgAdvance adv;
+  std::conditional_t<RIS, WgBLoadShared<BK, BN, 256>, WgBLoad<BK, BN, 256>> bld;
   const uint32_t a_step = (uint32_t)(BK * p.ldy * 2);
-  if constexpr (RI) {
-    ald.init(p, mbeg, i0, tid);
-    bld.init(p, mbeg, j0, tid);
-    adv = wg_advance(p, BK);
-  }
-  auto gload = [&](int kt) {
-    if constexpr (RI) {  // k-steps in order: the loaders hold k-step kt's rows
-      ald.load(dyr, mend, ra);
-      bld.load(p, xr, mend, rb);
-      ald.advance(a_step);
-      bld.advance(adv, p.stride_h);
-      return;
-    }
-    const int mb = mbeg + kt * BK;
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      const int m = mb + a_r0 + A_RSTEP * v;
-      ra[v] = buf_load16(dyr, (a_colok && m < mend) ? (uint32_t)(m * p.ldy + a_col) * 2u : HCB_OOB);
-    }
-#pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      const int m = mb + b_r0 + B_RSTEP * v;
-      uint32_t off = HCB_OOB;
-      if (b_colok && m < mend) {
-        const int n = (int)fdiv((uint32_t)m, p.fd_pq);
-        const int rem = m - n * p.P * p.Q;
-        const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
-        const int qq = rem - pp * p.Q;
-        const int h = pp * p.stride_h + b_dh, w = qq * p.stride_w + b_dw;
-        if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W)
-          off = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c) * 2u;
-      }
-      rb[v] = buf_load16(xr, off);
-    }
+  ald.init(p, mbeg, i0, tid);
+  bld.init(p, mbeg, j0, tid);
+  const WgAdvance adv = wg_advance(p, BK);
+  auto gload = [&]() {  // k-steps in order: the loaders hold the next k-step's rows
+    ald.load(dyr, mend, ra);
+    bld.load(p, xr, mend, rb);
+    ald.advance(a_step);
+    bld.advance(adv, p.stride_h);
   };
   auto lstore = [&](int buf) {
-    if constexpr (RI) {
 #pragma unroll
-      for (int v = 0; v < AV; ++v)
-        *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = ra[v];
+    for (int v = 0; v < AV; ++v)
+      *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = ra[v];
 #pragma unroll
-      for (int v = 0; v < BV; ++v)
-        *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = rb[v];
-      return;
-    }
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      const int row = a_r0 + A_RSTEP * v;
-      const int slot = (a_cv >> 1) ^ wg_swz<BM / 16>(row);
-      *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + row * BM * 2 + slot * 32 + (a_cv & 1) * 16) = ra[v];
-    }
-#pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      const int row = b_r0 + B_RSTEP * v;
-      const int slot = (b_cv >> 1) ^ wg_swz<BN / 16>(row);
-      *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + row * BN * 2 + slot * 32 + (b_cv & 1) * 16) = rb[v];
-    }
+    for (int v = 0; v < BV; ++v)
+      *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = rb[v];
   };
 
   const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
@@ -875,7 +703,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
 
   // the 64x64 (1,1,4) variant keeps the single-set loop: with two sets the compiler copies its 64
   // accumulators between register files every k-step (56 extra VALU per two k-steps)
-  constexpr bool PIPE2 = RI && !(WMt == 1 && WNt == 1);
+  constexpr bool PIPE2 = !(WMt == 1 && WNt == 1);
   if constexpr (PIPE2) {
     // two register sets, k-step k + 2 in flight while k is multiplied (see conv_wgrad_kernel)
     u32x4 sa[2][AV], sb[2][BV];
@@ -913,12 +741,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
       kstep(I1{});
     }
   } else {
-    gload(0);
+    gload();
     lstore(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nk) gload(kt + 1);
+      if (kt + 1 < nk) gload();
       mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
       if (kt + 1 < nk) lstore(cur ^ 1);
       __syncthreads();
@@ -949,12 +777,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kq_kernel(WgradParams p) {
   wgrad_store_tile(p, Cs, LDC, BM, BN, i0, j0, tid, 256, gridDim.x == ntiles);
 }
 
-// the row-incremental loaders need a thread's 16-byte vector inside one filter tap
-static bool wgrad_ri_ok(const WgradParams& p) { return (p.C % 8) == 0 && riv_enabled(); }
 // every column tile of width BN lies in one filter tap (shared-row X loader)
-static bool wgrad_one_tap(const WgradParams& p, int BN) {
-  return (p.R * p.S == 1 || (p.C % BN) == 0) && shared_rows_enabled();
-}
+static bool wgrad_one_tap(const WgradParams& p, int BN) { return p.R * p.S == 1 || (p.C % BN) == 0; }
 
 template <int WMt, int WNt, int KS>
 static void wlaunch_kq(const WgradParams& p, int splits, hipStream_t st) {
@@ -965,21 +789,17 @@ static void wlaunch_kq(const WgradParams& p, int splits, hipStream_t st) {
   const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, 0>,
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, 2>,
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kq_kernel<WMt, WNt, KS, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
   const dim3 grid(tiles * splits);
-  if (!wgrad_ri_ok(p))
-    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, 0>), grid, dim3(256), lds, st, p);
-  else if (wgrad_one_tap(p, BN))
-    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, 2>), grid, dim3(256), lds, st, p);
+  if (wgrad_one_tap(p, BN))
+    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, true>), grid, dim3(256), lds, st, p);
   else
-    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, 1>), grid, dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_kq_kernel<WMt, WNt, KS, false>), grid, dim3(256), lds, st, p);
 }
 
 template <int WM, int WN, int TM, int TN, int NST>
@@ -1011,28 +831,19 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
   size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2;
   size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-  const int ld = wgrad_ri_ok(p) ? (wgrad_one_tap(p, BN) ? 3 : 2) : ((p.C % BN) == 0 ? 1 : 0);
   dim3 grid(tiles * splits);
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 0>,
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, 3>,
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
-  if (ld == 3)
-    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 3>), grid, dim3(256), lds, st, p);
-  else if (ld == 2)
-    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 2>), grid, dim3(256), lds, st, p);
-  else if (ld == 1)
-    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 1>), grid, dim3(256), lds, st, p);
+  if (wgrad_one_tap(p, BN))
+    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true>), grid, dim3(256), lds, st, p);
   else
-    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, 0>), grid, dim3(256), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false>), grid, dim3(256), lds, st, p);
 }
 
 // cfg 0..2: register-staged {128x128, 64x128, 64x64}; 3..9: LDS-DMA ring {128x128 (4 waves of
@@ -1052,6 +863,8 @@ int wgrad_tile_n(int cfg) {
 }
 
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st) {
+  // the register-staged loaders keep a thread's 16-byte vector inside one filter tap (every
+  // weight pack already requires C % 8 == 0; bindings.cpp checks it)
   switch (cfg) {
     case 0: wlaunch<2, 2, 64, 64>(p, splits, st); break;  // 128 x 128
     case 1: wlaunch<1, 4, 64, 32>(p, splits, st); break;  // 64 x 128

@@ -49,7 +49,6 @@ struct EpiPrefetch {
   static constexpr int ITER = BM * SEGS / NT;
   static constexpr int CH = BNB ? (ITER < HCB_BNB_CH ? ITER : HCB_BNB_CH) : 1;
   u32x4 pr[CH], pz[CH], py[CH];
-  uint32_t pm[CH];  // mode 3: ReLU bit mask byte of the segment
   // forward GEMMs: the BN statistic shift of each of the lane's accumulator columns, loaded
   // before the main loop so the epilogue does not wait on it
   static constexpr int NKC = BNB ? 1 : TN / 16;
@@ -73,8 +72,6 @@ struct EpiPrefetch {
         pz[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_z) + o * p.bnb_ld + col);
         if (p.bnb_mode == 1)
           py[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_y) + o * p.bnb_ld + col);
-        else if (p.bnb_mode == 3)
-          pm[k] = reinterpret_cast<const uint8_t*>(p.bnb_y)[o * (size_t)(p.bnb_ld >> 3) + (col >> 3)];
       }
     }
   }
@@ -328,9 +325,6 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
         } else if (p.bnb_mode == 2) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = (zf[e] * bsc[e] + bsh[e]) > 0.f ? v[e] : 0.f;
-        } else if (p.bnb_mode == 3) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = ((pre.pm[k] >> e) & 1u) ? v[e] : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {

@@ -55,10 +55,9 @@ struct ConvParams {
   uint32_t x_bytes, w_bytes;
   // Fused BN-backward reduction (a data-grad GEMM whose output is the dy of a BN layer):
   // the epilogue gates its output with the layer's ReLU mask (bnb_mode 1: y > 0, 2: recomputed
-  // from z, 3: bit mask written by the forward apply kernel, 0: none), stores g instead of dy,
+  // from z, 0: none), stores g instead of dy,
   // and accumulates sum(g), sum(g * xhat) per channel into bnb_acc replicas [bnb_R][2][Nout].
-  // z / y rows share the output's row index (after remap) with row stride bnb_ld; in mode 3
-  // bnb_y is a uint8 [rows][bnb_ld / 8] mask (bit e of byte c/8 = y[row][c + e] > 0).
+  // z / y rows share the output's row index (after remap) with row stride bnb_ld.
   const void* bnb_z;
   const void* bnb_y;
   const float *bnb_mean, *bnb_invstd, *bnb_gamma, *bnb_beta;
@@ -94,9 +93,6 @@ struct WgradParams {
   uint32_t dy_bytes, x_bytes;
 };
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st);
-// row-incremental weight-grad loaders on (default) / off, for A/B runs
-void set_wgrad_ri(int on);
-bool riv_enabled();
 int wgrad_tile_m(int cfg);
 int wgrad_tile_n(int cfg);
 
@@ -134,8 +130,6 @@ void launch_bn_bwd_apply2(const void* dy, int lddy, const void* y, int ldyv, con
 
 // finalize-free variants: statistics accumulated in R replicas of [2][C] (fp32 atomics).
 // Blocks tile (row split) x (channel group) so each block only reduces its group's replicas.
-// mask (optional): uint8 [M][C/8] ReLU mask of the output (bit e of byte c/8 = y[m][c+e] > 0),
-// read back by the mode-3 fused BN-backward epilogue instead of the full bf16 output
 // A second BatchNorm applied to the residual operand inside the same pass (a projection
 // shortcut's conv output z_sc, whose statistics its conv epilogue accumulated): the block output
 // is act(BN(x) + BN_sc(res)) and BN_sc's normalised tensor is never written. Same M, C, R.
@@ -152,7 +146,7 @@ struct ResBN {
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         void* mask, const float* shift, const ResBN* res_bn, hipStream_t st);
+                         const float* shift, const ResBN* res_bn, hipStream_t st);
 // BN(acc statistics) + ReLU + max pool (NHWC, C contiguous): pooled y [N,P,Q] (row stride ldy) and
 // the uint8 window argmax [N,P,Q,C]; the BN+ReLU activation itself is not materialised
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
@@ -234,5 +228,7 @@ void launch_bucket_pack(const float* src, void* dst, int64_t n, float scale, int
                         hipStream_t st);
 void launch_bucket_unpack(const void* src, float* dst, int64_t n, float scale, int mode,
                           hipStream_t st);
+// debug: one wave sleeps ~ms milliseconds (bounded, s_memrealtime-timed) on stream st
+void launch_debug_sleep(int ms, hipStream_t st);
 
 }  // namespace hcb

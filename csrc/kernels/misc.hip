@@ -567,4 +567,17 @@ void launch_bucket_unpack(const void* src, float* dst, int64_t n, float scale, i
     hipLaunchKernelGGL(bucket_unpack_kernel<0>, dim3(pack_grid(n)), dim3(256), 0, st, src, dst, n, scale);
 }
 
+// Debug only (HCB_COMM_DEBUG_SLEEP_MS): a single wave that sleeps for ~ms milliseconds on the
+// 100 MHz real-time counter, so a stalled collective can be staged on one GPU. Bounded: the
+// loop exits after the requested time (ms is clamped to 10 s on the host).
+__global__ __launch_bounds__(64) void debug_sleep_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+void launch_debug_sleep(int ms, hipStream_t st) {
+  if (ms <= 0) return;
+  if (ms > 10000) ms = 10000;
+  hipLaunchKernelGGL(debug_sleep_kernel, dim3(1), dim3(64), 0, st, (uint64_t)ms * 100000ull);
+}
+
 }  // namespace hcb

@@ -15,7 +15,7 @@
 //           their slot e%2, read with system-scope (cache-bypassing) loads; the last
 //           workgroup advances the device epoch.
 // Ranks never write into a peer's memory; a peer's data is only read after its release.
-// Spins are bounded (HCB_XGMI_SPIN iterations of s_sleep(8), ~0.2 us each at 2.4 GHz; default
+// Spins are bounded (Xgmi::spin iterations of s_sleep(8), ~0.2 us each at 2.4 GHz; default
 // 2^25 ~ 7 s): on timeout the kernel raises the error word, POISONS its output with NaN (so a
 // reduction that did not synchronise can never pass for a good one: the loss goes NaN) and
 // completes, so a dead peer can never leave a wave running on the GPU. The host side checks

@@ -52,3 +52,30 @@ def test_spawned_worker_failure_propagates():
                          env=_env(HCB_BENCH_ONE_DEVICE="1", HIP_VISIBLE_DEVICES=""),
                          capture_output=True, text=True, timeout=300)
     assert out.returncode != 0
+
+
+def test_launcher_parent_never_loads_torch():
+    """The process that forks the workers counts GPUs from the KFD topology: torch (and with it
+    the HIP runtime) must not be loaded there, on the spawn path and on the refusal path."""
+    for extra in ({"HCB_BENCH_ONE_DEVICE": "1", "HCB_BENCH_STUB_WORKER": "1"}, {}):
+        out = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--steps", "1", "--warmup", "0"],
+                             env=_env(HCB_BENCH_REPORT_PARENT="1", **extra), capture_output=True, text=True,
+                             timeout=300)
+        assert "[bench] launcher parent: torch loaded = False" in out.stderr, out.stderr
+
+
+def test_visible_gpu_count_from_kfd_topology(tmp_path, monkeypatch):
+    from azure_hc_intel_tf_amd.launch import launcher
+
+    root = tmp_path / "class/kfd/kfd/topology/nodes"
+    for n, simd in enumerate([0, 256, 256, 256]):  # one CPU agent, three GPUs
+        d = root / str(n)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"simd_count {simd}\nlocation_id {n * 8}\ndomain 0\n")
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert launcher.visible_gpu_count(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2")
+    assert launcher.visible_gpu_count(str(tmp_path)) == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert launcher.visible_gpu_count(str(tmp_path)) == 0

@@ -100,6 +100,31 @@ def test_stall_watchdog_names_the_stalled_cycle():
         np.testing.assert_allclose(np.asarray(buf, np.float32), exp, rtol=1e-6)
 
 
+def test_graph_replay_heartbeat_lets_the_watchdog_see_captured_collectives():
+    """The default multi-GPU step replays a captured graph: its collectives make no engine call,
+    so the watchdog only learns about them through the per-step heartbeat (step_mark, called by
+    trainer.py after each replay). Rank 1 stalls in replayed step 2: with the heartbeat every
+    rank's watchdog warns and names step 3 (1-based watch cycle); without it the stall is
+    invisible -- the blind spot the heartbeat closes."""
+    world = 3
+    init = _init(world, 4096)
+    cycles = [[2048, 2048], [0, 2048]]
+    r = E.run(world, [x.tolist() for x in init], cycles, threshold_bytes=4096, replay_steps=4, stall_rank=1,
+              stall_step=2, stall_ms=400, warn_s=0.1)
+    warned = {w[0] for w in r["warnings"]}
+    assert warned == set(range(world)), r["warnings"]
+    for rank, cycle, last_seq, waited in r["warnings"]:
+        assert cycle == 3 and waited > 0.1, r["warnings"]
+    assert r["cycles"] == [4] * world
+    # four replays of the full-buffer sum: x_r -> sum over ranks, then world^k growth
+    exp = _expected(init, 0, False) * world ** 3
+    for buf in r["buffers"]:
+        np.testing.assert_allclose(np.asarray(buf, np.float32), exp, rtol=1e-5)
+    blind = E.run(world, [x.tolist() for x in init], cycles, threshold_bytes=4096, replay_steps=4, stall_rank=1,
+                  stall_step=2, stall_ms=400, warn_s=0.1, heartbeat=False)
+    assert blind["warnings"] == []
+
+
 def test_no_warning_without_stall():
     init = _init(2, 2048)
     r = E.run(2, [x.tolist() for x in init], [[0, 2048]], warn_s=0.2)

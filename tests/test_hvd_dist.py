@@ -117,6 +117,35 @@ def test_distributed_optimizer_reduces_buckets_with_unused_params(monkeypatch):
     run(2, _dist_optimizer_unused_param)
 
 
+def _dist_optimizer_rank_dependent_branch(hvd):
+    """A data-dependent branch unused on SOME ranks only: the buckets must still go out in the
+    same order on every rank (a rank whose middle bucket is incomplete must not launch the later
+    ones first), or the collectives pair up mismatched buffers / hang."""
+    torch.manual_seed(0)
+    a, b, c = torch.nn.Linear(32, 32), torch.nn.Linear(32, 32), torch.nn.Linear(32, 32)
+    params = list(a.parameters()) + list(b.parameters()) + list(c.parameters())
+    hvd.broadcast_parameters([p.data for p in params], root_rank=0)
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(params, lr=0.05))
+    assert len(opt._buckets) >= 3, "one bucket per layer expected"
+    for step in range(3):
+        opt.zero_grad()
+        x = torch.full((2, 32), 0.1 * float(hvd.rank() + step + 1))
+        h = a(x)
+        if (hvd.rank() + step) % 2 == 0:  # b used on half of the ranks only
+            h = b(h)
+        c(h).sum().backward()
+        opt.step()
+    w = torch.cat([p.detach().flatten() for p in params])
+    allw = hvd.allgather(w.view(1, -1))
+    for r in range(1, hvd.size()):
+        assert torch.allclose(allw[0], allw[r], atol=1e-5), "replicas diverged"
+
+
+def test_distributed_optimizer_rank_dependent_unused_branch(monkeypatch):
+    monkeypatch.setenv("HOROVOD_FUSION_THRESHOLD", "4096")  # the floor: ~one bucket per tensor (32x32 fp32 = 4 KiB)
+    run(4, _dist_optimizer_rank_dependent_branch)
+
+
 def _engine_training_world8(hvd):
     """world 8: overlapped, threshold-split range reductions keep every replica identical."""
     from azure_hc_intel_tf_amd.models import create_model

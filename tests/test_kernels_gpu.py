@@ -175,7 +175,7 @@ def test_conv_dgrad(case, accumulate):
 
 @pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[2], CONV_CASES[3], CONV_CASES[6]],
                          ids=["1x1", "3x3", "1x1s2", "cin80"])
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("cfg", [2, 4, 12])
 def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
@@ -204,8 +204,7 @@ def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
         keep[:, ::s, ::s] = True
         base = base * keep
     dx = base.clone() if accumulate else (torch.zeros_like(base) if strided_1x1 else torch.empty_like(base))
-    gate = Fn.pack_relu_mask(yact) if mode == 3 else yact  # mode 3: 1-bit ReLU mask of y
-    bnb = Fn.BNBwdFuse(z, gate, saved, gamma, beta, mode, acc, R)
+    bnb = Fn.BNBwdFuse(z, yact, saved, gamma, beta, mode, acc, R)
     Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate, cfg=cfg, bnb=bnb)
     ref = torch.empty(N, H, H, cin)
     Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), ref, False)
@@ -213,7 +212,7 @@ def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
         ref = ref + base.float().cpu()
     zc = z.float().cpu()
     cpu_bnb = Fn.BNBwdFuse(zc, yact.float().cpu(), Fn.BNSaved(mean.cpu(), invstd.cpu()), gamma.cpu(), beta.cpu(),
-                           1 if mode == 3 else mode, None, R)
+                           mode, None, R)
     g = cpu_bnb.gate_cpu(ref.clone())
     assert rel_err(dx, g) < 1e-2
     xhat = (zc - mean.cpu()) * invstd.cpu()
@@ -263,37 +262,30 @@ def test_conv_wgrad_all_configs(cfg):
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 10, 11, 12, 13, 14])
 def test_conv_wgrad_row_incremental_loaders(cfg):
-    """The row-incremental register-staged loaders (mixed-radix pixel stepping; per-lane rows,
+    """The register-staged row-incremental loaders (mixed-radix pixel stepping; per-lane rows,
     and rows shared through ds_bpermute when a column tile lies in one filter tap) against the
-    original divide-per-row loaders: with one split (no atomics) all run the
-    same MFMA sequence, so dW must be bitwise equal; plus the fp32 CPU reference. Geometries
-    cover a k-step spanning images (7x7 output: dn > 0), output-row carries, stride 2 with
-    padding, partial Nout / pixel tiles."""
-    hcb = _ext.ops()
+    fp32 CPU reference, one split (no atomics: two runs are bitwise equal). Geometries cover a
+    k-step spanning images (7x7 output: dn > 0), output-row carries, stride 2 with padding,
+    partial Nout / pixel tiles."""
     torch.manual_seed(8)
-    try:
-        for cin, cout, k, s, pads, H, N in [(64, 64, 3, 1, (1, 1, 1, 1), 14, 3),
-                                            (128, 72, 3, 1, (1, 1, 1, 1), 7, 5),
-                                            (96, 128, 3, 2, (1, 1, 1, 1), 15, 2),
-                                            (256, 192, 1, 1, (0, 0, 0, 0), 9, 4),
-                                            (64, 256, 1, 2, (0, 0, 0, 0), 13, 3)]:
-            spec, p, pk = make_conv(cin, cout, k, k, s, s, pads)
-            P, Q = spec.out_hw(H, H)
-            x = bf(torch.randn(N, H, H, cin, device=DEV))
-            dz = bf(torch.randn(N, P, Q, cout, device=DEV))
-            out = []
-            for ri in (0, 2, 1):  # original, row-incremental per-lane rows, shared rows (one tap per tile)
-                hcb.set_wgrad_ri(ri)
-                dw = torch.zeros(cout, spec.K, dtype=torch.float32, device=DEV)
-                Fn.conv_wgrad(dz, x, spec, dw, cfg=(cfg, 1))
-                out.append(dw)
-            assert torch.equal(out[0], out[1]), (cfg, cin, cout, k, s)
-            assert torch.equal(out[0], out[2]), (cfg, cin, cout, k, s)
-            ref = torch.zeros(cout, k, k, cin)
-            Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
-            assert rel_err(out[2], ref.view(cout, -1)) < 1e-2, (cfg, cin, cout, k)
-    finally:
-        hcb.set_wgrad_ri(1)
+    for cin, cout, k, s, pads, H, N in [(64, 64, 3, 1, (1, 1, 1, 1), 14, 3),
+                                        (128, 72, 3, 1, (1, 1, 1, 1), 7, 5),
+                                        (96, 128, 3, 2, (1, 1, 1, 1), 15, 2),
+                                        (256, 192, 1, 1, (0, 0, 0, 0), 9, 4),
+                                        (64, 256, 1, 2, (0, 0, 0, 0), 13, 3)]:
+        spec, p, pk = make_conv(cin, cout, k, k, s, s, pads)
+        P, Q = spec.out_hw(H, H)
+        x = bf(torch.randn(N, H, H, cin, device=DEV))
+        dz = bf(torch.randn(N, P, Q, cout, device=DEV))
+        out = []
+        for _ in range(2):
+            dw = torch.zeros(cout, spec.K, dtype=torch.float32, device=DEV)
+            Fn.conv_wgrad(dz, x, spec, dw, cfg=(cfg, 1))
+            out.append(dw)
+        assert torch.equal(out[0], out[1]), (cfg, cin, cout, k, s)
+        ref = torch.zeros(cout, k, k, cin)
+        Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
+        assert rel_err(out[0], ref.view(cout, -1)) < 1e-2, (cfg, cin, cout, k)
 
 
 def test_conv_wgrad_split_k_large_reduction():
@@ -479,12 +471,7 @@ def test_bn_finalize_free_path(C, relu, residual):
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     mean, invstd = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
     y = torch.empty_like(z)
-    mask = torch.full((N * H * H, C // 8), 0xAA, dtype=torch.uint8, device=DEV)
-    saved = Fn.bn_forward_acc(z, gamma, beta, rm, rv, 0.9, 1e-5, y, relu, acc_f, R, mean, invstd, residual=res,
-                              mask=mask)
-    # the ReLU bit mask (read by the mode-3 fused backward) is exactly the stored output's y > 0
-    assert torch.equal(mask, Fn.pack_relu_mask(y))
-    assert torch.equal(Fn.unpack_relu_mask(mask, y.shape), y > 0)
+    saved = Fn.bn_forward_acc(z, gamma, beta, rm, rv, 0.9, 1e-5, y, relu, acc_f, R, mean, invstd, residual=res)
     zc = z.float().cpu()
     yc = torch.empty(N, H, H, C)
     rmc, rvc = torch.zeros(C), torch.ones(C)

@@ -1,0 +1,68 @@
+#!/bin/bash
+# One parametrised GPU-box runner (gpurun): every step is named on the command line and runs under
+# its own time limit; the first failing step ends the script (no retries on the GPU).
+#
+#   gpurun -- bash tools/gpu_run.sh smoke tests bench prof
+#   gpurun -- bash tools/gpu_run.sh tests:tests/test_kernels_gpu.py bench:--steps=30 prof:--steps=10
+#   TAG=r3a gpurun -- bash tools/gpu_run.sh bench readme
+#
+# steps:
+#   smoke            __graft_entry__.smoke()
+#   tests[:files]    pytest -m gpu (whole suite, or the comma-separated files)
+#   bench[:args]     python bench.py (args comma-separated, e.g. bench:--batch_size=256)
+#   benchab:ENV      bench.py with and without ENV (e.g. benchab:HCB_X=0), interleaved 2 rounds
+#   prof[:args]      rocprofv3 --kernel-trace --stats of bench.py, summarised by tools/kstats.py
+#   pmc:COUNTERS     one rocprofv3 --pmc pass (counters comma-separated) over bench.py --steps 3
+#   readme           tools/gpu_readme_numbers.sh
+#   py:SCRIPT[,args] python SCRIPT args (a probe / diagnostic)
+# Outputs go to gpurun_out/${TAG}_<step>.*
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-run}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+
+fail() { echo "FAILED: $1"; [ -f "$2" ] && tail -40 "$2"; exit 1; }
+
+for step in "$@"; do
+  name=${step%%:*}; arg=""; [ "$name" != "$step" ] && arg=${step#*:}
+  args=${arg//,/ }
+  case $name in
+    smoke)
+      timeout -k 10 300 python __graft_entry__.py smoke > ${O}_smoke.log 2>&1 || fail smoke ${O}_smoke.log
+      tail -1 ${O}_smoke.log ;;
+    tests)
+      files=${args:-tests}
+      timeout -k 10 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread \
+        > ${O}_tests.log 2>&1 || fail tests ${O}_tests.log
+      tail -1 ${O}_tests.log ;;
+    bench)
+      timeout -k 10 400 python bench.py $args > ${O}_bench.json 2> ${O}_bench.err || fail bench ${O}_bench.err
+      cut -c1-260 ${O}_bench.json ;;
+    benchab)
+      for r in 1 2; do for v in base var; do
+        if [ $v = base ]; then e=""; else e="$args"; fi
+        env $e timeout -k 10 400 python bench.py --steps 40 --warmup 10 > ${O}_ab.json 2> ${O}_ab.err || fail benchab ${O}_ab.err
+        echo "$v [$e] $(python -c "import json;d=json.load(open('${O}_ab.json'));print(d['value'], d['ms_per_step'])")"
+      done; done ;;
+    prof)
+      pargs=${args:---steps 10 --warmup 3}
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_prof -o run \
+        -- python $R/bench.py $pargs > ${O}_prof.log 2>&1) || fail prof ${O}_prof.log
+      steps=$(python -c "import sys;a=sys.argv[1:];s=int(a[a.index('--steps')+1]) if '--steps' in a else 10;w=int(a[a.index('--warmup')+1]) if '--warmup' in a else 3;print(s+w)" $pargs)
+      python tools/kstats.py ${O}_prof/run_kernel_stats.csv --steps $steps > ${O}_kstats.txt || fail kstats
+      sed -n '/per class/,$p' ${O}_kstats.txt ;;
+    pmc)
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $args --kernel-trace --output-format csv -d ${O}_pmc -o run \
+        -- python $R/bench.py --steps 3 --warmup 2 > ${O}_pmc.log 2>&1) || fail pmc ${O}_pmc.log
+      echo "pmc done: ${O}_pmc" ;;
+    readme)
+      bash tools/gpu_readme_numbers.sh || fail readme ;;
+    py)
+      timeout -k 10 600 python -u $args > ${O}_py.log 2>&1 || fail py ${O}_py.log
+      tail -40 ${O}_py.log ;;
+    *) echo "unknown step $name"; exit 2 ;;
+  esac
+done
+echo "gpu_run done: $*"
