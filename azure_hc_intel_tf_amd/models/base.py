@@ -37,6 +37,9 @@ class CNNModel:
     """
 
     name = "model"
+    # every op of the model has an fp32 HIP kernel: --compute_dtype fp32 runs natively (bf16x3
+    # GEMMs + fp32 BN / pool / loss); otherwise fp32 takes the PyTorch (MIOpen) path
+    F32_NATIVE_OK = False
     default_image_size = 224
     default_batch_size = 64
     default_lr_per_256 = 0.1  # tf_cnn_benchmarks: lr = 0.1 * global_batch / 256 for ResNets
@@ -52,7 +55,8 @@ class CNNModel:
         from ..ops import functional as Fn
 
         self.native = self.device.type == "cuda" and (
-            self.compute_dtype == "bf16" or (self.compute_dtype == "fp16" and Fn.F16_NATIVE))
+            self.compute_dtype == "bf16" or (self.compute_dtype == "fp16" and Fn.F16_NATIVE)
+            or (self.compute_dtype == "fp32" and self.F32_NATIVE_OK))
         if image_channels is None:
             image_channels = 8 if self.native else 3
         assert image_channels in (3, 8) and (not self.native or image_channels == 8)
@@ -61,8 +65,9 @@ class CNNModel:
         self.ps = ParamStore(seed=seed)
         self.layers: List = []
         self.build()
-        self.ps.finalize(self.device, dtype_pack=TORCH_DTYPES[self.compute_dtype] if self.native else torch.bfloat16,
-                         pack=self.native)
+        f32n = self.native and self.compute_dtype == "fp32"
+        self.ps.finalize(self.device, dtype_pack=torch.bfloat16 if f32n or not self.native
+                         else TORCH_DTYPES[self.compute_dtype], pack=self.native, pack_lo=f32n)
 
     # -- to implement
     def build(self):
@@ -108,8 +113,10 @@ class CNNModel:
         different compute dtypes can coexist in one process)."""
         if self.device.type == "cuda":
             from ..nn.layers import set_gpu_compute_dtype
+            from ..ops import functional as Fn
 
             set_gpu_compute_dtype(TORCH_DTYPES[self.compute_dtype])
+            Fn.set_f32_native(self.compute_dtype == "fp32" and self.native)
 
     # -- helpers
     @property

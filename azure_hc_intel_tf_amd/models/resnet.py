@@ -72,6 +72,7 @@ class Bottleneck:
 
 class ResNet(CNNModel):
     default_image_size = 224
+    F32_NATIVE_OK = True  # --compute_dtype fp32 on the HIP kernels (bf16x3 GEMMs, fp32 BN / pool)
 
     def __init__(self, depth: int = 50, version: str = "v1", **kw):
         self.depth = depth
@@ -83,7 +84,7 @@ class ResNet(CNNModel):
         ps = self.ps
         S = self.image_size
         v15 = self.version == "v1.5"
-        if self.native and L.STEM_S2D:
+        if self.native and L.STEM_S2D and self.compute_dtype != "fp32":  # the fold kernels are 16-bit
             self.stem = StemS2D(ps, "conv0", (S, S, self.image_channels), 64, relu=True, need_dx=False,
                                 logical_cin=3)
         else:

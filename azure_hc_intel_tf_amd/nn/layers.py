@@ -283,6 +283,8 @@ class ConvBN(Layer):
         if not (self.bn and FUSE_BN_BWD) or self._saved is None:
             return None
         x, z, y, saved, had_res = self._saved
+        if z.dtype == torch.float32:  # the fused BN-backward epilogue is 16-bit only
+            return None
         mode = (1 if had_res else 2) if self.relu else 0
         self._pre_reduced = True
         _, acc_b, R = self._acc if self._acc is not None else (None, self.acc_b.data, STAT_R)
@@ -627,9 +629,9 @@ class Logits(Layer):
             dx = torch.empty((B, self.cin), dtype=x.dtype, device=x.device)
             C = self.ld
             geom = [B, 1, 1, C, C, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, self.cin, C, self.pack.Kpad_t, self.cin,
-                    0, 1, 1, 1, 1, 0, 0]
+                    0, 1, 1, 1, 1, 0, Fn._f32o(dx)]
             cfgd = Fn.conv_plan(B, self.cin, C)[0]
-            hcb.conv_igemm(dlogits, self.pack.tr, dx, None, None, None, geom, cfgd)
+            hcb.conv_igemm(dlogits, self.pack.tr, dx, None, None, None, geom, cfgd, None, Fn.lo_pack(self.pack.tr))
         else:
             g = dlogits[:, :self.ncls]
             self.w.grad.view(self.ncls, self.cin).add_((g.t() @ x).float())

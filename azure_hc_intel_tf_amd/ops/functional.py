@@ -68,12 +68,40 @@ def det_replicas(M: int) -> int:
 F16_NATIVE = True
 
 
+# fp32 activations through the HIP kernels (--compute_dtype fp32, the reference's precision):
+# bf16x3 GEMMs (every fp32 operand split into bf16 hi + lo while staged, hi*hi + hi*lo + lo*hi
+# MFMAs with fp32 accumulation) and fp32 BN / pool / loss kernels. Set by the active model
+# (CNNModel.activate) for the models whose whole op set has the fp32 kernels (ResNet v1 / v1.5);
+# other models keep the PyTorch path in fp32.
+_F32_NATIVE = [False]
+# data_ptr of a bf16 weight pack -> its residual pack w - bf16(w) (ParamStore, fp32 path)
+_LO = {}
+
+
+def set_f32_native(on: bool) -> None:
+    _F32_NATIVE[0] = bool(on)
+
+
+def register_lo(pack, lo) -> None:
+    _LO[pack.data_ptr()] = lo
+
+
+def lo_pack(w):
+    """The residual (lo) bf16 pack of weight pack ``w`` (fp32 path), or None."""
+    return None if w is None else _LO.get(w.data_ptr())
+
+
+def _f32o(t) -> int:
+    return 1 if t.dtype == torch.float32 else 0
+
+
 def native(t) -> bool:
     """True when ``t`` goes through the hand-written HIP kernels: a bf16 (or, with the fp16
-    build, IEEE-fp16) activation on the GPU. Other GPU tensors (the fp32 reference-precision
-    mode, --compute_dtype fp32) take the PyTorch path below (MIOpen / rocBLAS), the same code
-    as the CPU path."""
-    return t.is_cuda and (t.dtype == torch.bfloat16 or (t.dtype == torch.float16 and F16_NATIVE))
+    build, IEEE-fp16) activation on the GPU, or an fp32 one while an fp32-native model is
+    active. Other tensors take the PyTorch path below (MIOpen / rocBLAS on the GPU), the same
+    code as the CPU path."""
+    return t.is_cuda and (t.dtype == torch.bfloat16 or (t.dtype == torch.float16 and F16_NATIVE)
+                          or (t.dtype == torch.float32 and _F32_NATIVE[0]))
 
 
 @dataclass
@@ -277,7 +305,12 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
                 1 if residual is not None else 0, 1 if out_f32 else 0, 1 if relu else 0, int(stats_R), splits]
         if residual is not None:  # beta-accumulate epilogue: out = conv(x) + residual (same layout)
             assert ld(residual) == ld(out) and residual.shape == out.shape
-        _ext.ops().conv_igemm(x, wpack, out, residual, bias, stats, geom, cfg, stats_shift)
+        w_lo = None
+        if x.dtype == torch.float32:  # bf16x3: register-staged tiles, no split-K
+            w_lo = lo_pack(wpack)
+            assert w_lo is not None and out_f32, "fp32 conv needs the residual weight pack and an fp32 output"
+            geom[-1] = 1
+        _ext.ops().conv_igemm(x, wpack, out, residual, bias, stats, geom, cfg, stats_shift, w_lo)
         return out
     xt = x.permute(0, 3, 1, 2)
     if spec.pt or spec.pb or spec.pl or spec.pr:
@@ -408,19 +441,25 @@ def dgrad_phase(dz, spec: ConvSpec, wtr, dx, accumulate: bool, phase, cfg=None, 
     ph, pw, Hph, Wph, rs, ss, pad_t, pad_l = phase
     Cdz = spec.cout if spec.cout % 8 == 0 else _round_up(spec.cout, 8)
     sub, Kph = _phase_pack(wtr, spec, Cdz, rs, ss)
+    w_lo = None
+    if dz.dtype == torch.float32:
+        assert bnb is None, "no fused BN-backward epilogue on the fp32 path"
+        w_lo, _ = _phase_pack(lo_pack(wtr), spec, Cdz, rs, ss)
     M, _, taps = dgrad_phase_problem(spec, N, phase)
     geom = [N, P, Q, Cdz, ld(dz), Hph, Wph, len(rs), len(ss), 1, 1, pad_t, pad_l, 1, 1, 1, 1,
-            spec.cin_pad, Kph, sub.shape[1], ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, 0]
+            spec.cin_pad, Kph, sub.shape[1], ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, _f32o(dx)]
     if cfg is None and bnb is not None:
         cfg = _tuned.get(dgb_key(M, spec.cin_pad, Kph, taps))
     cfg, splits = _plan(cfg, M, spec.cin_pad, Kph, dz.device, taps)
+    if w_lo is not None:
+        splits = 1
     geom = geom + [0, 0, splits, ph, pw]
     if bnb is not None:
         _ext.ops().conv_igemm_bnb(dz, sub, dx, dx if accumulate else None, geom, cfg, bnb.z,
-                                  bnb.y if bnb.mode in (1, 3) else None, ld(bnb.z), bnb.saved.mean,
+                                  bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
                                   bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
     else:
-        _ext.ops().conv_igemm(dz, sub, dx, dx if accumulate else None, None, None, geom, cfg)
+        _ext.ops().conv_igemm(dz, sub, dx, dx if accumulate else None, None, None, geom, cfg, None, w_lo)
 
 
 def uses_dgrad_phases(spec: ConvSpec, H: int, W: int) -> bool:
@@ -449,25 +488,29 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
             # 1x1 strided: dense GEMM over dz pixels, scatter rows to (p*sh, q*sw)
             M = N * P * Q
             geom = [N, P, Q, Cdz, ld(dz), P, Q, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, spec.cin_pad, K, Kpad,
-                    ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, 0]
+                    ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, _f32o(dx)]
         else:
             M = N * H * W
             pt = spec.dh * (spec.kh - 1) - spec.pt
             pl = spec.dw * (spec.kw - 1) - spec.pl
             geom = [N, P, Q, Cdz, ld(dz), H, W, spec.kh, spec.kw, 1, 1, pt, pl, spec.dh, spec.dw,
                     spec.sh, spec.sw, spec.cin_pad, K, Kpad, ld(dx), 0, H, W, 1, 1,
-                    1 if accumulate else 0, 0]
+                    1 if accumulate else 0, _f32o(dx)]
         taps = spec.kh * spec.kw
         if cfg is None and bnb is not None:
             cfg = _tuned.get(dgb_key(M, spec.cin_pad, K, taps))
         cfg, splits = _plan(cfg, M, spec.cin_pad, K, dz.device, taps)
+        w_lo = None
+        if dz.dtype == torch.float32:
+            assert bnb is None, "no fused BN-backward epilogue on the fp32 path"
+            w_lo, splits = lo_pack(wtr), 1
         geom = geom + [0, 0, splits]
         if bnb is not None:
             _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
-                                      bnb.y if bnb.mode in (1, 3) else None, ld(bnb.z), bnb.saved.mean,
+                                      bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
                                       bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
         else:
-            _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg)
+            _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg, None, w_lo)
         return dx
     Hp = H + spec.pt + spec.pb
     Wp = W + spec.pl + spec.pr

@@ -6,6 +6,8 @@
 // passes geometry as an int list; the launcher validates shapes / byte ranges on the
 // host BEFORE anything reaches the GPU (an out-of-range gather must never be launched)
 // and enqueues on the current HIP stream.
+#include <algorithm>
+
 #include <torch/library.h>
 #include <ATen/core/Tensor.h>
 #include <ATen/ops/empty.h>
@@ -44,6 +46,21 @@ void check_act(const Tensor& t, const char* name) {
   check_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == kAct, "hcb: ", name, " must be " HCB_ACT_NAME " (the activation dtype of this build)");
 }
+// an activation of this build's 16-bit type, or (bf16 library only) fp32 -- the reference
+// precision path (--compute_dtype fp32); returns true for fp32
+bool check_act_or_f32(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+#ifndef HCB_F16
+  if (t.scalar_type() == at::kFloat) return true;
+#endif
+  TORCH_CHECK(t.scalar_type() == kAct, "hcb: ", name, " must be " HCB_ACT_NAME " or float32");
+  return false;
+}
+bool same_act(const Tensor& a, const Tensor& b, const char* name) {
+  const bool f = check_act_or_f32(b, name);
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), "hcb: ", name, " dtype differs from the other activations");
+  return f;
+}
 void check_f32(const Tensor& t, const char* name) {
   check_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == at::kFloat, "hcb: ", name, " must be float32");
@@ -67,7 +84,7 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
                             at::IntArrayRef g, int64_t cfg) {
   TORCH_CHECK(g.size() >= 28 && g.size() <= 33,
               "hcb.conv_igemm: geom must have 28 (+relu, +stats_R, +splits, +remap origin h, w) entries");
-  check_act(x, "x");
+  const bool f32 = check_act_or_f32(x, "x");  // fp32: bf16x3 path (w = high pack, w_lo set by the caller)
   check_act(w, "w");
   check_cuda(y, "y");
   hcb::ConvParams p{};
@@ -90,7 +107,8 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm: bad ldy");
   TORCH_CHECK(p.idil_h >= 1 && p.idil_w >= 1 && p.dil_h >= 1 && p.dil_w >= 1, "hcb.conv_igemm: bad dilation");
   TORCH_CHECK(p.M > 0 && p.Nout > 0, "hcb.conv_igemm: empty problem");
-  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * 2 + (int64_t)p.C * 2;
+  const int64_t xe = f32 ? 4 : 2;
+  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * xe + (int64_t)p.C * xe;
   int64_t wb = (int64_t)p.Nout * p.Kpad * 2;
   TORCH_CHECK(xb < (1ll << 31) && wb < (1ll << 31), "hcb.conv_igemm: operand exceeds 2 GiB buffer range");
   check_range(x, xb, "x");
@@ -103,6 +121,7 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
     TORCH_CHECK(p.oh0 == 0 && p.ow0 == 0, "hcb.conv_igemm: a remap origin needs remap");
   }
   int64_t esz = p.out_f32 ? 4 : 2;
+  TORCH_CHECK(!f32 || p.out_f32, "hcb.conv_igemm: fp32 inputs give an fp32 output (out_f32)");
   TORCH_CHECK(y.scalar_type() == (p.out_f32 ? at::kFloat : kAct), "hcb.conv_igemm: y dtype");
   check_range(y, rows * p.ldy * esz - (p.ldy - ((p.Nout + 7) / 8) * 8) * esz, "y");
   check_align16(x.data_ptr(), "x");
@@ -169,10 +188,22 @@ const float* opt_f32(const c10::optional<Tensor>& t, int64_t n, const char* what
 
 void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                 const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats,
-                at::IntArrayRef g, int64_t cfg, const c10::optional<Tensor>& stats_shift) {
+                at::IntArrayRef g, int64_t cfg, const c10::optional<Tensor>& stats_shift,
+                const c10::optional<Tensor>& w_lo) {
   hcb::ConvParams p = conv_params(x, w, y, yres, bias, stats, g, cfg);
   TORCH_CHECK(!stats_shift.has_value() || p.stats != nullptr, "hcb.conv_igemm: stats_shift without stats");
   p.stats_shift = opt_f32(stats_shift, p.Nout, "stats_shift");
+  p.w_lo = nullptr;
+  if (x.scalar_type() == at::kFloat) {  // fp32 path: hi / lo weight packs, register-staged, no split-K
+    TORCH_CHECK(w_lo.has_value(), "hcb.conv_igemm: fp32 x needs the residual weight pack w_lo");
+    TORCH_CHECK(w_lo->scalar_type() == w.scalar_type() && w_lo->numel() >= (int64_t)p.Nout * p.Kpad,
+                "hcb.conv_igemm: w_lo must match w");
+    check_align16(w_lo->data_ptr(), "w_lo");
+    TORCH_CHECK(p.splits == 1, "hcb.conv_igemm: no split-K on the fp32 path");
+    p.w_lo = w_lo->data_ptr();
+  } else {
+    TORCH_CHECK(!w_lo.has_value(), "hcb.conv_igemm: w_lo only with fp32 x");
+  }
   hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
 }
 
@@ -227,10 +258,11 @@ int64_t conv_tiles_m(int64_t M, int64_t cfg) {
 void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArrayRef g, int64_t cfg,
                 int64_t splits) {
   TORCH_CHECK(g.size() == 17, "hcb.conv_wgrad: geom must have 17 entries");
-  check_act(dy, "dy");
-  check_act(x, "x");
+  const bool f32 = same_act(dy, x, "x");  // fp32: bf16x3 path
   check_f32(dw, "dw");
   hcb::WgradParams p{};
+  p.f32in = f32 ? 1 : 0;
+  const int64_t e = f32 ? 4 : 2;
   p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];
   p.P = g[5]; p.Q = g[6]; p.R = g[7]; p.S = g[8];
   p.stride_h = g[9]; p.stride_w = g[10]; p.pad_h = g[11]; p.pad_w = g[12];
@@ -241,8 +273,8 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArra
   TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0, "hcb.conv_wgrad: C, ldx multiples of 8");
   TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= p.Nout, "hcb.conv_wgrad: bad ldy");
   TORCH_CHECK(splits >= 1, "hcb.conv_wgrad: splits >= 1");
-  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * 2 + (int64_t)p.C * 2;
-  int64_t yb = ((int64_t)p.M - 1) * p.ldy * 2 + (int64_t)((p.Nout + 7) / 8) * 16;
+  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * e + (int64_t)p.C * e;
+  int64_t yb = ((int64_t)p.M - 1) * p.ldy * e + (int64_t)((p.Nout + 7) / 8) * 8 * e;
   TORCH_CHECK(xb < (1ll << 31) && yb < (1ll << 31), "hcb.conv_wgrad: operand exceeds 2 GiB");
   check_range(x, xb, "x");
   check_range(dy, yb, "dy");
@@ -390,14 +422,15 @@ void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, a
                          const Tensor& saved_mean, const Tensor& saved_invstd, const Tensor& run_mean,
                          const Tensor& run_var, const c10::optional<Tensor>& shift) {
   TORCH_CHECK(g.size() == 13, "hcb.bn_relu_maxpool_acc: geom");
-  check_act(z, "z");
-  check_act(y, "y");
+  const bool f32 = check_act_or_f32(z, "z");
+  same_act(z, y, "y");
+  const int64_t e = f32 ? 4 : 2;
   check_cuda(amax, "amax");
   const int64_t N = g[0], H = g[1], W = g[2], C = g[3], P = g[4], Q = g[5], ldy = g[6];
   TORCH_CHECK(z.is_contiguous() && z.numel() == N * H * W * C, "hcb.bn_relu_maxpool_acc: z contiguous [N,H,W,C]");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldy % 8 == 0 && ldy >= C, "hcb.bn_relu_maxpool_acc: C / ldy");
   TORCH_CHECK(g[7] * g[8] <= 255, "hcb.bn_relu_maxpool_acc: window too large for the uint8 argmax");
-  check_range(y, ((N * P * Q - 1) * ldy + C) * 2, "y");
+  check_range(y, ((N * P * Q - 1) * ldy + C) * e, "y");
   TORCH_CHECK(amax.scalar_type() == at::kByte && amax.is_contiguous() && amax.numel() >= N * P * Q * C,
               "hcb.bn_relu_maxpool_acc: amax uint8 [N,P,Q,C]");
   TORCH_CHECK(N * P * Q < (1ll << 31) && N * H * W < (1ll << 31), "hcb.bn_relu_maxpool_acc: 32-bit index range");
@@ -409,7 +442,7 @@ void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, a
                                   g[10], g[11], g[12], acc.data_ptr<float>(), R, (float)eps, (float)momentum,
                                   gamma.data_ptr<float>(), beta.data_ptr<float>(), saved_mean.data_ptr<float>(),
                                   saved_invstd.data_ptr<float>(), run_mean.data_ptr<float>(),
-                                  run_var.data_ptr<float>(), opt_f32(shift, C, "shift"), cur_stream());
+                                  run_var.data_ptr<float>(), opt_f32(shift, C, "shift"), cur_stream(), f32);
 }
 
 // geom = [N,H,W,C,ldx,P,Q,ldy,kh,kw,sh,sw,ph,pw,is_max,incl_pad]
@@ -434,14 +467,20 @@ void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx
 void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx,
               const Tensor& dx, at::IntArrayRef g, bool accumulate) {
   TORCH_CHECK(g.size() == 16, "hcb.pool_bwd: geom");
-  check_act(dy, "dy");
-  check_act(x, "x");
-  check_act(y, "y");
-  check_act(dx, "dx");
-  check_range(x, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "x");
-  check_range(dx, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "dx");
-  check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "y");
-  check_range(dy, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "dy");
+  const bool f32 = check_act_or_f32(dy, "dy");
+  same_act(dy, x, "x");
+  same_act(dy, y, "y");
+  same_act(dy, dx, "dx");
+  const int64_t e = f32 ? 4 : 2;
+  check_range(x, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * e, "x");
+  check_range(dx, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * e, "dx");
+  check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * e, "y");
+  check_range(dy, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * e, "dy");
+  if (f32)  // the fp32 kernel set has the argmax-gather max-pool backward only
+    TORCH_CHECK(g[14] && idx.has_value() && g[8] == g[9] && g[10] == g[11] && (g[8] + g[10] - 1) / g[10] <= 3 &&
+                    g[0] * g[1] <= 65535 && g[0] * g[1] * g[2] * g[4] < (1ll << 31) &&
+                    g[0] * g[5] * g[6] * std::max(g[7], g[3]) < (1ll << 31),
+                "hcb.pool_bwd: fp32 supports the square max pool with its argmax only");
   TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_bwd: C/ld % 8");
   TORCH_CHECK(g[0] * g[1] * g[2] * (g[3] / 8) < (1ll << 31), "hcb.pool_bwd: 32-bit index range");
   if (idx.has_value())
@@ -449,24 +488,26 @@ void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::opt
                 "hcb.pool_bwd: idx must be contiguous uint8 [N,P,Q,C]");
   hcb::launch_pool_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), dx.data_ptr(), g[0], g[1], g[2], g[3],
                        g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], g[15],
-                       accumulate ? 1 : 0, idx.has_value() ? idx->data_ptr() : nullptr, cur_stream());
+                       accumulate ? 1 : 0, idx.has_value() ? idx->data_ptr() : nullptr, cur_stream(), f32);
 }
 
 void gap_fwd(const Tensor& x, const Tensor& y, int64_t N, int64_t HW, int64_t C) {
-  check_act(x, "x");
-  check_act(y, "y");
+  const bool f32 = check_act_or_f32(x, "x");
+  same_act(x, y, "y");
+  const int64_t e = f32 ? 4 : 2;
   TORCH_CHECK(C % 8 == 0, "hcb.gap_fwd: C % 8");
-  check_range(x, N * HW * C * 2, "x");
-  check_range(y, N * C * 2, "y");
-  hcb::launch_gap_fwd(x.data_ptr(), y.data_ptr(), (int)N, (int)HW, (int)C, cur_stream());
+  check_range(x, N * HW * C * e, "x");
+  check_range(y, N * C * e, "y");
+  hcb::launch_gap_fwd(x.data_ptr(), y.data_ptr(), (int)N, (int)HW, (int)C, cur_stream(), f32);
 }
 
 void gap_bwd(const Tensor& dy, const Tensor& dx, int64_t N, int64_t HW, int64_t C) {
-  check_act(dy, "dy");
-  check_act(dx, "dx");
-  check_range(dy, N * C * 2, "dy");
-  check_range(dx, N * HW * C * 2, "dx");
-  hcb::launch_gap_bwd(dy.data_ptr(), dx.data_ptr(), (int)N, (int)HW, (int)C, cur_stream());
+  const bool f32 = check_act_or_f32(dy, "dy");
+  same_act(dy, dx, "dx");
+  const int64_t e = f32 ? 4 : 2;
+  check_range(dy, N * C * e, "dy");
+  check_range(dx, N * HW * C * e, "dx");
+  hcb::launch_gap_bwd(dy.data_ptr(), dx.data_ptr(), (int)N, (int)HW, (int)C, cur_stream(), f32);
 }
 
 void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_t ncls,
@@ -475,14 +516,14 @@ void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_
   check_f32(logits, "logits");
   check_cuda(labels, "labels");
   TORCH_CHECK(labels.scalar_type() == at::kLong, "hcb.softmax_xent: labels int64");
-  check_act(dlogits, "dlogits");
+  const bool f32 = check_act_or_f32(dlogits, "dlogits");
   int64_t B = labels.numel();
   check_range(logits, B * ld * 4, "logits");
-  check_range(dlogits, B * lddl * 2, "dlogits");
+  check_range(dlogits, B * lddl * (f32 ? 4 : 2), "dlogits");
   TORCH_CHECK(row_loss.numel() >= B, "hcb.softmax_xent: row_loss");
   hcb::launch_softmax_xent(logits.data_ptr<float>(), (int)ld, labels.data_ptr<int64_t>(), (int)B, (int)ncls,
                            row_loss.data_ptr<float>(), dlogits.data_ptr(), (int)lddl, (float)scale,
-                           scale_dev.has_value() ? scale_dev->data_ptr<float>() : nullptr, cur_stream());
+                           scale_dev.has_value() ? scale_dev->data_ptr<float>() : nullptr, cur_stream(), f32);
 }
 
 void nonfinite(const Tensor& g, const Tensor& flag) {
@@ -528,7 +569,7 @@ void sgd_momentum(const Tensor& w, const Tensor& mom, const Tensor& g, int64_t n
                            nesterov ? 1 : 0, (int)hyper.numel(), cur_stream());
 }
 
-void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, int64_t max_work) {
+void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, int64_t max_work, int64_t lo) {
   check_f32(master, "master");
   check_act(pack, "pack");
   check_cuda(table, "table");
@@ -536,7 +577,7 @@ void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, 
   TORCH_CHECK(table.is_contiguous(), "hcb.weight_pack: table contiguous");
   hcb::launch_weight_pack(master.data_ptr<float>(), (uint16_t*)pack.data_ptr(),
                           reinterpret_cast<const hcb::WPackEntry*>(table.data_ptr<int64_t>()),
-                          (int)table.size(0), max_work, cur_stream());
+                          (int)table.size(0), max_work, cur_stream(), (int)lo);
 }
 
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {
@@ -564,18 +605,19 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                   const c10::optional<Tensor>& res_beta, const c10::optional<Tensor>& res_saved_mean,
                   const c10::optional<Tensor>& res_saved_invstd, const c10::optional<Tensor>& res_rm,
                   const c10::optional<Tensor>& res_rv, const c10::optional<Tensor>& res_shift) {
-  check_act(x, "x");
-  check_act(y, "y");
+  const bool f32 = check_act_or_f32(x, "x");
+  same_act(x, y, "y");
+  const int64_t e = f32 ? 4 : 2;
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldy % 8 == 0 && R >= 1, "hcb.bn_apply_acc: C/ld/R");
   TORCH_CHECK(acc.numel() >= R * 2 * C && saved_mean.numel() >= C && saved_invstd.numel() >= C, "hcb.bn_apply_acc: sizes");
-  check_range(x, ((M - 1) * ldx + C) * 2, "x");
-  check_range(y, ((M - 1) * ldy + C) * 2, "y");
+  check_range(x, ((M - 1) * ldx + C) * e, "x");
+  check_range(y, ((M - 1) * ldy + C) * e, "y");
   const void* rp = nullptr;
   if (res.has_value()) {
-    check_act(*res, "res");
+    same_act(x, *res, "res");
     TORCH_CHECK(ldr % 8 == 0, "hcb.bn_apply_acc: ldr");
-    check_range(*res, ((M - 1) * ldr + C) * 2, "res");
+    check_range(*res, ((M - 1) * ldr + C) * e, "res");
     rp = res->data_ptr();
   }
   // residual BN (projection shortcut): the residual is that BN's raw input z_sc
@@ -598,35 +640,37 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                            beta.data_ptr<float>(), (int)relu, saved_mean.data_ptr<float>(),
                            saved_invstd.data_ptr<float>(), rm.has_value() ? rm->data_ptr<float>() : nullptr,
                            rv.has_value() ? rv->data_ptr<float>() : nullptr, opt_f32(shift, C, "shift"),
-                           res_acc.has_value() ? &rb : nullptr, cur_stream());
+                           res_acc.has_value() ? &rb : nullptr, cur_stream(), f32);
 }
 
 void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
                        const Tensor& x, int64_t ldx, int64_t M, int64_t C, const Tensor& mean, const Tensor& invstd,
                        const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& acc, int64_t R,
                        const c10::optional<Tensor>& gout, int64_t ldg) {
-  check_act(dy, "dy");
-  check_act(x, "x");
+  const bool f32 = check_act_or_f32(dy, "dy");
+  same_act(dy, x, "x");
+  const int64_t e = f32 ? 4 : 2;
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_reduce_acc: C/R");
-  check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
-  check_range(x, ((M - 1) * ldx + C) * 2, "x");
+  check_range(dy, ((M - 1) * lddy + C) * e, "dy");
+  check_range(x, ((M - 1) * ldx + C) * e, "x");
   const void* yp = nullptr;
   if (relu == 1) {
     TORCH_CHECK(y.has_value(), "hcb.bn_bwd_reduce_acc: relu=1 needs y");
-    check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    same_act(dy, *y, "y");
+    check_range(*y, ((M - 1) * ldyv + C) * e, "y");
     yp = y->data_ptr();
   }
   void* gp = nullptr;
   if (gout.has_value()) {
-    check_act(*gout, "gout");
-    check_range(*gout, ((M - 1) * ldg + C) * 2, "gout");
+    same_act(dy, *gout, "gout");
+    check_range(*gout, ((M - 1) * ldg + C) * e, "gout");
     gp = gout->data_ptr();
   }
   hcb::launch_bn_bwd_reduce_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, (int)M, (int)C,
                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
                                 beta.data_ptr<float>(), (int)relu, acc.data_ptr<float>(), (int)R, gp, (int)ldg,
-                                cur_stream());
+                                cur_stream(), f32);
 }
 
 void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
@@ -634,25 +678,27 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
                       const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
                       const Tensor& acc, int64_t R, const Tensor& dgamma, const Tensor& dbeta, int64_t relu,
                       const c10::optional<Tensor>& shift_out) {
-  check_act(dy, "dy");
-  check_act(x, "x");
-  check_act(dx, "dx");
+  const bool f32 = check_act_or_f32(dy, "dy");
+  same_act(dy, x, "x");
+  same_act(dy, dx, "dx");
+  const int64_t e = f32 ? 4 : 2;
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_apply_acc: C/R");
-  check_range(dy, ((M - 1) * lddy + C) * 2, "dy");
-  check_range(x, ((M - 1) * ldx + C) * 2, "x");
-  check_range(dx, ((M - 1) * lddx + C) * 2, "dx");
+  check_range(dy, ((M - 1) * lddy + C) * e, "dy");
+  check_range(x, ((M - 1) * ldx + C) * e, "x");
+  check_range(dx, ((M - 1) * lddx + C) * e, "dx");
   const void* yp = nullptr;
   if (relu == 1) {
     TORCH_CHECK(y.has_value(), "hcb.bn_bwd_apply_acc: relu=1 needs y");
-    check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    same_act(dy, *y, "y");
+    check_range(*y, ((M - 1) * ldyv + C) * e, "y");
     yp = y->data_ptr();
   }
   hcb::launch_bn_bwd_apply_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, dx.data_ptr(),
                                (int)lddx, (int)M, (int)C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                gamma.data_ptr<float>(), beta.data_ptr<float>(), acc.data_ptr<float>(), (int)R,
                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu,
-                               const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream());
+                               const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream(), f32);
 }
 
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
@@ -704,10 +750,10 @@ void l2norm_sq(const Tensor& x, const Tensor& out) {
 }
 
 void synth_images(const Tensor& out, int64_t C, int64_t Cpad, double mean, double std, int64_t seed) {
-  check_act(out, "out");
+  const bool f32 = check_act_or_f32(out, "out");
   TORCH_CHECK(out.numel() % Cpad == 0, "hcb.synth_images: numel % Cpad");
   hcb::launch_synth_images(out.data_ptr(), out.numel() / Cpad, (int)C, (int)Cpad, (float)mean, (float)std,
-                           (uint64_t)seed, cur_stream());
+                           (uint64_t)seed, cur_stream(), f32);
 }
 
 void synth_labels(const Tensor& out, int64_t ncls, int64_t seed) {
@@ -818,7 +864,7 @@ void set_deterministic(bool on) { hcb::set_deterministic(on); }
 
 
 HCB_TORCH_LIBRARY(hcb, m) {
-  m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
+  m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None, Tensor? w_lo=None) -> ()");
   m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
@@ -839,7 +885,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("loss_scale_update(Tensor(a!) hyper, float world, bool dynamic) -> ()");
   m.def("colsum(Tensor g, int ld, int M, int N, Tensor(a!) out) -> ()");
   m.def("sgd_momentum(Tensor(a!) w, Tensor(b!) mom, Tensor g, int n_decay, Tensor hyper, Tensor(c!)? l2, bool nesterov) -> ()");
-  m.def("weight_pack(Tensor master, Tensor(a!) pack, Tensor table, int max_work) -> ()");
+  m.def("weight_pack(Tensor master, Tensor(a!) pack, Tensor table, int max_work, int lo=0) -> ()");
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()");
   m.def("add_bf16(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");

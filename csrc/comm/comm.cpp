@@ -173,6 +173,19 @@ bool capturing(hipStream_t s) {
   return st == hipStreamCaptureStatusActive;
 }
 
+// ncclCommAbort can itself wait for work already queued on the comm stream (measured: with a
+// stalled step queued it returned only once that step had drained), so it runs on a detached
+// thread and the process exits within a bounded time either way; the launcher then stops the
+// other ranks (launch/launcher.py fail-fast)
+[[noreturn]] void abort_and_exit(Comm* c, int code) {
+  c->aborted = true;
+  ncclComm_t comm = c->comm;
+  c->comm = nullptr;
+  if (comm) std::thread([comm] { ncclCommAbort(comm); }).detach();
+  std::this_thread::sleep_for(std::chrono::seconds(2));
+  std::_Exit(code);
+}
+
 void watchdog_loop(Comm* c) {
   using hcb::comm::StallWatch;
   while (!c->stop.load()) {
@@ -196,11 +209,8 @@ void watchdog_loop(Comm* c) {
       if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
         std::fprintf(stderr, "[hcb watchdog] rank %d: RCCL async error: %s -- aborting communicator\n", c->rank,
                      ncclGetErrorString(ae));
-        c->aborted = true;
-        ncclCommAbort(c->comm);
-        c->comm = nullptr;
         std::fflush(stderr);
-        std::_Exit(18);
+        abort_and_exit(c, 18);
       }
     }
     if (act == StallWatch::kWarn) {
@@ -215,10 +225,7 @@ void watchdog_loop(Comm* c) {
       std::fprintf(stderr, "[hcb watchdog] rank %d: stalled for %.0f s > HCB_STALL_ABORT_SECONDS; aborting\n", c->rank,
                    waited);
       std::fflush(stderr);
-      c->aborted = true;
-      ncclCommAbort(c->comm);
-      c->comm = nullptr;
-      std::_Exit(19);
+      abort_and_exit(c, 19);
     }
   }
 }

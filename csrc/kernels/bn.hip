@@ -21,8 +21,8 @@ namespace hcb {
 constexpr int BN_U = 4;  // rows in flight per thread in the streaming kernels
 
 // buffer-resource byte range covering rows [0, M) of a [M][ld] bf16 tensor (clamped to 2 GiB)
-__device__ __forceinline__ uint32_t rsrc_bytes(int M, int ld) {
-  size_t b = (size_t)M * (size_t)ld * 2u;
+__device__ __forceinline__ uint32_t rsrc_bytes(int M, int ld, int esz = 2) {
+  size_t b = (size_t)M * (size_t)ld * (size_t)esz;
   return b > 0x7fffffffu ? 0x7fffffffu : (uint32_t)b;
 }
 
@@ -223,6 +223,42 @@ __device__ __forceinline__ void bwd_math(const u32x4& dv, const u32x4& xvv, cons
   if (relu == 1) {
     float yv[8];
     unpack8(yvv, yv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? d[e] : 0.f;
+  } else if (relu == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (xv[e] * sc[e] + sh[e]) > 0.f ? d[e] : 0.f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = d[e];
+  }
+}
+
+// element-type generic forms (T = the build's 16-bit type or fp32) used by the finalize-free kernels
+template <typename T>
+struct BwdSrcT {
+  __amdgpu_buffer_rsrc_t dyr, xr, yr;
+  int lddy, ldx, ldyv, cv;
+  __device__ __forceinline__ void load(int m, int M, int relu, Act8<T>& d, Act8<T>& x, Act8<T>& y) const {
+    const bool ok = m < M;
+    constexpr uint32_t E = Act8<T>::ESZ;
+    d.load(dyr, ok ? (uint32_t)((size_t)m * lddy + cv * 8) * E : HCB_OOB);
+    x.load(xr, ok ? (uint32_t)((size_t)m * ldx + cv * 8) * E : HCB_OOB);
+    if (relu == 1) y.load(yr, ok ? (uint32_t)((size_t)m * ldyv + cv * 8) * E : HCB_OOB);
+  }
+};
+template <typename T>
+__device__ __forceinline__ void bwd_math_t(const Act8<T>& dv, const Act8<T>& xvv, const Act8<T>& yvv, int relu,
+                                           const float* mu, const float* is, const float* sc, const float* sh,
+                                           float* g, float* xh) {
+  float d[8], xv[8];
+  dv.to_f(d);
+  xvv.to_f(xv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xh[e] = (xv[e] - mu[e]) * is[e];
+  if (relu == 1) {
+    float yv[8];
+    yvv.to_f(yv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? d[e] : 0.f;
   } else if (relu == 2) {
@@ -549,9 +585,9 @@ __device__ __forceinline__ void reduce_group_replicas(const float* acc, int R, i
 
 // RBN: the residual operand is a projection shortcut's raw conv output normalised here (ResBN);
 // its own instantiation, so the common kernel keeps its register budget
-template <bool RBN>
+template <bool RBN, typename T = uint16_t>
 __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
-    const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ y, int ldy, const uint16_t* __restrict__ res,
+    const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, const T* __restrict__ res,
     int ldr, int M, int C, int CVB, const float* __restrict__ acc, int R, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
     float* saved_invstd, float* run_mean, float* run_var, const float* shift, ResBN rb) {
@@ -560,17 +596,18 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
   const int cl = (threadIdx.x % CVB) * 8;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx));
-  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx));
+  constexpr uint32_t E = Act8<T>::ESZ;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx, E));
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx, E));
   const int stride = gridDim.x * gm.rows;
   int m0 = blockIdx.x * gm.rows + gm.r0;
-  u32x4 xv[BN_U], rv[BN_U];
+  Act8<T> xv[BN_U], rv[BN_U];
   auto load_rows = [&](int mb) {
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       int m = mb + u * stride;
-      xv[u] = buf_load16(xr, m < M ? (uint32_t)((size_t)m * ldx + gm.cv * 8) * 2u : HCB_OOB);
-      if (res != nullptr) rv[u] = buf_load16(rr, m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * 2u : HCB_OOB);
+      xv[u].load(xr, m < M ? (uint32_t)((size_t)m * ldx + gm.cv * 8) * E : HCB_OOB);
+      if (res != nullptr) rv[u].load(rr, m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * E : HCB_OOB);
     }
   };
   // First rows and the affine parameters are in flight while the statistics are reduced.
@@ -633,12 +670,12 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
     for (int u = 0; u < BN_U; ++u) {
       int m = m0 + u * stride;
       float f[8];
-      unpack8(xv[u], f);
+      xv[u].to_f(f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] = f[e] * sc[e] + sh[e];
       if (res != nullptr) {
         float r[8];
-        unpack8(rv[u], r);
+        rv[u].to_f(r);
         if constexpr (RBN) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] += r[e] * sc2[e] + sh2[e];
@@ -651,15 +688,17 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
       }
-      if (m < M) *reinterpret_cast<u32x4*>(y + (size_t)m * ldy + gm.cv * 8) = pack8(f);
+      if (m < M) Act8<T>::store(y + (size_t)m * ldy + gm.cv * 8, f);
     }
   }
 }
 
+template <typename T = uint16_t>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
-    const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
-    const uint16_t* __restrict__ x, int ldx, int M, int C, int CVB, const float* mean, const float* invstd,
-    const float* gamma, const float* beta, int relu, float* acc, int R, uint16_t* gout, int ldg) {
+    const T* __restrict__ dy, int lddy, const T* __restrict__ y, int ldyv,
+    const T* __restrict__ x, int ldx, int M, int C, int CVB, const float* mean, const float* invstd,
+    const float* gamma, const float* beta, int relu, float* acc, int R, T* gout, int ldg) {
+  constexpr uint32_t E = Act8<T>::ESZ;
   extern __shared__ __attribute__((aligned(16))) float lds_f[];  // [2][rows][CB]
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
@@ -674,24 +713,25 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
       sc[e] = gamma[c] * is[e];
       sh[e] = beta[c] - mu[e] * sc[e];
     }
-    BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
-               make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, gm.cv};
+    BwdSrcT<T> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                   make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx, E)), lddy, ldx, ldyv,
+                   gm.cv};
     const int stride = gridDim.x * gm.rows;
     for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
-      u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
+      Act8<T> dv[BN_U], xv[BN_U], yv[BN_U];
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
         const int m = m0 + u * stride;
         float g[8], xh[8];
-        bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+        bwd_math_t<T>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {  // rows beyond M load zeros: g = 0 contributes nothing
           s1[e] += g[e];
           s2[e] += g[e] * xh[e];
         }
-        if (gout != nullptr && m < M) *reinterpret_cast<u32x4*>(gout + (size_t)m * ldg + gm.cv * 8) = pack8(g);
+        if (gout != nullptr && m < M) Act8<T>::store(gout + (size_t)m * ldg + gm.cv * 8, g);
       }
     }
   }
@@ -717,19 +757,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
   }
 }
 
+template <typename T = uint16_t>
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
-    const uint16_t* __restrict__ dy, int lddy, const uint16_t* __restrict__ y, int ldyv,
-    const uint16_t* __restrict__ x, int ldx, uint16_t* __restrict__ dx, int lddx, int M, int C, int CVB,
+    const T* __restrict__ dy, int lddy, const T* __restrict__ y, int ldyv,
+    const T* __restrict__ x, int ldx, T* __restrict__ dx, int lddx, int M, int C, int CVB,
     const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
     int R, float* dgamma, float* dbeta, int relu, float* shift_out) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]: dbeta, dgamma
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
-  BwdSrc src{make_rsrc(dy, rsrc_bytes(M, lddy)), make_rsrc(x, rsrc_bytes(M, ldx)),
-             make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx)), lddy, ldx, ldyv, gm.cv};
+  constexpr uint32_t E = Act8<T>::ESZ;
+  BwdSrcT<T> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                 make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx, E)), lddy, ldx, ldyv, gm.cv};
   const int stride = gridDim.x * gm.rows;
   const int mfirst = blockIdx.x * gm.rows + gm.r0;
-  u32x4 dv[BN_U], xv[BN_U], yv[BN_U];
+  Act8<T> dv[BN_U], xv[BN_U], yv[BN_U];
   float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
   // First rows and the per-channel parameters are in flight while dgamma/dbeta are reduced.
   if (active) {
@@ -773,10 +815,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     for (int u = 0; u < BN_U; ++u) {
       const int m = m0 + u * stride;
       float g[8], xh[8], o[8];
-      bwd_math(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+      bwd_math_t<T>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
-      if (m < M) *reinterpret_cast<u32x4*>(dx + (size_t)m * lddx + gm.cv * 8) = pack8(o);
+      if (m < M) Act8<T>::store(dx + (size_t)m * lddx + gm.cv * 8, o);
     }
   }
 }
@@ -788,9 +830,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
 // recomputes the ReLU mask from z (mode 2), so nothing else needs the full-size activation.
 // K3: the 3x3 window unrolled, its 9 loads in flight together (buffer loads, out-of-image taps
 // excluded by a select) instead of one dependent loop trip per tap.
-template <bool K3>
+template <bool K3, typename T = uint16_t>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
-    const uint16_t* __restrict__ z, int H, int W, int C, int CVB, uint16_t* __restrict__ y, int P, int Q, int ldy,
+    const T* __restrict__ z, int H, int W, int C, int CVB, T* __restrict__ y, int P, int Q, int ldy,
     uint8_t* __restrict__ amax, int kh, int kw, int sh, int sw, int ph, int pw, int Nimg, int M,
     const float* __restrict__ acc, int R, float eps, float momentum, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
@@ -840,21 +882,22 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
       arg[e] = 255;
     }
     if constexpr (K3) {
-      const __amdgpu_buffer_rsrc_t zr = make_rsrc(z, (uint32_t)M * (uint32_t)C * 2u);
+      constexpr uint32_t E = Act8<T>::ESZ;
+      const __amdgpu_buffer_rsrc_t zr = make_rsrc(z, (uint32_t)M * (uint32_t)C * E);
       const int base = ((n * H + h0) * W + w0) * C + gm.cv * 8;  // element offset of tap (0, 0)
-      u32x4 v[9];
+      Act8<T> v[9];
       bool okt[9];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
           okt[r * 3 + t] = (unsigned)(h0 + r) < (unsigned)H && (unsigned)(w0 + t) < (unsigned)W;
-          v[r * 3 + t] = buf_load16(zr, okt[r * 3 + t] ? (uint32_t)(base + (r * W + t) * C) * 2u : HCB_OOB);
+          v[r * 3 + t].load(zr, okt[r * 3 + t] ? (uint32_t)(base + (r * W + t) * C) * E : HCB_OOB);
         }
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
         float f[8];
-        unpack8(v[k], f);
+        v[k].to_f(f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float val = okt[k] ? fmaxf(f[e] * sc[e] + sft[e], 0.f) : -INFINITY;
@@ -872,7 +915,9 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
         const int w = w0 + s;
         if ((unsigned)w >= (unsigned)W) continue;
         float f[8];
-        unpack8(*reinterpret_cast<const u32x4*>(z + ((size_t)(n * H + h) * W + w) * C + gm.cv * 8), f);
+        Act8<T> zv;
+        zv.load(z + ((size_t)(n * H + h) * W + w) * C + gm.cv * 8);
+        zv.to_f(f);
         const int pos = r * kw + s;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -884,7 +929,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
         }
       }
     }
-    *reinterpret_cast<u32x4*>(y + (size_t)op * ldy + gm.cv * 8) = pack8(best);
+    Act8<T>::store(y + (size_t)op * ldy + gm.cv * 8, best);
     u32x2 a;
     a[0] = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
     a[1] = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
@@ -914,60 +959,85 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
   return dim3(s, groups);
 }
 
-void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
-                         const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
-                         int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         const float* shift, const ResBN* res_bn, hipStream_t st) {
+template <typename T>
+static void bn_apply_acc_t(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
+                           const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
+                           int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
+                           const float* shift, const ResBN* res_bn, hipStream_t st) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   const ResBN rb = res_bn != nullptr ? *res_bn : ResBN{};
   if (res_bn != nullptr)
-    hipLaunchKernelGGL(bn_apply_acc_kernel<true>, grid, dim3(256), (size_t)4 * cvb * 8 * 4, st, (const uint16_t*)x,
-                       ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma,
-                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, shift, rb);
+    hipLaunchKernelGGL((bn_apply_acc_kernel<true, T>), grid, dim3(256), (size_t)4 * cvb * 8 * 4, st, (const T*)x, ldx,
+                       (T*)y, ldy, (const T*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta, relu, saved_mean,
+                       saved_invstd, run_mean, run_var, shift, rb);
   else
-    hipLaunchKernelGGL(bn_apply_acc_kernel<false>, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)x,
-                       ldx, (uint16_t*)y, ldy, (const uint16_t*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma,
-                       beta, relu, saved_mean, saved_invstd, run_mean, run_var, shift, rb);
+    hipLaunchKernelGGL((bn_apply_acc_kernel<false, T>), grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const T*)x,
+                       ldx, (T*)y, ldy, (const T*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta, relu,
+                       saved_mean, saved_invstd, run_mean, run_var, shift, rb);
+}
+void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
+                         const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
+                         int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
+                         const float* shift, const ResBN* res_bn, hipStream_t st, bool f32) {
+  (f32 ? bn_apply_acc_t<float> : bn_apply_acc_t<uint16_t>)(x, ldx, y, ldy, res, ldr, M, C, acc, R, eps, momentum,
+                                                           gamma, beta, relu, saved_mean, saved_invstd, run_mean,
+                                                           run_var, shift, res_bn, st);
 }
 
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
                                 int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
                                 float momentum, const float* gamma, const float* beta, float* saved_mean,
                                 float* saved_invstd, float* run_mean, float* run_var, const float* shift,
-                                hipStream_t st) {
+                                hipStream_t st, bool f32) {
   int cvb;
   dim3 grid = bn_grid_groups(N * P * Q, C, &cvb);
-  const bool k3 = kh == 3 && kw == 3 && (long)N * H * W * C < (1l << 30);
-  hipLaunchKernelGGL(k3 ? bn_relu_maxpool_acc_kernel<true> : bn_relu_maxpool_acc_kernel<false>, grid, dim3(256),
-                     (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W, C, cvb, (uint16_t*)y, P, Q, ldy,
-                     (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps, momentum, gamma, beta,
-                     saved_mean, saved_invstd, run_mean, run_var, shift);
+  const bool k3 = kh == 3 && kw == 3 && (long)N * H * W * C * (f32 ? 2 : 1) < (1l << 30);
+  if (f32)
+    hipLaunchKernelGGL((k3 ? bn_relu_maxpool_acc_kernel<true, float> : bn_relu_maxpool_acc_kernel<false, float>), grid,
+                       dim3(256), (size_t)2 * cvb * 8 * 4, st, (const float*)z, H, W, C, cvb, (float*)y, P, Q, ldy,
+                       (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps, momentum, gamma, beta,
+                       saved_mean, saved_invstd, run_mean, run_var, shift);
+  else
+    hipLaunchKernelGGL(k3 ? bn_relu_maxpool_acc_kernel<true> : bn_relu_maxpool_acc_kernel<false>, grid, dim3(256),
+                       (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W, C, cvb, (uint16_t*)y, P, Q, ldy,
+                       (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps, momentum, gamma, beta,
+                       saved_mean, saved_invstd, run_mean, run_var, shift);
 }
 
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
-                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st) {
+                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   // every block adds into replica blockIdx.x % R; deterministic mode: at most R row blocks, so
   // each replica slot gets one add (the kernel strides over the rows with any grid)
   if (deterministic() && (int)grid.x > R) grid.x = R;
   size_t lds = (size_t)2 * (256 / cvb) * cvb * 8 * 4;
-  hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
-                     (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu,
-                     acc, R, (uint16_t*)gout, ldg);
+  if (f32)
+    hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel<float>, grid, dim3(256), lds, st, (const float*)dy, lddy,
+                       (const float*)y, ldyv, (const float*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu, acc, R,
+                       (float*)gout, ldg);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel<uint16_t>, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
+                       (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu,
+                       acc, R, (uint16_t*)gout, ldg);
 }
 
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
-                             float* shift_out, hipStream_t st) {
+                             float* shift_out, hipStream_t st, bool f32) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
-  hipLaunchKernelGGL(bn_bwd_apply_acc_kernel, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)dy,
-                     lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, (uint16_t*)dx, lddx, M, C, cvb, mean,
-                     invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out);
+  if (f32)
+    hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<float>, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const float*)dy,
+                       lddy, (const float*)y, ldyv, (const float*)x, ldx, (float*)dx, lddx, M, C, cvb, mean, invstd,
+                       gamma, beta, acc, R, dgamma, dbeta, relu, shift_out);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<uint16_t>, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st,
+                       (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, (uint16_t*)dx,
+                       lddx, M, C, cvb, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out);
 }
 
 }  // namespace hcb

@@ -75,12 +75,78 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return r;
 }
 
+// fp32 path (--compute_dtype fp32): 8 fp32 values (two 16-byte loads a, b) -> bf16 high parts
+// and bf16 rounding residuals, hi + lo = x to ~2^-16 relative (bf16x3 GEMMs: hi*hi + hi*lo +
+// lo*hi with fp32 accumulation). Always bf16, whatever the 16-bit type of the library build.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split_hilo8(const u32x4& a, const u32x4& b, u32x4& hi, u32x4& lo) {
+  float f[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[i] = __uint_as_float(a[i]);
+    f[4 + i] = __uint_as_float(b[i]);
+  }
+  bf16x8 h, l;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[i] = (__bf16)f[i];
+    l[i] = (__bf16)(f[i] - (float)h[i]);
+  }
+  hi = __builtin_bit_cast(u32x4, h);
+  lo = __builtin_bit_cast(u32x4, l);
+}
+__device__ __forceinline__ f32x4 mfma_bf16(const u32x4& a, const u32x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
+
+// A vector of 8 consecutive channels of an activation tensor whose element type T is the 16-bit
+// type of the build (uint16_t storage) or fp32 (the --compute_dtype fp32 path): one 16-byte
+// access, or two. Byte offsets are element offsets * ESZ; an HCB_OOB offset reads zeros.
+template <typename T>
+struct Act8;
+template <>
+struct Act8<uint16_t> {
+  static constexpr uint32_t ESZ = 2;
+  u32x4 v;
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t off) { v = buf_load16(r, off); }
+  __device__ __forceinline__ void load(const uint16_t* p) { v = *reinterpret_cast<const u32x4*>(p); }
+  __device__ __forceinline__ void to_f(float* f) const { unpack8(v, f); }
+  __device__ __forceinline__ static void store(uint16_t* p, const float* f) {
+    *reinterpret_cast<u32x4*>(p) = pack8(f);
+  }
+};
+template <>
+struct Act8<float> {
+  static constexpr uint32_t ESZ = 4;
+  u32x4 a, b;
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    a = buf_load16(r, off);
+    b = buf_load16(r, off + 16u);  // HCB_OOB + 16 stays out of range
+  }
+  __device__ __forceinline__ void load(const float* p) {
+    a = reinterpret_cast<const u32x4*>(p)[0];
+    b = reinterpret_cast<const u32x4*>(p)[1];
+  }
+  __device__ __forceinline__ void to_f(float* f) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[i] = __uint_as_float(a[i]);
+      f[4 + i] = __uint_as_float(b[i]);
+    }
+  }
+  __device__ __forceinline__ static void store(float* p, const float* f) {
+    reinterpret_cast<f32x4*>(p)[0] = f32x4{f[0], f[1], f[2], f[3]};
+    reinterpret_cast<f32x4*>(p)[1] = f32x4{f[4], f[5], f[6], f[7]};
+  }
+};
 
 // LDS-DMA: 16 bytes per lane from the buffer straight into LDS at (wave-uniform) lds + lane*16.
 // Kept in a __device__ helper so the host compilation pass never sees the LDS address-space

@@ -58,8 +58,8 @@ constexpr size_t glds_param_off(int BM, int BN, int WM, int NST) {
 // the CBIG path (C % 64 == 0: a 64-deep k-step never straddles a tap) the per-row work is
 // two adds, two unsigned compares and a select; invalid rows carry h0 = INT_MIN/2 so the
 // bounds test rejects them without a separate flag.
-template <int AV, bool CBIG, bool LHSDIL, int RP = 32>  // RP: rows covered per load pass (threads / 8)
-struct ALoader {
+template <int AV, bool CBIG, bool LHSDIL, int RP = 32, int ESZ = 2>  // RP: rows per load pass (threads / 8)
+struct ALoader {                                                       // ESZ: bytes per element (4: fp32 x)
   int h0[AV], w0[AV];
   int rowoff[AV];  // byte offset of (pixel of tap (0,0)) * ldx + lane chunk, may be negative
   int pix[AV];     // generic path: first pixel of the image, -1 = row beyond M
@@ -79,7 +79,7 @@ struct ALoader {
         pix[v] = n * p.H * p.W;
         h0[v] = pp * p.stride_h - p.pad_h;
         w0[v] = qq * p.stride_w - p.pad_w;
-        rowoff[v] = ((pix[v] + h0[v] * p.W + w0[v]) * p.ldx + chunk * 8) * 2;
+        rowoff[v] = ((pix[v] + h0[v] * p.W + w0[v]) * p.ldx + chunk * 8) * ESZ;
       } else {
         pix[v] = -1;
         h0[v] = -0x40000000;
@@ -100,7 +100,7 @@ struct ALoader {
   __device__ __forceinline__ void offsets(const ConvParams& p, int kt, int chunk, uint32_t (&off)[AV]) {
     if constexpr (CBIG && !LHSDIL) {
       const int dh = tr * p.dil_h, dw = ts * p.dil_w;
-      const int uoff = ((dh * p.W + dw) * p.ldx + tc) * 2;
+      const int uoff = ((dh * p.W + dw) * p.ldx + tc) * ESZ;
       const bool tap_ok = tr < p.R;
 #pragma unroll
       for (int v = 0; v < AV; ++v) {
@@ -141,7 +141,7 @@ struct ALoader {
           w /= p.idil_w;
         }
         ok = ok && h < p.H && w < p.W;
-        off[v] = ok ? (uint32_t)((pix[v] + h * p.W + w) * p.ldx + c) * 2u : HCB_OOB;
+        off[v] = ok ? (uint32_t)((pix[v] + h * p.W + w) * p.ldx + c) * (uint32_t)ESZ : HCB_OOB;
       }
     }
   }
@@ -175,16 +175,55 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
   }
 }
 
+// bf16x3 step of the fp32 path: the A / B tiles staged as bf16 high parts and residuals
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void mfma_tile_step3(const u32x4* Ah, const u32x4* Al, const u32x4* Bh, const u32x4* Bl,
+                                                f32x4 (&acc)[TM / 16][TN / 16], int wm, int wn, int lane) {
+  constexpr int MI = TM / 16, NI = TN / 16;
+  const int frow = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    u32x4 ah[MI], al[MI], bh[NI], bl[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * TM + i * 16 + frow, ch = ks * 4 + fq;
+      ah[i] = Ah[row * 8 + (ch ^ ((row >> 1) & 7))];
+      al[i] = Al[row * 8 + (ch ^ ((row >> 1) & 7))];
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wn * TN + j * 16 + frow, ch = ks * 4 + fq;
+      bh[j] = Bh[row * 8 + (ch ^ ((row >> 1) & 7))];
+      bl[j] = Bl[row * 8 + (ch ^ ((row >> 1) & 7))];
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {  // small terms first
+        acc[i][j] = mfma_bf16(al[i], bh[j], acc[i][j]);
+        acc[i][j] = mfma_bf16(ah[i], bl[j], acc[i][j]);
+        acc[i][j] = mfma_bf16(ah[i], bh[j], acc[i][j]);
+      }
+  }
+}
+
 // ============================================================== register-staged main loop
-template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB>
+// F32: fp32 x and hi / lo bf16 weight packs (ConvParams::w_lo), split into bf16 hi + lo images
+// while staged, bf16x3 MFMAs (the --compute_dtype fp32 path); the epilogue writes fp32
+template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB, bool F32 = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AV = BM / 32, BV = BN / 32;  // 16-byte vectors per thread per k-step
+  constexpr int ESZ = F32 ? 4 : 2;
   static_assert(WM * WN == 4, "4 waves");
+  static_assert(!(F32 && BNB), "no fused BN-backward epilogue on the fp32 path");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  u32x4* As = reinterpret_cast<u32x4*>(smem);  // [2][BM*8] ([1][..] for a single k-step)
-  u32x4* Bs = As + (p.Kpad > 64 ? 2 : 1) * BM * 8;  // [2][BN*8]
+  const int NB = p.Kpad > 64 ? 2 : 1;  // LDS buffers (one for a single k-step)
+  u32x4* As = reinterpret_cast<u32x4*>(smem);  // [NB][BM*8]
+  u32x4* Bs = As + NB * BM * 8;                 // [NB][BN*8]
+  u32x4* Asl = Bs + NB * BN * 8;                // fp32 path: the residual (lo) images
+  u32x4* Bsl = Asl + NB * BM * 8;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -196,7 +235,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
-  ALoader<AV, CBIG, LHSDIL> al;
+  const __amdgpu_buffer_rsrc_t wlr = make_rsrc(F32 ? p.w_lo : p.w, p.w_bytes);
+  ALoader<AV, CBIG, LHSDIL, 32, ESZ> al;
   al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
 #pragma unroll
@@ -205,7 +245,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
   }
 
-  u32x4 ra[AV], rb[BV];
+  // F32: ra / ra2 hold the two 16-byte halves of each 8-value fp32 vector, rb2 the lo weights
+  u32x4 ra[AV], rb[BV], ra2[F32 ? AV : 1], rb2[F32 ? BV : 1];
   f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -216,21 +257,35 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     uint32_t off[AV];
     al.offsets(p, kt, chunk, off);
 #pragma unroll
-    for (int v = 0; v < AV; ++v) ra[v] = buf_load16(xr, off[v]);
+    for (int v = 0; v < AV; ++v) {
+      ra[v] = buf_load16(xr, off[v]);
+      if constexpr (F32) ra2[v] = buf_load16(xr, off[v] + 16u);  // HCB_OOB + 16 stays out of range
+    }
 #pragma unroll
-    for (int v = 0; v < BV; ++v)
-      rb[v] = buf_load16(wr, b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
+    for (int v = 0; v < BV; ++v) {
+      const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u;
+      rb[v] = buf_load16(wr, o);
+      if constexpr (F32) rb2[v] = buf_load16(wlr, o);
+    }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
-      int row = (tid >> 3) + 32 * v;
-      As[buf * BM * 8 + row * 8 + (chunk ^ ((row >> 1) & 7))] = ra[v];
+      const int row = (tid >> 3) + 32 * v, idx = buf * BM * 8 + row * 8 + (chunk ^ ((row >> 1) & 7));
+      if constexpr (F32) {
+        u32x4 hi, lo;
+        split_hilo8(ra[v], ra2[v], hi, lo);
+        As[idx] = hi;
+        Asl[idx] = lo;
+      } else {
+        As[idx] = ra[v];
+      }
     }
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
-      int row = (tid >> 3) + 32 * v;
-      Bs[buf * BN * 8 + row * 8 + (chunk ^ ((row >> 1) & 7))] = rb[v];
+      const int row = (tid >> 3) + 32 * v, idx = buf * BN * 8 + row * 8 + (chunk ^ ((row >> 1) & 7));
+      Bs[idx] = rb[v];
+      if constexpr (F32) Bsl[idx] = rb2[v];
     }
   };
 
@@ -247,7 +302,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    mfma_tile_step<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
+    if constexpr (F32)
+      mfma_tile_step3<WM, WN, TM, TN>(As + cur * BM * 8, Asl + cur * BM * 8, Bs + cur * BN * 8, Bsl + cur * BN * 8,
+                                      acc, wm, wn, lane);
+    else
+      mfma_tile_step<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
@@ -402,8 +461,10 @@ template <int WM, int WN, int TM, int TN, bool BNB>
 static void launch_reg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
-  // a single k-step (1x1 over <= 64 channels) uses one buffer pair
-  size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16;
+  const bool f32 = p.w_lo != nullptr;
+  // a single k-step (1x1 over <= 64 channels) uses one buffer pair; the fp32 path stages a
+  // second (residual) image of both operands
+  size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16 * (f32 ? 2 : 1);
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   if (BNB) lds = reg_param_off(BM, BN, WM) + bnb_param_lds(BN);
@@ -415,7 +476,30 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, true, BNB>);
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, false, BNB>);
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>);
+    if constexpr (!BNB) {
+      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, false, false, true>);
+      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, true, false, true>);
+      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, false, false, true>);
+      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, true, false, true>);
+    }
     once = true;
+  }
+  if constexpr (!BNB) {
+    if (f32) {
+      if (cbig && !lhs)
+        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, false, false, true>), dim3(tiles), dim3(256), lds,
+                           st, p);
+      else if (cbig && lhs)
+        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, true, false, true>), dim3(tiles), dim3(256), lds,
+                           st, p);
+      else if (!cbig && !lhs)
+        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, false, false, true>), dim3(tiles), dim3(256), lds,
+                           st, p);
+      else
+        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true, false, true>), dim3(tiles), dim3(256), lds,
+                           st, p);
+      return;
+    }
   }
   if (cbig && !lhs)
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, false, BNB>), dim3(tiles), dim3(256), lds, st, p);
@@ -504,6 +588,12 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
 }
 
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
+  if (p.w_lo != nullptr) {  // fp32 path: the register-staged config of the same tile, no split-K
+    const int bm = conv_tile_m(cfg), bn = conv_tile_n(cfg);
+    const int rc = bm == 64 ? (bn == 64 ? 2 : 3) : (bn == 64 ? 1 : 0);
+    launch_cfg<false>(p, rc, st);
+    return;
+  }
   if (p.bnb_acc != nullptr)
     launch_cfg<true>(p, cfg, st);
   else

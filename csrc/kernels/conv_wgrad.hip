@@ -63,10 +63,10 @@ __device__ __forceinline__ void wgrad_store_tile(const WgradParams& p, const flo
 struct WgAdvance {  // wave-uniform per-k-step increments (bytes / input rows / input cols)
   int dqw, dqo, qs, qco, dph, dpo, ps, pco, dno;
 };
-__device__ __forceinline__ WgAdvance wg_advance(const WgradParams& p, int rows) {
+__device__ __forceinline__ WgAdvance wg_advance(const WgradParams& p, int rows, int esz = 2) {
   const int PQ = p.P * p.Q;
   const int dn = rows / PQ, rem = rows - dn * PQ, dp = rem / p.Q, dq = rem - dp * p.Q;
-  const int pix = p.ldx * 2, rowb = p.W * pix;
+  const int pix = p.ldx * esz, rowb = p.W * pix;
   WgAdvance a;
   a.dqw = dq * p.stride_w;
   a.dqo = dq * p.stride_w * pix;
@@ -101,8 +101,9 @@ struct WgSeg {
   }
 };
 
-// dY operand: rows m, columns = output channels [i0, i0 + COLS)
-template <int ROWS, int COLS, int NT>
+// dY operand: rows m, columns = output channels [i0, i0 + COLS). ESZ 4 (fp32 path): a vector of 8
+// values is two 16-byte loads, the second into d2
+template <int ROWS, int COLS, int NT, int ESZ = 2>
 struct WgALoad {
   using G = WgSeg<ROWS, COLS, NT>;
   uint32_t off[G::RPT];
@@ -115,15 +116,20 @@ struct WgALoad {
 #pragma unroll
     for (int i = 0; i < G::RPT; ++i) {
       m[i] = mbeg + tid / G::TPR + G::RSTEP * i;
-      off[i] = (uint32_t)(m[i] * p.ldy + col) * 2u;
+      off[i] = (uint32_t)(m[i] * p.ldy + col) * (uint32_t)ESZ;
     }
   }
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int mend, u32x4 (&d)[G::V]) const {
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int mend, u32x4 (&d)[G::V],
+                                       u32x4* d2 = nullptr) const {
 #pragma unroll
     for (int i = 0; i < G::RPT; ++i) {
       const uint32_t base = m[i] < mend ? off[i] : HCB_OOB;
 #pragma unroll
-      for (int s = 0; s < G::SEGV; ++s) d[i * G::SEGV + s] = buf_load16(r, colok[s] ? base + 16u * s : HCB_OOB);
+      for (int s = 0; s < G::SEGV; ++s) {
+        const uint32_t o = colok[s] ? base + 16u * ESZ / 2 * s : HCB_OOB;
+        d[i * G::SEGV + s] = buf_load16(r, o);
+        if constexpr (ESZ == 4) d2[i * G::SEGV + s] = buf_load16(r, o + 16u);
+      }
     }
   }
   __device__ __forceinline__ void advance(uint32_t step_bytes) {
@@ -137,7 +143,7 @@ struct WgALoad {
 
 // X operand (implicit im2col): rows m, columns j = (r, s, c) in [j0, j0 + COLS); the thread's
 // segment lies in one tap, so its (dh, dw, c) are constant over the k-loop
-template <int ROWS, int COLS, int NT>
+template <int ROWS, int COLS, int NT, int ESZ = 2>
 struct WgBLoad {
   using G = WgSeg<ROWS, COLS, NT>;
   int hh[G::RPT], ww[G::RPT], m[G::RPT];
@@ -159,17 +165,21 @@ struct WgBLoad {
       const int n = m[i] / PQ, rem = m[i] - n * PQ, pp = rem / p.Q, qq = rem - pp * p.Q;
       hh[i] = pp * p.stride_h + dh;
       ww[i] = qq * p.stride_w + dw;
-      off[i] = (((n * p.H + hh[i]) * p.W + ww[i]) * p.ldx + c) * 2;
+      off[i] = (((n * p.H + hh[i]) * p.W + ww[i]) * p.ldx + c) * ESZ;
     }
   }
   __device__ __forceinline__ void load(const WgradParams& p, __amdgpu_buffer_rsrc_t r, int mend,
-                                       u32x4 (&d)[G::V]) const {
+                                       u32x4 (&d)[G::V], u32x4* d2 = nullptr) const {
 #pragma unroll
     for (int i = 0; i < G::RPT; ++i) {
       const bool ok = m[i] < mend && (unsigned)hh[i] < (unsigned)p.H && (unsigned)ww[i] < (unsigned)p.W;
       const uint32_t base = ok ? (uint32_t)off[i] : HCB_OOB;
 #pragma unroll
-      for (int s = 0; s < G::SEGV; ++s) d[i * G::SEGV + s] = buf_load16(r, colok[s] ? base + 16u * s : HCB_OOB);
+      for (int s = 0; s < G::SEGV; ++s) {
+        const uint32_t o = colok[s] ? base + 16u * ESZ / 2 * s : HCB_OOB;
+        d[i * G::SEGV + s] = buf_load16(r, o);
+        if constexpr (ESZ == 4) d2[i * G::SEGV + s] = buf_load16(r, o + 16u);
+      }
     }
   }
   __device__ __forceinline__ void advance(const WgAdvance& a, int sh) {
@@ -198,7 +208,7 @@ struct WgBLoad {
 // pixel, so instead of each lane stepping all RPT of its rows (VPR lanes redundantly per row),
 // lane t of a wave steps just wave row t and the loads fetch their row's byte offset from the
 // owning lane with one ds_bpermute (__shfl) + the lane's channel offset.
-template <int ROWS, int COLS, int NT>
+template <int ROWS, int COLS, int NT, int ESZ = 2>
 struct WgBLoadShared {
   using G = WgSeg<ROWS, COLS, NT>;
   static constexpr int RW = 64 / G::TPR;   // rows per load instruction per wave
@@ -213,7 +223,7 @@ struct WgBLoadShared {
     const int lane = tid & 63, w = tid >> 6;
     const int col = j0 + (tid % G::TPR) * 8;
     colok = col < p.K;
-    lane_c = (uint32_t)((tid % G::TPR) * 16);
+    lane_c = (uint32_t)((tid % G::TPR) * 8 * ESZ);
     const int tap = j0 / p.C, c0 = j0 - tap * p.C;  // the tile's tap (uniform)
     const int r = tap / p.S, s = tap - r * p.S;
     dh = r * p.dil_h - p.pad_h;
@@ -227,16 +237,18 @@ struct WgBLoadShared {
     const int n = tm / PQ, rem = tm - n * PQ, pp = rem / p.Q, qq = rem - pp * p.Q;
     th = pp * p.stride_h + dh;
     tw = qq * p.stride_w + dw;
-    toff = (((n * p.H + th) * p.W + tw) * p.ldx + c0) * 2;
+    toff = (((n * p.H + th) * p.W + tw) * p.ldx + c0) * ESZ;
   }
   __device__ __forceinline__ void load(const WgradParams& p, __amdgpu_buffer_rsrc_t r, int mend,
-                                       u32x4 (&d)[G::V]) const {
+                                       u32x4 (&d)[G::V], u32x4* d2 = nullptr) const {
     const bool ok = tm < mend && (unsigned)th < (unsigned)p.H && (unsigned)tw < (unsigned)p.W;
     const int val = ok ? toff : (int)HCB_OOB;
 #pragma unroll
     for (int i = 0; i < G::RPT; ++i) {
       const uint32_t o = (uint32_t)__shfl(val, src[i], 64);  // OOB + lane_c stays out of range
-      d[i] = buf_load16(r, colok ? o + lane_c : HCB_OOB);
+      const uint32_t oo = colok ? o + lane_c : HCB_OOB;
+      d[i] = buf_load16(r, oo);
+      if constexpr (ESZ == 4) d2[i] = buf_load16(r, oo + 16u);
     }
   }
   __device__ __forceinline__ void advance(const WgAdvance& a, int sh) {
@@ -256,17 +268,21 @@ struct WgBLoadShared {
 };
 
 // RIS: the X loader shares rows across lanes (every column of a tile in one filter tap), else
-// per-lane rows
-template <int WM, int WN, int TM, int TN, bool RIS>
+// per-lane rows. F32: fp32 dY / X (--compute_dtype fp32), split into bf16 high parts and
+// residuals while staged to LDS, bf16x3 MFMAs (hi*hi + hi*lo + lo*hi, fp32 accumulation).
+template <int WM, int WN, int TM, int TN, bool RIS, bool F32 = false>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AVR = BM / 8, BVR = BN / 8;        // 16-byte vectors per LDS row
   constexpr int AV = BK * AVR / 256, BV = BK * BVR / 256;  // vectors per thread
+  constexpr int ESZ = F32 ? 4 : 2;
   static_assert(WM * WN == 4, "4 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* As = smem;                       // [2][BK][BM] bf16, 2*BM bytes per row
   char* Bs = smem + 2 * BK * BM * 2;     // [2][BK][BN]
+  char* Asl = Bs + 2 * BK * BN * 2;      // fp32 path: the residual (lo) images
+  char* Bsl = Asl + 2 * BK * BM * 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -296,12 +312,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   using GA = WgSeg<BK, BM, 256>;
   using GB = WgSeg<BK, BN, 256>;
   static_assert(GA::V == AV && GB::V == BV, "loader mapping");
-  WgALoad<BK, BM, 256> ald;
-  std::conditional_t<RIS, WgBLoadShared<BK, BN, 256>, WgBLoad<BK, BN, 256>> bld;
-  const uint32_t a_step = (uint32_t)(BK * p.ldy * 2);
+  WgALoad<BK, BM, 256, ESZ> ald;
+  std::conditional_t<RIS, WgBLoadShared<BK, BN, 256, ESZ>, WgBLoad<BK, BN, 256, ESZ>> bld;
+  const uint32_t a_step = (uint32_t)(BK * p.ldy * ESZ);
   ald.init(p, kt_begin * BK, i0, tid);
   bld.init(p, kt_begin * BK, j0, tid);
-  const WgAdvance adv = wg_advance(p, BK);
+  const WgAdvance adv = wg_advance(p, BK, ESZ);
 
   const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
   // lane supplies row (row + q4), columns col + 4*p4 (col a multiple of 16); rows are NSLOT*32 B
@@ -343,29 +359,78 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
           acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
   };
+  // fp32 path: hi / lo fragments of both operands (same transposed reads on the two images)
+  auto frag = [&](auto rd, const char* base, int krow, int col) -> u32x4 {
+    short4v lo = rd(base, krow, col);
+    short4v hi = rd(base, krow + 4, col);
+    short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(u32x4, t);
+  };
+  auto mfma_kstep3 = [&](const char* Ah, const char* Al, const char* Bh, const char* Bl) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 ah[MI], al[MI], bh[NI], bl[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        ah[i] = frag(tr_read_a, Ah, ks * 32 + 8 * g, wm * TM + i * 16);
+        al[i] = frag(tr_read_a, Al, ks * 32 + 8 * g, wm * TM + i * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        bh[j] = frag(tr_read_b, Bh, ks * 32 + 8 * g, wn * TN + j * 16);
+        bl[j] = frag(tr_read_b, Bl, ks * 32 + 8 * g, wn * TN + j * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          acc[i][j] = mfma_bf16(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma_bf16(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma_bf16(ah[i], bh[j], acc[i][j]);
+        }
+    }
+  };
 
   // Two register sets: the loads of k-step k+2 are issued while k-step k is multiplied and
   // k+1 is stored to LDS, so a load has two k-steps (not one) of MFMA time to land -- the
   // 64x64 tile's 8 MFMAs per wave and k-step are far shorter than an L2 round trip.
-  u32x4 sa[2][AV], sb[2][BV];
+  u32x4 sa[2][AV], sb[2][BV], sa2[2][F32 ? AV : 1], sb2[2][F32 ? BV : 1];
   // rows past this split's range come back as zeros without memory traffic, so the loads
   // and stores of the pipeline tail need no conditions (straight-line k-loop)
   const int mend = min(kt_end * BK, p.M);
   auto ld = [&](auto set_c) {
     constexpr int S = decltype(set_c)::value;
-    ald.load(dyr, mend, sa[S]);
-    bld.load(p, xr, mend, sb[S]);
+    ald.load(dyr, mend, sa[S], F32 ? sa2[S] : nullptr);
+    bld.load(p, xr, mend, sb[S], F32 ? sb2[S] : nullptr);
     ald.advance(a_step);
     bld.advance(adv, p.stride_h);
   };
   auto st = [&](auto set_c, int buf) {
     constexpr int S = decltype(set_c)::value;
 #pragma unroll
-    for (int v = 0; v < AV; ++v)
-      *reinterpret_cast<u32x4*>(As + buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV)) = sa[S][v];
+    for (int v = 0; v < AV; ++v) {
+      const int o = buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV);
+      if constexpr (F32) {
+        u32x4 hi, lo;
+        split_hilo8(sa[S][v], sa2[S][v], hi, lo);
+        *reinterpret_cast<u32x4*>(As + o) = hi;
+        *reinterpret_cast<u32x4*>(Asl + o) = lo;
+      } else {
+        *reinterpret_cast<u32x4*>(As + o) = sa[S][v];
+      }
+    }
 #pragma unroll
-    for (int v = 0; v < BV; ++v)
-      *reinterpret_cast<u32x4*>(Bs + buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV)) = sb[S][v];
+    for (int v = 0; v < BV; ++v) {
+      const int o = buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV);
+      if constexpr (F32) {
+        u32x4 hi, lo;
+        split_hilo8(sb[S][v], sb2[S][v], hi, lo);
+        *reinterpret_cast<u32x4*>(Bs + o) = hi;
+        *reinterpret_cast<u32x4*>(Bsl + o) = lo;
+      } else {
+        *reinterpret_cast<u32x4*>(Bs + o) = sb[S][v];
+      }
+    }
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -377,7 +442,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   auto kstep = [&](auto cur_c, int k) {
     constexpr int cur = decltype(cur_c)::value;
     ld(cur_c);  // k-step k + 2 into set `cur` (stored to LDS one k-step ago)
-    mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
+    if constexpr (F32)
+      mfma_kstep3(As + cur * BK * BM * 2, Asl + cur * BK * BM * 2, Bs + cur * BK * BN * 2, Bsl + cur * BK * BN * 2);
+    else
+      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
     st(std::integral_constant<int, cur ^ 1>{}, cur ^ 1);  // k-step k + 1
     __syncthreads();
   };
@@ -828,7 +896,7 @@ template <int WM, int WN, int TM, int TN>
 static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
-  size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2;
+  size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2 * (p.f32in ? 2 : 1);
   size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   dim3 grid(tiles * splits);
@@ -838,12 +906,23 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     once = true;
   }
-  if (wgrad_one_tap(p, BN))
+  const bool shared = wgrad_one_tap(p, BN);
+  if (p.f32in) {
+    if (shared)
+      hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true, true>), grid, dim3(256), lds, st, p);
+    else
+      hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false, true>), grid, dim3(256), lds, st, p);
+  } else if (shared) {
     hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true>), grid, dim3(256), lds, st, p);
-  else
+  } else {
     hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false>), grid, dim3(256), lds, st, p);
+  }
 }
 
 // cfg 0..2: register-staged {128x128, 64x128, 64x64}; 3..9: LDS-DMA ring {128x128 (4 waves of
@@ -865,6 +944,14 @@ int wgrad_tile_n(int cfg) {
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st) {
   // the register-staged loaders keep a thread's 16-byte vector inside one filter tap (every
   // weight pack already requires C % 8 == 0; bindings.cpp checks it)
+  if (p.f32in) {  // fp32 path: the register-staged kernel of the nearest tile (split-K kept)
+    const int bm = wgrad_tile_m(cfg), bn = wgrad_tile_n(cfg);
+    if (bm >= 128 && bn >= 128) wlaunch<2, 2, 64, 64>(p, splits, st);
+    else if (bm >= 128) wlaunch<2, 2, 64, 32>(p, splits, st);
+    else if (bn >= 128) wlaunch<1, 4, 64, 32>(p, splits, st);
+    else wlaunch<2, 2, 32, 32>(p, splits, st);
+    return;
+  }
   switch (cfg) {
     case 0: wlaunch<2, 2, 64, 64>(p, splits, st); break;  // 128 x 128
     case 1: wlaunch<1, 4, 64, 32>(p, splits, st); break;  // 64 x 128

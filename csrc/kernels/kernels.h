@@ -70,6 +70,12 @@ struct ConvParams {
   int splits;
   float* ws;
   unsigned* cnt;
+  // fp32 activations (the reference's precision, --compute_dtype fp32): x is fp32 NHWC and the
+  // weights come as two bf16 packs, w (high part) and w_lo (the rounding residual); the
+  // register-staged loop splits every loaded fp32 value into bf16 hi + lo while staging it to
+  // LDS and issues hi*hi + hi*lo + lo*hi MFMAs (bf16x3, ~2^-16 relative per product, fp32
+  // accumulation); output fp32 (out_f32). Register-staged tile configs only, no split-K.
+  const void* w_lo;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
 // deterministic reductions (misc.hip): colsum / BN-backward reduce grids limited so that
@@ -81,8 +87,8 @@ int conv_tile_n(int cfg);
 
 // weight-gradient implicit GEMM: dW[Nout][K] += sum_m dY[m][Nout] * im2col(X)[m][K]
 struct WgradParams {
-  const void* dy;  // [M][ldy] bf16
-  const void* x;   // NHWC bf16, pixel stride ldx
+  const void* dy;  // [M][ldy] bf16 (fp32 when f32in)
+  const void* x;   // NHWC bf16 (fp32 when f32in), pixel stride ldx
   float* dw;       // [Nout][K] fp32 (atomically accumulated)
   int N, H, W, C, ldx;
   int P, Q, R, S;
@@ -91,6 +97,7 @@ struct WgradParams {
   int ksteps_per_split;
   FastDiv fd_pq, fd_q, fd_c, fd_s;
   uint32_t dy_bytes, x_bytes;
+  int f32in;  // fp32 operands, split into bf16 hi + lo while staged (register-staged cfgs only)
 };
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st);
 int wgrad_tile_m(int cfg);
@@ -146,19 +153,21 @@ struct ResBN {
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         const float* shift, const ResBN* res_bn, hipStream_t st);
+                         const float* shift, const ResBN* res_bn, hipStream_t st, bool f32 = false);
 // BN(acc statistics) + ReLU + max pool (NHWC, C contiguous): pooled y [N,P,Q] (row stride ldy) and
 // the uint8 window argmax [N,P,Q,C]; the BN+ReLU activation itself is not materialised
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
                                 int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
                                 float momentum, const float* gamma, const float* beta, float* saved_mean,
-                                float* saved_invstd, float* run_mean, float* run_var, const float* shift, hipStream_t st);
+                                float* saved_invstd, float* run_mean, float* run_var, const float* shift, hipStream_t st,
+                                bool f32 = false);
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
-                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st);
+                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32 = false);
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
-                             const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu, float* shift_out, hipStream_t st);
+                             const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu, float* shift_out, hipStream_t st,
+                             bool f32 = false);
 
 // ---------------------------------------------------------------- pooling
 void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,
@@ -167,14 +176,14 @@ void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx
 void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int N, int H, int W,
                      int C, int ldx, int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph,
                      int pw, int is_max, int count_include_pad, int accum, const void* idx,
-                     hipStream_t st);
-void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
-void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
+                     hipStream_t st, bool f32 = false);
+void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, bool f32 = false);
+void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st, bool f32 = false);
 
 // ---------------------------------------------------------------- loss / fc helpers
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
                          float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
-                         hipStream_t st);
+                         hipStream_t st, bool f32 = false);
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st);
 
 // ---------------------------------------------------------------- optimizer / weights
@@ -192,7 +201,7 @@ struct WPackEntry {  // all int64 so the table is a plain int64 tensor [n][9]
   int64_t Nout, R, S, C, Kpad, Kpad_t;
 };
 void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
-                        int n_entries, int64_t max_work, hipStream_t st);
+                        int n_entries, int64_t max_work, hipStream_t st, int lo = 0);
 // dropout on bf16 activations (n % 8 == 0): mask = 1 bit per element packed 8 per byte
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
                         const int64_t* step, hipStream_t st);
@@ -206,7 +215,7 @@ void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st);
 
 // ---------------------------------------------------------------- data
 void launch_synth_images(void* out, int64_t n_pix, int C, int Cpad, float mean, float std,
-                         uint64_t seed, hipStream_t st);
+                         uint64_t seed, hipStream_t st, bool f32 = false);
 void launch_synth_labels(int64_t* out, int n, int ncls, uint64_t seed, hipStream_t st);
 // real data: batch of RGB uint8 crops (desc [B][4] = byte offset, h, w, flip) -> bilinear resize
 // to S x S, optional horizontal flip, x*scale[c]+bias[c], NHWC bf16 with Cpad channels

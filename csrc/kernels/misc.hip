@@ -21,10 +21,11 @@
 namespace hcb {
 
 // ------------------------------------------------------------------ softmax xent
+template <typename T = uint16_t>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits, int ld,
                                                            const int64_t* __restrict__ labels,
                                                            int ncls, float* row_loss,
-                                                           uint16_t* dl, int lddl, float scale,
+                                                           T* dl, int lddl, float scale,
                                                            const float* scale_dev) {
   __shared__ float red[8];
   if (scale_dev != nullptr) scale *= *scale_dev;  // device-resident loss scale
@@ -50,7 +51,10 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   for (int c = tid; c < lddl; c += 256) {
     float g = 0.f;
     if (c < ncls) g = (__expf(lr[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * scale;
-    dl[(size_t)row * lddl + c] = f2act(g);
+    if constexpr (sizeof(T) == 4)
+      dl[(size_t)row * lddl + c] = g;
+    else
+      dl[(size_t)row * lddl + c] = f2act(g);
   }
 }
 
@@ -166,9 +170,12 @@ __global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ x
 // (B) the flipped/transposed data-grad operand [C][tap*Nout + kk] <- W[kk][R-1-r][S-1-s][c],
 // a 64x64 LDS-tiled transpose per (tap, kk-tile, c-tile) so both the fp32 reads (along c) and
 // the bf16 writes (along kk) are coalesced. Blocks grid-stride over A chunks then B tiles.
+// lo: pack the bf16 ROUNDING RESIDUAL w - bf16(w) instead of w (the second operand of the fp32
+// path's bf16x3 GEMMs), into a buffer of the same layout
+__device__ __forceinline__ float wp_val(float v, int lo) { return lo ? v - bf2f(f2bf(v)) : v; }
 __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ master,
                                                           uint16_t* __restrict__ pack,
-                                                          const WPackEntry* __restrict__ ents) {
+                                                          const WPackEntry* __restrict__ ents, int lo) {
   __shared__ float tile[64][65];
   const WPackEntry e = ents[blockIdx.y];
   const int R = (int)e.R, S = (int)e.S, C = (int)e.C, Nout = (int)e.Nout;
@@ -187,10 +194,10 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
         const float4* s4 = reinterpret_cast<const float4*>(src + (size_t)j * K + k8 * 8);
         const float4 a = s4[0], b = s4[1];
         u32x4 v;
-        v[0] = pack2(a.x, a.y);
-        v[1] = pack2(a.z, a.w);
-        v[2] = pack2(b.x, b.y);
-        v[3] = pack2(b.z, b.w);
+        v[0] = pack2(wp_val(a.x, lo), wp_val(a.y, lo));
+        v[1] = pack2(wp_val(a.z, lo), wp_val(a.w, lo));
+        v[2] = pack2(wp_val(b.x, lo), wp_val(b.y, lo));
+        v[3] = pack2(wp_val(b.z, lo), wp_val(b.w, lo));
         *reinterpret_cast<u32x4*>(pack + e.pack_off + (size_t)j * Kpad + k8 * 8) = v;
       }
       continue;
@@ -210,10 +217,10 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
       if (kk0 + row < Nout && c0 + c4 < C)
         v = *reinterpret_cast<const float4*>(src + ((size_t)((kk0 + row) * R + (R - 1 - rr)) * S + (S - 1 - ss)) * C +
                                              c0 + c4);
-      tile[row][c4] = v.x;
-      tile[row][c4 + 1] = v.y;
-      tile[row][c4 + 2] = v.z;
-      tile[row][c4 + 3] = v.w;
+      tile[row][c4] = wp_val(v.x, lo);
+      tile[row][c4 + 1] = wp_val(v.y, lo);
+      tile[row][c4 + 2] = wp_val(v.z, lo);
+      tile[row][c4 + 3] = wp_val(v.w, lo);
     }
     __syncthreads();
     {
@@ -334,7 +341,8 @@ __device__ __forceinline__ float u01(uint64_t key) {
   return ((mix32(key) >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
-__global__ void synth_images_kernel(uint16_t* out, int64_t n_pix, int C, int Cpad, float mean,
+template <typename T = uint16_t>
+__global__ void synth_images_kernel(T* out, int64_t n_pix, int C, int Cpad, float mean,
                                     float std, uint64_t seed) {
   const int64_t total = n_pix * Cpad;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -353,7 +361,10 @@ __global__ void synth_images_kernel(uint16_t* out, int64_t n_pix, int C, int Cpa
       }
       v = mean + std * z;
     }
-    out[i] = f2act(v);
+    if constexpr (sizeof(T) == 4)
+      out[i] = v;
+    else
+      out[i] = f2act(v);
   }
 }
 
@@ -434,9 +445,13 @@ static int grid_for(int64_t n) {
 
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
                          float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
-                         hipStream_t st) {
-  hipLaunchKernelGGL(softmax_xent_kernel, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls,
-                     row_loss, (uint16_t*)dlogits, lddl, scale, scale_dev);
+                         hipStream_t st, bool f32) {
+  if (f32)
+    hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls, row_loss,
+                       (float*)dlogits, lddl, scale, scale_dev);
+  else
+    hipLaunchKernelGGL(softmax_xent_kernel<uint16_t>, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls, row_loss,
+                       (uint16_t*)dlogits, lddl, scale, scale_dev);
 }
 
 // ------------------------------------------------------------------ loss scaling
@@ -502,11 +517,11 @@ void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st) {
   hipLaunchKernelGGL(l2norm_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, out);
 }
 void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
-                        int n_entries, int64_t max_work, hipStream_t st) {
+                        int n_entries, int64_t max_work, hipStream_t st, int lo) {
   int64_t units = max_work / 2048 + 2;  // A chunks are 2048 elements, B tiles 4096
   int gx = units > 1024 ? 1024 : (int)units;
   hipLaunchKernelGGL(weight_pack_kernel, dim3(gx, n_entries), dim3(256), 0, st, master, pack,
-                     entries_dev);
+                     entries_dev, lo);
 }
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
                         const int64_t* step, hipStream_t st) {
@@ -536,9 +551,13 @@ void launch_scale_f32(float* x, int64_t n, float s, hipStream_t st) {
   hipLaunchKernelGGL(scale_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, s);
 }
 void launch_synth_images(void* out, int64_t n_pix, int C, int Cpad, float mean, float std,
-                         uint64_t seed, hipStream_t st) {
-  hipLaunchKernelGGL(synth_images_kernel, dim3(grid_for(n_pix * Cpad)), dim3(256), 0, st,
-                     (uint16_t*)out, n_pix, C, Cpad, mean, std, seed);
+                         uint64_t seed, hipStream_t st, bool f32) {
+  if (f32)
+    hipLaunchKernelGGL(synth_images_kernel<float>, dim3(grid_for(n_pix * Cpad)), dim3(256), 0, st, (float*)out, n_pix,
+                       C, Cpad, mean, std, seed);
+  else
+    hipLaunchKernelGGL(synth_images_kernel<uint16_t>, dim3(grid_for(n_pix * Cpad)), dim3(256), 0, st,
+                       (uint16_t*)out, n_pix, C, Cpad, mean, std, seed);
 }
 void launch_synth_labels(int64_t* out, int n, int ncls, uint64_t seed, hipStream_t st) {
   hipLaunchKernelGGL(synth_labels_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out, n, ncls,

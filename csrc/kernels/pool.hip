@@ -301,9 +301,9 @@ __global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const uint16_t* __r
 // (w, channel vector) pairs of one input row, y = n * H + h, so the row / image indices are
 // wave-uniform (no per-thread divisions: the earlier flat index cost four runtime-divisor
 // divides per 8-channel item) and offsets are 32-bit.
-template <int NPW>
+template <int NPW, typename T = uint16_t>
 __global__ __launch_bounds__(256) void maxpool_bwd_amax_kernel(
-    const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N, int H, int W, int C, int ldx, int P, int Q,
+    const T* __restrict__ dy, T* __restrict__ dx, int N, int H, int W, int C, int ldx, int P, int Q,
     int ldy, int kw, int sh, int sw, int ph, int pw, int accum, const uint8_t* __restrict__ amax, int cv_shift) {
   const int CV = C >> 3;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_amax_kernel(
   const int n = t / H, h = t - n * H;
   // windows p with p*sh - ph <= h, i.e. p <= (h+ph)/sh, and h < p*sh - ph + kh
   const int p_hi = (h + ph) / sh, q_hi = (w + pw) / sw;
-  u32x4 d[NPW][NPW];
+  Act8<T> d[NPW][NPW];
   u32x2 a[NPW][NPW];
   bool ok[NPW][NPW];
 #pragma unroll
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_amax_kernel(
       const int q = q_hi - j;
       ok[i][j] = pok && q >= 0 && q < Q && w - (q * sw - pw) < kw;  // kh == kw
       const uint32_t o = prow + (uint32_t)(ok[i][j] ? q : 0);
-      d[i][j] = *reinterpret_cast<const u32x4*>(dy + o * (uint32_t)ldy + cv * 8);
+      d[i][j].load(dy + o * (uint32_t)ldy + cv * 8);
       a[i][j] = *reinterpret_cast<const u32x2*>(amax + o * (uint32_t)C + cv * 8);
     }
   }
@@ -342,24 +342,26 @@ __global__ __launch_bounds__(256) void maxpool_bwd_amax_kernel(
       const int mine = (h - (p * sh - ph)) * kw + (w - (q * sw - pw));
       if (!ok[i][j]) continue;
       float f[8];
-      unpack8(d[i][j], f);
+      d[i][j].to_f(f);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if ((int)((a[i][j][e >> 2] >> (8 * (e & 3))) & 0xff) == mine) g[e] += f[e];
     }
-  uint16_t* dp = dx + ((uint32_t)t * (uint32_t)W + (uint32_t)w) * (uint32_t)ldx + cv * 8;
+  T* dp = dx + ((uint32_t)t * (uint32_t)W + (uint32_t)w) * (uint32_t)ldx + cv * 8;
   if (accum) {
     float o[8];
-    unpack8(*reinterpret_cast<const u32x4*>(dp), o);
+    Act8<T> ov;
+    ov.load(dp);
+    ov.to_f(o);
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] += o[e];
   }
-  *reinterpret_cast<u32x4*>(dp) = pack8(g);
+  Act8<T>::store(dp, g);
 }
 
 // global average pool [N][HW][C] -> [N][C]
-__global__ __launch_bounds__(256) void gap_fwd_kernel(const uint16_t* __restrict__ x,
-                                                      uint16_t* __restrict__ y, int N, int HW,
+template <typename T = uint16_t>
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int HW,
                                                       int C) {
   const int CV = C >> 3;
   int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -368,18 +370,20 @@ __global__ __launch_bounds__(256) void gap_fwd_kernel(const uint16_t* __restrict
   float acc[8] = {0};
   for (int i = 0; i < HW; ++i) {
     float f[8];
-    unpack8(*reinterpret_cast<const u32x4*>(x + ((size_t)n * HW + i) * C + cv * 8), f);
+    Act8<T> v;
+    v.load(x + ((size_t)n * HW + i) * C + cv * 8);
+    v.to_f(f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] += f[e];
   }
   float inv = 1.f / (float)HW;
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] *= inv;
-  *reinterpret_cast<u32x4*>(y + (size_t)n * C + cv * 8) = pack8(acc);
+  Act8<T>::store(y + (size_t)n * C + cv * 8, acc);
 }
 
-__global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict__ dy,
-                                                      uint16_t* __restrict__ dx, int N, int HW,
+template <typename T = uint16_t>
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int N, int HW,
                                                       int C) {
   const int CV = C >> 3;
   const long total = (long)N * HW * CV;
@@ -390,10 +394,12 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict
     long pix = idx / CV;
     int n = (int)(pix / HW);
     float f[8];
-    unpack8(*reinterpret_cast<const u32x4*>(dy + (size_t)n * C + cv * 8), f);
+    Act8<T> v;
+    v.load(dy + (size_t)n * C + cv * 8);
+    v.to_f(f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] *= inv;
-    *reinterpret_cast<u32x4*>(dx + (size_t)pix * C + cv * 8) = pack8(f);
+    Act8<T>::store(dx + (size_t)pix * C + cv * 8, f);
   }
 }
 
@@ -427,7 +433,7 @@ void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx
 void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int N, int H, int W,
                      int C, int ldx, int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph,
                      int pw, int is_max, int count_include_pad, int accum, const void* idx,
-                     hipStream_t st) {
+                     hipStream_t st, bool f32) {
   long total = (long)N * H * W * (C / 8);
   // argmax gather: 2-D grid (input row, w x channel vector); 32-bit offsets
   const bool amax_ok = is_max && idx != nullptr && kh == kw && sh == sw && (long)N * H <= 65535 &&
@@ -435,6 +441,16 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
   const int cvn = C / 8;
   const int cv_shift = (cvn & (cvn - 1)) == 0 ? __builtin_ctz((unsigned)cvn) : -1;
   const dim3 agrid((unsigned)((W * cvn + 255) / 256), (unsigned)(N * H));
+  if (f32) {  // fp32 path: the argmax gather only (the stem pool of the ResNets)
+    if (!amax_ok || (kh + sh - 1) / sh > 3) return;  // rejected on the host (bindings.cpp)
+    if ((kh + sh - 1) / sh <= 2)
+      hipLaunchKernelGGL((maxpool_bwd_amax_kernel<2, float>), agrid, dim3(256), 0, st, (const float*)dy, (float*)dx, N,
+                         H, W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx, cv_shift);
+    else
+      hipLaunchKernelGGL((maxpool_bwd_amax_kernel<3, float>), agrid, dim3(256), 0, st, (const float*)dy, (float*)dx, N,
+                         H, W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx, cv_shift);
+    return;
+  }
   if (amax_ok && (kh + sh - 1) / sh <= 2) {
     hipLaunchKernelGGL(maxpool_bwd_amax_kernel<2>, agrid, dim3(256), 0, st, (const uint16_t*)dy, (uint16_t*)dx, N, H,
                        W, C, ldx, P, Q, ldy, kw, sh, sw, ph, pw, accum, (const uint8_t*)idx, cv_shift);
@@ -457,16 +473,24 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
                      (const uint8_t*)idx);
 }
 
-void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
+void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, bool f32) {
   int total = N * (C / 8);
-  hipLaunchKernelGGL(gap_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, st,
-                     (const uint16_t*)x, (uint16_t*)y, N, HW, C);
+  if (f32)
+    hipLaunchKernelGGL(gap_fwd_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, (const float*)x, (float*)y,
+                       N, HW, C);
+  else
+    hipLaunchKernelGGL(gap_fwd_kernel<uint16_t>, dim3((total + 255) / 256), dim3(256), 0, st, (const uint16_t*)x,
+                       (uint16_t*)y, N, HW, C);
 }
 
-void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
+void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st, bool f32) {
   long total = (long)N * HW * (C / 8);
-  hipLaunchKernelGGL(gap_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
-                     (uint16_t*)dx, N, HW, C);
+  if (f32)
+    hipLaunchKernelGGL(gap_bwd_kernel<float>, dim3(ew_grid(total)), dim3(256), 0, st, (const float*)dy, (float*)dx, N,
+                       HW, C);
+  else
+    hipLaunchKernelGGL(gap_bwd_kernel<uint16_t>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
+                       (uint16_t*)dx, N, HW, C);
 }
 
 }  // namespace hcb

@@ -1,7 +1,8 @@
-"""Reference-precision compute modes on the GPU: --compute_dtype fp32 (and IEEE fp16 with
-HCB_F16_NATIVE=0) through the PyTorch path (MIOpen / rocBLAS) of ops/functional.py, the same
-code the CPU path runs. fp32 is the reference's precision (run-tf-sing-ucx-openmpi.sh:62-81
-passes no --use_fp16). The default fp16 mode runs the HIP kernels: test_fp16_native_gpu.py."""
+"""Reference-precision compute modes on the GPU. fp32 is the reference's precision
+(run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16): on ResNet it runs the HIP kernels
+(bf16x3 GEMMs, fp32 BN / pool; kernel checks in test_fp32_native_gpu.py), on the other models
+the PyTorch path (MIOpen / rocBLAS) of ops/functional.py -- as does IEEE fp16 with
+Fn.F16_NATIVE off (the default fp16 mode runs the HIP kernels: test_fp16_native_gpu.py)."""
 import pytest
 import torch
 
@@ -12,12 +13,12 @@ pytestmark = pytest.mark.gpu
 
 
 def test_fp32_gpu_matches_fp32_cpu_step():
-    """One fp32 training step on the GPU equals the fp32 CPU step: the loss to fp32 tolerance,
-    the gradient as a whole (direction and norm)."""
-    kw = dict(image_size=64, seed=7)
+    """One fp32 training step on the GPU (HIP kernels: bf16x3 GEMMs) equals the fp32 CPU step:
+    the loss to fp32 tolerance, the gradient as a whole (direction and norm)."""
+    kw = dict(image_size=64, seed=7, image_channels=8)
     mg = create_model("resnet50", device="cuda", compute_dtype="fp32", **kw)
     mc = create_model("resnet50", device="cpu", **kw)
-    assert not mg.native and mg.image_channels == 3
+    assert mg.native and mg.image_channels == 8
     assert torch.equal(mg.ps.master.cpu(), mc.ps.master)
     img_c, lab_c = synthetic_batch(mc, 4, seed=3)
     img_c = (img_c - 127.0) / 60.0
@@ -28,7 +29,7 @@ def test_fp32_gpu_matches_fp32_cpu_step():
     torch.cuda.synchronize()
     assert abs(lg - lc) <= 1e-4 * abs(lc), (lg, lc)
     # whole-network gradients of a random-init BN net are chaotic in the rounding order
-    # (MIOpen vs oneDNN accumulation): compared as a whole, not elementwise
+    # (bf16x3 MFMA vs oneDNN accumulation): compared as a whole, not elementwise
     gg, gc = mg.ps.grad.cpu(), mc.ps.grad
     assert (gg - gc).norm() / gc.norm() < 5e-2
     assert float(gg @ gc / (gg.norm() * gc.norm())) > 0.999
@@ -36,9 +37,12 @@ def test_fp32_gpu_matches_fp32_cpu_step():
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 def test_reference_precision_training_learns(dtype, monkeypatch):
+    """The PyTorch (MIOpen) path: ResNet-50 with the fp32 / fp16 HIP paths switched off."""
+    from azure_hc_intel_tf_amd.models.resnet import ResNet
     from azure_hc_intel_tf_amd.ops import functional as Fn
 
     monkeypatch.setattr(Fn, "F16_NATIVE", False)  # fp16 through MIOpen, not the fp16 kernel build
+    monkeypatch.setattr(ResNet, "F32_NATIVE_OK", False)  # fp32 through MIOpen, not bf16x3
     torch.manual_seed(0)
     m = create_model("resnet50", image_size=64, device="cuda", compute_dtype=dtype)
     assert not m.native
