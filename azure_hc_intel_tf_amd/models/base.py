@@ -37,7 +37,7 @@ class CNNModel:
     """
 
     name = "model"
-    # every op of the model has an fp32 HIP kernel: --compute_dtype fp32 runs natively (bf16x3
+    # every op of the model has an fp32 HIP kernel: --compute_dtype fp32 runs natively (bf16x6
     # GEMMs + fp32 BN / pool / loss); otherwise fp32 takes the PyTorch (MIOpen) path
     F32_NATIVE_OK = False
     default_image_size = 224

@@ -72,7 +72,7 @@ class Bottleneck:
 
 class ResNet(CNNModel):
     default_image_size = 224
-    F32_NATIVE_OK = True  # --compute_dtype fp32 on the HIP kernels (bf16x3 GEMMs, fp32 BN / pool)
+    F32_NATIVE_OK = True  # --compute_dtype fp32 on the HIP kernels (bf16x6 GEMMs, fp32 BN / pool)
 
     def __init__(self, depth: int = 50, version: str = "v1", **kw):
         self.depth = depth

@@ -171,9 +171,10 @@ class ParamStore:
     # ------------------------------------------------------------------ finalize
     def finalize(self, device, dtype_pack=torch.bfloat16, pack: bool = True, pack_lo: bool = False):
         """Allocate the flat buffers on ``device``; ``pack``: also the bf16 GEMM operands of the
-        HIP kernels (GPU; not in the PyTorch path); ``pack_lo``: also their bf16 rounding
-        residuals w - bf16(w), the second operand of the fp32 path's bf16x3 GEMMs (same layout,
-        registered with ops.functional.register_lo)."""
+        HIP kernels (GPU; not in the PyTorch path); ``pack_lo``: also the mid and lo terms of
+        the three-way bf16 split w = hi + mid + lo, the weight operands of the fp32 path's bf16x6
+        GEMMs (pack_buf_lo [2][pack_total], same layout; each pack's [2][n] view registered with
+        ops.functional.register_lo)."""
         order = [p for p in self.params if p.decay] + [p for p in self.params if not p.decay]
         off = 0
         self.n_decay = 0
@@ -238,7 +239,8 @@ class ParamStore:
                 assert pk.C % 8 == 0 and pk.Kpad % 64 == 0, f"pack of {pk.param.name}: C % 8, Kpad % 64"
             self.pack_buf = torch.zeros(max(poff, ALIGN), dtype=dtype_pack, device=device)
             self.pack_table = torch.tensor(rows, dtype=torch.int64, device=device)
-            self.pack_buf_lo = torch.zeros_like(self.pack_buf) if pack_lo else None
+            self.pack_buf_lo = (torch.zeros((2, self.pack_buf.numel()), dtype=dtype_pack, device=device)
+                                if pack_lo else None)
             from ..ops import functional as Fn
 
             for pk in self.packs:
@@ -246,9 +248,9 @@ class ParamStore:
                 if pk.want_tr:
                     pk.tr = self.pack_buf[pk.tr_off:pk.tr_off + pk.C * pk.Kpad_t]
                 if pack_lo:
-                    Fn.register_lo(pk.pack, self.pack_buf_lo[pk.pack_off:pk.pack_off + pk.Nout * pk.Kpad])
+                    Fn.register_lo(pk.pack, self.pack_buf_lo[:, pk.pack_off:pk.pack_off + pk.Nout * pk.Kpad])
                     if pk.want_tr:
-                        Fn.register_lo(pk.tr, self.pack_buf_lo[pk.tr_off:pk.tr_off + pk.C * pk.Kpad_t])
+                        Fn.register_lo(pk.tr, self.pack_buf_lo[:, pk.tr_off:pk.tr_off + pk.C * pk.Kpad_t])
         else:
             self.pack_buf = None
             self.pack_buf_lo = None
@@ -264,8 +266,9 @@ class ParamStore:
         from ..ops import _ext
 
         _ext.ops().weight_pack(self.master, self.pack_buf, self.pack_table, self.pack_max_work)
-        if self.pack_buf_lo is not None:  # fp32 path: the residual packs
-            _ext.ops().weight_pack(self.master, self.pack_buf_lo, self.pack_table, self.pack_max_work, 1)
+        if self.pack_buf_lo is not None:  # fp32 path: the mid and lo packs
+            _ext.ops().weight_pack(self.master, self.pack_buf_lo[0], self.pack_table, self.pack_max_work, 1)
+            _ext.ops().weight_pack(self.master, self.pack_buf_lo[1], self.pack_table, self.pack_max_work, 2)
 
     def zero_grad(self):
         self.grad.zero_()

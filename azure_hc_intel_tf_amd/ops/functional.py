@@ -69,12 +69,12 @@ F16_NATIVE = True
 
 
 # fp32 activations through the HIP kernels (--compute_dtype fp32, the reference's precision):
-# bf16x3 GEMMs (every fp32 operand split into bf16 hi + lo while staged, hi*hi + hi*lo + lo*hi
-# MFMAs with fp32 accumulation) and fp32 BN / pool / loss kernels. Set by the active model
+# bf16x6 GEMMs (every fp32 operand split into bf16 hi + mid + lo while staged, the six MFMA
+# products down to 2^-16 relative, fp32 accumulation) and fp32 BN / pool / loss kernels. Set by the active model
 # (CNNModel.activate) for the models whose whole op set has the fp32 kernels (ResNet v1 / v1.5);
 # other models keep the PyTorch path in fp32.
 _F32_NATIVE = [False]
-# data_ptr of a bf16 weight pack -> its residual pack w - bf16(w) (ParamStore, fp32 path)
+# data_ptr of a bf16 weight pack -> its [2][n] mid / lo packs (ParamStore, fp32 path)
 _LO = {}
 
 
@@ -87,7 +87,7 @@ def register_lo(pack, lo) -> None:
 
 
 def lo_pack(w):
-    """The residual (lo) bf16 pack of weight pack ``w`` (fp32 path), or None."""
+    """The [2][n] mid / lo bf16 packs of weight pack ``w`` (fp32 path), or None."""
     return None if w is None else _LO.get(w.data_ptr())
 
 
@@ -306,7 +306,7 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
         if residual is not None:  # beta-accumulate epilogue: out = conv(x) + residual (same layout)
             assert ld(residual) == ld(out) and residual.shape == out.shape
         w_lo = None
-        if x.dtype == torch.float32:  # bf16x3: register-staged tiles, no split-K
+        if x.dtype == torch.float32:  # bf16x6: register-staged tiles, no split-K
             w_lo = lo_pack(wpack)
             assert w_lo is not None and out_f32, "fp32 conv needs the residual weight pack and an fp32 output"
             geom[-1] = 1
@@ -413,18 +413,19 @@ def _phase_pack(wtr, spec: ConvSpec, Cdz: int, rs, ss):
     sub-kernel's order; refreshed from the current pack on every call."""
     C = spec.cin_pad
     K = len(rs) * len(ss) * Cdz
-    key = (wtr.data_ptr(), tuple(rs), tuple(ss))
+    lead = tuple(wtr.shape[:-1])  # () for a pack, (2,) for the fp32 path's mid / lo pair
+    key = (wtr.data_ptr(), lead, tuple(rs), tuple(ss))
     ent = _phase_packs.get(key)
     if ent is None:
         Kp = _round_up(K, 64)
         taps = [(spec.kh - 1 - r) * spec.kw + (spec.kw - 1 - s) for r in rs for s in ss]
-        ent = (torch.zeros((C, Kp), dtype=wtr.dtype, device=wtr.device),
+        ent = (torch.zeros(lead + (C, Kp), dtype=wtr.dtype, device=wtr.device),
                torch.tensor(taps, dtype=torch.int64, device=wtr.device))
         _phase_packs[key] = ent
     sub, idx = ent
-    trv = wtr.view(C, -1)[:, :spec.kh * spec.kw * Cdz].view(C, spec.kh * spec.kw, Cdz)
-    sub[:, :K].view(C, len(rs) * len(ss), Cdz).copy_(trv.index_select(1, idx))
-    return sub, K
+    trv = wtr.view(*lead, C, -1)[..., :spec.kh * spec.kw * Cdz].view(*lead, C, spec.kh * spec.kw, Cdz)
+    sub[..., :K].view(*lead, C, len(rs) * len(ss), Cdz).copy_(trv.index_select(-2, idx))
+    return (sub.view(*lead, -1) if lead else sub), K
 
 
 def dgrad_phase_problem(spec: ConvSpec, N: int, phase):

@@ -75,24 +75,30 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return r;
 }
 
-// fp32 path (--compute_dtype fp32): 8 fp32 values (two 16-byte loads a, b) -> bf16 high parts
-// and bf16 rounding residuals, hi + lo = x to ~2^-16 relative (bf16x3 GEMMs: hi*hi + hi*lo +
-// lo*hi with fp32 accumulation). Always bf16, whatever the 16-bit type of the library build.
+// fp32 path (--compute_dtype fp32): 8 fp32 values (two 16-byte loads a, b) split into three
+// bf16 terms x = hi + mid + lo (8 + 8 + 8 significant bits: the fp32 value to ~2^-24, where a
+// two-term split keeps only ~2^-17 -- measured too coarse: that per-element operand error is
+// amplified ~30x by the batch sums of BN backward). The GEMMs then issue the six products
+// hi*hi + hi*mid + mid*hi + mid*mid + hi*lo + lo*hi (bf16x6, fp32 accumulation); the dropped
+// mid*lo, lo*mid, lo*lo are ~2^-24. Always bf16, whatever the 16-bit type of the library build.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ void split_hilo8(const u32x4& a, const u32x4& b, u32x4& hi, u32x4& lo) {
+__device__ __forceinline__ void split3_8(const u32x4& a, const u32x4& b, u32x4& hi, u32x4& mid, u32x4& lo) {
   float f[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     f[i] = __uint_as_float(a[i]);
     f[4 + i] = __uint_as_float(b[i]);
   }
-  bf16x8 h, l;
+  bf16x8 h, m, l;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     h[i] = (__bf16)f[i];
-    l[i] = (__bf16)(f[i] - (float)h[i]);
+    const float r = f[i] - (float)h[i];  // exact (Sterbenz)
+    m[i] = (__bf16)r;
+    l[i] = (__bf16)(r - (float)m[i]);
   }
   hi = __builtin_bit_cast(u32x4, h);
+  mid = __builtin_bit_cast(u32x4, m);
   lo = __builtin_bit_cast(u32x4, l);
 }
 __device__ __forceinline__ f32x4 mfma_bf16(const u32x4& a, const u32x4& b, const f32x4& c) {

@@ -175,41 +175,45 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
   }
 }
 
-// bf16x3 step of the fp32 path: the A / B tiles staged as bf16 high parts and residuals
+// bf16x6 step of the fp32 path: the A / B tiles staged as three bf16 images each (hi, mid, lo
+// at IMG u32x4 apart); the six products down to 2^-16 relative, small terms first
 template <int WM, int WN, int TM, int TN>
-__device__ __forceinline__ void mfma_tile_step3(const u32x4* Ah, const u32x4* Al, const u32x4* Bh, const u32x4* Bl,
+__device__ __forceinline__ void mfma_tile_step6(const u32x4* A, const u32x4* B, int aimg, int bimg,
                                                 f32x4 (&acc)[TM / 16][TN / 16], int wm, int wn, int lane) {
   constexpr int MI = TM / 16, NI = TN / 16;
   const int frow = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    u32x4 ah[MI], al[MI], bh[NI], bl[NI];
+    u32x4 a[3][MI], b[3][NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const int row = wm * TM + i * 16 + frow, ch = ks * 4 + fq;
-      ah[i] = Ah[row * 8 + (ch ^ ((row >> 1) & 7))];
-      al[i] = Al[row * 8 + (ch ^ ((row >> 1) & 7))];
+      const int row = wm * TM + i * 16 + frow, ch = ks * 4 + fq, o = row * 8 + (ch ^ ((row >> 1) & 7));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[t][i] = A[t * aimg + o];
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int row = wn * TN + j * 16 + frow, ch = ks * 4 + fq;
-      bh[j] = Bh[row * 8 + (ch ^ ((row >> 1) & 7))];
-      bl[j] = Bl[row * 8 + (ch ^ ((row >> 1) & 7))];
+      const int row = wn * TN + j * 16 + frow, ch = ks * 4 + fq, o = row * 8 + (ch ^ ((row >> 1) & 7));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) b[t][j] = B[t * bimg + o];
     }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {  // small terms first
-        acc[i][j] = mfma_bf16(al[i], bh[j], acc[i][j]);
-        acc[i][j] = mfma_bf16(ah[i], bl[j], acc[i][j]);
-        acc[i][j] = mfma_bf16(ah[i], bh[j], acc[i][j]);
+      for (int j = 0; j < NI; ++j) {
+        acc[i][j] = mfma_bf16(a[2][i], b[0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0][i], b[2][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[1][i], b[1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[1][i], b[0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0][i], b[1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0][i], b[0][j], acc[i][j]);
       }
   }
 }
 
 // ============================================================== register-staged main loop
-// F32: fp32 x and hi / lo bf16 weight packs (ConvParams::w_lo), split into bf16 hi + lo images
-// while staged, bf16x3 MFMAs (the --compute_dtype fp32 path); the epilogue writes fp32
+// F32: fp32 x split into bf16 hi / mid / lo images while staged, the weights as three bf16 packs
+// (ConvParams::w, w_lo, w_lo2), bf16x6 MFMAs (the --compute_dtype fp32 path); fp32 epilogue
 template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB, bool F32 = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
@@ -222,8 +226,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   const int NB = p.Kpad > 64 ? 2 : 1;  // LDS buffers (one for a single k-step)
   u32x4* As = reinterpret_cast<u32x4*>(smem);  // [NB][BM*8]
   u32x4* Bs = As + NB * BM * 8;                 // [NB][BN*8]
-  u32x4* Asl = Bs + NB * BN * 8;                // fp32 path: the residual (lo) images
-  u32x4* Bsl = Asl + NB * BM * 8;
+  // fp32 path: the images are [3][NB][BM*8] (A) and [3][NB][BN*8] (B), hi first
+  u32x4* Bs3 = As + 3 * NB * BM * 8;
+  if constexpr (F32) Bs = Bs3;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -236,6 +241,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   const __amdgpu_buffer_rsrc_t wlr = make_rsrc(F32 ? p.w_lo : p.w, p.w_bytes);
+  const __amdgpu_buffer_rsrc_t wlr2 = make_rsrc(F32 ? p.w_lo2 : p.w, p.w_bytes);
   ALoader<AV, CBIG, LHSDIL, 32, ESZ> al;
   al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
@@ -245,8 +251,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
   }
 
-  // F32: ra / ra2 hold the two 16-byte halves of each 8-value fp32 vector, rb2 the lo weights
-  u32x4 ra[AV], rb[BV], ra2[F32 ? AV : 1], rb2[F32 ? BV : 1];
+  // F32: ra / ra2 hold the two 16-byte halves of each 8-value fp32 vector, rb2 / rb3 the mid
+  // and lo weights
+  u32x4 ra[AV], rb[BV], ra2[F32 ? AV : 1], rb2[F32 ? BV : 1], rb3[F32 ? BV : 1];
   f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -265,7 +272,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     for (int v = 0; v < BV; ++v) {
       const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u;
       rb[v] = buf_load16(wr, o);
-      if constexpr (F32) rb2[v] = buf_load16(wlr, o);
+      if constexpr (F32) {
+        rb2[v] = buf_load16(wlr, o);
+        rb3[v] = buf_load16(wlr2, o);
+      }
     }
   };
   auto lstore = [&](int buf) {
@@ -273,10 +283,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     for (int v = 0; v < AV; ++v) {
       const int row = (tid >> 3) + 32 * v, idx = buf * BM * 8 + row * 8 + (chunk ^ ((row >> 1) & 7));
       if constexpr (F32) {
-        u32x4 hi, lo;
-        split_hilo8(ra[v], ra2[v], hi, lo);
+        u32x4 hi, mid, lo;
+        split3_8(ra[v], ra2[v], hi, mid, lo);
         As[idx] = hi;
-        Asl[idx] = lo;
+        As[NB * BM * 8 + idx] = mid;
+        As[2 * NB * BM * 8 + idx] = lo;
       } else {
         As[idx] = ra[v];
       }
@@ -285,7 +296,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     for (int v = 0; v < BV; ++v) {
       const int row = (tid >> 3) + 32 * v, idx = buf * BN * 8 + row * 8 + (chunk ^ ((row >> 1) & 7));
       Bs[idx] = rb[v];
-      if constexpr (F32) Bsl[idx] = rb2[v];
+      if constexpr (F32) {
+        Bs[NB * BN * 8 + idx] = rb2[v];
+        Bs[2 * NB * BN * 8 + idx] = rb3[v];
+      }
     }
   };
 
@@ -303,8 +317,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
     if constexpr (F32)
-      mfma_tile_step3<WM, WN, TM, TN>(As + cur * BM * 8, Asl + cur * BM * 8, Bs + cur * BN * 8, Bsl + cur * BN * 8,
-                                      acc, wm, wn, lane);
+      mfma_tile_step6<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, NB * BM * 8, NB * BN * 8, acc, wm,
+                                      wn, lane);
     else
       mfma_tile_step<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
     if (kt + 1 < nk) lstore(cur ^ 1);
@@ -462,9 +476,10 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
   const bool f32 = p.w_lo != nullptr;
-  // a single k-step (1x1 over <= 64 channels) uses one buffer pair; the fp32 path stages a
-  // second (residual) image of both operands
-  size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16 * (f32 ? 2 : 1);
+  // a single k-step (1x1 over <= 64 channels) uses one buffer pair; the fp32 path stages three
+  // images (hi / mid / lo) of both operands -- no 128x128 tile (192 KB)
+  constexpr bool F32OK = !BNB && 2 * (BM + BN) * 128 * 3 <= 160 * 1024;
+  size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16 * (f32 ? 3 : 1);
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   if (BNB) lds = reg_param_off(BM, BN, WM) + bnb_param_lds(BN);
@@ -476,7 +491,7 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, true, BNB>);
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, false, BNB>);
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>);
-    if constexpr (!BNB) {
+    if constexpr (F32OK) {
       set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, false, false, true>);
       set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, true, false, true>);
       set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, false, false, true>);
@@ -484,7 +499,7 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     }
     once = true;
   }
-  if constexpr (!BNB) {
+  if constexpr (F32OK) {
     if (f32) {
       if (cbig && !lhs)
         hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, false, false, true>), dim3(tiles), dim3(256), lds,
@@ -588,9 +603,9 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
 }
 
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
-  if (p.w_lo != nullptr) {  // fp32 path: the register-staged config of the same tile, no split-K
+  if (p.w_lo != nullptr) {  // fp32 path: a register-staged config of <= 128x64 / 64x128, no split-K
     const int bm = conv_tile_m(cfg), bn = conv_tile_n(cfg);
-    const int rc = bm == 64 ? (bn == 64 ? 2 : 3) : (bn == 64 ? 1 : 0);
+    const int rc = bm == 64 ? (bn == 64 ? 2 : 3) : 1;
     launch_cfg<false>(p, rc, st);
     return;
   }

@@ -268,8 +268,8 @@ struct WgBLoadShared {
 };
 
 // RIS: the X loader shares rows across lanes (every column of a tile in one filter tap), else
-// per-lane rows. F32: fp32 dY / X (--compute_dtype fp32), split into bf16 high parts and
-// residuals while staged to LDS, bf16x3 MFMAs (hi*hi + hi*lo + lo*hi, fp32 accumulation).
+// per-lane rows. F32: fp32 dY / X (--compute_dtype fp32), split into bf16 hi / mid / lo while
+// staged to LDS, bf16x6 MFMAs (the six products down to 2^-16 relative, fp32 accumulation).
 template <int WM, int WN, int TM, int TN, bool RIS, bool F32 = false>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
@@ -281,8 +281,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* As = smem;                       // [2][BK][BM] bf16, 2*BM bytes per row
   char* Bs = smem + 2 * BK * BM * 2;     // [2][BK][BN]
-  char* Asl = Bs + 2 * BK * BN * 2;      // fp32 path: the residual (lo) images
+  char* Asl = Bs + 2 * BK * BN * 2;      // fp32 path: the lo and mid images
   char* Bsl = Asl + 2 * BK * BM * 2;
+  char* Asm = Bsl + 2 * BK * BN * 2;
+  char* Bsm = Asm + 2 * BK * BM * 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -366,26 +368,31 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(u32x4, t);
   };
-  auto mfma_kstep3 = [&](const char* Ah, const char* Al, const char* Bh, const char* Bl) {
+  auto mfma_kstep6 = [&](int off_a, int off_b) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      u32x4 ah[MI], al[MI], bh[NI], bl[NI];
+      u32x4 ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        ah[i] = frag(tr_read_a, Ah, ks * 32 + 8 * g, wm * TM + i * 16);
-        al[i] = frag(tr_read_a, Al, ks * 32 + 8 * g, wm * TM + i * 16);
+        ah[i] = frag(tr_read_a, As + off_a, ks * 32 + 8 * g, wm * TM + i * 16);
+        am[i] = frag(tr_read_a, Asm + off_a, ks * 32 + 8 * g, wm * TM + i * 16);
+        al[i] = frag(tr_read_a, Asl + off_a, ks * 32 + 8 * g, wm * TM + i * 16);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        bh[j] = frag(tr_read_b, Bh, ks * 32 + 8 * g, wn * TN + j * 16);
-        bl[j] = frag(tr_read_b, Bl, ks * 32 + 8 * g, wn * TN + j * 16);
+        bh[j] = frag(tr_read_b, Bs + off_b, ks * 32 + 8 * g, wn * TN + j * 16);
+        bm[j] = frag(tr_read_b, Bsm + off_b, ks * 32 + 8 * g, wn * TN + j * 16);
+        bl[j] = frag(tr_read_b, Bsl + off_b, ks * 32 + 8 * g, wn * TN + j * 16);
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
+        for (int j = 0; j < NI; ++j) {  // small terms first
           acc[i][j] = mfma_bf16(al[i], bh[j], acc[i][j]);
           acc[i][j] = mfma_bf16(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma_bf16(am[i], bm[j], acc[i][j]);
+          acc[i][j] = mfma_bf16(am[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma_bf16(ah[i], bm[j], acc[i][j]);
           acc[i][j] = mfma_bf16(ah[i], bh[j], acc[i][j]);
         }
     }
@@ -411,9 +418,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     for (int v = 0; v < AV; ++v) {
       const int o = buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV);
       if constexpr (F32) {
-        u32x4 hi, lo;
-        split_hilo8(sa[S][v], sa2[S][v], hi, lo);
+        u32x4 hi, mid, lo;
+        split3_8(sa[S][v], sa2[S][v], hi, mid, lo);
         *reinterpret_cast<u32x4*>(As + o) = hi;
+        *reinterpret_cast<u32x4*>(Asm + o) = mid;
         *reinterpret_cast<u32x4*>(Asl + o) = lo;
       } else {
         *reinterpret_cast<u32x4*>(As + o) = sa[S][v];
@@ -423,9 +431,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     for (int v = 0; v < BV; ++v) {
       const int o = buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV);
       if constexpr (F32) {
-        u32x4 hi, lo;
-        split_hilo8(sb[S][v], sb2[S][v], hi, lo);
+        u32x4 hi, mid, lo;
+        split3_8(sb[S][v], sb2[S][v], hi, mid, lo);
         *reinterpret_cast<u32x4*>(Bs + o) = hi;
+        *reinterpret_cast<u32x4*>(Bsm + o) = mid;
         *reinterpret_cast<u32x4*>(Bsl + o) = lo;
       } else {
         *reinterpret_cast<u32x4*>(Bs + o) = sb[S][v];
@@ -443,7 +452,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     constexpr int cur = decltype(cur_c)::value;
     ld(cur_c);  // k-step k + 2 into set `cur` (stored to LDS one k-step ago)
     if constexpr (F32)
-      mfma_kstep3(As + cur * BK * BM * 2, Asl + cur * BK * BM * 2, Bs + cur * BK * BN * 2, Bsl + cur * BK * BN * 2);
+      mfma_kstep6(cur * BK * BM * 2, cur * BK * BN * 2);
     else
       mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
     st(std::integral_constant<int, cur ^ 1>{}, cur ^ 1);  // k-step k + 1
@@ -896,7 +905,9 @@ template <int WM, int WN, int TM, int TN>
 static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
-  size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2 * (p.f32in ? 2 : 1);
+  // fp32: three staged images per operand (no 128x128 tile: 192 KB)
+  constexpr bool F32OK = 2 * 64 * (BM + BN) * 2 * 3 <= 160 * 1024;
+  size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2 * (p.f32in ? 3 : 1);
   size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   dim3 grid(tiles * splits);
@@ -906,19 +917,25 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if constexpr (F32OK) {
+      (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    }
     once = true;
   }
   const bool shared = wgrad_one_tap(p, BN);
-  if (p.f32in) {
-    if (shared)
-      hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true, true>), grid, dim3(256), lds, st, p);
-    else
-      hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false, true>), grid, dim3(256), lds, st, p);
-  } else if (shared) {
+  if constexpr (F32OK) {
+    if (p.f32in) {
+      if (shared)
+        hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true, true>), grid, dim3(256), lds, st, p);
+      else
+        hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false, true>), grid, dim3(256), lds, st, p);
+      return;
+    }
+  }
+  if (shared) {
     hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true>), grid, dim3(256), lds, st, p);
   } else {
     hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false>), grid, dim3(256), lds, st, p);
@@ -946,8 +963,7 @@ void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st
   // weight pack already requires C % 8 == 0; bindings.cpp checks it)
   if (p.f32in) {  // fp32 path: the register-staged kernel of the nearest tile (split-K kept)
     const int bm = wgrad_tile_m(cfg), bn = wgrad_tile_n(cfg);
-    if (bm >= 128 && bn >= 128) wlaunch<2, 2, 64, 64>(p, splits, st);
-    else if (bm >= 128) wlaunch<2, 2, 64, 32>(p, splits, st);
+    if (bm >= 128) wlaunch<2, 2, 64, 32>(p, splits, st);
     else if (bn >= 128) wlaunch<1, 4, 64, 32>(p, splits, st);
     else wlaunch<2, 2, 32, 32>(p, splits, st);
     return;

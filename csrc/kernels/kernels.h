@@ -71,11 +71,13 @@ struct ConvParams {
   float* ws;
   unsigned* cnt;
   // fp32 activations (the reference's precision, --compute_dtype fp32): x is fp32 NHWC and the
-  // weights come as two bf16 packs, w (high part) and w_lo (the rounding residual); the
-  // register-staged loop splits every loaded fp32 value into bf16 hi + lo while staging it to
-  // LDS and issues hi*hi + hi*lo + lo*hi MFMAs (bf16x3, ~2^-16 relative per product, fp32
-  // accumulation); output fp32 (out_f32). Register-staged tile configs only, no split-K.
+  // weights come as three bf16 packs, w (high part), w_lo (bf16 of the residual) and w_lo2 (bf16
+  // of what is left); the register-staged loop splits every loaded fp32 value into bf16
+  // hi + mid + lo the same way while staging it to LDS and issues the six MFMA products down to
+  // 2^-16 relative (bf16x6: ~2^-24 per product, fp32 accumulation); output fp32 (out_f32).
+  // Register-staged tile configs of <= 128x64 only, no split-K.
   const void* w_lo;
+  const void* w_lo2;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
 // deterministic reductions (misc.hip): colsum / BN-backward reduce grids limited so that

@@ -170,9 +170,14 @@ __global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ x
 // (B) the flipped/transposed data-grad operand [C][tap*Nout + kk] <- W[kk][R-1-r][S-1-s][c],
 // a 64x64 LDS-tiled transpose per (tap, kk-tile, c-tile) so both the fp32 reads (along c) and
 // the bf16 writes (along kk) are coalesced. Blocks grid-stride over A chunks then B tiles.
-// lo: pack the bf16 ROUNDING RESIDUAL w - bf16(w) instead of w (the second operand of the fp32
-// path's bf16x3 GEMMs), into a buffer of the same layout
-__device__ __forceinline__ float wp_val(float v, int lo) { return lo ? v - bf2f(f2bf(v)) : v; }
+// lo: pack the later terms of the fp32 path's three-way bf16 split w = hi + mid + lo (the bf16x6
+// GEMMs' weight operands) instead of w, into a buffer of the same layout: lo = 1 the residual
+// r = w - bf16(w) (stored as bf16: mid), lo = 2 what is left, r - bf16(r) (stored as bf16: lo)
+__device__ __forceinline__ float wp_val(float v, int lo) {
+  if (lo == 0) return v;
+  const float r = v - bf2f(f2bf(v));
+  return lo == 1 ? r : r - bf2f(f2bf(r));
+}
 __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ master,
                                                           uint16_t* __restrict__ pack,
                                                           const WPackEntry* __restrict__ ents, int lo) {

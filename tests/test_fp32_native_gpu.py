@@ -49,7 +49,7 @@ CASES = [(64, 256, 1, 1, 0, 14), (64, 64, 3, 1, 1, 14), (128, 128, 3, 2, 1, 14),
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}s{c[3]}")
 @pytest.mark.parametrize("cfg", [None, 0, 2, 12])
 def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
-    """bf16x3 (hi*hi + hi*lo + lo*hi) reproduces the fp32 convolution to ~1e-5: fwd, data grad
+    """bf16x6 reproduces the fp32 convolution to fp32 accuracy (~1e-6): fwd, data grad
     (incl. the stride-phase and strided-1x1 remap forms) and weight grad (incl. split-K); an
     LDS-DMA cfg (12) is mapped to the register-staged kernel of its tile."""
     cin, cout, k, s, pad, H = case
@@ -64,18 +64,18 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     ref = torch.nn.functional.conv2d(xd, wd, stride=s, padding=pad).permute(0, 2, 3, 1)
     y = torch.empty(N, P, Q, cout, dtype=torch.float32, device=DEV)
     Fn.conv_forward(x, spec, pk.pack, p.data, y, cfg=cfg)
-    assert rel_err(y, ref) < 1e-4
+    assert rel_err(y, ref) < 3e-6
     dz = torch.randn(N, P, Q, cout, device=DEV)
     xr = xd.clone().requires_grad_(True)
     wr = wd.clone().requires_grad_(True)
     torch.nn.functional.conv2d(xr, wr, stride=s, padding=pad).backward(dz.double().cpu().permute(0, 3, 1, 2))
     dx = torch.zeros(N, H, H, cin, dtype=torch.float32, device=DEV)
     Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, False, cfg=cfg)
-    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-4
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 3e-6
     for wcfg in ((2, 1), (0, 4), (10, 8)):
         dw = torch.zeros(cout, spec.K, device=DEV)
         Fn.conv_wgrad(dz, x, spec, dw, cfg=wcfg)
-        assert rel_err(dw.view(cout, k, k, cin), wr.grad.permute(0, 2, 3, 1)) < 1e-4, wcfg
+        assert rel_err(dw.view(cout, k, k, cin), wr.grad.permute(0, 2, 3, 1)) < 3e-6, wcfg
 
 
 @pytest.mark.parametrize("C", [64, 256, 2048])
@@ -126,7 +126,7 @@ def test_fp32_model_runs_the_hip_kernels():
     m = create_model("resnet50", image_size=64, device=DEV, compute_dtype="fp32", seed=3)
     try:
         assert m.native and m.image_channels == 8 and m.act_dtype == torch.float32
-        assert m.ps.pack_buf.dtype == torch.bfloat16 and m.ps.pack_buf_lo is not None
+        assert m.ps.pack_buf.dtype == torch.bfloat16 and m.ps.pack_buf_lo.shape[0] == 2
         img, lab = synthetic_batch(m, 8)
         assert img.dtype == torch.float32
         img = (img - 127.0) / 60.0

@@ -1,6 +1,6 @@
 """Reference-precision compute modes on the GPU. fp32 is the reference's precision
 (run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16): on ResNet it runs the HIP kernels
-(bf16x3 GEMMs, fp32 BN / pool; kernel checks in test_fp32_native_gpu.py), on the other models
+(bf16x6 GEMMs, fp32 BN / pool; kernel checks in test_fp32_native_gpu.py), on the other models
 the PyTorch path (MIOpen / rocBLAS) of ops/functional.py -- as does IEEE fp16 with
 Fn.F16_NATIVE off (the default fp16 mode runs the HIP kernels: test_fp16_native_gpu.py)."""
 import pytest
@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_fp32_gpu_matches_fp32_cpu_step():
-    """One fp32 training step on the GPU (HIP kernels: bf16x3 GEMMs) equals the fp32 CPU step:
+    """One fp32 training step on the GPU (HIP kernels: bf16x6 GEMMs) equals the fp32 CPU step:
     the loss to fp32 tolerance, the gradient as a whole (direction and norm)."""
     kw = dict(image_size=64, seed=7, image_channels=8)
     mg = create_model("resnet50", device="cuda", compute_dtype="fp32", **kw)
@@ -29,7 +29,7 @@ def test_fp32_gpu_matches_fp32_cpu_step():
     torch.cuda.synchronize()
     assert abs(lg - lc) <= 1e-4 * abs(lc), (lg, lc)
     # whole-network gradients of a random-init BN net are chaotic in the rounding order
-    # (bf16x3 MFMA vs oneDNN accumulation): compared as a whole, not elementwise
+    # (bf16x6 MFMA vs oneDNN accumulation): compared as a whole, not elementwise
     gg, gc = mg.ps.grad.cpu(), mc.ps.grad
     assert (gg - gc).norm() / gc.norm() < 5e-2
     assert float(gg @ gc / (gg.norm() * gc.norm())) > 0.999
@@ -42,7 +42,7 @@ def test_reference_precision_training_learns(dtype, monkeypatch):
     from azure_hc_intel_tf_amd.ops import functional as Fn
 
     monkeypatch.setattr(Fn, "F16_NATIVE", False)  # fp16 through MIOpen, not the fp16 kernel build
-    monkeypatch.setattr(ResNet, "F32_NATIVE_OK", False)  # fp32 through MIOpen, not bf16x3
+    monkeypatch.setattr(ResNet, "F32_NATIVE_OK", False)  # fp32 through MIOpen, not bf16x6
     torch.manual_seed(0)
     m = create_model("resnet50", image_size=64, device="cuda", compute_dtype=dtype)
     assert not m.native

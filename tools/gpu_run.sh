@@ -15,6 +15,7 @@
 #   pmc:COUNTERS     one rocprofv3 --pmc pass (counters comma-separated) over bench.py --steps 3
 #   readme           tools/gpu_readme_numbers.sh
 #   py:SCRIPT[,args] python SCRIPT args (a probe / diagnostic)
+# env: TAG (output prefix), PYTEST_X (default -x; PYTEST_X= runs every test), PYTEST_K (-k filter)
 # Outputs go to gpurun_out/${TAG}_<step>.*
 set -o pipefail
 mkdir -p gpurun_out
@@ -34,7 +35,8 @@ for step in "$@"; do
       tail -1 ${O}_smoke.log ;;
     tests)
       files=${args:-tests}
-      timeout -k 10 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest $files ${PYTEST_K:+-k "$PYTEST_K"} -m gpu ${PYTEST_X--x} -v -s \
+        --timeout 300 --timeout-method thread \
         > ${O}_tests.log 2>&1 || fail tests ${O}_tests.log
       tail -1 ${O}_tests.log ;;
     bench)
