@@ -25,6 +25,31 @@ import time
 from typing import Dict, List, Optional
 
 
+# RCCL collective tuning for the intra-node xGMI mesh (the reference's transport choice,
+# run-tf-sing-ucx-openmpi.sh:85-92 `-mca coll_hcoll_enable 1`, `UCX_TLS=rc_x,sm,self`).
+# An MI355X talks to each of its 7 peers over its own xGMI link, so a ring all-reduce is bound by
+# ONE link per hop; RCCL spreads its channels (one ring each) over the links, and every channel is
+# a workgroup that occupies a CU while backward still runs on the others. Values are only set
+# when asked for (the CLI below); a value already in the environment always wins.
+RCCL_KNOBS = {"channels": ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS"), "algo": ("NCCL_ALGO",),
+              "proto": ("NCCL_PROTO",)}
+
+
+def rccl_env(channels: Optional[int] = None, algo: Optional[str] = None, proto: Optional[str] = None,
+             base: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+    """NCCL_* variables for the requested RCCL channel count / algorithm (Ring, Tree) / protocol
+    (Simple, LL, LL128); names already set in ``base`` (default: os.environ) are left alone."""
+    base = os.environ if base is None else base
+    out = {}
+    for key, val in (("channels", channels), ("algo", algo), ("proto", proto)):
+        if val is None or val == "":
+            continue
+        for name in RCCL_KNOBS[key]:
+            if name not in base:
+                out[name] = str(val)
+    return out
+
+
 def fabric_env(fabric: str) -> Dict[str, str]:
     if fabric in ("ib", "xgmi", "", None):
         return {}
@@ -144,7 +169,8 @@ def free_port() -> int:
 
 
 def worker_env(base: Dict[str, str], rank: int, local_rank: int, world: int, nproc: int, node_rank: int,
-               master_addr: str, master_port: int, fabric: str, omp_threads: Optional[int]) -> Dict[str, str]:
+               master_addr: str, master_port: int, fabric: str, omp_threads: Optional[int],
+               rccl: Optional[Dict[str, str]] = None) -> Dict[str, str]:
     env = dict(base)
     env.update({"RANK": str(rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
                 "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": str(node_rank), "NODE_RANK": str(node_rank),
@@ -152,6 +178,7 @@ def worker_env(base: Dict[str, str], rank: int, local_rank: int, world: int, npr
                 "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     env.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")  # see azure_hc_intel_tf_amd/__init__.py
     env.update(fabric_env(fabric))
+    env.update(rccl or {})
     if omp_threads:
         env["OMP_NUM_THREADS"] = str(omp_threads)
     return env
@@ -160,15 +187,17 @@ def worker_env(base: Dict[str, str], rank: int, local_rank: int, world: int, npr
 def launch(cmd: List[str], nproc_per_node: int, nnodes: int = 1, node_rank: int = 0,
            master_addr: str = "127.0.0.1", master_port: Optional[int] = None, fabric: str = "ib",
            pin_cpus: bool = True, omp_threads: Optional[int] = None, env: Optional[Dict[str, str]] = None,
-           poll_s: float = 0.2) -> int:
+           poll_s: float = 0.2, rccl: Optional[Dict[str, str]] = None) -> int:
     world = nproc_per_node * nnodes
     port = master_port or int(os.environ.get("MASTER_PORT", 0)) or free_port()
     base = dict(os.environ if env is None else env)
+    rccl = {k: v for k, v in (rccl or {}).items() if k not in base}
     shares = cpu_shares(nproc_per_node) if pin_cpus else [None] * nproc_per_node
     procs = []
     for lr in range(nproc_per_node):
         rank = node_rank * nproc_per_node + lr
-        e = worker_env(base, rank, lr, world, nproc_per_node, node_rank, master_addr, port, fabric, omp_threads)
+        e = worker_env(base, rank, lr, world, nproc_per_node, node_rank, master_addr, port, fabric, omp_threads,
+                       rccl)
         share = shares[lr]
 
         def pre(share=share):
@@ -235,13 +264,17 @@ def main(argv=None) -> int:
     ap.add_argument("--fabric", default="ib")
     ap.add_argument("--no_pin", action="store_true")
     ap.add_argument("--omp_threads", type=int, default=None)
+    ap.add_argument("--rccl_channels", type=int, default=None, help="NCCL_MIN/MAX_NCHANNELS")
+    ap.add_argument("--rccl_algo", default=None, help="NCCL_ALGO (Ring, Tree)")
+    ap.add_argument("--rccl_proto", default=None, help="NCCL_PROTO (Simple, LL, LL128)")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
     if not cmd:
         ap.error("missing worker command")
     return launch(cmd, a.nproc_per_node, a.nnodes, a.node_rank, a.master_addr, a.master_port or None, a.fabric,
-                  pin_cpus=not a.no_pin, omp_threads=a.omp_threads)
+                  pin_cpus=not a.no_pin, omp_threads=a.omp_threads,
+                  rccl=rccl_env(a.rccl_channels, a.rccl_algo, a.rccl_proto))
 
 
 if __name__ == "__main__":

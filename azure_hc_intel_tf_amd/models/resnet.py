@@ -73,6 +73,9 @@ class Bottleneck:
 class ResNet(CNNModel):
     default_image_size = 224
     F32_NATIVE_OK = True  # --compute_dtype fp32 on the HIP kernels (bf16x6 GEMMs, fp32 BN / pool)
+    # gradient-reduction granularity of the overlapped multi-GPU step (backward_segments):
+    # "stage" (default) or "block" (per block in stages 3-4, stage 1 split from the stem)
+    segments = "stage"
 
     def __init__(self, depth: int = 50, version: str = "v1", **kw):
         self.depth = depth
@@ -124,14 +127,21 @@ class ResNet(CNNModel):
 
     def backward_segments(self, dlogits):
         """One segment per stage, last stage first (its ~60 % of the parameters are reduced
-        while stages 3..1 are still in backward)."""
+        while stages 3..1 are still in backward). segments == "block": every block of stages
+        3-4 is its own segment (ResNet-50: stage 4's 15 M parameters go out in three ~20 MB
+        pieces, the first while blocks 2..1 still run), and stage 1 is cut from the stem so
+        only the stem's 9.4 k parameters are reduced after the last backward kernel."""
+        fine = self.segments == "block"
         dfeat = self.fc.backward(dlogits)
         dx = self.gap.backward(dfeat)
         seg = [self.fc, self.gap]
         for i in range(len(self.blocks) - 1, -1, -1):
             dx = self.blocks[i].backward(dx, self.blocks[i - 1].c3 if i > 0 else None)
             seg += self.blocks[i].layers()
-            if i > 0 and self.blocks[i].stage != self.blocks[i - 1].stage:
+            cut = i > 0 and self.blocks[i].stage != self.blocks[i - 1].stage
+            if fine and (self.blocks[i].stage >= 2 or i == 0):
+                cut = True
+            if cut:
                 yield seg, False
                 seg = []
         dx = self.pool.backward(dx)

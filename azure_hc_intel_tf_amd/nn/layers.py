@@ -601,6 +601,7 @@ class Logits(Layer):
         kt = (self.ld + 63) // 64 * 64
         self.pack = ps.add_pack(self.w, ncls, 1, 1, in_features, self.spec.Kpad, kt, want_tr=True)
         self._x = None
+        self.dl32 = None  # fp32 copy of 16-bit dlogits (Trainer): the bias gradient's source
 
     def forward(self, x):
         B = x.shape[0]
@@ -620,7 +621,10 @@ class Logits(Layer):
         """dlogits: [B, ld] (bf16 on GPU, zero in the padding columns)."""
         x = self._x
         B = x.shape[0]
-        Fn.colsum(dlogits, B, self.ncls, self.b.grad)
+        if self.dl32 is not None and Fn.native(x) and dlogits.dtype != torch.float32:
+            Fn._ext.ops().colsum(self.dl32, self.ld, B, self.ncls, self.b.grad)
+        else:
+            Fn.colsum(dlogits, B, self.ncls, self.b.grad)
         if Fn.native(x):
             hcb = Fn._ext.ops()
             geom = [B, 1, 1, self.cin, self.cin, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, self.ncls, self.ld]

@@ -793,12 +793,16 @@ def gap_backward(dy, dx):
 
 
 # ------------------------------------------------------------------------- loss
-def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None):
+def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None, dl32=None):
     """Per-row cross entropy (into row_loss) and dlogits = (softmax - onehot) * scale
-    (* scale_dev[0], a device-resident loss scale, when given)."""
+    (* scale_dev[0], a device-resident loss scale, when given); ``dl32``: with 16-bit dlogits,
+    also the unrounded fp32 values (same layout), from which the classifier's bias gradient is
+    summed (its batch sum cancels to ~1% of the terms: bf16 rounding of each term would cost
+    ~5x the error of the fp32-loss reference, tools/bf16_floor.py)."""
     B = labels.numel()
     if native(dlogits):
-        _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale, scale_dev)
+        _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale, scale_dev,
+                                dl32)
         return
     if scale_dev is not None:
         scale = scale * float(scale_dev.reshape(-1)[0])

@@ -35,6 +35,7 @@ from typing import Callable, Optional
 
 import torch
 
+from .nn.layers import Logits
 from .ops import functional as Fn
 from .ops import _ext
 from .utils.tracing import range_
@@ -112,6 +113,14 @@ class Trainer:
         self.hyper = torch.tensor(h, dtype=torch.float32, device=self.dev)
         self.row_loss = torch.zeros(batch_size, dtype=torch.float32, device=self.dev)
         self.dlogits = torch.zeros((batch_size, ld), dtype=model.act_dtype, device=self.dev)
+        # 16-bit dlogits on the HIP path: the loss kernel also writes them unrounded, the
+        # classifier's bias gradient source (nn/layers.py Logits.backward)
+        self.dlogits32 = None
+        fc = getattr(model, "fc", None)
+        if (self.dev.type == "cuda" and getattr(model, "native", False) and model.act_dtype != torch.float32
+                and isinstance(fc, Logits)):
+            self.dlogits32 = torch.zeros((batch_size, ld), dtype=torch.float32, device=self.dev)
+            fc.dl32 = self.dlogits32
         self.l2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.steps_done = 0
@@ -142,7 +151,7 @@ class Trainer:
             logits = self.model.forward(images)
         self.logits = logits
         Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B,
-                        self.hyper[5:6] if self.loss_scaling else None)
+                        self.hyper[5:6] if self.loss_scaling else None, self.dlogits32)
 
     def _forward_backward(self, images, labels):
         self._forward(images, labels)

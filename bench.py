@@ -56,7 +56,19 @@ def parse_args(argv=None):
                          "loss scaling; with --compute_dtype bf16: the HIP kernels plus loss scaling")
     ap.add_argument("--compute_dtype", default=None, choices=[None, "bf16", "fp16", "fp32"],
                     help="activation / GEMM precision (default bf16; fp32 = the reference's precision)")
+    ap.add_argument("--backward_segments", default="stage", choices=["stage", "block"],
+                    help="gradient-reduction granularity of the overlapped multi-GPU step (ResNet): one segment "
+                         "per stage, or per block in stages 3-4 with stage 1 split from the stem")
+    ap.add_argument("--rccl_channels", type=int, default=None, help="NCCL_MIN/MAX_NCHANNELS for the workers")
+    ap.add_argument("--rccl_algo", default=None, help="NCCL_ALGO for the workers (Ring, Tree)")
+    ap.add_argument("--rccl_proto", default=None, help="NCCL_PROTO for the workers (Simple, LL, LL128)")
     return ap.parse_args(argv)
+
+
+def _rccl(args):
+    from azure_hc_intel_tf_amd.launch.launcher import rccl_env
+
+    return rccl_env(args.rccl_channels, args.rccl_algo, args.rccl_proto)
 
 
 def spawn_workers(args, argv) -> int:
@@ -77,7 +89,7 @@ def spawn_workers(args, argv) -> int:
     env = dict(os.environ)
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     env["HCB_BENCH_SPAWNED"] = "1"
-    return launch(cmd, nproc_per_node=args.gpus, master_addr="127.0.0.1", env=env)
+    return launch(cmd, nproc_per_node=args.gpus, master_addr="127.0.0.1", env=env, rccl=_rccl(args))
 
 
 def main(argv=None):
@@ -129,6 +141,7 @@ def main(argv=None):
     backend = None
     rccl_nranks = None
     if world > 1:
+        os.environ.update(_rccl(args))  # before the communicators exist (torchrun-launched workers)
         backend = os.environ.get("HCB_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -169,6 +182,8 @@ def main(argv=None):
         reducer = NativeReducer(compression=args.compression, force=True)
         rccl_nranks = reducer.comm.size()
     model = create_model(args.model, device=dev, compute_dtype=dtype)
+    if hasattr(model, "segments"):
+        model.segments = args.backward_segments
     B = args.batch_size
     from azure_hc_intel_tf_amd.ops import autotune
 

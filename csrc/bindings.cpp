@@ -517,7 +517,7 @@ void gap_bwd(const Tensor& dy, const Tensor& dx, int64_t N, int64_t HW, int64_t 
 
 void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_t ncls,
                   const Tensor& row_loss, const Tensor& dlogits, int64_t lddl, double scale,
-                  const c10::optional<Tensor>& scale_dev) {
+                  const c10::optional<Tensor>& scale_dev, const c10::optional<Tensor>& dl32) {
   check_f32(logits, "logits");
   check_cuda(labels, "labels");
   TORCH_CHECK(labels.scalar_type() == at::kLong, "hcb.softmax_xent: labels int64");
@@ -526,9 +526,16 @@ void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_
   check_range(logits, B * ld * 4, "logits");
   check_range(dlogits, B * lddl * (f32 ? 4 : 2), "dlogits");
   TORCH_CHECK(row_loss.numel() >= B, "hcb.softmax_xent: row_loss");
+  float* d32 = nullptr;
+  if (dl32.has_value()) {  // 16-bit dlogits: also the unrounded fp32 values (the bias gradient's source)
+    TORCH_CHECK(!f32, "hcb.softmax_xent: dl32 only with 16-bit dlogits");
+    check_f32(*dl32, "dl32");
+    check_range(*dl32, B * lddl * 4, "dl32");
+    d32 = dl32->data_ptr<float>();
+  }
   hcb::launch_softmax_xent(logits.data_ptr<float>(), (int)ld, labels.data_ptr<int64_t>(), (int)B, (int)ncls,
                            row_loss.data_ptr<float>(), dlogits.data_ptr(), (int)lddl, (float)scale,
-                           scale_dev.has_value() ? scale_dev->data_ptr<float>() : nullptr, cur_stream(), f32);
+                           scale_dev.has_value() ? scale_dev->data_ptr<float>() : nullptr, cur_stream(), f32, d32);
 }
 
 void nonfinite(const Tensor& g, const Tensor& flag) {
@@ -885,7 +892,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("pool_bwd(Tensor dy, Tensor x, Tensor y, Tensor? idx, Tensor(a!) dx, int[] geom, bool accumulate) -> ()");
   m.def("gap_fwd(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx, int N, int HW, int C) -> ()");
-  m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale, Tensor? scale_dev=None) -> ()");
+  m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale, Tensor? scale_dev=None, Tensor(c!)? dl32=None) -> ()");
   m.def("nonfinite(Tensor g, Tensor(a!) flag) -> ()");
   m.def("loss_scale_update(Tensor(a!) hyper, float world, bool dynamic) -> ()");
   m.def("colsum(Tensor g, int ld, int M, int N, Tensor(a!) out) -> ()");

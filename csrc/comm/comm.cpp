@@ -49,6 +49,7 @@
 #include <vector>
 
 #include "comm/engine.h"
+#include "comm/host.h"
 #include "kernels/kernels.h"
 
 using at::Tensor;
@@ -85,13 +86,6 @@ ncclDataType_t nccl_type(const Tensor& t) {
   }
 }
 
-struct TimelineRec {
-  std::string name;
-  int bucket;
-  int64_t bytes;
-  hipEvent_t b, e;
-};
-
 struct Comm {
   // process exit without destroy() (static destruction of g_comms): stop and join the
   // watchdog thread -- a joinable std::thread would std::terminate -- and touch nothing else
@@ -108,12 +102,11 @@ struct Comm {
   // compression scratch (grown on demand, owned by the engine)
   void* cbuf = nullptr;
   size_t cbuf_bytes = 0;
-  // timeline
+  // timeline (HIP-free bookkeeping in comm/host.h)
   std::string timeline_path;
-  std::vector<TimelineRec> pending;  // recorded, not yet written
-  std::vector<hipEvent_t> free_events;
-  std::ofstream tl;
-  bool tl_first = true;
+  std::ofstream tl_file;
+  hcb::comm::Timeline<hipEvent_t> timeline;
+  hcb::comm::EventPool<hipEvent_t> events;
   int64_t cycle = 0;
   int64_t buckets_issued = 0;  // lifetime count of bucket collectives
   // watchdog
@@ -129,7 +122,7 @@ struct Comm {
   // thread only compares `done` with `enq` and the clock. Only when the caller has been
   // quiet for > 1 s (blocked on a hung collective, or idle) does the watchdog query the
   // watch event itself, under `mu`, which every enqueue also holds.
-  hcb::comm::StallWatch watch;
+  hcb::comm::WatchState ws;  // guarded by mu (ws.watch's counters are atomics)
   std::unique_ptr<hcb::comm::Transport> transport;  // RcclTransport, created on first use
   std::unique_ptr<hcb::comm::BucketEngine> engine;  // lifetime bucket numbering
   int64_t fusion_bytes = 128ll << 20;  // HOROVOD_FUSION_THRESHOLD
@@ -137,34 +130,35 @@ struct Comm {
   // debug (HCB_COMM_DEBUG_SLEEP_MS): a bounded device sleep on the comm stream at every fork, so a
   // stalled collective can be staged on one GPU (it is captured into the step graph like the rest)
   int debug_sleep_ms = 0;
-  int64_t steps_marked = 0;  // step_mark() heartbeats (graph-replayed steps)
-  std::atomic<int64_t> first_mark_cycle{-1};  // first watch cycle enqueued by step_mark()
   hipEvent_t watch_ev = nullptr;
-  int64_t watch_cycle = 0;
-  std::chrono::steady_clock::time_point last_call = std::chrono::steady_clock::now();
   std::atomic<bool> aborted{false};
 
   hipEvent_t get_event() {
-    if (!free_events.empty()) {
-      hipEvent_t e = free_events.back();
-      free_events.pop_back();
+    return events.get([] {
+      hipEvent_t e;
+      HCB_HIP(hipEventCreate(&e));
       return e;
-    }
-    hipEvent_t e;
-    HCB_HIP(hipEventCreate(&e));
-    return e;
+    });
+  }
+  bool watch_done() { return hipEventQuery(watch_ev) == hipSuccess; }
+  void flush_timeline(bool block) {
+    timeline.flush(
+        block, events, [](hipEvent_t e) { return hipEventQuery(e) == hipSuccess; },
+        [](hipEvent_t e) { hipEventSynchronize(e); },
+        [this](hipEvent_t e) {
+          float t = 0.f;
+          hipEventElapsedTime(&t, base_ev, e);
+          return (double)t;
+        });
   }
 };
 
-std::mutex g_mu;
-std::map<int64_t, std::unique_ptr<Comm>> g_comms;
-int64_t g_next = 1;
+hcb::comm::HandleTable<Comm> g_comms;
 
 Comm* get(int64_t h) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_comms.find(h);
-  TORCH_CHECK(it != g_comms.end(), "hcb_comm: invalid communicator handle ", h);
-  return it->second.get();
+  Comm* c = g_comms.get(h);
+  TORCH_CHECK(c != nullptr, "hcb_comm: invalid communicator handle ", h);
+  return c;
 }
 
 bool capturing(hipStream_t s) {
@@ -197,12 +191,10 @@ void watchdog_loop(Comm* c) {
     auto now = std::chrono::steady_clock::now();
     {
       std::lock_guard<std::mutex> lk(c->mu);
-      if (c->watch.completed() < c->watch_cycle &&
-          std::chrono::duration<double>(now - c->last_call).count() > 1.0 && hipEventQuery(c->watch_ev) == hipSuccess)
-        c->watch.complete(c->watch_cycle);
+      c->ws.poll_quiet(now, 1.0, [c] { return c->watch_done(); });
     }
     double waited = 0;
-    const StallWatch::Action act = c->watch.evaluate(now, &waited);
+    const StallWatch::Action act = c->ws.watch.evaluate(now, &waited);
     if (act == StallWatch::kIdle || act == StallWatch::kProgress) continue;
     if (waited > 1.0 && c->comm) {  // stalled: only now ask RCCL whether a peer failed
       ncclResult_t ae = ncclSuccess;
@@ -214,12 +206,17 @@ void watchdog_loop(Comm* c) {
       }
     }
     if (act == StallWatch::kWarn) {
-      const int64_t cyc = c->watch.completed() + 1, fm = c->first_mark_cycle.load();
+      const int64_t cyc = c->ws.watch.completed() + 1;
+      bool graph_cycle;
+      {
+        std::lock_guard<std::mutex> lk(c->mu);
+        graph_cycle = c->ws.is_graph_cycle(cyc);
+      }
       std::fprintf(stderr,
                    "[hcb watchdog] rank %d: gradient reduction cycle %lld%s (buckets up to #%lld) has not completed "
                    "after %.0f s; one or more ranks may have stalled (HOROVOD_STALL_CHECK_TIME_SECONDS=%.0f)\n",
-                   c->rank, (long long)cyc, fm >= 0 && cyc >= fm ? " (graph-replayed step)" : "",
-                   (long long)c->watch.last_seq(), waited, c->watch.warn_s());
+                   c->rank, (long long)cyc, graph_cycle ? " (graph-replayed step)" : "",
+                   (long long)c->ws.watch.last_seq(), waited, c->ws.watch.warn_s());
       std::fflush(stderr);
     } else if (act == StallWatch::kAbort && c->comm) {
       std::fprintf(stderr, "[hcb watchdog] rank %d: stalled for %.0f s > HCB_STALL_ABORT_SECONDS; aborting\n", c->rank,
@@ -266,8 +263,8 @@ struct RcclTransport final : hcb::comm::Transport {
     if (!tl) return;
     hipEvent_t e1 = c->get_event();
     HCB_HIP(hipEventRecord(e1, c->stream));
-    c->pending.push_back({w != hcb::comm::Wire::F32 ? "PACK_ALLREDUCE_UNPACK" : "ALLREDUCE", (int)b.seq,
-                          b.len * hcb::comm::wire_bytes(w), e0, e1});
+    c->timeline.record({w != hcb::comm::Wire::F32 ? "PACK_ALLREDUCE_UNPACK" : "ALLREDUCE", b.seq,
+                        b.len * hcb::comm::wire_bytes(w), e0, e1});
   }
   void join() override {
     HCB_HIP(hipEventRecord(c->join_ev, c->stream));
@@ -316,11 +313,11 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
       std::string p(tl);
       if (c->world > 1) p += "." + std::to_string(c->rank);
       c->timeline_path = p;
-      c->tl.open(p);
-      c->tl << "[\n";
+      c->tl_file.open(p);
+      c->timeline.open(&c->tl_file, c->rank);
     }
   }
-  c->watch.configure(env_double("HOROVOD_STALL_CHECK_TIME_SECONDS", 60.0), env_double("HCB_STALL_ABORT_SECONDS", 0.0));
+  c->ws.watch.configure(env_double("HOROVOD_STALL_CHECK_TIME_SECONDS", 60.0), env_double("HCB_STALL_ABORT_SECONDS", 0.0));
   {
     const double fb = env_double("HOROVOD_FUSION_THRESHOLD", 128.0 * 1024 * 1024);
     c->fusion_bytes = fb > 0 ? (int64_t)fb : 0;
@@ -329,63 +326,21 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
   c->debug_sleep_ms = (int)std::min(10000.0, std::max(0.0, env_double("HCB_COMM_DEBUG_SLEEP_MS", 0.0)));
   Comm* raw = c.get();
   if (env_double("HCB_COMM_WATCHDOG", 1.0) != 0.0) raw->wd = std::thread(watchdog_loop, raw);
-  std::lock_guard<std::mutex> lk(g_mu);
-  int64_t h = g_next++;
-  g_comms[h] = std::move(c);
-  return h;
-}
-
-void flush_timeline(Comm* c, bool block) {
-  if (!c->tl.is_open()) {
-    for (auto& r : c->pending) {
-      c->free_events.push_back(r.b);
-      c->free_events.push_back(r.e);
-    }
-    c->pending.clear();
-    return;
-  }
-  std::vector<TimelineRec> keep;
-  for (auto& r : c->pending) {
-    if (!block && hipEventQuery(r.e) != hipSuccess) {
-      keep.push_back(r);
-      continue;
-    }
-    hipEventSynchronize(r.e);
-    float t0 = 0.f, t1 = 0.f;
-    hipEventElapsedTime(&t0, c->base_ev, r.b);
-    hipEventElapsedTime(&t1, c->base_ev, r.e);
-    if (!c->tl_first) c->tl << ",\n";
-    c->tl_first = false;
-    c->tl << "{\"name\":\"" << r.name << "\",\"ph\":\"X\",\"pid\":" << c->rank << ",\"tid\":" << r.bucket
-          << ",\"ts\":" << (double)t0 * 1000.0 << ",\"dur\":" << (double)(t1 - t0) * 1000.0
-          << ",\"args\":{\"bytes\":" << r.bytes << ",\"bucket\":" << r.bucket << "}}";
-    c->free_events.push_back(r.b);
-    c->free_events.push_back(r.e);
-  }
-  c->pending.swap(keep);
-  c->tl.flush();
+  return g_comms.add(std::move(c));
 }
 
 void destroy(int64_t h) {
-  std::unique_ptr<Comm> c;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_comms.find(h);
-    if (it == g_comms.end()) return;
-    c = std::move(it->second);
-    g_comms.erase(it);
-  }
+  std::unique_ptr<Comm> c = g_comms.take(h);
+  if (!c) return;
   c->stop = true;
   c->cv.notify_all();
   if (c->wd.joinable()) c->wd.join();
   hipStreamSynchronize(c->stream);
-  flush_timeline(c.get(), true);
-  if (c->tl.is_open()) {
-    c->tl << "\n]\n";
-    c->tl.close();
-  }
+  c->flush_timeline(true);
+  c->timeline.close();
+  if (c->tl_file.is_open()) c->tl_file.close();
   if (c->comm) ncclCommDestroy(c->comm);
-  for (auto e : c->free_events) hipEventDestroy(e);
+  c->events.drain([](hipEvent_t e) { hipEventDestroy(e); });
   hipEventDestroy(c->fork_ev);
   hipEventDestroy(c->join_ev);
   hipEventDestroy(c->base_ev);
@@ -465,18 +420,21 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
   for (int64_t i = 0; i < nb; ++i)
     TORCH_CHECK(bk[2 * i] >= 0 && bk[2 * i + 1] > 0 && bk[2 * i] + bk[2 * i + 1] <= n, "hcb_comm: bucket out of range");
   std::lock_guard<std::mutex> call_lk(c->mu);  // excludes the watchdog's (rare) event query
-  c->last_call = std::chrono::steady_clock::now();
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   const bool cap = capturing(cur);
-  if (!cap) flush_timeline(c, false);
-  if (!cap && c->wd.joinable() && c->watch.completed() < c->watch_cycle && hipEventQuery(c->watch_ev) == hipSuccess)
-    c->watch.complete(c->watch_cycle);
-  if (compress && c->cbuf_bytes < (size_t)n * 2) {
+  if (!cap) c->flush_timeline(false);
+  if (!cap && c->wd.joinable())
+    c->ws.enter([c] { return c->watch_done(); });
+  else
+    c->ws.last_call = std::chrono::steady_clock::now();
+  if (const size_t grow = hcb::comm::scratch_bytes(c->cbuf_bytes, n, (hcb::comm::Wire)compress)) {
     TORCH_CHECK(!cap, "hcb_comm: first compressed reduction must run outside graph capture");
     HCB_HIP(hipStreamSynchronize(c->stream));
     if (c->cbuf) HCB_HIP(hipFree(c->cbuf));
-    HCB_HIP(hipMalloc(&c->cbuf, (size_t)n * 2));
-    c->cbuf_bytes = (size_t)n * 2;
+    c->cbuf = nullptr;
+    c->cbuf_bytes = 0;
+    HCB_HIP(hipMalloc(&c->cbuf, grow));
+    c->cbuf_bytes = grow;
   }
   if (!c->engine) {
     c->transport = std::make_unique<RcclTransport>(c);
@@ -484,14 +442,14 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
   }
   auto* tr = static_cast<RcclTransport*>(c->transport.get());
   tr->cap = cap;
-  tr->tl = c->tl.is_open() && !cap;
+  tr->tl = c->timeline.is_open() && !cap;
   std::vector<hcb::comm::Bucket> issued =
       c->engine->submit(flat.data_ptr<float>(), n, bk, nb, (hcb::comm::Wire)compress, average,
                  fusion_bytes > 0 ? fusion_bytes : c->fusion_bytes, do_join);
   c->buckets_issued += (int64_t)issued.size();
   if (!cap && c->wd.joinable()) {
     HCB_HIP(hipEventRecord(c->watch_ev, c->stream));
-    c->watch_cycle = c->watch.enqueue(c->buckets_issued - 1);
+    c->ws.enqueue(c->buckets_issued - 1, false);
   }
   c->cycle++;
 }
@@ -523,16 +481,20 @@ void step_mark(int64_t h) {
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   TORCH_CHECK(!capturing(cur), "hcb_comm.step_mark: call after a replay, not inside a capture");
   std::lock_guard<std::mutex> lk(c->mu);
-  c->last_call = std::chrono::steady_clock::now();
-  c->steps_marked++;
-  if (!c->wd.joinable()) return;
-  if (c->watch.completed() < c->watch_cycle && hipEventQuery(c->watch_ev) == hipSuccess)
-    c->watch.complete(c->watch_cycle);
+  if (!c->wd.joinable()) {
+    c->ws.last_call = std::chrono::steady_clock::now();
+    c->ws.marks++;
+    return;
+  }
+  c->ws.enter([c] { return c->watch_done(); });
   HCB_HIP(hipEventRecord(c->watch_ev, cur));
-  c->watch_cycle = c->watch.enqueue(c->buckets_issued - 1);
-  if (c->first_mark_cycle.load() < 0) c->first_mark_cycle = c->watch_cycle;
+  c->ws.enqueue(c->buckets_issued - 1, true);
 }
-int64_t steps_marked(int64_t h) { return get(h)->steps_marked; }
+int64_t steps_marked(int64_t h) {
+  Comm* c = get(h);
+  std::lock_guard<std::mutex> lk(c->mu);
+  return c->ws.marks;
+}
 
 int64_t buckets_issued(int64_t h) { return get(h)->buckets_issued; }
 int64_t fusion_threshold(int64_t h) { return get(h)->fusion_bytes; }
@@ -554,36 +516,27 @@ void barrier(int64_t h) {
 // IPC-shared staging regions (csrc/kernels/xgmi.hip has the protocol). Independent of the
 // RCCL communicator: handles are exchanged by the Python side over torch.distributed.
 struct Xgmi {
-  int rank = 0, world = 1, device = 0;
-  int64_t cap = 0;                  // floats per slot
+  hcb::comm::XgmiBook book;         // rank / world / capacity / peer mapping (comm/host.h)
+  int device = 0;
   unsigned spin = 1u << 25;         // bounded-wait iterations
   float* region = nullptr;          // own region: 2 slots + flags
   unsigned* err = nullptr;          // device error word (spin timeout)
-  std::vector<float*> peers;        // every rank's region as mapped here (own = region)
-  std::vector<bool> opened;
 };
-std::mutex g_xmu;
-std::map<int64_t, std::unique_ptr<Xgmi>> g_xgmi;
-int64_t g_xnext = 1;
+hcb::comm::HandleTable<Xgmi> g_xgmi;
 
 Xgmi* xget(int64_t h) {
-  std::lock_guard<std::mutex> lk(g_xmu);
-  auto it = g_xgmi.find(h);
-  TORCH_CHECK(it != g_xgmi.end(), "hcb_comm: invalid xgmi handle ", h);
-  return it->second.get();
+  Xgmi* x = g_xgmi.get(h);
+  TORCH_CHECK(x != nullptr, "hcb_comm: invalid xgmi handle ", h);
+  return x;
 }
 
 int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, int64_t device) {
-  TORCH_CHECK(world >= 1 && world <= hcb::xgmi_max_ranks() && rank >= 0 && rank < world,
-              "hcb_comm.xgmi_create: 1..", hcb::xgmi_max_ranks(), " ranks");
-  TORCH_CHECK(cap > 0 && cap % 4 == 0, "hcb_comm.xgmi_create: capacity must be a positive multiple of 4 floats");
+  const std::string bad = hcb::comm::XgmiBook::check_create(rank, world, cap, hcb::xgmi_max_ranks());
+  TORCH_CHECK(bad.empty(), "hcb_comm.xgmi_create: ", bad);
   auto x = std::make_unique<Xgmi>();
-  x->rank = (int)rank;
-  x->world = (int)world;
   x->device = (int)device;
-  x->cap = cap;
   HCB_HIP(hipSetDevice(x->device));
-  const size_t bytes = (size_t)2 * cap * 4 + 256;
+  const size_t bytes = hcb::comm::XgmiBook::region_bytes(cap);
   // uncached (fine-grained) device memory: peers on OTHER GPUs spin on the ready / epoch words
   // and read the slots over xGMI while this GPU is still running; coarse-grained memory is only
   // coherent across devices at kernel boundaries
@@ -593,13 +546,8 @@ int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, int64_t device) {
   HCB_HIP(hipMalloc(&x->err, 4));
   HCB_HIP(hipMemset(x->err, 0, 4));
   HCB_HIP(hipDeviceSynchronize());
-  x->peers.assign(world, nullptr);
-  x->opened.assign(world, false);
-  x->peers[rank] = x->region;
-  std::lock_guard<std::mutex> lk(g_xmu);
-  int64_t h = g_xnext++;
-  g_xgmi[h] = std::move(x);
-  return h;
+  x->book.init((int)rank, (int)world, cap, x->region);
+  return g_xgmi.add(std::move(x));
 }
 
 Tensor xgmi_handle(int64_t h) {
@@ -614,17 +562,17 @@ Tensor xgmi_handle(int64_t h) {
 void xgmi_open(int64_t h, const Tensor& handles) {
   Xgmi* x = xget(h);
   TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.dim() == 2 &&
-                  handles.size(0) == x->world && handles.size(1) == (int64_t)sizeof(hipIpcMemHandle_t),
+                  handles.size(0) == x->book.world && handles.size(1) == (int64_t)sizeof(hipIpcMemHandle_t),
               "hcb_comm.xgmi_open: handles uint8 [world][", sizeof(hipIpcMemHandle_t), "] on CPU");
+  const at::Tensor hc = handles.contiguous();
   HCB_HIP(hipSetDevice(x->device));
-  for (int r = 0; r < x->world; ++r) {
-    if (r == x->rank) continue;
+  for (int r = 0; r < x->book.world; ++r) {
+    if (r == x->book.rank) continue;
     hipIpcMemHandle_t mh;
-    std::memcpy(&mh, handles.data_ptr<uint8_t>() + (size_t)r * sizeof(mh), sizeof(mh));
+    std::memcpy(&mh, hc.data_ptr<uint8_t>() + (size_t)r * sizeof(mh), sizeof(mh));
     void* p = nullptr;
     HCB_HIP(hipIpcOpenMemHandle(&p, mh, hipIpcMemLazyEnablePeerAccess));
-    x->peers[r] = static_cast<float*>(p);
-    x->opened[r] = true;
+    x->book.set_peer(r, p);
   }
 }
 
@@ -632,12 +580,14 @@ void xgmi_allreduce_(int64_t h, const Tensor& t, double scale) {
   Xgmi* x = xget(h);
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat,
               "hcb_comm.xgmi_allreduce_: contiguous fp32 GPU tensor");
-  TORCH_CHECK(t.numel() <= x->cap, "hcb_comm.xgmi_allreduce_: ", t.numel(), " floats > capacity ", x->cap);
-  for (int r = 0; r < x->world; ++r) TORCH_CHECK(x->peers[r] != nullptr, "hcb_comm.xgmi: peer ", r, " not opened");
+  const std::string bad = x->book.check_reduce(t.numel());
+  TORCH_CHECK(bad.empty(), "hcb_comm.xgmi_allreduce_: ", bad);
   if (t.numel() == 0) return;
-  std::vector<const float*> b(x->peers.begin(), x->peers.end());
-  hcb::launch_xgmi_allreduce(b.data(), x->world, x->rank, t.data_ptr<float>(), t.data_ptr<float>(), t.numel(),
-                             x->cap, (float)scale, x->err, x->spin, c10::hip::getCurrentHIPStream().stream());
+  std::vector<const float*> b;
+  for (void* p : x->book.peers) b.push_back(static_cast<const float*>(p));
+  hcb::launch_xgmi_allreduce(b.data(), x->book.world, x->book.rank, t.data_ptr<float>(), t.data_ptr<float>(),
+                             t.numel(), x->book.cap, (float)scale, x->err, x->spin,
+                             c10::hip::getCurrentHIPStream().stream());
 }
 
 int64_t xgmi_error(int64_t h) {
@@ -648,18 +598,12 @@ int64_t xgmi_error(int64_t h) {
 }
 
 void xgmi_destroy(int64_t h) {
-  std::unique_ptr<Xgmi> x;
-  {
-    std::lock_guard<std::mutex> lk(g_xmu);
-    auto it = g_xgmi.find(h);
-    if (it == g_xgmi.end()) return;
-    x = std::move(it->second);
-    g_xgmi.erase(it);
-  }
+  std::unique_ptr<Xgmi> x = g_xgmi.take(h);
+  if (!x) return;
   hipSetDevice(x->device);
   hipDeviceSynchronize();
-  for (int r = 0; r < x->world; ++r)
-    if (x->opened[r]) hipIpcCloseMemHandle(x->peers[r]);
+  for (int r = 0; r < x->book.world; ++r)
+    if (x->book.opened[r]) hipIpcCloseMemHandle(x->book.peers[r]);
   hipFree(x->region);
   hipFree(x->err);
 }

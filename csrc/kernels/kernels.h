@@ -185,7 +185,7 @@ void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t 
 // ---------------------------------------------------------------- loss / fc helpers
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
                          float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
-                         hipStream_t st, bool f32 = false);
+                         hipStream_t st, bool f32 = false, float* dl32 = nullptr);
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st);
 
 // ---------------------------------------------------------------- optimizer / weights

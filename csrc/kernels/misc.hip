@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
                                                            const int64_t* __restrict__ labels,
                                                            int ncls, float* row_loss,
                                                            T* dl, int lddl, float scale,
-                                                           const float* scale_dev) {
+                                                           const float* scale_dev, float* dl32) {
   __shared__ float red[8];
   if (scale_dev != nullptr) scale *= *scale_dev;  // device-resident loss scale
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -51,10 +51,12 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   for (int c = tid; c < lddl; c += 256) {
     float g = 0.f;
     if (c < ncls) g = (__expf(lr[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * scale;
-    if constexpr (sizeof(T) == 4)
+    if constexpr (sizeof(T) == 4) {
       dl[(size_t)row * lddl + c] = g;
-    else
+    } else {
       dl[(size_t)row * lddl + c] = f2act(g);
+      if (dl32 != nullptr) dl32[(size_t)row * lddl + c] = g;  // unrounded: the bias gradient's source
+    }
   }
 }
 
@@ -450,13 +452,13 @@ static int grid_for(int64_t n) {
 
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
                          float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
-                         hipStream_t st, bool f32) {
+                         hipStream_t st, bool f32, float* dl32) {
   if (f32)
     hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls, row_loss,
-                       (float*)dlogits, lddl, scale, scale_dev);
+                       (float*)dlogits, lddl, scale, scale_dev, (float*)nullptr);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<uint16_t>, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls, row_loss,
-                       (uint16_t*)dlogits, lddl, scale, scale_dev);
+                       (uint16_t*)dlogits, lddl, scale, scale_dev, dl32);
 }
 
 // ------------------------------------------------------------------ loss scaling

@@ -146,3 +146,18 @@ def test_wire_conversions_match_numpy():
         assert E.f32_to_f16_bits(float(x)) == int(np.float16(x).view(np.uint16)), x
     u = struct.unpack("<I", struct.pack("<f", 1.00390625))[0]
     assert E.f32_to_bf16_bits(1.00390625) == ((u + 0x7FFF + ((u >> 16) & 1)) >> 16)
+
+
+def test_comm_engine_and_host_bookkeeping_under_sanitizers(tmp_path):
+    """tools/sanitize/run_engine_sanitizers.sh: the bucket engine with its fake 8-rank fabric
+    AND the RCCL runtime's HIP-free host bookkeeping (csrc/comm/host.h, the header comm.cpp
+    compiles: handle tables, event pool / timeline, watch state, xGMI checks), each built with
+    ASan + UBSan and with TSan and stress-driven."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["bash", os.path.join(root, "tools", "sanitize", "run_engine_sanitizers.sh")], cwd=root,
+                       env=dict(os.environ, OUT=str(tmp_path)), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("comm_host_stress: ok") == 2 and r.stdout.count("ENGINE STRESS OK") == 2

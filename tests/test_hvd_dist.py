@@ -342,6 +342,49 @@ def test_segmented_backward_equals_plain_backward(name, size, monkeypatch):
     assert torch.allclose(m.ps.grad, g_plain, rtol=1e-4, atol=1e-6)
 
 
+def test_resnet_block_segments():
+    """segments="block" (bench.py --backward_segments block): one segment per block of stages
+    3-4, stage 2 whole, stage 1 cut from the stem -- ResNet-50: 3 + 6 + 1 + 1 + stem = 12
+    segments, the same gradients as the plain backward, every parameter exactly once."""
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.trainer import synthetic_batch
+
+    torch.manual_seed(0)
+    m = create_model("resnet50", image_size=32, device="cpu")
+    img, lab = synthetic_batch(m, 2)
+    dl = torch.randn(2, m.num_classes) * 0.1
+    if dl.shape[1] != getattr(m.fc, "ld", dl.shape[1]):
+        dl = torch.nn.functional.pad(dl, (0, m.fc.ld - dl.shape[1]))
+    m.ps.zero_grad()
+    m.forward(img)
+    m.backward(dl)
+    g_plain = m.ps.grad.clone()
+    m.segments = "block"
+    m.ps.zero_grad()
+    m.forward(img)
+    cover = torch.zeros(m.ps.grad.numel(), dtype=torch.int32)
+    sizes = []
+    for layers, last in m.backward_segments(dl):
+        rng = m.grad_ranges(layers)
+        sizes.append(sum(n for _, n in rng))
+        for off, n in rng:
+            cover[off:off + n] += 1
+    assert last and len(sizes) == 12, sizes
+    assert sizes[-1] < 10_000  # only the stem (conv 7x7x3x64 + BN) after the last block
+    assert int(cover.max()) == 1 and int(cover.sum()) >= m.num_params() - 64
+    assert torch.allclose(m.ps.grad, g_plain, rtol=1e-4, atol=1e-6)
+
+
+def test_rccl_env_plumbing(monkeypatch):
+    from azure_hc_intel_tf_amd.launch.launcher import rccl_env, worker_env
+
+    monkeypatch.delenv("NCCL_ALGO", raising=False)
+    e = rccl_env(channels=16, algo="Ring", proto=None, base={"NCCL_MAX_NCHANNELS": "8"})
+    assert e == {"NCCL_MIN_NCHANNELS": "16", "NCCL_ALGO": "Ring"}  # a value already set wins
+    w = worker_env({}, 1, 1, 2, 2, 0, "127.0.0.1", 29500, "ib", None, rccl=e)
+    assert w["NCCL_ALGO"] == "Ring" and w["NCCL_MIN_NCHANNELS"] == "16" and w["RANK"] == "1"
+
+
 def _comm_check(hvd):
     """The overlapped-allreduce race detector (Trainer comm_check) passes on a correct engine and
     fails loudly when a reduction reads gradients that are not final."""
