@@ -69,19 +69,21 @@ def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
     raise ValueError(mode)
 
 
-# ResNet stem: BN+ReLU+max pool in one kernel on the GPU (HCB_FUSE_STEM_POOL=0 to disable)
-FUSE_STEM_POOL = os.environ.get("HCB_FUSE_STEM_POOL", "1") != "0"
+# Fusion switches (module attributes, set before a model is built; the tests flip them to
+# compare against the unfused forms):
+# ResNet stem: BN+ReLU+max pool in one kernel on the GPU
+FUSE_STEM_POOL = True
 # replicas of the BN statistic accumulators (spreads the fp32 atomic contention)
-STAT_R = max(1, int(os.environ.get("HCB_STAT_R", "8")))
+STAT_R = 8
 # fold a BN layer's backward reduction into the data-grad GEMM that produces its dy
-FUSE_BN_BWD = os.environ.get("HCB_FUSE_BN_BWD", "1") != "0"
+FUSE_BN_BWD = True
 # projection blocks: the shortcut's BN is applied inside the block output's BN pass
 # (act(BN3(z3) + BN_sc(z_sc)) in one kernel), so the shortcut's normalised tensor is never written
-FUSE_RES_BN = os.environ.get("HCB_FUSE_RES_BN", "1") != "0"
+FUSE_RES_BN = True
 # shifted single-pass BN statistics: the conv epilogue sums (v - K), (v - K)^2 with K = the
 # layer's previous batch mean, so E[x^2] - E[x]^2 does not cancel in fp32 when |mean| >> std
-# (HCB_BN_SHIFT=0: K = 0, the plain single-pass form)
-BN_SHIFT = os.environ.get("HCB_BN_SHIFT", "1") != "0"
+# (False: K = 0, the plain single-pass form)
+BN_SHIFT = True
 class _FixedParam:
     """A non-trainable per-channel constant with a scratch gradient sink (BN scale=False)."""
 
@@ -352,8 +354,8 @@ class ConvBN(Layer):
         self._pre_reduced = False
 
 
-# GPU ResNet stem as a space-to-depth 4x4/1 GEMM (HCB_STEM_S2D=0: the direct padded 7x7/2 form)
-STEM_S2D = os.environ.get("HCB_STEM_S2D", "1") != "0"
+# GPU ResNet stem as a space-to-depth 4x4/1 GEMM (False: the direct padded 7x7/2 form)
+STEM_S2D = True
 
 
 class StemS2D(ConvBN):

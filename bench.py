@@ -77,8 +77,8 @@ def spawn_workers(args, argv) -> int:
     from azure_hc_intel_tf_amd.launch.launcher import launch, visible_gpu_count
 
     one_device = os.environ.get("HCB_BENCH_ONE_DEVICE") == "1"
-    if os.environ.get("HCB_BENCH_REPORT_PARENT") == "1":  # tests: the parent never loads torch / HIP
-        print(f"[bench] launcher parent: torch loaded = {'torch' in sys.modules}", file=sys.stderr, flush=True)
+    # the parent never loads torch / HIP (tests/test_bench_spawn.py checks this line)
+    print(f"[bench] launcher parent: torch loaded = {'torch' in sys.modules}", file=sys.stderr, flush=True)
     if not one_device:
         visible = visible_gpu_count()  # KFD topology: no torch, no HIP runtime in this process
         if visible < args.gpus:
@@ -107,10 +107,15 @@ def main(argv=None):
     if world != args.gpus:
         print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to run", file=sys.stderr)
         return 3
+    # stdout carries exactly ONE line, the result JSON: libraries that print banners on stdout
+    # (RCCL announces its version when a communicator is created) write to stderr instead
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if os.environ.get("HCB_BENCH_STUB_WORKER") == "1":  # CPU test of the spawn path: report the rank env
         print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
                                                          "MASTER_ADDR", "MASTER_PORT", "HCB_BENCH_SPAWNED")}),
-              flush=True)
+              file=result_out, flush=True)
         return 0
 
     import torch
@@ -272,7 +277,7 @@ def main(argv=None):
                        "kernels": "hip" if model.native else "pytorch-reference (MIOpen/rocBLAS)",
                        "final_loss": round(loss, 4)},
         }
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=result_out, flush=True)
     if reducer is not None and hasattr(reducer, "close"):
         reducer.close()
     if world > 1:

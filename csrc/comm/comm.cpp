@@ -126,7 +126,6 @@ struct Comm {
   std::unique_ptr<hcb::comm::Transport> transport;  // RcclTransport, created on first use
   std::unique_ptr<hcb::comm::BucketEngine> engine;  // lifetime bucket numbering
   int64_t fusion_bytes = 128ll << 20;  // HOROVOD_FUSION_THRESHOLD
-  bool skip_rccl = false;  // debug (HCB_COMM_SKIP_RCCL=1): stream fork/join without the collective
   // debug (HCB_COMM_DEBUG_SLEEP_MS): a bounded device sleep on the comm stream at every fork, so a
   // stalled collective can be staged on one GPU (it is captured into the step graph like the rest)
   int debug_sleep_ms = 0;
@@ -255,7 +254,7 @@ struct RcclTransport final : hcb::comm::Transport {
       HCB_NCCL(ncclAllReduce(cb, cb, b.len, w == hcb::comm::Wire::BF16 ? ncclBfloat16 : ncclFloat16, op, c->comm,
                              c->stream));
       hcb::launch_bucket_unpack(cb, flat + b.off, b.len, 1.0f, mode, c->stream);
-    } else if (!c->skip_rccl) {
+    } else {
       HCB_NCCL(ncclAllReduce(flat + b.off, flat + b.off, b.len, ncclFloat32, op, c->comm, c->stream));
     }
   }
@@ -322,7 +321,6 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
     const double fb = env_double("HOROVOD_FUSION_THRESHOLD", 128.0 * 1024 * 1024);
     c->fusion_bytes = fb > 0 ? (int64_t)fb : 0;
   }
-  c->skip_rccl = env_double("HCB_COMM_SKIP_RCCL", 0.0) != 0.0;
   c->debug_sleep_ms = (int)std::min(10000.0, std::max(0.0, env_double("HCB_COMM_DEBUG_SLEEP_MS", 0.0)));
   Comm* raw = c.get();
   if (env_double("HCB_COMM_WATCHDOG", 1.0) != 0.0) raw->wd = std::thread(watchdog_loop, raw);

@@ -11,11 +11,10 @@
 #include "common.h"
 #include "kernels.h"
 
-#ifndef HCB_BNB_CH
-#define HCB_BNB_CH 4  // fused BN-backward epilogue: output segments prefetched per chunk and thread
-#endif
-
 namespace hcb {
+
+// fused BN-backward epilogue: output segments prefetched per chunk and thread
+constexpr int BNB_PREFETCH_CH = 4;
 
 // Bytes of LDS the epilogue needs for a BM x BN tile computed by WM x WN waves. s16: the plain
 // bf16-output epilogue without beta / bias stages the tile as 16-bit values (rounded once, the
@@ -47,7 +46,7 @@ template <int WM, int WN, int TM, int TN, bool BNB>
 struct EpiPrefetch {
   static constexpr int BM = WM * TM, BN = WN * TN, SEGS = BN / 8, NT = WM * WN * 64;
   static constexpr int ITER = BM * SEGS / NT;
-  static constexpr int CH = BNB ? (ITER < HCB_BNB_CH ? ITER : HCB_BNB_CH) : 1;
+  static constexpr int CH = BNB ? (ITER < BNB_PREFETCH_CH ? ITER : BNB_PREFETCH_CH) : 1;
   u32x4 pr[CH], pz[CH], py[CH];
   // forward GEMMs: the BN statistic shift of each of the lane's accumulator columns, loaded
   // before the main loop so the epilogue does not wait on it

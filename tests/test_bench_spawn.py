@@ -59,7 +59,7 @@ def test_launcher_parent_never_loads_torch():
     the HIP runtime) must not be loaded there, on the spawn path and on the refusal path."""
     for extra in ({"HCB_BENCH_ONE_DEVICE": "1", "HCB_BENCH_STUB_WORKER": "1"}, {}):
         out = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--steps", "1", "--warmup", "0"],
-                             env=_env(HCB_BENCH_REPORT_PARENT="1", **extra), capture_output=True, text=True,
+                             env=_env(**extra), capture_output=True, text=True,
                              timeout=300)
         assert "[bench] launcher parent: torch loaded = False" in out.stderr, out.stderr
 

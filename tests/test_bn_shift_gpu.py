@@ -1,4 +1,4 @@
-"""Shifted single-pass BN statistics (HCB_BN_SHIFT, ConvParams::stats_shift): the conv epilogue
+"""Shifted single-pass BN statistics (nn.layers.BN_SHIFT, ConvParams::stats_shift): the conv epilogue
 sums (v - K) and (v - K)^2 with K = the layer's previous batch mean (written by its BN backward),
 so the variance E[(v-K)^2] - E[v-K]^2 does not cancel in fp32 when |mean| >> std. Checked against
 an fp64 reference of the same GEMM (bf16 operands)."""
@@ -40,7 +40,7 @@ def _forward(layer, ps, x):
     return mean, var
 
 
-@pytest.mark.skipif(not L.BN_SHIFT, reason="HCB_BN_SHIFT=0")
+@pytest.mark.skipif(not L.BN_SHIFT, reason="BN_SHIFT off")
 def test_shifted_statistics_match_fp64_when_mean_dominates():
     layer, ps = _layer()
     g = torch.Generator().manual_seed(11)

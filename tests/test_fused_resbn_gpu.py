@@ -1,4 +1,4 @@
-"""Projection-shortcut BN fused into the block output's BN pass (HCB_FUSE_RES_BN, ResBN in
+"""Projection-shortcut BN fused into the block output's BN pass (nn.layers.FUSE_RES_BN, ResBN in
 csrc/kernels/bn.hip): act(BN3(z3) + BN_sc(z_sc)) in one kernel, the shortcut's normalised
 tensor never written. Checked against the unfused path (shortcut BN apply, then the add)."""
 import pytest

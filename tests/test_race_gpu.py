@@ -23,6 +23,11 @@ from azure_hc_intel_tf_amd.ops import functional as Fn
 from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 
 Fn.set_deterministic(True)
+from azure_hc_intel_tf_amd.nn import layers as L
+for kv in filter(None, os.environ.get("RACE_SWITCHES", "").split(",")):  # e.g. L.FUSE_BN_BWD=0 (bisection)
+    k, v = kv.split("=")
+    mod, attr = k.split(".")
+    setattr({"L": L, "Fn": Fn}[mod], attr, type(getattr({"L": L, "Fn": Fn}[mod], attr))(int(v)))
 dp = sys.argv[2] == "dp"
 size, batch = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (64, 8)
 if len(sys.argv) > 5 and sys.argv[5] == "tuned":  # the autotuned kernel configs bench.py runs

@@ -65,8 +65,9 @@ def main():
         t_copy = tm(lambda: o.copy_(a))
         t_add = tm(lambda: torch.add(a, b, out=o))
         t_3 = tm(lambda: torch.addcmul(a, b, c, out=o))
-        print(f"  torch stream: copy(1R1W) {t_copy:.1f} us = {2 * mb / t_copy / 1e3:.2f} TB/s; add(2R1W) {t_add:.1f} "
-              f"= {3 * mb / t_add / 1e3:.2f} TB/s; addcmul(3R1W) {t_3:.1f} = {4 * mb / t_3 / 1e3:.2f} TB/s", flush=True)
+        # mb is MB and the times are us: MB / us = TB/s
+        print(f"  torch stream: copy(1R1W) {t_copy:.1f} us = {2 * mb / t_copy:.2f} TB/s; add(2R1W) {t_add:.1f} "
+              f"= {3 * mb / t_add:.2f} TB/s; addcmul(3R1W) {t_3:.1f} = {4 * mb / t_3:.2f} TB/s", flush=True)
 
 
 if __name__ == "__main__":

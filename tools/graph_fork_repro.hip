@@ -16,8 +16,15 @@
 // mode 5: mode 2 plus, in every link of the chain, a hipMemsetAsync node zeroing an accumulator
 //   that the next kernel adds into (the training step's zero-initialised BN accumulators /
 //   split-K dx buffers: torch.zeros inside the capture); mode 6: the same without the forks.
-// Any ordering violation (a kernel started before its predecessor finished) shows up as a
-// nonzero error count.
+// mode 7: the dependent chain with a CROSS-XCD dependency: link k+1 reads element i + 256 of
+//   link k's output, written by the NEXT workgroup (blockIdx + 1: the neighbouring XCD of the
+//   8), so a stale per-XCD L2 line (a missing write-back / invalidate between two graph kernels)
+//   shows up; no forks. mode 8: mode 7 with a memset node + accumulate per link.
+// mode 9: a chain through a SCALAR value: link k reads s_k with a wave-uniform load (an s_load
+//   through the scalar cache) that link k-1 wrote, fills x with it and writes s_{k+1} = s_k + 1;
+//   a scalar cache left uninvalidated between two graph kernels reads a stale s_k.
+// Any ordering violation (a kernel started before its predecessor finished) or cross-XCD
+// visibility gap shows up as a nonzero error count.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -42,6 +49,18 @@ __global__ void k_copy_add(const float* a, float* b, int n, float add) {
 }
 __global__ void k_scale(const float* a, float* b, int n, float s) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b[i] = a[i] * s;
+}
+__global__ void k_rot_add(const float* a, float* b, int n, int shift) {  // b[i] = a[i + shift] + 1
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b[i] = a[(i + shift) % n] + 1.f;
+}
+__global__ void k_rot_accum(const float* a, float* acc, int n, int shift) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    acc[i] += a[(i + shift) % n] + 1.f;
+}
+__global__ void k_scalar_link(const float* s_in, float* s_out, float* x, int n) {
+  const float v = s_in[0];  // uniform address: scalar load
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = v;
+  if (blockIdx.x == 0 && threadIdx.x == 0) s_out[0] = v + 1.f;
 }
 __global__ void k_accum(const float* a, float* acc, int n) {  // acc = 0 (memset) + a + 1
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) acc[i] += a[i] + 1.f;
@@ -103,18 +122,29 @@ int main(int argc, char** argv) {
   } else {
     float* a = x;
     float* o = t0;
-    const bool memset_mode = mode >= 5;
+    const bool memset_mode = mode == 5 || mode == 6 || mode == 8;
+    const bool rot = mode == 7 || mode == 8;
+    const bool scal = mode == 9;
+    if (scal) hipLaunchKernelGGL(k_copy_add, dim3(1), dim3(64), 0, s, x, t1, 64, 0.f);  // s_0 = e (t1[0])
     for (int k = 0; k < chain; ++k) {
-      if (memset_mode) {  // o = 0 by a memset node, then o += a + 1
+      if (scal) {
+        // s_k lives in t1[k & 1]... alternate two scalar slots: read slot k&1, write the other
+        hipLaunchKernelGGL(k_scalar_link, g, b, 0, s, t1 + (k & 1), t1 + ((k + 1) & 1), o, n);
+      } else if (memset_mode) {  // o = 0 by a memset node, then o += a + 1
         CK(hipMemsetAsync(o, 0, n * 4, s));
-        hipLaunchKernelGGL(k_accum, g, b, 0, s, a, o, n);
+        if (rot)
+          hipLaunchKernelGGL(k_rot_accum, g, b, 0, s, a, o, n, 256);
+        else
+          hipLaunchKernelGGL(k_accum, g, b, 0, s, a, o, n);
+      } else if (rot) {
+        hipLaunchKernelGGL(k_rot_add, g, b, 0, s, a, o, n, 256);
       } else {
         hipLaunchKernelGGL(k_copy_add, g, b, 0, s, a, o, n, 1.f);
       }
       float* t = a;
       a = o;
       o = t;
-      if ((k + 1) % seg == 0 && mode != 6) {
+      if ((k + 1) % seg == 0 && mode != 6 && !rot && !scal) {
         CK(hipEventRecord(fork, s));
         CK(hipStreamWaitEvent(c, fork, 0));
         // comm branch: reads the segment's result into a side buffer (like a bucket pack)
@@ -122,8 +152,11 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(join, c));
       }
     }
-    CK(hipStreamWaitEvent(s, join, 0));
-    hipLaunchKernelGGL(k_check, g, b, 0, s, epoch, a, (float)chain, nullptr, 0.f, n, errors);
+    if (!rot && !scal && mode != 6) CK(hipStreamWaitEvent(s, join, 0));
+    if (scal)  // the last link filled its buffer with s_255 = e + 255, and wrote s_256 = e + 256
+      hipLaunchKernelGGL(k_check, g, b, 0, s, epoch, a, (float)(chain - 1), nullptr, 0.f, n, errors);
+    else
+      hipLaunchKernelGGL(k_check, g, b, 0, s, epoch, a, (float)chain, nullptr, 0.f, n, errors);
     // z holds the LAST segment's value (e + chain) when the comm branch ran in order
     if (mode == 1 || mode == 3) hipLaunchKernelGGL(k_check, g, b, 0, s, epoch, z, (float)chain, nullptr, 0.f, n, errors);
   }
