@@ -247,10 +247,12 @@ class ParamStore:
                 pk.pack = self.pack_buf[pk.pack_off:pk.pack_off + pk.Nout * pk.Kpad]
                 if pk.want_tr:
                     pk.tr = self.pack_buf[pk.tr_off:pk.tr_off + pk.C * pk.Kpad_t]
-                if pack_lo:
-                    Fn.register_lo(pk.pack, self.pack_buf_lo[:, pk.pack_off:pk.pack_off + pk.Nout * pk.Kpad])
-                    if pk.want_tr:
-                        Fn.register_lo(pk.tr, self.pack_buf_lo[:, pk.tr_off:pk.tr_off + pk.C * pk.Kpad_t])
+                # always (re)register: a pack without lo terms clears whatever an earlier, freed
+                # pack at the same address left behind
+                lo = self.pack_buf_lo
+                Fn.register_lo(pk.pack, None if lo is None else lo[:, pk.pack_off:pk.pack_off + pk.Nout * pk.Kpad])
+                if pk.want_tr:
+                    Fn.register_lo(pk.tr, None if lo is None else lo[:, pk.tr_off:pk.tr_off + pk.C * pk.Kpad_t])
         else:
             self.pack_buf = None
             self.pack_buf_lo = None

@@ -116,7 +116,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
         y = torch.empty((N, P, Q, Cout), dtype=_act(), device=dev)
         best = None
         acc = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
-        for cfg in Fn.fwd_candidates(Cout):
+        for cfg in Fn.fwd_candidates(Cout, Fn.patch_eligible(spec)):
             for sp in Fn.splitk_candidates(cfg, M, Cout, spec.K):
                 plan = cfg if sp == 1 else [cfg, sp]
                 t = _time(lambda: Fn.conv_forward(x, spec, layer.pack.pack, None, y, stats=acc, cfg=plan,
@@ -128,10 +128,11 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     # data gradient
     if layer.need_dx:
         dx = torch.zeros((N, H, W, Cin), dtype=_act(), device=dev)
+        dpatch = Fn.patch_eligible(spec, dgrad=True) and not phases
         k = Fn.fwd_key(geo[0], Cin, geo[1], taps)
         if k not in Fn._tuned:
             best = None
-            for cfg in Fn.fwd_candidates(Cin):
+            for cfg in Fn.fwd_candidates(Cin, dpatch):
                 for sp in Fn.splitk_candidates(cfg, geo[0], Cin, geo[1]):
                     plan = cfg if sp == 1 else [cfg, sp]
                     t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=plan))
@@ -149,7 +150,7 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
             bacc = torch.zeros(8 * 2 * Cin, dtype=torch.float32, device=dev)
             bnb = Fn.BNBwdFuse(z, yv, Fn.BNSaved(stats[0], stats[1]), stats[2], stats[3], 1, bacc, 8)
             best = None
-            for cfg in Fn.fwd_candidates(Cin):
+            for cfg in Fn.fwd_candidates(Cin, dpatch):
                 for sp in Fn.splitk_candidates(cfg, geo[0], Cin, geo[1]):
                     plan = cfg if sp == 1 else [cfg, sp]
                     t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, True, cfg=plan, bnb=bnb))

@@ -83,12 +83,22 @@ def set_f32_native(on: bool) -> None:
 
 
 def register_lo(pack, lo) -> None:
-    _LO[pack.data_ptr()] = lo
+    """Record (lo = None: forget) the mid / lo packs of ``pack``."""
+    if lo is None:
+        _LO.pop(pack.data_ptr(), None)
+    else:
+        _LO[pack.data_ptr()] = lo
 
 
 def lo_pack(w):
     """The [2][n] mid / lo bf16 packs of weight pack ``w`` (fp32 path), or None."""
-    return None if w is None else _LO.get(w.data_ptr())
+    if w is None:
+        return None
+    lo = _LO.get(w.data_ptr())
+    # an address can be reused by a later, unrelated pack: the entry must describe THIS one
+    if lo is None or lo.shape[-1] != w.numel() or lo.device != w.device:
+        return None
+    return lo
 
 
 def _f32o(t) -> int:
@@ -157,7 +167,10 @@ def same_pads(size: int, k: int, s: int, d: int = 1):
 _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                4: (128, 128), 5: (128, 64), 6: (64, 64), 7: (64, 128),
                8: (128, 128), 9: (128, 128), 10: (128, 64), 11: (64, 128),
-               12: (128, 128), 13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (64, 128)}
+               12: (128, 128), 13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (64, 128),
+               # 3x3 / stride-1 kernels with the input patch resident in LDS (conv3x3_patch.hip)
+               17: (128, 128), 18: (256, 128), 19: (256, 64), 20: (128, 64), 21: (128, 128)}
+PATCH_CFG0 = 17
 # weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
@@ -182,11 +195,24 @@ def wgrad_key(Nout: int, K: int, M: int, taps: int = 1):
     return ("wgrad", Nout, K, M, taps)
 
 
-def fwd_candidates(N: int):
+def fwd_candidates(N: int, patch: bool = False):
+    """Tile configs worth timing for a GEMM with N output columns; ``patch``: the problem is a
+    3x3 / stride-1 / pad-1 conv over a multiple of 64 channels (patch_eligible), so the
+    LDS-resident-patch kernels are candidates too."""
     if N <= 64:
-        return [1, 2, 5, 6, 10]
+        return [1, 2, 5, 6, 10] + ([19, 20] if patch else [])
     c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16]
-    return c + [15] if N > 128 else c
+    c = c + [15] if N > 128 else c
+    return c + ([17, 18, 19, 20, 21] if patch else [])
+
+
+def patch_eligible(spec: "ConvSpec", dgrad: bool = False) -> bool:
+    """The forward (or, ``dgrad``, the data-gradient) GEMM of this conv can run on the 3x3
+    patch kernels: 3x3, stride 1, pad 1 (same-size output), undilated, and the GEMM's input
+    channels (cin, or cout for the data gradient) a multiple of 64."""
+    c = spec.cout if dgrad else spec.cin_pad
+    return (spec.kh == 3 and spec.kw == 3 and spec.sh == 1 and spec.sw == 1 and spec.pt == 1 and spec.pl == 1
+            and spec.pb == 1 and spec.pr == 1 and spec.dh == 1 and spec.dw == 1 and c % 64 == 0)
 
 
 def wgrad_candidates(Nout: int, K: int, M: int):
@@ -235,6 +261,8 @@ def splitk_candidates(cfg: int, M: int, N: int, K: int):
     out = [1]
     for s in (2, 3, 4, 6, 8):
         if tiles * (s - 1) >= 2 * N_CU or ksteps // s < 4 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
+            break
+        if cfg >= PATCH_CFG0 and s > ksteps // 9:  # the patch kernels split over 64-channel slabs
             break
         out.append(s)
     return out
@@ -414,10 +442,13 @@ def _phase_pack(wtr, spec: ConvSpec, Cdz: int, rs, ss):
     C = spec.cin_pad
     K = len(rs) * len(ss) * Cdz
     lead = tuple(wtr.shape[:-1])  # () for a pack, (2,) for the fp32 path's mid / lo pair
-    key = (wtr.data_ptr(), lead, tuple(rs), tuple(ss))
+    # the sub-pack's CONTENT is refreshed below on every call; the key pins what must match for
+    # the buffer itself to be reusable (a freed pack's address can come back with another dtype,
+    # e.g. the fp16 build's packs followed by bf16 ones)
+    Kp = _round_up(K, 64)
+    key = (wtr.data_ptr(), wtr.dtype, wtr.device, lead, C, Kp, tuple(rs), tuple(ss))
     ent = _phase_packs.get(key)
     if ent is None:
-        Kp = _round_up(K, 64)
         taps = [(spec.kh - 1 - r) * spec.kw + (spec.kw - 1 - s) for r in rs for s in ss]
         ent = (torch.zeros(lead + (C, Kp), dtype=wtr.dtype, device=wtr.device),
                torch.tensor(taps, dtype=torch.int64, device=wtr.device))

@@ -147,11 +147,42 @@ struct ALoader {                                                       // ESZ: b
   }
 };
 
+// HCB_FRAG_SCHED (build define): 1 = issue every fragment read of the 64-deep k-step (both
+// 32-deep halves) before the first MFMA, behind a scheduling barrier, so the second half's LDS
+// reads overlap the first half's MFMAs (the compiler otherwise interleaves one read per MFMA
+// group with an lgkmcnt wait on it, exposing the LDS latency MI times per half)
+#ifndef HCB_FRAG_SCHED
+#define HCB_FRAG_SCHED 0
+#endif
 template <int WM, int WN, int TM, int TN>
 __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb, f32x4 (&acc)[TM / 16][TN / 16],
                                                int wm, int wn, int lane) {
   constexpr int MI = TM / 16, NI = TN / 16;
   const int frow = lane & 15, fq = lane >> 4;
+#if HCB_FRAG_SCHED
+  act16x8 af[2][MI], bfr[2][NI];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int ch = ks * 4 + fq;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * TM + i * 16 + frow;
+      af[ks][i] = __builtin_bit_cast(act16x8, Ab[row * 8 + (ch ^ ((row >> 1) & 7))]);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wn * TN + j * 16 + frow;
+      bfr[ks][j] = __builtin_bit_cast(act16x8, Bb[row * 8 + (ch ^ ((row >> 1) & 7))]);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[ks][i], bfr[ks][j], acc[i][j]);
+#else
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     act16x8 af[MI], bfr[NI];
@@ -173,6 +204,7 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
       for (int j = 0; j < NI; ++j)
         acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
   }
+#endif
 }
 
 // bf16x6 step of the fp32 path: the A / B tiles staged as three bf16 images each (hi, mid, lo
@@ -423,42 +455,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
                                    acc, wm, wn, lane);
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
-  if (S > 1) {
-    // split-K hand-off (cdna guide Guideline 16, counter form): park the partial tile, publish
-    // it with one agent-scope release + ticket; the last arriver acquires and sums the others.
-    constexpr int FR = MI * NI;  // f32x4 fragments per thread
-    f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)tile * S * FR * NT;
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) slab[((size_t)split * FR + i * NI + j) * NT + tid] = acc[i][j];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned t = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = t == (unsigned)(S - 1);
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      *flag = last;
-    }
-    __syncthreads();
-    const int last = *flag;
-    __syncthreads();  // the flag word is epilogue staging space next
-    if (!last) return;
-    for (int s2 = 0; s2 < S; ++s2) {
-      if (s2 == split) continue;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] += slab[((size_t)s2 * FR + i * NI + j) * NT + tid];
-    }
-  }
+  if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
   igemm_epilogue<WM, WN, TM, TN, BNB>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early,
                                       PARAM_LDS ? smem + PARAM_OFF : nullptr);
 }
@@ -567,14 +564,17 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
 // LDS-DMA ring (NST 3, 3, 4, 3); 8..11 deeper rings for latency-bound few-tile layers
 // (128x128 NST 4 and 5, 128x64 NST 6, 64x128 NST 6); 12..16 eight-wave workgroups (two
 // waves per SIMD when a layer has only ~1 tile per CU): 128x128 as 2x4 waves of 64x32 and as
-// 4x2 of 32x64, 256x128 (4x2 of 64x64), 128x256 (2x4 of 64x64), 64x128 (2x4 of 32x32)
-constexpr int N_CONV_CFG = 17;
+// 4x2 of 32x64, 256x128 (4x2 of 64x64), 128x256 (2x4 of 64x64), 64x128 (2x4 of 32x32);
+// 17..21 the 3x3 patch kernels (conv3x3_patch.hip): 128x128, 256x128, 256x64, 128x64, 128x128
+constexpr int N_CONV_CFG = 22;
 int conv_tile_m(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64, 128, 128, 256, 128, 64};
+  static const int t[N_CONV_CFG] = {128, 128, 64, 64, 128, 128, 64, 64, 128, 128, 128,
+                                    64,  128, 128, 256, 128, 64, 128, 256, 256, 128, 128};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64, 128, 128, 128, 128, 256, 128};
+  static const int t[N_CONV_CFG] = {128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64,
+                                    128, 128, 128, 128, 256, 128, 128, 128, 64, 64, 128};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 
@@ -607,6 +607,20 @@ void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
     const int bm = conv_tile_m(cfg), bn = conv_tile_n(cfg);
     const int rc = bm == 64 ? (bn == 64 ? 2 : 3) : 1;
     launch_cfg<false>(p, rc, st);
+    return;
+  }
+  if (cfg >= CONV_PATCH_CFG0) {
+    if (launch_conv3x3_patch(p, cfg, st)) return;
+    // not a 3x3 / stride-1 problem (or its patch does not fit LDS): an LDS-DMA kernel of the
+    // same row tile (so per-tile statistics slabs keep their size), without split-K
+    static const int fallback[N_CONV_CFG - CONV_PATCH_CFG0] = {13, 14, 14, 5, 13};
+    ConvParams q = p;
+    q.splits = 1;
+    cfg = fallback[(cfg - CONV_PATCH_CFG0) % (N_CONV_CFG - CONV_PATCH_CFG0)];
+    if (q.bnb_acc != nullptr)
+      launch_cfg<true>(q, cfg, st);
+    else
+      launch_cfg<false>(q, cfg, st);
     return;
   }
   if (p.bnb_acc != nullptr)

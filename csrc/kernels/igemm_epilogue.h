@@ -91,6 +91,49 @@ __device__ __forceinline__ void stage_bnb_params(const ConvParams& p, int n0, ch
   }
 }
 
+// In-launch split-K hand-off (cdna guide Guideline 16, counter form), shared by the LDS-DMA
+// kernels: every split parks its partial tile in a workspace slab, publishes it with one
+// agent-scope release + ticket; the last arriver acquires and sums the others into acc and
+// returns true (it then runs the epilogue), the others return false. Call after the main
+// loop's final barrier (smem word 0 is used as the broadcast flag).
+template <int MI, int NI, int NT>
+__device__ __forceinline__ bool splitk_gather(const ConvParams& p, f32x4 (&acc)[MI][NI], char* smem, int tile,
+                                              int split, int S, int tid) {
+  constexpr int FR = MI * NI;  // f32x4 fragments per thread
+  f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)tile * S * FR * NT;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) slab[((size_t)split * FR + i * NI + j) * NT + tid] = acc[i][j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == (unsigned)(S - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const int last = *flag;
+  __syncthreads();  // the flag word is epilogue staging space next
+  if (!last) return false;
+  for (int s2 = 0; s2 < S; ++s2) {
+    if (s2 == split) continue;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] += slab[((size_t)s2 * FR + i * NI + j) * NT + tid];
+  }
+  return true;
+}
+
 template <int WM, int WN, int TM, int TN, bool BNB>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)[TM / 16][TN / 16], char* smem,
                                                int tm, int m0, int n0, int wm, int wn, int lane, int tid,

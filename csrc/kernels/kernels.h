@@ -78,8 +78,16 @@ struct ConvParams {
   // Register-staged tile configs of <= 128x64 only, no split-K.
   const void* w_lo;
   const void* w_lo2;
+  // 3x3 / stride-1 patch kernels (conv3x3_patch.hip; set by their launcher): LDS rows reserved
+  // per input-patch buffer
+  int patch_rows;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
+// cfg >= CONV_PATCH_CFG0: the 3x3 / stride 1 / pad 1 kernels with the input patch resident in
+// LDS. Returns false (nothing launched) when the problem or the LDS budget does not fit them.
+constexpr int CONV_PATCH_CFG0 = 17;
+bool launch_conv3x3_patch(const ConvParams& p, int cfg, hipStream_t st);
+bool conv3x3_patch_eligible(const ConvParams& p);
 // deterministic reductions (misc.hip): colsum / BN-backward reduce grids limited so that
 // every fp32 accumulator slot receives a single add
 void set_deterministic(bool on);

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Drop the forward / data-grad (plain and fused BN-backward) entries of the in-tree autotune
 cache for the given model configs' problems and re-tune them (after a change to the conv
-kernels' launch resources); weight-grad entries are kept. Default: resnet50 bs64 only."""
+kernels' launch resources); weight-grad entries are kept. Default: resnet50 bs64 only.
+--taps T: drop only the entries of T-tap filters (e.g. 9 after a change to the 3x3 kernels)."""
 import os
 import shutil
 import sys
@@ -17,9 +18,16 @@ from tune_all import CONFIGS
 
 
 def main():
-    only = sys.argv[1:] or ["resnet50"]
+    args = sys.argv[1:]
+    taps = None
+    if "--taps" in args:
+        i = args.index("--taps")
+        taps = int(args[i + 1])
+        del args[i:i + 2]
+    only = args or ["resnet50"]
     autotune.load_cache()
-    dropped = [k for k in list(Fn._tuned) if isinstance(k, tuple) and k[0] in ("fwd", "dgb")]
+    dropped = [k for k in list(Fn._tuned) if isinstance(k, tuple) and k[0] in ("fwd", "dgb")
+               and (taps is None or k[-1] == taps)]
     for k in dropped:
         del Fn._tuned[k]
     print(f"dropped {len(dropped)} fwd/dgb entries", flush=True)
