@@ -4,17 +4,22 @@ Azure HC): hand-written HIP/CDNA4 kernels, HIP-graph captured training steps and
 Importing the package sets HIP runtime defaults that must be in place before the GPU is first
 touched (the HIP runtime reads them once, at initialisation):
 
-* ``DEBUG_CLR_GRAPH_PACKET_CAPTURE=0``: with the runtime's default pre-recorded graph packets,
-  training-step graphs that fork a communication stream (fork / join event edges, the
-  multi-GPU overlap path) intermittently ran kernels ahead of their predecessors on MI355X
-  (corrupted gradients within a few steps; reproduced with ``tools/dp_variants.sh`` even with
-  the collective itself removed). With it off the same graphs are exact and the step time is
-  unchanged (7.80 vs 7.81 ms/step, ResNet-50 bs=64). Set it explicitly to override.
-  Investigation (profiles/r2f_graph_packet_capture.txt): only graphs with SEVERAL fork/join
-  pairs between backward segments diverge (also with empty comm branches and with a distinct
-  event per edge); no-fork and single-fork step graphs, and the standalone fork/join repro
-  ``tools/graph_fork_repro.hip`` (same API sequence), are exact with packet capture on.
+* ``DEBUG_CLR_GRAPH_PACKET_CAPTURE=0`` (FORCED): with the runtime's default pre-recorded graph
+  packets the captured training step replays inexactly on MI355X -- the single-graph step (no
+  comm fork) diverges from its kernel-serialised run, and the data-parallel overlap step blows up
+  to inf/NaN in 4 of 6 runs -- while every API-level shape of that graph (forks, re-recorded join
+  events, memset nodes, cross-XCD and scalar-cache producer/consumer chains) replays exactly in
+  ``tools/graph_fork_repro.hip`` and no fusion switch removes it; no trigger smaller than the full
+  step was found (profiles/r2f_graph_packet_capture.txt, profiles/r3_packet_capture_recheck.txt).
+  With packet capture off every graph is exact and the step time is unchanged. A value of 1 set
+  by the user is overridden (with a warning): it would silently corrupt training. (Investigation
+  tools re-set it in os.environ after this import and before the GPU is first touched.)
 """
 import os as _os
+import warnings as _warnings
 
-_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+if _os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0") != "0":
+    _warnings.warn("azure_hc_intel_tf_amd: DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 makes the captured training step "
+                   "replay inexactly on MI355X (profiles/r3_packet_capture_recheck.txt); forcing it to 0",
+                   RuntimeWarning, stacklevel=2)
+_os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = "0"

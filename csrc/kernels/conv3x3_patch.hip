@@ -86,7 +86,7 @@ __device__ __forceinline__ u32x4 frag_read(const u32x4* base, int row, int ch, i
 }
 
 #ifndef HCB_FRAG_SCHED
-#define HCB_FRAG_SCHED 0
+#define HCB_FRAG_SCHED 1
 #endif
 template <int WM, int WN, int TM, int TN>
 __device__ __forceinline__ void mfma_patch_step(const u32x4* Pb, const u32x4* Bb, const int (&prow)[TM / 16], int tapoff,

@@ -151,15 +151,20 @@ struct ALoader {                                                       // ESZ: b
 // 32-deep halves) before the first MFMA, behind a scheduling barrier, so the second half's LDS
 // reads overlap the first half's MFMAs (the compiler otherwise interleaves one read per MFMA
 // group with an lgkmcnt wait on it, exposing the LDS latency MI times per half)
+// (on for the LDS-DMA and patch kernels: +0.7% bench after a retune, 3-8% on the 3x3 layers;
+// HCB_FRAG_SCHED_REG the same for the register-staged kernels, whose prefetch registers it competes with)
 #ifndef HCB_FRAG_SCHED
-#define HCB_FRAG_SCHED 0
+#define HCB_FRAG_SCHED 1
 #endif
-template <int WM, int WN, int TM, int TN>
+#ifndef HCB_FRAG_SCHED_REG
+#define HCB_FRAG_SCHED_REG 0
+#endif
+template <int WM, int WN, int TM, int TN, bool SCHED = false>
 __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb, f32x4 (&acc)[TM / 16][TN / 16],
                                                int wm, int wn, int lane) {
   constexpr int MI = TM / 16, NI = TN / 16;
   const int frow = lane & 15, fq = lane >> 4;
-#if HCB_FRAG_SCHED
+  if constexpr (SCHED) {
   act16x8 af[2][MI], bfr[2][NI];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
@@ -182,7 +187,7 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[ks][i], bfr[ks][j], acc[i][j]);
-#else
+  } else {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     act16x8 af[MI], bfr[NI];
@@ -204,7 +209,7 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
       for (int j = 0; j < NI; ++j)
         acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
   }
-#endif
+  }
 }
 
 // bf16x6 step of the fp32 path: the A / B tiles staged as three bf16 images each (hi, mid, lo
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
       mfma_tile_step6<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, NB * BM * 8, NB * BN * 8, acc, wm,
                                       wn, lane);
     else
-      mfma_tile_step<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
+      mfma_tile_step<WM, WN, TM, TN, HCB_FRAG_SCHED_REG>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
@@ -451,7 +456,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
     asm volatile("" ::: "memory");
     if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, kb + kt + NST - 1);
     const char* sb = smem + (kt % NST) * STAGE;
-    mfma_tile_step<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + BM * 128),
+    mfma_tile_step<WM, WN, TM, TN, HCB_FRAG_SCHED>(reinterpret_cast<const u32x4*>(sb),
+                                                   reinterpret_cast<const u32x4*>(sb + BM * 128),
                                    acc, wm, wn, lane);
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
