@@ -77,8 +77,14 @@ def test_shallow_net_gradients_elementwise_vs_fp32_cpu():
     """Stem + one bottleneck block: every parameter gradient of the GPU backward against the
     fp32 CPU path, element by element (max error scaled by each tensor's largest gradient).
 
-    * The fp32 reference-precision GPU path must agree to fp32 rounding (<1e-3): this pins the
-      comparison itself.
+    * The fp32 reference-precision GPU path must agree to fp32 rounding: 1e-6-level relative
+      errors (measured 1e-7..5e-6 per tensor). It is only bounded at 5e-3 / cosine 0.99999 because
+      ReLU is discontinuous: the block output holds ~262k exact zeros, and ONE element whose
+      pre-activation lies within fp32 rounding of 0 can land on the other side of the mask than in
+      the CPU run (it depends on the fp32 atomic order of the BN statistics); that single flip
+      shifts the first BN backward's dgamma by 4e-4 and, through the BN mean subtraction, every
+      earlier gradient by ~1.8e-3 (tools/diag_fp32_shallow.py --bncmp: "relu mask flips: 1 of
+      524288"). A real fp32 defect (e.g. a two-term bf16 split, 2^-17) shows up as >1e-2.
     * The hand-written bf16 path (bf16 activations, fused BN epilogues, space-to-depth stem):
       measured on MI355X the error grows with backward depth -- classifier 0.3 %, block
       conv3 / BN 1.5 %, conv2 ~10 %, conv1 / stem ~12-15 % of the largest gradient, every tensor
@@ -101,7 +107,7 @@ def test_shallow_net_gradients_elementwise_vs_fp32_cpu():
     torch.cuda.synchronize()
     for err, rel, cos, name in _grad_errors(mf, mc):
         print("fp32 GPU grad check", err, rel, cos, name)
-        assert err < 1e-3 and rel < 1e-3, (name, err, rel)
+        assert rel < 5e-3 and err < 5e-2 and cos > 0.99999, (name, err, rel, cos)
     for err, rel, cos, name in _grad_errors(mg, mc):
         print("bf16 GPU grad check", err, rel, cos, name)
         assert err < 0.25 and rel < 0.2 and cos > 0.985, (name, err, rel, cos)
