@@ -169,8 +169,11 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                8: (128, 128), 9: (128, 128), 10: (128, 64), 11: (64, 128),
                12: (128, 128), 13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (64, 128),
                # 3x3 / stride-1 kernels with the input patch resident in LDS (conv3x3_patch.hip)
-               17: (128, 128), 18: (256, 128), 19: (256, 64), 20: (128, 64), 21: (128, 128)}
+               17: (128, 128), 18: (256, 128), 19: (256, 64), 20: (128, 64), 21: (128, 128),
+               # LDS-DMA rings with two 64-deep k-steps per stage (one barrier per 128 of K)
+               22: (64, 128), 23: (128, 128), 24: (128, 128), 25: (64, 128), 26: (64, 64)}
 PATCH_CFG0 = 17
+PATCH_CFGS = (17, 18, 19, 20, 21)
 # weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
@@ -199,6 +202,9 @@ def fwd_candidates(N: int, patch: bool = False):
     """Tile configs worth timing for a GEMM with N output columns; ``patch``: the problem is a
     3x3 / stride-1 / pad-1 conv over a multiple of 64 channels (patch_eligible), so the
     LDS-resident-patch kernels are candidates too."""
+    # (cfg 22-26, two k-steps per LDS-DMA stage, are not offered: they win the isolated per-layer
+    # timing -- stage-3 3x3 23.2 vs 24.3 us -- but a cache that picks them runs the whole step 1.2%
+    # slower, same box, 3 alternating runs: profiles/r3x_ku2_cache_ab.txt)
     if N <= 64:
         return [1, 2, 5, 6, 10] + ([19, 20] if patch else [])
     c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16]
@@ -262,7 +268,7 @@ def splitk_candidates(cfg: int, M: int, N: int, K: int):
     for s in (2, 3, 4, 6, 8):
         if tiles * (s - 1) >= 2 * N_CU or ksteps // s < 4 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
             break
-        if cfg >= PATCH_CFG0 and s > ksteps // 9:  # the patch kernels split over 64-channel slabs
+        if cfg in PATCH_CFGS and s > ksteps // 9:  # the patch kernels split over 64-channel slabs
             break
         out.append(s)
     return out

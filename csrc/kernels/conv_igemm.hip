@@ -370,15 +370,18 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB>
+// KU: 64-deep k-steps per ring stage (one wait + barrier per stage: KU = 2 halves the barriers
+// and doubles the MFMA run between them; a block's last stage may carry an all-zero k-step)
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB, int KU = 1>
 __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, RP = NT / 8;  // threads; tile rows per load pass
   constexpr int AV = BM / RP, BV = BN / RP;
-  constexpr int LOADS = AV + BV;  // LDS-DMA instructions per thread per stage
-  constexpr int STAGE = (BM + BN) * 128;
-  static_assert((WM * WN == 4 || WM * WN == 8) && NST >= 2 && NST <= 6, "config");
+  constexpr int LOADS = KU * (AV + BV);  // LDS-DMA instructions per thread per stage
+  constexpr int SUB = (BM + BN) * 128;   // one k-step's A + B image
+  constexpr int STAGE = KU * SUB;
+  static_assert((WM * WN == 4 || WM * WN == 8) && NST >= 2 && NST <= 6 && (KU == 1 || KU == 2), "config");
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 2) <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -413,31 +416,39 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto issue = [&](int stage, int kt) {
-    uint32_t off[AV];
-    al.offsets(p, kt, chunk, off);
-    char* sbase = smem + stage * STAGE;
-#pragma unroll
-    for (int v = 0; v < AV; ++v) glds16(xr, sbase + (wid * 8 + RP * v) * 128, off[v]);
-#pragma unroll
-    for (int v = 0; v < BV; ++v)
-      glds16(wr, sbase + BM * 128 + (wid * 8 + RP * v) * 128,
-             b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
-  };
-
   const int nk_all = p.Kpad / BK;
-  const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's k-steps
+  const int kb = split * nk_all / S, nk_steps = (split + 1) * nk_all / S - kb;  // this block's k-steps
+  // stage g holds k-steps kb + g*KU + u; one past the block's range (odd count, KU = 2) is
+  // loaded as zeros (out-of-range offsets), so its MFMAs add nothing
+  auto issue = [&](int stage, int g) {
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int kl = g * KU + u;
+      const bool live = KU == 1 || kl < nk_steps;
+      const int kt = kb + kl;
+      uint32_t off[AV];
+      if (live) al.offsets(p, kt, chunk, off);
+      char* sbase = smem + stage * STAGE + u * SUB;
+#pragma unroll
+      for (int v = 0; v < AV; ++v) glds16(xr, sbase + (wid * 8 + RP * v) * 128, live ? off[v] : HCB_OOB);
+#pragma unroll
+      for (int v = 0; v < BV; ++v)
+        glds16(wr, sbase + BM * 128 + (wid * 8 + RP * v) * 128,
+               (!live || b_off[v] == HCB_OOB) ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
+    }
+  };
+  const int nk = (nk_steps + KU - 1) / KU;  // ring stages of this block
   if (kb > 0) al.seek(p, kb);
   EpiPrefetch<WM, WN, TM, TN, BNB> pre;
   pre.load_shift(p, n0, wn, lane);
-  constexpr size_t PARAM_OFF = glds_param_off(BM, BN, WM, NST);
+  constexpr size_t PARAM_OFF = glds_param_off(BM, BN, WM, NST * KU);
   constexpr bool PARAM_LDS = PARAM_OFF + bnb_param_lds(BN) <= 160 * 1024;
   if constexpr (BNB && PARAM_LDS) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
-  const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS;
+  const bool early = BNB && S == 1 && nk_steps <= EARLY_EPI_KSTEPS;
   if (early) pre.load(p, 0, m0, n0, tid);
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
-    if (s < nk) issue(s, kb + s);
+    if (s < nk) issue(s, s);
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed for this thread once at most min(NST-2, nk-1-kt) later stages
     // are still outstanding; the barrier then publishes every thread's DMA.
@@ -454,11 +465,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
       wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, kb + kt + NST - 1);
-    const char* sb = smem + (kt % NST) * STAGE;
-    mfma_tile_step<WM, WN, TM, TN, HCB_FRAG_SCHED>(reinterpret_cast<const u32x4*>(sb),
-                                                   reinterpret_cast<const u32x4*>(sb + BM * 128),
-                                   acc, wm, wn, lane);
+    if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, kt + NST - 1);
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const char* sb = smem + (kt % NST) * STAGE + u * SUB;
+      mfma_tile_step<WM, WN, TM, TN, HCB_FRAG_SCHED>(reinterpret_cast<const u32x4*>(sb),
+                                                     reinterpret_cast<const u32x4*>(sb + BM * 128), acc, wm, wn, lane);
+    }
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
   if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
@@ -529,40 +542,41 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>), dim3(tiles), dim3(256), lds, st, p);
 }
 
-template <int WM, int WN, int TM, int TN, int NST, bool BNB>
+template <int WM, int WN, int TM, int TN, int NST, bool BNB, int KU = 1>
 static void launch_glds(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
-  // a block never touches more ring stages than it has k-steps: short-K layers (1x1 over 64-256
+  // a block never touches more ring stages than it has: short-K layers (1x1 over 64-256
   // channels: 1-4 k-steps) get the LDS of the stages they use, so more workgroups fit per CU
   const int ksteps = (p.Kpad / 64 + p.splits - 1) / p.splits;
-  const int stages = ksteps < NST ? (ksteps > 0 ? ksteps : 1) : NST;
-  size_t lds_main = (size_t)stages * (BM + BN) * 128;
+  const int groups = (ksteps + KU - 1) / KU;
+  const int stages = groups < NST ? (groups > 0 ? groups : 1) : NST;
+  size_t lds_main = (size_t)stages * KU * (BM + BN) * 128;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-  if (BNB && glds_param_off(BM, BN, WM, NST) + bnb_param_lds(BN) <= 160 * 1024)
-    lds = glds_param_off(BM, BN, WM, NST) + bnb_param_lds(BN);
+  if (BNB && glds_param_off(BM, BN, WM, NST * KU) + bnb_param_lds(BN) <= 160 * 1024)
+    lds = glds_param_off(BM, BN, WM, NST * KU) + bnb_param_lds(BN);
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>), dim3(tiles), dim3(NT),
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU>), dim3(tiles), dim3(NT),
                        lds, st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU>), dim3(tiles), dim3(NT), lds,
                        st, p);
 }
 
@@ -571,16 +585,18 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
 // (128x128 NST 4 and 5, 128x64 NST 6, 64x128 NST 6); 12..16 eight-wave workgroups (two
 // waves per SIMD when a layer has only ~1 tile per CU): 128x128 as 2x4 waves of 64x32 and as
 // 4x2 of 32x64, 256x128 (4x2 of 64x64), 128x256 (2x4 of 64x64), 64x128 (2x4 of 32x32);
-// 17..21 the 3x3 patch kernels (conv3x3_patch.hip): 128x128, 256x128, 256x64, 128x64, 128x128
-constexpr int N_CONV_CFG = 22;
+// 17..21 the 3x3 patch kernels (conv3x3_patch.hip): 128x128, 256x128, 256x64, 128x64, 128x128;
+// 22..26 LDS-DMA rings with two k-steps per stage (KU = 2): 64x128 (1x4 waves of 64x32),
+// 128x128 (4x2 of 32x64), 128x128 (2x4 of 64x32), 64x128 (2x4 of 32x32), 64x64 (2x2 of 32x32)
+constexpr int N_CONV_CFG = 27;
 int conv_tile_m(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 128, 64, 64, 128, 128, 64, 64, 128, 128, 128,
-                                    64,  128, 128, 256, 128, 64, 128, 256, 256, 128, 128};
+  static const int t[N_CONV_CFG] = {128, 128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128,
+                                    256, 128, 64,  128, 256, 256, 128, 128, 64,  128, 128, 64, 64};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 64, 64, 128, 128, 64, 64, 128, 128, 128, 64,
-                                    128, 128, 128, 128, 256, 128, 128, 128, 64, 64, 128};
+  static const int t[N_CONV_CFG] = {128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 128,
+                                    128, 256, 128, 128, 128, 64,  64,  128, 128, 128, 128, 128, 64};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 
@@ -604,6 +620,11 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
     case 14: launch_glds<4, 2, 64, 64, 3, BNB>(p, st); break;
     case 15: launch_glds<2, 4, 64, 64, 3, BNB>(p, st); break;
     case 16: launch_glds<2, 4, 32, 32, 4, BNB>(p, st); break;
+    case 22: launch_glds<1, 4, 64, 32, 2, BNB, 2>(p, st); break;
+    case 23: launch_glds<4, 2, 32, 64, 2, BNB, 2>(p, st); break;
+    case 24: launch_glds<2, 4, 64, 32, 2, BNB, 2>(p, st); break;
+    case 25: launch_glds<2, 4, 32, 32, 2, BNB, 2>(p, st); break;
+    case 26: launch_glds<2, 2, 32, 32, 3, BNB, 2>(p, st); break;
     default: launch_reg<2, 2, 64, 64, BNB>(p, st); break;
   }
 }
@@ -615,14 +636,14 @@ void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
     launch_cfg<false>(p, rc, st);
     return;
   }
-  if (cfg >= CONV_PATCH_CFG0) {
+  if (cfg >= CONV_PATCH_CFG0 && cfg < CONV_PATCH_CFG0 + 5) {
     if (launch_conv3x3_patch(p, cfg, st)) return;
     // not a 3x3 / stride-1 problem (or its patch does not fit LDS): an LDS-DMA kernel of the
     // same row tile (so per-tile statistics slabs keep their size), without split-K
-    static const int fallback[N_CONV_CFG - CONV_PATCH_CFG0] = {13, 14, 14, 5, 13};
+    static const int fallback[5] = {13, 14, 14, 5, 13};
     ConvParams q = p;
     q.splits = 1;
-    cfg = fallback[(cfg - CONV_PATCH_CFG0) % (N_CONV_CFG - CONV_PATCH_CFG0)];
+    cfg = fallback[cfg - CONV_PATCH_CFG0];
     if (q.bnb_acc != nullptr)
       launch_cfg<true>(q, cfg, st);
     else

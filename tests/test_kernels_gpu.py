@@ -78,7 +78,8 @@ def test_conv_fwd_and_stats(case):
 
 @pytest.mark.parametrize("case", CONV_CASES[:-1], ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}{c[3]}s{c[4]}")
 def test_conv_lds_dma_kernels_all_geometries(case):
-    """The LDS-DMA ring kernels (cfg 4-7) on every geometry, forward and data-gradient."""
+    """The LDS-DMA ring kernels (cfg 4-16, and 22-26 with two k-steps per ring stage) on every
+    geometry, forward and data-gradient."""
     cin, cout, kh, kw, s, pads, H = case
     torch.manual_seed(12)
     cpad = cin if cin % 8 == 0 else 8
@@ -90,7 +91,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
     dz = bf(torch.randn(N, P, Q, cout, device=DEV))
     dref = torch.empty(N, H, H, cpad)
     Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), dref, False)
-    for cfg in range(4, 17):
+    for cfg in list(range(4, 17)) + [22, 23, 24, 25, 26]:
         y = torch.empty(N, P, Q, cout, dtype=torch.bfloat16, device=DEV)
         slab = torch.empty(math.ceil(N * P * Q / Fn._CONV_TILES[cfg][0]) * 2 * cout, device=DEV)
         Fn.conv_forward(x, spec, pk.pack, p.data, y, stats=slab, cfg=cfg)
@@ -101,7 +102,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
             assert rel_err(dx, dref) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("cfg", list(range(17)))
+@pytest.mark.parametrize("cfg", list(range(27)))
 def test_conv_fwd_all_tile_configs(cfg):
     torch.manual_seed(1)
     spec, p, pk = make_conv(128, 192, 3, 3, 1, 1, (1, 1, 1, 1))
@@ -111,7 +112,8 @@ def test_conv_fwd_all_tile_configs(cfg):
     assert rel_err(y, cpu_ref_conv(x, spec, bf(p.data))) < 1e-2
 
 
-@pytest.mark.parametrize("plan", [(4, 2), (4, 3), (12, 2), (13, 4), (14, 2), (16, 3), (6, 5)])
+@pytest.mark.parametrize("plan", [(4, 2), (4, 3), (12, 2), (13, 4), (14, 2), (16, 3), (6, 5), (22, 3), (23, 2),
+                                  (26, 5)])
 def test_conv_split_k_in_launch_reduction(plan):
     """split-K: partial tiles parked in the workspace, the last arriver (agent-scope ticket)
     sums them and runs the normal epilogue (BN statistics, beta-accumulate, BN-bwd fusion)."""
@@ -177,7 +179,7 @@ def test_conv_dgrad(case, accumulate):
                          ids=["1x1", "3x3", "1x1s2", "cin80"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [2, 4, 12])
+@pytest.mark.parametrize("cfg", [2, 4, 12, 23, 26])
 def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
     """data-grad GEMM with the consuming BN layer's ReLU gating and backward sums fused into
     its epilogue (ConvParams::bnb_*), vs the CPU gating + fp32 reductions."""

@@ -26,7 +26,7 @@ def fetched_mb(cfg, M, N, C, H, W):
     tiles_m, tiles_n = math.ceil(M / bm), math.ceil(N / bn)
     K = 9 * C
     b = tiles_m * tiles_n * K * bn * 2  # weight tiles
-    if cfg >= Fn.PATCH_CFG0:
+    if cfg in Fn.PATCH_CFGS:
         span = bm + 2 * math.ceil(bm / W) + 2 * (W + 2) + 3  # typical (non image-crossing) patch
         b += tiles_m * tiles_n * (C // 64) * span * 128
     else:
@@ -91,7 +91,7 @@ def main():
         flop = 2.0 * M * ncol * 9 * (C if a.which == "fwd" else K)
         print(f"== {layer.name} {a.which} M={M} N={ncol} K={9 * (C if a.which == 'fwd' else K)} H={H}", flush=True)
         for us, cfg, sp, mb in rows[:a.top]:
-            tag = "patch" if cfg >= Fn.PATCH_CFG0 else "igemm"
+            tag = "patch" if cfg in Fn.PATCH_CFGS else ("igemm-ku2" if cfg >= 22 else "igemm")
             print(f"   cfg {cfg:2d} x{sp} {tag} {Fn._CONV_TILES[cfg]}: {us:7.1f} us  {flop / us / 1e6:6.0f} TF  "
                   f"fetch {mb:6.0f} MB = {mb / us:5.1f} TB/s", flush=True)
 
