@@ -62,10 +62,28 @@ def save_cache(path: str = DEFAULT_CACHE) -> None:
         json.dump({"arch": "gfx950", "version": CACHE_VERSION, "entries": old}, f, indent=0, sort_keys=True)
 
 
+_SCRATCH = {}
+
+
 def _time(fn, reps=None) -> float:
     # HCB_TUNE_REPS: timed launches per candidate (default 5; more = less noise, slower tuning)
     reps = reps or int(os.environ.get("HCB_TUNE_REPS", "5"))
     fn()
+    if os.environ.get("HCB_TUNE_ISOLATE") == "1":
+        # step-like timing: each launch timed on its own, after a 64 MB write that evicts the
+        # candidate's operands from L2 and ends any overlap with the previous launch (back-to-back
+        # launches of one kernel favour configs the training step does not: profiles/r3x_ku2_cache_ab.txt)
+        buf = _SCRATCH.get("buf")
+        if buf is None:
+            buf = _SCRATCH["buf"] = torch.empty(16 << 20, dtype=torch.float32, device="cuda")
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for s, e in ev:
+            buf.fill_(1.0)
+            s.record()
+            fn()
+            e.record()
+        ev[-1][1].synchronize()
+        return sorted(s.elapsed_time(e) for s, e in ev)[reps // 2]
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
     s.record()

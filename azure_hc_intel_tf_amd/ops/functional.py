@@ -202,12 +202,13 @@ def fwd_candidates(N: int, patch: bool = False):
     """Tile configs worth timing for a GEMM with N output columns; ``patch``: the problem is a
     3x3 / stride-1 / pad-1 conv over a multiple of 64 channels (patch_eligible), so the
     LDS-resident-patch kernels are candidates too."""
-    # (cfg 22-26, two k-steps per LDS-DMA stage, are not offered: they win the isolated per-layer
-    # timing -- stage-3 3x3 23.2 vs 24.3 us -- but a cache that picks them runs the whole step 1.2%
-    # slower, same box, 3 alternating runs: profiles/r3x_ku2_cache_ab.txt)
+    # cfg 22-26 (two k-steps per LDS-DMA stage) only with HCB_TUNE_KU2=1: under back-to-back
+    # timing they win per layer (stage-3 3x3 23.2 vs 24.3 us) yet the step runs 1.2% slower with
+    # them (profiles/r3x_ku2_cache_ab.txt)
+    ku2 = [22, 23, 24, 25, 26] if os.environ.get("HCB_TUNE_KU2") == "1" else []
     if N <= 64:
-        return [1, 2, 5, 6, 10] + ([19, 20] if patch else [])
-    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16]
+        return [1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([19, 20] if patch else [])
+    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2
     c = c + [15] if N > 128 else c
     return c + ([17, 18, 19, 20, 21] if patch else [])
 
