@@ -55,53 +55,30 @@ __device__ __forceinline__ int patch_lp(const ConvParams& p, int m) {
   return (n * (p.H + 2) + pp) * (p.W + 2) + qq;
 }
 
-// Diagnostic builds only (tools/build_variant.py -DHCB_PATCH_ABLATE=n): 1 skips the patch loads
-// after the first slab, 2 the weight-tile loads, 3 both (numerically wrong; timing bounds)
-#ifndef HCB_PATCH_ABLATE
-#define HCB_PATCH_ABLATE 0
-#endif
-// Fragment reads. The patch rows a fragment reads start at an arbitrary row (the tap offset), so
-// the 16-byte XOR-swizzled reads of the generic kernels conflict: a ds_read_b128 lane group mixes
-// two k-chunk columns (lanes 0-3,12-15 of one, 4-11 of the next) over 16 rows, and with a start
-// row off the 16-row grid the two halves land on common banks (measured 32-39% extra LDS cycles).
-// Here every fragment is two ds_read_b64: a lane of an even k-chunk column reads its chunk's low
-// half first, a lane of an odd column its high half first, so in each instruction the two columns
-// of a 32-lane group occupy disjoint bank halves, and 16 consecutive rows of one column are
-// distinct banks for ANY start row ((row & 1, (row >> 1) & 7) is a bijection of row mod 16). The
-// odd columns thus hold their k-chunk as (high, low): the weight fragments are read the same way,
-// so every MFMA pairs the same k indices (a per-lane permutation of the dot product's terms).
-#ifndef HCB_PATCH_B64
-#define HCB_PATCH_B64 0
-#endif
-__device__ __forceinline__ u32x4 frag_read(const u32x4* base, int row, int ch, int fq) {
-  const int idx = row * 8 + (ch ^ ((row >> 1) & 7));
-#if HCB_PATCH_B64
-  const u32x2* b2 = reinterpret_cast<const u32x2*>(base) + idx * 2;
-  const int h = fq & 1;
-  const u32x2 lo = b2[h], hi = b2[h ^ 1];
-  return u32x4{lo[0], lo[1], hi[0], hi[1]};
-#else
-  return base[idx];
-#endif
+// Fragment reads: 16-byte XOR-swizzled ds_read_b128 as in the generic kernels. The patch rows a
+// fragment reads start at an arbitrary row (the tap offset), so a b128 lane group (lanes 0-3,12-15
+// of one k-chunk column and 4-11 of the next) can meet 2-way bank conflicts (32-39% extra LDS
+// cycles measured); a conflict-free form with two ds_read_b64 per fragment (each column's halves
+// read in opposite order) was measured slower -- twice the LDS instructions cost more than the
+// conflicts (profiles/r3k_patch_sched_retune.txt, variant b128 vs main).
+__device__ __forceinline__ u32x4 frag_read(const u32x4* base, int row, int ch) {
+  return base[row * 8 + (ch ^ ((row >> 1) & 7))];
 }
 
-#ifndef HCB_FRAG_SCHED
-#define HCB_FRAG_SCHED 1
-#endif
+// every fragment read of the step first, then the MFMAs (see conv_igemm.hip mfma_tile_step SCHED)
 template <int WM, int WN, int TM, int TN>
 __device__ __forceinline__ void mfma_patch_step(const u32x4* Pb, const u32x4* Bb, const int (&prow)[TM / 16], int tapoff,
                                                 f32x4 (&acc)[TM / 16][TN / 16], int wn, int lane) {
   constexpr int MI = TM / 16, NI = TN / 16;
   const int frow = lane & 15, fq = lane >> 4;
-#if HCB_FRAG_SCHED  // every fragment read of the step first (see conv_igemm.hip mfma_tile_step)
   act16x8 af[2][MI], bfr[2][NI];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int ch = ks * 4 + fq;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) af[ks][i] = __builtin_bit_cast(act16x8, frag_read(Pb, prow[i] + tapoff, ch, fq));
+    for (int i = 0; i < MI; ++i) af[ks][i] = __builtin_bit_cast(act16x8, frag_read(Pb, prow[i] + tapoff, ch));
 #pragma unroll
-    for (int j = 0; j < NI; ++j) bfr[ks][j] = __builtin_bit_cast(act16x8, frag_read(Bb, wn * TN + j * 16 + frow, ch, fq));
+    for (int j = 0; j < NI; ++j) bfr[ks][j] = __builtin_bit_cast(act16x8, frag_read(Bb, wn * TN + j * 16 + frow, ch));
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -110,21 +87,6 @@ __device__ __forceinline__ void mfma_patch_step(const u32x4* Pb, const u32x4* Bb
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[ks][i], bfr[ks][j], acc[i][j]);
-#else
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int ch = ks * 4 + fq;
-    act16x8 af[MI], bfr[NI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i) af[i] = __builtin_bit_cast(act16x8, frag_read(Pb, prow[i] + tapoff, ch, fq));
-#pragma unroll
-    for (int j = 0; j < NI; ++j) bfr[j] = __builtin_bit_cast(act16x8, frag_read(Bb, wn * TN + j * 16 + frow, ch, fq));
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-  }
-#endif
 }
 
 // LDS bytes of the main loop / the BN-backward parameter offset, shared by kernel and launcher
@@ -227,16 +189,14 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch_kernel(ConvParams p
   };
   // group g: the weight tile of step g, then (tap NST-1 of a slab with a successor) the next
   // slab's patch
-  auto carries = [&](int g) { return !(HCB_PATCH_ABLATE & 1) && g % 9 == NST - 1 && g / 9 + 1 < nslab; };
+  auto carries = [&](int g) { return g % 9 == NST - 1 && g / 9 + 1 < nslab; };
   auto issue = [&](int g) {
     const int sl = g / 9, t = g - sl * 9;
     char* sb = ring + (g % NST) * BSTAGE;
     const uint32_t kb = (uint32_t)(t * p.C + (cs0 + sl) * 64) * 2u;
-    if (!(HCB_PATCH_ABLATE & 2)) {
 #pragma unroll
-      for (int v = 0; v < BV; ++v)
-        glds16(wr, sb + (wid * 8 + RP * v) * 128, b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + kb);
-    }
+    for (int v = 0; v < BV; ++v)
+      glds16(wr, sb + (wid * 8 + RP * v) * 128, b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + kb);
     if (carries(g)) load_patch(sl + 1);
   };
 
@@ -249,7 +209,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch_kernel(ConvParams p
     // its own patch loads (if it carries the next patch) and the groups k+1 .. k+ahead
     const int ahead = min(NST - 2, nk - 1 - k);
     int cnt = carries(k) ? passes : 0;
-    for (int a = 1; a <= ahead; ++a) cnt += ((HCB_PATCH_ABLATE & 2) ? 0 : BV) + (carries(k + a) ? passes : 0);
+    for (int a = 1; a <= ahead; ++a) cnt += BV + (carries(k + a) ? passes : 0);
     wait_vmcnt_rt(cnt);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");

@@ -147,18 +147,12 @@ struct ALoader {                                                       // ESZ: b
   }
 };
 
-// HCB_FRAG_SCHED (build define): 1 = issue every fragment read of the 64-deep k-step (both
-// 32-deep halves) before the first MFMA, behind a scheduling barrier, so the second half's LDS
-// reads overlap the first half's MFMAs (the compiler otherwise interleaves one read per MFMA
-// group with an lgkmcnt wait on it, exposing the LDS latency MI times per half)
-// (on for the LDS-DMA and patch kernels: +0.7% bench after a retune, 3-8% on the 3x3 layers;
-// HCB_FRAG_SCHED_REG the same for the register-staged kernels, whose prefetch registers it competes with)
-#ifndef HCB_FRAG_SCHED
-#define HCB_FRAG_SCHED 1
-#endif
-#ifndef HCB_FRAG_SCHED_REG
-#define HCB_FRAG_SCHED_REG 0
-#endif
+// SCHED: issue every fragment read of the 64-deep k-step (both 32-deep halves) before the first
+// MFMA, behind a scheduling barrier, so the second half's LDS reads overlap the first half's MFMAs
+// (the compiler otherwise interleaves one read per MFMA group with an lgkmcnt wait on it, exposing
+// the LDS latency MI times per half). On for the LDS-DMA and patch kernels (3-8% on the 3x3
+// layers, +0.7% step after a retune); measured neutral on the register-staged kernels, whose
+// prefetch registers it competes with, so off there (profiles/r3k_patch_sched_retune.txt).
 template <int WM, int WN, int TM, int TN, bool SCHED = false>
 __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb, f32x4 (&acc)[TM / 16][TN / 16],
                                                int wm, int wn, int lane) {
@@ -357,7 +351,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
       mfma_tile_step6<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, NB * BM * 8, NB * BN * 8, acc, wm,
                                       wn, lane);
     else
-      mfma_tile_step<WM, WN, TM, TN, HCB_FRAG_SCHED_REG>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
+      mfma_tile_step<WM, WN, TM, TN, false>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
@@ -469,7 +463,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParam
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const char* sb = smem + (kt % NST) * STAGE + u * SUB;
-      mfma_tile_step<WM, WN, TM, TN, HCB_FRAG_SCHED>(reinterpret_cast<const u32x4*>(sb),
+      mfma_tile_step<WM, WN, TM, TN, true>(reinterpret_cast<const u32x4*>(sb),
                                                      reinterpret_cast<const u32x4*>(sb + BM * 128), acc, wm, wn, lane);
     }
   }
