@@ -119,16 +119,31 @@ struct ALoader {                                                       // ESZ: b
       }
     } else {
       const int k0 = kt * 64;
-      int tap, c;
+      int tap, c, r, s;
       if constexpr (CBIG) {
         tap = k0 / p.C;
         c = k0 - tap * p.C + chunk * 8;
       } else {
-        int k = k0 + chunk * 8;
-        tap = k / p.C;
-        c = k - tap * p.C;
+        // per-lane k (the chunk): shifts when C is a power of two (the space-to-depth stem's 16
+        // channels) instead of a VALU integer division per thread and k-step
+        const int k = k0 + chunk * 8;
+        if ((p.C & (p.C - 1)) == 0) {
+          const int lc = __builtin_ctz((unsigned)p.C);
+          tap = k >> lc;
+          c = k & (p.C - 1);
+        } else {
+          tap = k / p.C;
+          c = k - tap * p.C;
+        }
       }
-      const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+      if ((p.S & (p.S - 1)) == 0) {
+        const int ls = __builtin_ctz((unsigned)p.S);
+        r = tap >> ls;
+        s = tap & (p.S - 1);
+      } else {
+        r = tap / p.S;
+        s = tap - r * p.S;
+      }
       const bool tap_ok = tap < p.R * p.S;
 #pragma unroll
       for (int v = 0; v < AV; ++v) {
