@@ -63,13 +63,17 @@ def save_cache(path: str = DEFAULT_CACHE) -> None:
 
 
 _SCRATCH = {}
+# per-launch isolated timing (module switch): each candidate launch timed on its own after a 64 MB
+# eviction write, median of the launches. Measured against the default back-to-back timing:
+# +0.3% step (within run-to-run noise), equal with the KU=2 configs offered (profiles/r3x_ku2_cache_ab.txt)
+TUNE_ISOLATE = False
 
 
 def _time(fn, reps=None) -> float:
     # HCB_TUNE_REPS: timed launches per candidate (default 5; more = less noise, slower tuning)
     reps = reps or int(os.environ.get("HCB_TUNE_REPS", "5"))
     fn()
-    if os.environ.get("HCB_TUNE_ISOLATE") == "1":
+    if TUNE_ISOLATE:
         # step-like timing: each launch timed on its own, after a 64 MB write that evicts the
         # candidate's operands from L2 and ends any overlap with the previous launch (back-to-back
         # launches of one kernel favour configs the training step does not: profiles/r3x_ku2_cache_ab.txt)

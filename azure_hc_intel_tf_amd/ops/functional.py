@@ -174,6 +174,7 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                22: (64, 128), 23: (128, 128), 24: (128, 128), 25: (64, 128), 26: (64, 64)}
 PATCH_CFG0 = 17
 PATCH_CFGS = (17, 18, 19, 20, 21)
+TUNE_KU2 = False  # offer cfg 22-26 to the autotuner (see fwd_candidates)
 # weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
@@ -202,10 +203,10 @@ def fwd_candidates(N: int, patch: bool = False):
     """Tile configs worth timing for a GEMM with N output columns; ``patch``: the problem is a
     3x3 / stride-1 / pad-1 conv over a multiple of 64 channels (patch_eligible), so the
     LDS-resident-patch kernels are candidates too."""
-    # cfg 22-26 (two k-steps per LDS-DMA stage) only with HCB_TUNE_KU2=1: under back-to-back
-    # timing they win per layer (stage-3 3x3 23.2 vs 24.3 us) yet the step runs 1.2% slower with
-    # them (profiles/r3x_ku2_cache_ab.txt)
-    ku2 = [22, 23, 24, 25, 26] if os.environ.get("HCB_TUNE_KU2") == "1" else []
+    # cfg 22-26 (two k-steps per LDS-DMA stage) only with the module switch TUNE_KU2: under
+    # back-to-back timing they win per layer (stage-3 3x3 23.2 vs 24.3 us) yet the step runs 1.2%
+    # slower with them, and equal under per-launch isolated timing (profiles/r3x_ku2_cache_ab.txt)
+    ku2 = [22, 23, 24, 25, 26] if TUNE_KU2 else []
     if N <= 64:
         return [1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([19, 20] if patch else [])
     c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2

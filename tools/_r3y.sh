@@ -1,10 +1,10 @@
-# tuner timing fidelity: retune resnet50 with per-launch isolated timing (HCB_TUNE_ISOLATE=1), then a
+# tuner timing fidelity: retune resnet50 with per-launch isolated timing (autotune.TUNE_ISOLATE), then a
 # same-box A/B of the resulting cache against the current one
 set -o pipefail
 mkdir -p gpurun_out
 T=azure_hc_intel_tf_amd/tuned
 cp $T/mi355x.json /tmp/cache_cur.json
-HCB_TUNE_ISOLATE=1 HCB_TUNE_REPS=15 timeout -k 10 900 python -u tools/retune_conv.py resnet50 > gpurun_out/r3y_tune.log 2>&1 || exit 1
+HCB_TUNE_REPS=15 timeout -k 10 900 python -u -c "import sys; sys.argv=['x','resnet50']; sys.path.insert(0,'tools'); from azure_hc_intel_tf_amd.ops import autotune; autotune.TUNE_ISOLATE=True; import retune_conv; retune_conv.main()" > gpurun_out/r3y_tune.log 2>&1 || exit 1
 cp $T/mi355x.json /tmp/cache_iso.json
 cp /tmp/cache_iso.json gpurun_out/r3y_cache_iso.json
 O=gpurun_out/r3y_ab.txt

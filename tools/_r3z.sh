@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 T=azure_hc_intel_tf_amd/tuned
 cp gpurun_out/r3y_cache_iso.json /tmp/cache_iso.json
 cp /tmp/cache_iso.json $T/mi355x.json
-HCB_TUNE_KU2=1 HCB_TUNE_ISOLATE=1 HCB_TUNE_REPS=15 timeout -k 10 900 python -u tools/retune_conv.py resnet50 > gpurun_out/r3z_tune.log 2>&1 || exit 1
+HCB_TUNE_REPS=15 timeout -k 10 900 python -u -c "import sys; sys.argv=['x','resnet50']; sys.path.insert(0,'tools'); from azure_hc_intel_tf_amd.ops import autotune, functional as Fn; autotune.TUNE_ISOLATE=True; Fn.TUNE_KU2=True; import retune_conv; retune_conv.main()" > gpurun_out/r3z_tune.log 2>&1 || exit 1
 cp $T/mi355x.json /tmp/cache_ku2.json
 cp /tmp/cache_ku2.json gpurun_out/r3z_cache_isoku2.json
 O=gpurun_out/r3z_ab.txt
