@@ -89,14 +89,18 @@ __device__ __forceinline__ void mfma_patch_step(const u32x4* Pb, const u32x4* Bb
       for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[ks][i], bfr[ks][j], acc[i][j]);
 }
 
-// LDS bytes of the main loop / the BN-backward parameter offset, shared by kernel and launcher
+// LDS bytes of the main loop / the BN-backward parameter offset, shared by kernel and launcher.
+// The patch is double buffered only when some block reduces more than one 64-channel slab (a
+// single-slab problem -- the stage-1 3x3 layers over 64 channels -- keeps one buffer: half the
+// patch LDS, more workgroups per CU).
+__host__ __device__ inline int patch_buffers(const ConvParams& p) { return p.C / 64 > p.splits ? 2 : 1; }
 template <int BM, int BN, int WM, int NST>
-__host__ __device__ constexpr size_t patch_main_lds(int patch_rows) {
-  return (size_t)NST * BN * 128 + (size_t)2 * patch_rows * 128;
+__host__ __device__ inline size_t patch_main_lds(const ConvParams& p) {
+  return (size_t)NST * BN * 128 + (size_t)patch_buffers(p) * p.patch_rows * 128;
 }
 template <int BM, int BN, int WM, int NST>
-__host__ __device__ inline size_t patch_param_off(int patch_rows) {
-  const size_t a = patch_main_lds<BM, BN, WM, NST>(patch_rows), b = igemm_epilogue_lds(BM, BN, WM);
+__host__ __device__ inline size_t patch_param_off(const ConvParams& p) {
+  const size_t a = patch_main_lds<BM, BN, WM, NST>(p), b = igemm_epilogue_lds(BM, BN, WM);
   return a > b ? a : b;
 }
 
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch_kernel(ConvParams p
 
   EpiPrefetch<WM, WN, TM, TN, BNB> pre;
   pre.load_shift(p, n0, wn, lane);
-  const size_t param_off = patch_param_off<BM, BN, WM, NST>(p.patch_rows);
+  const size_t param_off = patch_param_off<BM, BN, WM, NST>(p);
   if constexpr (BNB) stage_bnb_params<BN, NT>(p, n0, smem + param_off);  // published by the first barrier
 
   auto load_patch = [&](int sl) {  // the patch of local slab sl into buffer sl & 1
@@ -253,10 +257,10 @@ static bool launch_patch(ConvParams p, hipStream_t st) {
   if (passes > PMAX) return false;
   p.patch_rows = passes * RP;
   const bool bnb = p.bnb_acc != nullptr;
-  const size_t main_b = patch_main_lds<BM, BN, WM, NST>(p.patch_rows);
+  const size_t main_b = patch_main_lds<BM, BN, WM, NST>(p);
   const size_t epi_b = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = main_b > epi_b ? main_b : epi_b;
-  if (bnb) lds = patch_param_off<BM, BN, WM, NST>(p.patch_rows) + bnb_param_lds(BN);
+  if (bnb) lds = patch_param_off<BM, BN, WM, NST>(p) + bnb_param_lds(BN);
   if (lds > 160 * 1024) return false;
   static bool once = false;
   if (!once) {
