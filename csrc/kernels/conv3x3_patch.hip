@@ -49,9 +49,8 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
 
 // padded linear index of output pixel m (P == H, Q == W)
 __device__ __forceinline__ int patch_lp(const ConvParams& p, int m) {
-  const int PQ = p.H * p.W;
-  const int n = m / PQ, r = m - n * PQ;
-  const int pp = r / p.W, qq = r - pp * p.W;
+  const int n = (int)fdiv((uint32_t)m, p.fd_hw), r = m - n * p.H * p.W;
+  const int pp = (int)fdiv((uint32_t)r, p.fd_w), qq = r - pp * p.W;
   return (n * (p.H + 2) + pp) * (p.W + 2) + qq;
 }
 
@@ -144,8 +143,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch_kernel(ConvParams p
       uint32_t o = HCB_OOB;
       if (j < prows) {
         const int L = lbase + j;
-        const int n = L / HW2, rem = L - n * HW2;
-        const int hh = rem / W2, ww = rem - hh * W2;
+        const int n = (int)fdiv((uint32_t)L, p.fd_hw2), rem = L - n * HW2;
+        const int hh = (int)fdiv((uint32_t)rem, p.fd_w2), ww = rem - hh * W2;
         if (n < p.N && hh >= 1 && hh <= p.H && ww >= 1 && ww <= p.W)
           o = (uint32_t)((((n * p.H + hh - 1) * p.W + ww - 1) * p.ldx + chunk * 8) * 2);
       }
@@ -256,6 +255,10 @@ static bool launch_patch(ConvParams p, hipStream_t st) {
   const int passes = (span + RP - 1) / RP;
   if (passes > PMAX) return false;
   p.patch_rows = passes * RP;
+  p.fd_hw = make_fastdiv((uint32_t)(p.H * p.W));
+  p.fd_w = make_fastdiv((uint32_t)p.W);
+  p.fd_hw2 = make_fastdiv((uint32_t)((p.H + 2) * (p.W + 2)));
+  p.fd_w2 = make_fastdiv((uint32_t)(p.W + 2));
   const bool bnb = p.bnb_acc != nullptr;
   const size_t main_b = patch_main_lds<BM, BN, WM, NST>(p);
   const size_t epi_b = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));

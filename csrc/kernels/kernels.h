@@ -79,8 +79,10 @@ struct ConvParams {
   const void* w_lo;
   const void* w_lo2;
   // 3x3 / stride-1 patch kernels (conv3x3_patch.hip; set by their launcher): LDS rows reserved
-  // per input-patch buffer
+  // per input-patch buffer, and division-free index math (output pixel -> (n, p, q), padded
+  // linear index -> (n, h', w'))
   int patch_rows;
+  FastDiv fd_hw, fd_w, fd_hw2, fd_w2;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
 // cfg >= CONV_PATCH_CFG0: the 3x3 / stride 1 / pad 1 kernels with the input patch resident in
