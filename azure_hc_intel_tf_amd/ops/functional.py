@@ -906,6 +906,18 @@ def nonfinite(g, flag):
         flag.view(-1)[0] = 1.0
 
 
+def loss_total(row_loss, B: int, l2, half_wd: float, loss):
+    """loss[0] = mean(row_loss[:B]) + half_wd * l2[0] (l2 None: the mean alone) -- the step's reported
+    loss in one launch (tf_cnn_benchmarks' total_loss = cross entropy + weight decay * l2 term)."""
+    if row_loss.is_cuda:
+        _ext.ops().loss_total(row_loss, B, l2, half_wd, loss)
+        return
+    t = row_loss[:B].mean()
+    if l2 is not None:
+        t = t + half_wd * l2.view(-1)[0]
+    loss.view(-1)[0] = t
+
+
 def loss_scale_update(hyper, world: int, dynamic: bool):
     """hyper = [lr, mu, wd, grad_scale, found_inf, loss_scale, good_steps, interval]: dynamic
     loss-scale step (halve on overflow, double after `interval` clean steps), then

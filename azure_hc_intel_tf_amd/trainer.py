@@ -172,7 +172,7 @@ class Trainer:
 
     def _optimizer_body(self):
         if self.forward_only:
-            self.loss.copy_(self.row_loss.mean().view(1))
+            Fn.loss_total(self.row_loss, self.B, None, 0.0, self.loss)
             return
         self.l2.zero_()
         if self.loss_scaling:
@@ -182,7 +182,7 @@ class Trainer:
                         self.nesterov)
         if self.loss_scaling:
             Fn.loss_scale_update(self.hyper, self.world, self.dynamic_ls)
-        self.loss.copy_((self.row_loss.mean() + 0.5 * self.wd * self.l2).view(1))
+        Fn.loss_total(self.row_loss, self.B, self.l2, 0.5 * self.wd, self.loss)
 
     def _reduce(self):
         if self.reducer is not None and self.world > 1 and not self.forward_only and not self._skip_comm:

@@ -546,6 +546,21 @@ void nonfinite(const Tensor& g, const Tensor& flag) {
   hcb::launch_nonfinite(g.data_ptr<float>(), g.numel(), flag.data_ptr<float>(), cur_stream());
 }
 
+void loss_total(const Tensor& row_loss, int64_t B, const c10::optional<Tensor>& l2, double half_wd,
+                const Tensor& loss) {
+  check_f32(row_loss, "row_loss");
+  check_f32(loss, "loss");
+  TORCH_CHECK(B >= 1 && row_loss.numel() >= B && loss.numel() >= 1, "hcb.loss_total: args");
+  const float* l2p = nullptr;
+  if (l2.has_value()) {
+    check_f32(*l2, "l2");
+    TORCH_CHECK(l2->numel() >= 1, "hcb.loss_total: l2");
+    l2p = l2->data_ptr<float>();
+  }
+  hcb::launch_loss_total(row_loss.data_ptr<float>(), (int)B, l2p, (float)half_wd, loss.data_ptr<float>(),
+                         cur_stream());
+}
+
 void loss_scale_update(const Tensor& hyper, double world, bool dynamic) {
   check_f32(hyper, "hyper");
   TORCH_CHECK(hyper.numel() >= 8 && hyper.is_contiguous(), "hcb.loss_scale_update: hyper[8]");
@@ -894,6 +909,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx, int N, int HW, int C) -> ()");
   m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale, Tensor? scale_dev=None, Tensor(c!)? dl32=None) -> ()");
   m.def("nonfinite(Tensor g, Tensor(a!) flag) -> ()");
+  m.def("loss_total(Tensor row_loss, int B, Tensor? l2, float half_wd, Tensor(a!) loss) -> ()");
   m.def("loss_scale_update(Tensor(a!) hyper, float world, bool dynamic) -> ()");
   m.def("colsum(Tensor g, int ld, int M, int N, Tensor(a!) out) -> ()");
   m.def("sgd_momentum(Tensor(a!) w, Tensor(b!) mom, Tensor g, int n_decay, Tensor hyper, Tensor(c!)? l2, bool nesterov) -> ()");
@@ -926,6 +942,7 @@ HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("conv_igemm", conv_igemm);
   m.impl("conv_igemm_bnb", conv_igemm_bnb);
   m.impl("nonfinite", nonfinite);
+  m.impl("loss_total", loss_total);
   m.impl("loss_scale_update", loss_scale_update);
   m.impl("set_splitk_workspace", set_splitk_workspace);
   m.impl("conv_wgrad", conv_wgrad);

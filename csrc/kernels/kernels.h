@@ -205,6 +205,7 @@ void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out,
 void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
                          const float* hyper, float* l2_out, int nesterov, int hyper_n, hipStream_t st);
 void launch_nonfinite(const float* g, int64_t n, float* flag, hipStream_t st);
+void launch_loss_total(const float* row_loss, int B, const float* l2, float half_wd, float* loss, hipStream_t st);
 void launch_loss_scale_update(float* hyper, float world, int dynamic, hipStream_t st);
 struct WPackEntry {  // all int64 so the table is a plain int64 tensor [n][9]
   int64_t src_off;   // fp32 master offset (elements)

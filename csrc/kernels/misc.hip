@@ -494,6 +494,27 @@ __global__ void loss_scale_update_kernel(float* hyper, float world, int dynamic)
   }
   hyper[3] = 1.f / (world * S);
 }
+// loss[0] = mean(row_loss[0:B]) + half_wd * l2[0] (l2 may be null): the step's reported loss in
+// one launch (one workgroup, fixed reduction order) instead of mean / mul / add / copy kernels.
+__global__ __launch_bounds__(256) void loss_total_kernel(const float* __restrict__ row_loss, int B,
+                                                         const float* __restrict__ l2, float half_wd,
+                                                         float* __restrict__ loss) {
+  __shared__ float part[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < B; i += 256) s += row_loss[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = ((part[0] + part[1]) + (part[2] + part[3])) / (float)B;
+    if (l2) t += half_wd * l2[0];
+    loss[0] = t;
+  }
+}
+void launch_loss_total(const float* row_loss, int B, const float* l2, float half_wd, float* loss, hipStream_t st) {
+  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(256), 0, st, row_loss, B, l2, half_wd, loss);
+}
 void launch_nonfinite(const float* g, int64_t n, float* flag, hipStream_t st) {
   hipLaunchKernelGGL(nonfinite_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, g, n, flag);
 }
