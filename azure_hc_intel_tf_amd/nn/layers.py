@@ -603,7 +603,10 @@ class Logits(Layer):
         kt = (self.ld + 63) // 64 * 64
         self.pack = ps.add_pack(self.w, ncls, 1, 1, in_features, self.spec.Kpad, kt, want_tr=True)
         self._x = None
-        self.dl32 = None  # fp32 copy of 16-bit dlogits (Trainer): the bias gradient's source
+        # fp32 copy of 16-bit dlogits (Trainer): the bias gradient's source -- only for the exact
+        # dlogits tensor it was written with (dl32_src), never for another caller's dlogits
+        self.dl32 = None
+        self.dl32_src = None
 
     def forward(self, x):
         B = x.shape[0]
@@ -623,7 +626,8 @@ class Logits(Layer):
         """dlogits: [B, ld] (bf16 on GPU, zero in the padding columns)."""
         x = self._x
         B = x.shape[0]
-        if self.dl32 is not None and Fn.native(x) and dlogits.dtype != torch.float32:
+        if (self.dl32 is not None and dlogits is self.dl32_src and self.dl32.shape[0] == B and Fn.native(x)
+                and dlogits.dtype != torch.float32):
             Fn._ext.ops().colsum(self.dl32, self.ld, B, self.ncls, self.b.grad)
         else:
             Fn.colsum(dlogits, B, self.ncls, self.b.grad)

@@ -85,8 +85,9 @@ class Trainer:
         self.forward_only = forward_only
         if forward_only and hasattr(model, "set_training"):
             model.set_training(False)  # inference BN / no dropout (tf_cnn_benchmarks phase_train=False)
-        # graphs for the HIP-kernel path; the reference-precision PyTorch path (fp32 / fp16
-        # --compute_dtype) runs eagerly (MIOpen's first-call searches are not capturable)
+        # every model whose ops run on the HIP kernels (bf16, the IEEE-fp16 build, and fp32 on the
+        # bf16-plane GEMMs) is graph-captured; models on the PyTorch path (CPU, or fp32 for a model
+        # without the fp32 kernels) run eagerly (MIOpen's first-call searches are not capturable)
         # comm_check (HCB_COMM_CHECK=1 / --comm_check): the race detector of the overlapped
         # allreduce -- every async segment reduction is re-done by a blocking reference
         # allreduce of a snapshot taken before it was issued and the two must agree (a missing
@@ -121,6 +122,7 @@ class Trainer:
                 and isinstance(fc, Logits)):
             self.dlogits32 = torch.zeros((batch_size, ld), dtype=torch.float32, device=self.dev)
             fc.dl32 = self.dlogits32
+            fc.dl32_src = self.dlogits
         self.l2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.steps_done = 0

@@ -15,11 +15,15 @@ at :99-109).
         each process is one rank (RANK / LOCAL_RANK / WORLD_SIZE from the environment);
         WORLD_SIZE must equal --gpus.
 
-One process per MI355X; gradients averaged with RCCL over xGMI. W untimed warmup steps
-(the first ones also capture the HIP graph), then EXACTLY K timed steps bracketed by
-barrier + device sync; the max time over ranks is used; rank 0 prints one JSON line that
-also carries ``world`` (torch.distributed) and ``rccl_nranks`` (read back from the native
-RCCL communicator), and every rank prints its own ``total images/sec`` line on stderr.
+One process per MI355X; gradients averaged with RCCL over xGMI. The headline ``value`` is the
+reference's precision, fp32 (tf_cnn_benchmarks with MKL-DNN trains fp32: no --use_fp16 in
+run-tf-sing-ucx-openmpi.sh:62-81), on the hand-written HIP kernels; the same invocation then
+times the bf16 step and reports it as ``bf16_value`` / ``bf16_ms_per_step``. Per dtype: W
+untimed warmup steps (the first ones also capture the HIP graph), then EXACTLY K timed steps
+bracketed by barrier + device sync; the max time over ranks is used; rank 0 prints one JSON line
+that also carries ``world`` (torch.distributed) and ``rccl_nranks`` (read back from the native
+RCCL communicator), and every rank prints its own ``total images/sec`` lines on stderr. A native
+engine that fails its self-test at N>1 ends the run with exit code 5 (unless --engine torch).
 """
 from __future__ import annotations
 
@@ -52,10 +56,14 @@ def parse_args(argv=None):
                     help="N=1 only: run the multi-GPU step (one graph with the collectives on a forked comm "
                          "stream, async RCCL engine on a 1-rank communicator) to time its overhead on one GPU")
     ap.add_argument("--use_fp16", action="store_true",
-                    help="tf_cnn_benchmarks --use_fp16: IEEE fp16 compute (PyTorch reference path) with automatic "
-                         "loss scaling; with --compute_dtype bf16: the HIP kernels plus loss scaling")
+                    help="tf_cnn_benchmarks --use_fp16: IEEE fp16 compute on the fp16 build of the HIP kernels with "
+                         "automatic loss scaling")
     ap.add_argument("--compute_dtype", default=None, choices=[None, "bf16", "fp16", "fp32"],
-                    help="activation / GEMM precision (default bf16; fp32 = the reference's precision)")
+                    help="activation / GEMM precision of the reported value (default fp32 = the reference's "
+                         "precision, with bf16 timed as a secondary figure in the same run)")
+    ap.add_argument("--secondary", default="auto", choices=["auto", "none", "bf16", "fp16", "fp32"],
+                    help="a second compute dtype timed in the same run and reported as <dtype>_value "
+                         "(auto: bf16 when the primary is the default fp32, else none)")
     ap.add_argument("--backward_segments", default="stage", choices=["stage", "block"],
                     help="gradient-reduction granularity of the overlapped multi-GPU step (ResNet): one segment "
                          "per stage, or per block in stages 3-4 with stage 1 split from the stem")
@@ -90,6 +98,173 @@ def spawn_workers(args, argv) -> int:
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     env["HCB_BENCH_SPAWNED"] = "1"
     return launch(cmd, nproc_per_node=args.gpus, master_addr="127.0.0.1", env=env, rccl=_rccl(args))
+
+
+def setup_native_reducer(args, world, rank, dev, make_reducer, all_min):
+    """The native C++ RCCL engine for a multi-rank run, self-tested against the known sum before
+    it is trusted. Returns (reducer, rccl_nranks). A failing engine is an ERROR (exit non-zero via
+    EngineUnavailable) unless --engine torch was asked for: a scaling run must never silently
+    measure a different engine than the one it reports (``all_min``: the cross-rank MIN of an int,
+    so every rank takes the same branch)."""
+    import torch
+
+    ok = 1
+    reducer, err = None, None
+    try:
+        reducer = make_reducer("native", compression=args.compression)
+        t = torch.full((4096,), float(rank + 1), device=dev)
+        reducer.comm.allreduce_(t)
+        torch.cuda.synchronize()
+        ok = 1 if torch.allclose(t, torch.full_like(t, world * (world + 1) / 2)) else 0
+        if not ok:
+            err = "self-test sum mismatch"
+    except Exception as e:  # noqa: BLE001
+        ok, err = 0, f"{type(e).__name__}: {e}"
+    if all_min(ok) != 1:
+        raise EngineUnavailable(err or "another rank's native engine failed its self-test")
+    return reducer, reducer.comm.size()
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+def init_comm(args, world, rank, dev, all_min, make_reducer=None, init_pg=True):
+    """Process group + gradient reducer of a multi-rank run. Returns (exit code, reducer, backend,
+    rccl_nranks); a non-zero code ends the run (5: the native engine failed its self-test)."""
+    if world <= 1:
+        return 0, None, None, None
+    import torch.distributed as dist
+
+    os.environ.update(_rccl(args))  # before the communicators exist (torchrun-launched workers)
+    backend = os.environ.get("HCB_BENCH_BACKEND", "nccl")
+    if init_pg:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    if backend != "nccl":
+        args.engine = "torch"
+    if make_reducer is None:
+        from azure_hc_intel_tf_amd.parallel import make_reducer
+    reducer, rccl_nranks = None, None
+    if args.engine == "native":
+        try:
+            reducer, rccl_nranks = setup_native_reducer(args, world, rank, dev, make_reducer, all_min)
+        except EngineUnavailable as e:
+            print(f"[rank {rank}] native RCCL engine failed its self-test ({e}); refusing to report a "
+                  f"torch.distributed run as the native engine (pass --engine torch for that)", file=sys.stderr)
+            if init_pg:
+                dist.destroy_process_group()
+            return 5, None, backend, None
+    else:
+        reducer = make_reducer("torch", compression=args.compression)
+    if rccl_nranks is None and backend == "nccl" and init_pg:
+        rccl_nranks = dist.get_world_size()
+    if rccl_nranks is not None and rccl_nranks != world:
+        print(f"[bench] RCCL communicator has {rccl_nranks} ranks, expected {world}", file=sys.stderr)
+        return 4, None, backend, None
+    return 0, reducer, backend, rccl_nranks
+
+
+def _all_min_fn(world, dev):
+    import torch
+    import torch.distributed as dist
+
+    def all_min(v: int) -> int:
+        if world <= 1:
+            return int(v)
+        t = torch.tensor([int(v)], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item())
+
+    return all_min
+
+
+def run_model(args, dtype, world, rank, dev, reducer, all_min):
+    """Build, tune, warm up and time one model at one compute dtype; returns its result dict."""
+    import torch
+    import torch.distributed as dist
+
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.ops import autotune
+    from azure_hc_intel_tf_amd.trainer import Trainer, resnet_lr_schedule, synthetic_batch
+    from azure_hc_intel_tf_amd.utils import tracing
+
+    model = create_model(args.model, device=dev, compute_dtype=dtype)
+    if hasattr(model, "segments"):
+        model.segments = args.backward_segments
+    B = args.batch_size
+    autotune.load_cache()
+    if not args.no_tune and model.native:
+        n = autotune.tune_model(model, B, save=(rank == 0))
+        if n and rank == 0:
+            print(f"[bench] {dtype}: autotuned {n} conv problems", file=sys.stderr)
+    if reducer is not None:
+        reducer.broadcast_(model.ps.master, 0)
+        reducer.broadcast_(model.ps.buf, 0)
+    images, labels = synthetic_batch(model, B, seed=rank)
+    fp16 = args.use_fp16 or dtype == "fp16"
+    trainer = Trainer(model, B, resnet_lr_schedule(B * world), reducer=reducer, world_size=world,
+                      use_graph=not args.no_graph, dynamic_loss_scale=fp16, force_overlap=args.force_dp_path)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    warmup = max(args.warmup, 0)
+    with tracing.range_(f"bench.warmup.{dtype}"):
+        for _ in range(warmup):
+            trainer.step(images, labels)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    trace = torch.zeros(args.steps, device=dev) if os.environ.get("HCB_BENCH_LOSS_TRACE") == "1" else None
+    t0 = time.perf_counter()
+    with tracing.range_(f"bench.timed.{dtype}"):
+        for i in range(args.steps):
+            trainer.step(images, labels)
+            if trace is not None:  # device-side copy, no host sync (debug only)
+                trace[i:i + 1].copy_(trainer.loss)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = own = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = float(trainer.loss.item())
+    comm = None
+    if reducer is not None:
+        if hasattr(reducer, "check_errors"):
+            reducer.check_errors()
+        if os.environ.get("HCB_BENCH_COMM_PROFILE", "1") == "1":  # after the timed region
+            failed = 0
+            try:  # restores the training state itself
+                comm = trainer.comm_profile(images, labels)
+            except RuntimeError as e:
+                if "comm check" in str(e):  # the race detector's verdict is never swallowed
+                    raise
+                comm, failed = {"error": f"{type(e).__name__}: {e}"}, 1
+            except Exception as e:  # noqa: BLE001
+                comm, failed = {"error": f"{type(e).__name__}: {e}"}, 1
+            # a rank that failed here must not leave the others blocked in the profile's
+            # collectives, nor turn a correctness error into a field of a valid result line
+            if all_min(1 - failed) != 1:
+                raise RuntimeError(f"comm profile failed on at least one rank ({comm})")
+    # tf_cnn_benchmarks prints "total images/sec" on every rank (run-tf-sing-ucx-openmpi.sh:99-113
+    # runs it under mpirun); stderr keeps stdout to the one JSON line
+    print(f"[rank {rank}] {dtype} total images/sec: {world * B * args.steps / own:.2f} "
+          f"(own {1000.0 * own / args.steps:.3f} ms/step)", file=sys.stderr, flush=True)
+    if trace is not None and rank == 0:
+        print(f"[bench] {dtype} losses " + " ".join(f"{v:.4f}" for v in trace.tolist()), file=sys.stderr)
+    res = {"dtype": dtype, "ips": world * B * args.steps / elapsed, "ms": 1000.0 * elapsed / args.steps,
+           "loss": loss, "comm": comm, "graph": trainer.use_graph, "native": model.native,
+           "image_size": model.image_size}
+    del trainer, model
+    torch.cuda.synchronize()
+    return res
 
 
 def main(argv=None):
@@ -129,154 +304,75 @@ def main(argv=None):
     if os.environ.get("HCB_BENCH_ONE_DEVICE") == "1":
         local_rank = 0
     if local_rank >= torch.cuda.device_count():
-        print(f"[bench] rank {rank}: LOCAL_RANK {local_rank} but {torch.cuda.device_count()} GPU(s) visible",
+        print(f"[rank {rank}] LOCAL_RANK {local_rank} but {torch.cuda.device_count()} GPU(s) visible",
               file=sys.stderr)
         return 3
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from azure_hc_intel_tf_amd.models import create_model
-    from azure_hc_intel_tf_amd.trainer import Trainer, resnet_lr_schedule, synthetic_batch
     from azure_hc_intel_tf_amd.ops import _ext
-    from azure_hc_intel_tf_amd.utils import tracing
 
     _ext.load()
-    dtype = args.compute_dtype or ("fp16" if args.use_fp16 else "bf16")
-    reducer = None
-    backend = None
-    rccl_nranks = None
-    if world > 1:
-        os.environ.update(_rccl(args))  # before the communicators exist (torchrun-launched workers)
-        backend = os.environ.get("HCB_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-            args.engine = "torch"
-        from azure_hc_intel_tf_amd.parallel import make_reducer
-
-        if args.engine == "native":
-            try:
-                reducer = make_reducer("native", compression=args.compression)
-                # self-test of the C++ RCCL engine against the known sum before trusting it
-                t = torch.full((4096,), float(rank + 1), device=dev)
-                reducer.comm.allreduce_(t)
-                torch.cuda.synchronize()
-                ok = torch.tensor([1 if torch.allclose(t, torch.full_like(t, world * (world + 1) / 2)) else 0],
-                                  device=dev)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-                if int(ok.item()) != 1:
-                    raise RuntimeError("self-test mismatch")
-                rccl_nranks = reducer.comm.size()
-            except Exception as e:  # pragma: no cover - exercised only on multi-GPU nodes
-                print(f"[bench] native RCCL engine unavailable ({e}); falling back to torch.distributed",
-                      file=sys.stderr)
-                args.engine = "torch"
-                reducer = make_reducer("torch", compression=args.compression)
-        else:
-            reducer = make_reducer("torch", compression=args.compression)
-        if rccl_nranks is None and backend == "nccl":
-            rccl_nranks = dist.get_world_size()
-        if rccl_nranks is not None and rccl_nranks != world:
-            print(f"[bench] RCCL communicator has {rccl_nranks} ranks, expected {world}", file=sys.stderr)
-            return 4
+    # the headline is measured at the reference's precision: tf_cnn_benchmarks trains fp32
+    # (MKL-DNN, run-tf-sing-ucx-openmpi.sh:62-81, no --use_fp16); the same invocation also times
+    # the bf16 step as a secondary figure
+    primary = args.compute_dtype or ("fp16" if args.use_fp16 else "fp32")
+    secondary = args.secondary if args.secondary != "auto" else (
+        "bf16" if (args.compute_dtype is None and not args.use_fp16) else "none")
+    all_min = _all_min_fn(world, dev)
+    code, reducer, backend, rccl_nranks = init_comm(args, world, rank, dev, all_min)
+    if code:
+        return code
 
     if world == 1 and args.force_dp_path:
         from azure_hc_intel_tf_amd.parallel.native import NativeReducer
 
         reducer = NativeReducer(compression=args.compression, force=True)
         rccl_nranks = reducer.comm.size()
-    model = create_model(args.model, device=dev, compute_dtype=dtype)
-    if hasattr(model, "segments"):
-        model.segments = args.backward_segments
+    results = [run_model(args, primary, world, rank, dev, reducer, all_min)]
+    if secondary not in ("none", primary):
+        results.append(run_model(args, secondary, world, rank, dev, reducer, all_min))
+    main_r = results[0]
     B = args.batch_size
-    from azure_hc_intel_tf_amd.ops import autotune
-
-    autotune.load_cache()
-    if not args.no_tune and model.native:
-        n = autotune.tune_model(model, B, save=(rank == 0))
-        if n and rank == 0:
-            print(f"[bench] autotuned {n} conv problems", file=sys.stderr)
-    if reducer is not None:
-        reducer.broadcast_(model.ps.master, 0)
-        reducer.broadcast_(model.ps.buf, 0)
-    images, labels = synthetic_batch(model, B, seed=rank)
-    trainer = Trainer(model, B, resnet_lr_schedule(B * world), reducer=reducer, world_size=world,
-                      use_graph=not args.no_graph, dynamic_loss_scale=(args.use_fp16 or dtype == "fp16"),
-                      force_overlap=args.force_dp_path)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    warmup = max(args.warmup, 0)
-    with tracing.range_("bench.warmup"):
-        for _ in range(warmup):
-            trainer.step(images, labels)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    trace = torch.zeros(args.steps, device=dev) if os.environ.get("HCB_BENCH_LOSS_TRACE") == "1" else None
-    t0 = time.perf_counter()
-    with tracing.range_("bench.timed"):
-        for i in range(args.steps):
-            trainer.step(images, labels)
-            if trace is not None:  # device-side copy, no host sync (debug only)
-                trace[i:i + 1].copy_(trainer.loss)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    own = elapsed
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    loss = float(trainer.loss.item())
-    comm = None
-    if reducer is not None:
-        if hasattr(reducer, "check_errors"):
-            reducer.check_errors()
-        if os.environ.get("HCB_BENCH_COMM_PROFILE", "1") == "1":  # after the timed region
-            try:  # restores the training state itself; a failure must not lose the timed result
-                comm = trainer.comm_profile(images, labels)
-            except Exception as e:  # noqa: BLE001
-                comm = {"error": f"{type(e).__name__}: {e}"}
-                print(f"[bench] comm profile failed: {e}", file=sys.stderr)
-    # tf_cnn_benchmarks prints "total images/sec" on every rank (run-tf-sing-ucx-openmpi.sh:99-113
-    # runs it under mpirun); stderr keeps stdout to the one JSON line
-    print(f"[rank {rank}] total images/sec: {world * B * args.steps / own:.2f} "
-          f"(own {1000.0 * own / args.steps:.3f} ms/step)", file=sys.stderr, flush=True)
-    if trace is not None and rank == 0:
-        print("[bench] losses " + " ".join(f"{v:.4f}" for v in trace.tolist()), file=sys.stderr)
-    ips = world * B * args.steps / elapsed
     if rank == 0:
         res = {
             "metric": METRIC if (args.model == "resnet50" and B == 64)
             else f"images/sec (whole node) {args.model} bs={B}/worker",
-            "value": round(ips, 2),
+            "value": round(main_r["ips"], 2),
             "unit": "images/sec",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": warmup,
-            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "warmup": max(args.warmup, 0),
+            "ms_per_step": round(main_r["ms"], 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (ips / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": dtype,
-            "data": f"synthetic (truncated-normal ImageNet {model.image_size}x{model.image_size}, random-init weights)",
+            "vs_baseline": (main_r["ips"] / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": primary,
+            "data": f"synthetic (truncated-normal ImageNet {main_r['image_size']}x{main_r['image_size']}, "
+                    "random-init weights)",
             "world": world,
             "rccl_nranks": rccl_nranks,
-            "comm": comm,
-            "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
-                       "image_size": model.image_size, "parallelism": f"dp{world}",
-                       "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": trainer.use_graph,
-                       "engine": args.engine if (world > 1 or args.force_dp_path) else None,
-                       "backend": backend, "compression": args.compression,
-                       "loss_scaling": "dynamic" if (args.use_fp16 or dtype == "fp16") else None,
-                       "kernels": "hip" if model.native else "pytorch-reference (MIOpen/rocBLAS)",
-                       "final_loss": round(loss, 4)},
+            "comm": main_r["comm"],
         }
+        for r in results[1:]:
+            d = r["dtype"]
+            res[f"{d}_value"] = round(r["ips"], 2)
+            res[f"{d}_ms_per_step"] = round(r["ms"], 3)
+            res[f"{d}_final_loss"] = round(r["loss"], 4)
+            res[f"{d}_comm"] = r["comm"]
+        res["config"] = {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
+                         "image_size": main_r["image_size"], "parallelism": f"dp{world}",
+                         "optimizer": "momentum(0.9)+wd4e-5, fp32 master", "graph": main_r["graph"],
+                         "engine": args.engine if (world > 1 or args.force_dp_path) else None,
+                         "backend": backend, "compression": args.compression,
+                         "backward_segments": args.backward_segments,
+                         "loss_scaling": "dynamic" if primary == "fp16" else None,
+                         "precision": {"fp32": "fp32 activations/accumulation; every GEMM operand as bf16 "
+                                                "hi+mid+lo planes, six MFMA products (bf16x6, ~2^-24 per product)",
+                                       "bf16": "bf16 activations, fp32 accumulation/statistics/masters",
+                                       "fp16": "IEEE fp16 activations, fp32 accumulation, loss scaling"}.get(primary),
+                         "kernels": "hip" if main_r["native"] else "pytorch-reference (MIOpen/rocBLAS)",
+                         "final_loss": round(main_r["loss"], 4)}
         print(json.dumps(res), file=result_out, flush=True)
     if reducer is not None and hasattr(reducer, "close"):
         reducer.close()

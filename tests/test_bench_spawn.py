@@ -79,3 +79,49 @@ def test_visible_gpu_count_from_kfd_topology(tmp_path, monkeypatch):
     assert launcher.visible_gpu_count(str(tmp_path)) == 2
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert launcher.visible_gpu_count(str(tmp_path)) == 0
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_under_test", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_native_engine_failure_is_a_nonzero_exit(monkeypatch):
+    """A native RCCL engine that fails its self-test at N>1 must end the run with a non-zero code
+    (never a silent torch.distributed fallback reported as the native engine)."""
+    bench = _bench_module()
+    monkeypatch.delenv("HCB_BENCH_BACKEND", raising=False)
+    args = bench.parse_args(["--gpus", "2"])
+    assert args.engine == "native"
+
+    def broken(kind, compression=None):
+        raise RuntimeError("ncclCommInitRank failed")
+
+    code, reducer, backend, n = bench.init_comm(args, 2, 0, "cpu", lambda v: v, make_reducer=broken,
+                                                init_pg=False)
+    assert code == 5 and reducer is None and backend == "nccl"
+    # the same failure on ANOTHER rank (this one healthy) must end this rank too
+    with __import__("pytest").raises(bench.EngineUnavailable):
+        bench.setup_native_reducer(args, 2, 1, "cpu", broken, lambda v: 0)
+    # --engine torch is the explicit opt-in to the torch.distributed reducer
+    args_t = bench.parse_args(["--gpus", "2", "--engine", "torch"])
+    made = []
+    code, reducer, _, _ = bench.init_comm(args_t, 2, 0, "cpu", lambda v: v,
+                                          make_reducer=lambda k, compression=None: made.append(k) or object(),
+                                          init_pg=False)
+    assert code == 0 and made == ["torch"]
+
+
+def test_default_headline_is_reference_precision():
+    """bench.py reports fp32 (the reference's MKL-DNN precision) as the headline value and times bf16
+    as the secondary figure in the same invocation."""
+    bench = _bench_module()
+    a = bench.parse_args([])
+    assert a.compute_dtype is None and a.secondary == "auto" and not a.use_fp16
+    src = open(BENCH).read()
+    assert 'primary = args.compute_dtype or ("fp16" if args.use_fp16 else "fp32")' in src
+    assert 'res[f"{d}_value"]' in src

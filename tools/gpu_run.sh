@@ -14,6 +14,7 @@
 #   prof[:args]      rocprofv3 --kernel-trace --stats of bench.py, summarised by tools/kstats.py
 #   pmc:COUNTERS     one rocprofv3 --pmc pass (counters comma-separated) over bench.py --steps 3
 #   readme           tools/gpu_readme_numbers.sh
+#   race             tools/race_full.py (serialised vs async bitwise race check at full size)
 #   py:SCRIPT[,args] python SCRIPT args (a probe / diagnostic)
 # env: TAG (output prefix), PYTEST_X (default -x; PYTEST_X= runs every test), PYTEST_K (-k filter)
 # Outputs go to gpurun_out/${TAG}_<step>.*
@@ -61,6 +62,9 @@ for step in "$@"; do
       echo "pmc done: ${O}_pmc" ;;
     readme)
       bash tools/gpu_readme_numbers.sh || fail readme ;;
+    race)
+      timeout -k 10 1000 python -u tools/race_full.py $args > ${O}_race.txt 2>&1 || fail race ${O}_race.txt
+      tail -5 ${O}_race.txt ;;
     py)
       timeout -k 10 600 python -u $args > ${O}_py.log 2>&1 || fail py ${O}_py.log
       tail -40 ${O}_py.log ;;
