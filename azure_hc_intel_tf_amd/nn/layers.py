@@ -52,6 +52,14 @@ def empty_act(shape, device, zero=False):
     return f(shape, dtype=act_dtype(device), device=device)
 
 
+def empty_op(shape, device):
+    """A tensor that a GEMM consumes next (a BN output, a BN-backward dz): on the fp32 path the
+    Planes format the bf16x6 GEMMs read (written by the producing kernel); otherwise empty_act."""
+    if torch.device(device).type == "cuda" and Fn.planes_mode():
+        return Fn.Planes.empty(tuple(shape), device)
+    return empty_act(shape, device)
+
+
 def resolve_pads(mode, H, W, kh, kw, sh, sw, dh=1, dw=1):
     """Padding (pt, pb, pl, pr) for tf_cnn_benchmarks modes 'SAME', 'VALID', 'SAME_RESNET'."""
     if isinstance(mode, (tuple, list)):
@@ -220,8 +228,8 @@ class ConvBN(Layer):
             return y
         if self.bn:
             z = empty_act((N, P, Q, C), dev)
-            y = out if out is not None else empty_act((N, P, Q, C), dev)
             if Fn.native(x):
+                y = out if out is not None else empty_op((N, P, Q, C), dev)
                 # conv epilogue accumulates the batch statistics; the apply kernel finalizes them
                 x = self._conv_fwd_stats(x, z)
                 acc_f, _, R = self._acc
@@ -233,6 +241,7 @@ class ConvBN(Layer):
                                           shift=self._shift(),
                                           res_bn=residual_bn.res_bn_args() if residual_bn is not None else None)
             else:
+                y = out if out is not None else empty_act((N, P, Q, C), dev)
                 Fn.conv_forward(x, self.spec, None, self.w.data, z)
                 saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
                                       self.decay, self.eps, y, self.relu, residual=residual)
@@ -255,7 +264,7 @@ class ConvBN(Layer):
         P, Q, C = self.out_shape
         z = empty_act((N, P, Q, C), x.device)
         x = self._conv_fwd_stats(x, z)
-        y = empty_act((N,) + tuple(pool.out_shape), x.device)
+        y = empty_op((N,) + tuple(pool.out_shape), x.device)
         amax = torch.empty((N,) + tuple(pool.out_shape), dtype=torch.uint8, device=x.device)
         acc_f, _, R = self._acc
         saved = Fn.bn_relu_maxpool_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
@@ -269,6 +278,8 @@ class ConvBN(Layer):
         """GPU conv with the BN statistics in its epilogue; returns the tensor the weight
         gradient will read (the conv's GEMM input)."""
         acc_f, _, R = self._stat_bufs(x.shape[0], x.device)
+        if Fn.planes_mode() and not Fn.is_planes(x):  # fp32 path: the GEMM (and wgrad) operand as planes
+            x = Fn.to_planes(x)
         Fn.conv_forward(x, self.spec, self.pack.pack, self.w.data, z, stats=acc_f, stats_R=R,
                         stats_shift=self._shift())
         return x
@@ -285,8 +296,8 @@ class ConvBN(Layer):
         if not (self.bn and FUSE_BN_BWD) or self._saved is None:
             return None
         x, z, y, saved, had_res = self._saved
-        if z.dtype == torch.float32:  # the fused BN-backward epilogue is 16-bit only
-            return None
+        if z.dtype == torch.float32 and not (Fn.planes_mode() and z.is_cuda):
+            return None  # fp32 fusion runs on the plane GEMMs (conv_p3.hip) only
         mode = (1 if had_res else 2) if self.relu else 0
         self._pre_reduced = True
         _, acc_b, R = self._acc if self._acc is not None else (None, self.acc_b.data, STAT_R)
@@ -304,7 +315,7 @@ class ConvBN(Layer):
         if self.bn and self._pre_reduced:
             # dy is already g = dy * mask and (GPU) acc_b holds sum(g), sum(g*xhat)
             self._pre_reduced = False
-            dz = empty_act((N, P, Q, C), dev)
+            dz = empty_op((N, P, Q, C), dev) if Fn.native(dy) else empty_act((N, P, Q, C), dev)
             if Fn.native(dy):
                 _, acc_b, R = self._acc
                 Fn.bn_backward_acc(dy, None, z, saved, self.gamma.data, self.beta.data, 0, self.gamma.grad,
@@ -315,7 +326,7 @@ class ConvBN(Layer):
             if want_gres:
                 gres = dy
         elif self.bn:
-            dz = empty_act((N, P, Q, C), dev)
+            dz = empty_op((N, P, Q, C), dev) if Fn.native(dy) else empty_act((N, P, Q, C), dev)
             if want_gres:
                 gres = empty_act((N, P, Q, C), dev)
             relu_mode = (1 if had_res else 2) if self.relu else 0
@@ -577,9 +588,11 @@ class GlobalAvgPool(Layer):
 
     def forward(self, x):
         N = x.shape[0]
-        y = torch.empty((N, self.in_shape[2]), dtype=x.dtype, device=x.device)
-        Fn.gap_forward(x, y)
-        return y
+        if Fn.is_planes(x):  # fp32 path: the pooled features feed the classifier GEMM as planes
+            y = Fn.Planes.empty((N, self.in_shape[2]), x.device)
+        else:
+            y = torch.empty((N, self.in_shape[2]), dtype=x.dtype, device=x.device)
+        return Fn.gap_forward(x, y)
 
     def backward(self, dy):
         N = dy.shape[0]
@@ -631,7 +644,14 @@ class Logits(Layer):
             Fn._ext.ops().colsum(self.dl32, self.ld, B, self.ncls, self.b.grad)
         else:
             Fn.colsum(dlogits, B, self.ncls, self.b.grad)
-        if Fn.native(x):
+        if Fn.native(x) and x.dtype == torch.float32:  # fp32 path: Planes operands (conv_p3.hip)
+            dlp = Fn.to_planes(dlogits)
+            Fn.conv_wgrad(dlp.view(B, 1, 1, self.ld), x.view(B, 1, 1, self.cin), self._wgrad_spec(),
+                          self.w.grad.view(self.ncls, self.cin))
+            dx = torch.empty((B, self.cin), dtype=torch.float32, device=x.device)
+            Fn.conv_dgrad(dlp.view(B, 1, 1, self.ld), self._dgrad_spec(), self.pack.tr, None,
+                          dx.view(B, 1, 1, self.cin), False)
+        elif Fn.native(x):
             hcb = Fn._ext.ops()
             geom = [B, 1, 1, self.cin, self.cin, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, self.ncls, self.ld]
             cfg, splits = 2, 1
@@ -649,6 +669,15 @@ class Logits(Layer):
             dx = g @ self.w.data.view(self.ncls, self.cin).to(x.dtype)
         self._x = None
         return dx
+
+    def _wgrad_spec(self):
+        """dW[ncls, cin] = dlogits^T x as a 1x1 conv's weight gradient (dz rows of ld columns)."""
+        return ConvSpec(cin=self.cin, cin_pad=self.cin, cout=self.ncls, kh=1, kw=1)
+
+    def _dgrad_spec(self):
+        """dx = dlogits W as a 1x1 conv's data gradient: the reduction runs over the padded logits
+        width (the transposed pack's Kpad_t covers it)."""
+        return ConvSpec(cin=self.cin, cin_pad=self.cin, cout=self.ld, kh=1, kw=1)
 
     def flops(self, batch):
         return 2 * batch * self.cin * self.ncls

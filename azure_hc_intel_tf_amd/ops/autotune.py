@@ -219,15 +219,92 @@ def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
     return out
 
 
+def _planes(shape, dev):
+    return Fn.Planes(torch.randn((3,) + tuple(shape), device=dev).to(torch.bfloat16))
+
+
+def _best(cands, run):
+    best = None
+    for plan in cands:
+        t = _time(lambda: run(plan))
+        if best is None or t < best[0]:
+            best = (t, plan)
+    return best
+
+
+def tune_conv_layer_p3(layer, batch: int, dev, verbose=False) -> List[Tuple]:
+    """fp32 path: tune the bf16-plane GEMMs (conv_p3.hip) of one ConvBN layer -- forward, data
+    gradient (or its stride phases), weight gradient -- over their own tile / split-K sets."""
+    spec = layer.spec
+    H, W, Cin = layer.in_shape
+    P, Q, Cout = layer.out_shape
+    N = batch
+    M = N * P * Q
+    taps = spec.kh * spec.kw
+    geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
+    phases = Fn.dgrad_phases(spec, H, W) if layer.need_dx and Fn.uses_dgrad_phases(spec, H, W) else []
+    keys = [Fn.fwd3_key(M, Cout, spec.K, taps), Fn.wgrad3_key(Cout, spec.K, M, taps)]
+    if layer.need_dx and not phases:
+        keys.append(Fn.fwd3_key(geo[0], Cin, geo[1], taps))
+    for ph in phases:
+        pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
+        keys.append(Fn.fwd3_key(pm, Cin, pk, pt))
+    out = []
+    if all(k in Fn._tuned for k in keys):
+        return out
+    x = _planes((N, H, W, Cin), dev)
+    dz = _planes((N, P, Q, Cout), dev)
+    k = keys[0]
+    if k not in Fn._tuned:
+        y = torch.empty((N, P, Q, Cout), dtype=torch.float32, device=dev)
+        acc = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
+        best = _best(Fn.p3_candidates(M, Cout, spec.K),
+                     lambda plan: Fn.conv_forward(x, spec, layer.pack.pack, None, y, stats=acc, cfg=plan, stats_R=8))
+        Fn._tuned[k] = list(best[1])
+        out.append((k, best))
+    if layer.need_dx:
+        dx = torch.zeros((N, H, W, Cin), dtype=torch.float32, device=dev)
+        if not phases:
+            k = Fn.fwd3_key(geo[0], Cin, geo[1], taps)
+            if k not in Fn._tuned:
+                best = _best(Fn.p3_candidates(geo[0], Cin, geo[1]),
+                             lambda plan: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=plan))
+                Fn._tuned[k] = list(best[1])
+                out.append((k, best))
+        for ph in phases:
+            pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
+            k = Fn.fwd3_key(pm, Cin, pk, pt)
+            if k in Fn._tuned:
+                continue
+            best = _best(Fn.p3_candidates(pm, Cin, pk),
+                         lambda plan: Fn.dgrad_phase(dz, spec, layer.pack.tr, dx, True, ph, cfg=plan))
+            Fn._tuned[k] = list(best[1])
+            out.append((k, best))
+    k = Fn.wgrad3_key(Cout, spec.K, M, taps)
+    if k not in Fn._tuned:
+        dw = torch.zeros((Cout, spec.K), dtype=torch.float32, device=dev)
+        best = _best(Fn.wgrad_p3_candidates(Cout, spec.K, M), lambda plan: Fn.conv_wgrad(dz, x, spec, dw, cfg=plan))
+        Fn._tuned[k] = list(best[1])
+        out.append((k, best))
+    if verbose:
+        for kk, (t, c) in out:
+            print(f"  tuned {kk}: cfg={c} {t * 1000:.1f} us")
+    return out
+
+
 def tune_model(model, batch: int, verbose=False, cache: str = DEFAULT_CACHE, save=True) -> int:
     from ..nn.layers import ConvBN
 
     dev = model.device
     model.ps.repack()
     n = 0
+    p3 = getattr(model, "compute_dtype", None) == "fp32" and model.native
+    if hasattr(model, "activate"):
+        model.activate()
     for l in model.all_layers():
         if isinstance(l, ConvBN) and l.bn:
-            n += len(tune_conv_layer(l.tune_view() if hasattr(l, "tune_view") else l, batch, dev, verbose))
+            view = l.tune_view() if hasattr(l, "tune_view") else l
+            n += len((tune_conv_layer_p3 if p3 else tune_conv_layer)(view, batch, dev, verbose))
     torch.cuda.synchronize()
     if save and n and cache:
         try:

@@ -25,8 +25,8 @@ import torch.nn.functional as F
 from . import _ext
 
 
-def ld(t: torch.Tensor) -> int:
-    """Pixel stride (elements) of an NHWC activation (supports channel-slice views)."""
+def ld(t) -> int:
+    """Pixel stride (elements) of an NHWC activation (supports channel-slice views and Planes)."""
     if t.dim() == 4:
         assert t.stride(3) == 1, "activation channels must be contiguous"
         return t.stride(2)
@@ -74,8 +74,6 @@ F16_NATIVE = True
 # (CNNModel.activate) for the models whose whole op set has the fp32 kernels (ResNet v1 / v1.5);
 # other models keep the PyTorch path in fp32.
 _F32_NATIVE = [False]
-# data_ptr of a bf16 weight pack -> its [2][n] mid / lo packs (ParamStore, fp32 path)
-_LO = {}
 
 
 def set_f32_native(on: bool) -> None:
@@ -83,19 +81,16 @@ def set_f32_native(on: bool) -> None:
 
 
 def register_lo(pack, lo) -> None:
-    """Record (lo = None: forget) the mid / lo packs of ``pack``."""
-    if lo is None:
-        _LO.pop(pack.data_ptr(), None)
-    else:
-        _LO[pack.data_ptr()] = lo
+    """Attach (lo = None: detach) the mid / lo packs to the pack tensor ``pack``."""
+    pack.hcb_lo = lo
 
 
 def lo_pack(w):
-    """The [2][n] mid / lo bf16 packs of weight pack ``w`` (fp32 path), or None."""
+    """The [2][n] mid / lo bf16 packs of weight pack ``w`` (fp32 path), or None. Held on the pack
+    tensor itself (``w.hcb_lo``, set by ParamStore.finalize), so it lives and dies with the pack."""
     if w is None:
         return None
-    lo = _LO.get(w.data_ptr())
-    # an address can be reused by a later, unrelated pack: the entry must describe THIS one
+    lo = getattr(w, "hcb_lo", None)
     if lo is None or lo.shape[-1] != w.numel() or lo.device != w.device:
         return None
     return lo
@@ -105,11 +100,125 @@ def _f32o(t) -> int:
     return 1 if t.dtype == torch.float32 else 0
 
 
+class Planes:
+    """An fp32 tensor held as three bf16 PLANES, hi / mid / lo (``t``: bf16 ``[3, *shape]``; hi + mid +
+    lo == the fp32 value exactly, 8 + 8 + 8 significant bits): the fp32 path's GEMM-operand format.
+    The producing kernel (BN apply, BN backward, the split kernel) writes it, so the bf16x6 GEMMs
+    (csrc/kernels/conv_p3.hip) stage plain bf16 tiles by LDS-DMA with no per-use split. It stands in
+    for an fp32 activation: ``shape`` / ``dtype`` (float32) / ``device`` / ``stride`` / ``view`` are
+    those of the logical tensor."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t: torch.Tensor):
+        assert t.dtype == torch.bfloat16 and t.dim() >= 2 and t.shape[0] == 3, "planes are bf16 [3, ...]"
+        self.t = t
+
+    @staticmethod
+    def empty(shape, device) -> "Planes":
+        return Planes(torch.empty((3,) + tuple(shape), dtype=torch.bfloat16, device=device))
+
+    @property
+    def shape(self):
+        return self.t.shape[1:]
+
+    @property
+    def dtype(self):
+        return torch.float32
+
+    @property
+    def device(self):
+        return self.t.device
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.t.is_cuda
+
+    def dim(self) -> int:
+        return self.t.dim() - 1
+
+    def stride(self, i: int) -> int:
+        return self.t.stride(i + 1 if i >= 0 else i)
+
+    def numel(self) -> int:
+        return self.t[0].numel()
+
+    def is_contiguous(self) -> bool:
+        return self.t.is_contiguous()
+
+    def view(self, *shape) -> "Planes":
+        if len(shape) == 1 and isinstance(shape[0], (tuple, list, torch.Size)):
+            shape = tuple(shape[0])
+        return Planes(self.t.view((3,) + tuple(shape)))
+
+    def reshape(self, *shape) -> "Planes":
+        return self.view(*shape)
+
+    def float(self) -> torch.Tensor:
+        """The fp32 value (hi + (mid + lo), exact)."""
+        return self.t[0].float() + (self.t[1].float() + self.t[2].float())
+
+
+def is_planes(t) -> bool:
+    return isinstance(t, Planes)
+
+
+def planes_mode() -> bool:
+    """True while an fp32-native model is active: its GEMM operands are stored as Planes."""
+    return _F32_NATIVE[0]
+
+
+def to_planes(x: torch.Tensor) -> Planes:
+    """fp32 [..., C] (C % 8 == 0; rows may be strided) -> Planes of the same logical shape (one
+    launch on the GPU)."""
+    if isinstance(x, Planes):
+        return x
+    assert x.dtype == torch.float32 and x.shape[-1] % 8 == 0
+    out = Planes.empty(tuple(x.shape), x.device)
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if x.is_cuda:
+        xv = x if x.dim() >= 2 else x.view(1, -1)
+        ldx = xv.stride(-2) if xv.dim() >= 2 and xv.shape[-2] > 1 else C
+        if not _rows_uniform(xv, C):
+            xv = xv.contiguous()
+            ldx = C
+        _ext.ops().split_planes(xv, ldx, rows, C, out.t, C)
+        return out
+    h = x.to(torch.bfloat16)
+    r = x - h.float()
+    m = r.to(torch.bfloat16)
+    out.t[0].copy_(h)
+    out.t[1].copy_(m)
+    out.t[2].copy_((r - m.float()).to(torch.bfloat16))
+    return out
+
+
+def _rows_uniform(x: torch.Tensor, C: int) -> bool:
+    """x's rows of C channels are evenly strided (one row stride over every leading dim)."""
+    if x.stride(-1) != 1:
+        return False
+    ld = x.stride(-2) if x.dim() >= 2 else C
+    exp = ld
+    for d in range(x.dim() - 2, -1, -1):
+        if x.shape[d] > 1 and x.stride(d) != exp:
+            return False
+        exp *= x.shape[d]
+    return True
+
+
+def _pl(t):
+    """The tensor a kernel binding receives for t (Planes -> its [3, ...] bf16 storage)."""
+    return t.t if isinstance(t, Planes) else t
+
+
 def native(t) -> bool:
     """True when ``t`` goes through the hand-written HIP kernels: a bf16 (or, with the fp16
     build, IEEE-fp16) activation on the GPU, or an fp32 one while an fp32-native model is
     active. Other tensors take the PyTorch path below (MIOpen / rocBLAS on the GPU), the same
     code as the CPU path."""
+    if isinstance(t, Planes):
+        return t.is_cuda
     return t.is_cuda and (t.dtype == torch.bfloat16 or (t.dtype == torch.float16 and F16_NATIVE)
                           or (t.dtype == torch.float32 and _F32_NATIVE[0]))
 
@@ -323,6 +432,96 @@ def set_tuned(table: dict) -> None:
     _tuned.update(table)
 
 
+# ---- fp32 path (Planes operands, conv_p3.hip): its own tile sets and tuning keys
+_P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128)}
+_WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64)}
+
+
+def fwd3_key(M: int, N: int, K: int, taps: int = 1):
+    return ("fwd3", M, N, K, taps)
+
+
+def wgrad3_key(Nout: int, K: int, M: int, taps: int = 1):
+    return ("wgrad3", Nout, K, M, taps)
+
+
+def p3_candidates(M: int, N: int, K: int):
+    """(cfg, splits) worth timing for an fp32 (Planes) forward / data-grad GEMM: every tile, and
+    split-K while the grid is below ~1 workgroup per CU (one fits per CU: 144 KB of LDS) and every
+    split keeps >= 3 k-steps."""
+    out = []
+    ksteps = math.ceil(K / 64)
+    for c, (bm, bn) in _P3_TILES.items():
+        if N <= 64 and bn > 64:
+            continue
+        tiles = math.ceil(M / bm) * math.ceil(N / bn)
+        out.append((c, 1))
+        for s in (2, 3, 4, 6, 8):
+            if tiles * (s - 1) >= N_CU or ksteps // s < 3 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
+                break
+            out.append((c, s))
+    return out
+
+
+def p3_plan(M: int, N: int, K: int, taps: int = 1):
+    """(cfg, splits) of an fp32 (Planes) forward / data-grad GEMM: tuned, else 128x64 (64x128 for
+    wide outputs) with split-K up to ~one workgroup per CU."""
+    key = fwd3_key(M, N, K, taps)
+    if key in _tuned:
+        c = _tuned[key]
+        return (int(c[0]), int(c[1])) if isinstance(c, (tuple, list)) else (int(c), 1)
+    cfg = 1 if N >= 128 and M < 4096 else 0
+    bm, bn = _P3_TILES[cfg]
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    ksteps = math.ceil(K / 64)
+    s = 1
+    while tiles * (s + 1) <= N_CU and ksteps // (s + 1) >= 3 and s < 8:
+        s += 1
+    return cfg, s
+
+
+def wgrad_p3_candidates(Nout: int, K: int, M: int):
+    ksteps = math.ceil(M / 64)
+    out = []
+    for c, (bm, bn) in _WP3_TILES.items():
+        tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
+        for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+            if s > 1 and ksteps // s < 2:
+                break
+            if tiles * s > 4 * N_CU:
+                break
+            out.append((c, s))
+    return out
+
+
+def wgrad_p3_plan(Nout: int, K: int, M: int, taps: int = 1):
+    key = wgrad3_key(Nout, K, M, taps)
+    if key in _tuned:
+        c = _tuned[key]
+        return int(c[0]), int(c[1])
+    c = 0 if Nout >= 128 else (1 if K >= 128 else 2)
+    bm, bn = _WP3_TILES[c]
+    tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
+    ksteps = math.ceil(M / 64)
+    splits = max(1, min(ksteps // 4 if ksteps >= 4 else 1, math.ceil(2 * N_CU / tiles)))
+    return c, splits
+
+
+def _plan3(cfg, M, N, K, device, taps: int = 1):
+    if cfg is None:
+        cfg, splits = p3_plan(M, N, K, taps)
+    elif isinstance(cfg, (tuple, list)):
+        cfg, splits = cfg
+    else:
+        splits = 1
+    splits = max(1, min(int(splits), max(K // 64, 1)))
+    if _DET[0]:
+        splits = 1
+    if splits > 1:
+        ensure_splitk_workspace(device)
+    return int(cfg), int(splits)
+
+
 # ---------------------------------------------------------------- conv forward
 def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None, cfg=None, relu=False,
                  stats_R: int = 0, residual=None, stats_shift=None):
@@ -330,6 +529,8 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
     statistics: per-tile slab (stats_R=0) or fp32 atomics into stats_R replicas of [2][cout].
     ``stats_shift`` (fp32 [cout]): the statistics are sums of (v - shift) and (v - shift)^2, which
     keeps the single-pass variance exact when |mean| >> std; the BN apply gets the same shift."""
+    if is_planes(x) or (native(x) and x.dtype == torch.float32):
+        return _conv_forward_p3(x, spec, wpack, out, stats, bias, cfg, relu, stats_R, residual, stats_shift)
     N, H, W, _ = x.shape
     P, Q = spec.out_hw(H, W)
     if native(x):
@@ -359,6 +560,25 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
     if residual is not None:
         y = y + residual
     out.copy_(y)
+    return out
+
+
+def _conv_forward_p3(x, spec: ConvSpec, wpack, out, stats, bias, cfg, relu, stats_R, residual, stats_shift):
+    """fp32 forward conv on bf16 planes (bf16x6 MFMA GEMM, conv_p3.hip): x Planes (an fp32 tensor
+    is split first), fp32 out with the fused BN statistics / bias / ReLU / residual epilogue."""
+    x = to_planes(x)
+    N, H, W, _ = x.shape
+    P, Q = spec.out_hw(H, W)
+    M = N * P * Q
+    cfg, splits = _plan3(cfg, M, spec.cout, spec.K, x.device, spec.kh * spec.kw)
+    w_lo = lo_pack(wpack)
+    assert w_lo is not None and out.dtype == torch.float32, "fp32 conv needs the mid / lo weight packs and an fp32 output"
+    if residual is not None:
+        assert ld(residual) == ld(out) and residual.shape == out.shape and residual.dtype == torch.float32
+    geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
+            spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1,
+            1 if residual is not None else 0, 1, 1 if relu else 0, int(stats_R), splits]
+    _ext.ops().conv_p3(x.t, wpack, w_lo, out, residual, bias, stats, geom, cfg, stats_shift)
     return out
 
 
@@ -481,25 +701,41 @@ def dgrad_phase(dz, spec: ConvSpec, wtr, dx, accumulate: bool, phase, cfg=None, 
     ph, pw, Hph, Wph, rs, ss, pad_t, pad_l = phase
     Cdz = spec.cout if spec.cout % 8 == 0 else _round_up(spec.cout, 8)
     sub, Kph = _phase_pack(wtr, spec, Cdz, rs, ss)
-    w_lo = None
-    if dz.dtype == torch.float32:
-        assert bnb is None, "no fused BN-backward epilogue on the fp32 path"
-        w_lo, _ = _phase_pack(lo_pack(wtr), spec, Cdz, rs, ss)
     M, _, taps = dgrad_phase_problem(spec, N, phase)
+    if dz.dtype == torch.float32:  # fp32 path: Planes operands
+        lo = lo_pack(wtr)
+        assert lo is not None, "fp32 data gradient needs the mid / lo weight packs"
+        w_lo, _ = _phase_pack(lo, spec, Cdz, rs, ss)
+        dz = to_planes(dz)
+        cfg, splits = _plan3(cfg, M, spec.cin_pad, Kph, dz.device, taps)
+        geom = [N, P, Q, Cdz, ld(dz), Hph, Wph, len(rs), len(ss), 1, 1, pad_t, pad_l, 1, 1, 1, 1,
+                spec.cin_pad, Kph, sub.shape[1], ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, 1,
+                0, 0, splits, ph, pw]
+        _p3_dgrad_launch(dz, sub, w_lo, dx, accumulate, geom, cfg, bnb)
+        return
     geom = [N, P, Q, Cdz, ld(dz), Hph, Wph, len(rs), len(ss), 1, 1, pad_t, pad_l, 1, 1, 1, 1,
             spec.cin_pad, Kph, sub.shape[1], ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, _f32o(dx)]
     if cfg is None and bnb is not None:
         cfg = _tuned.get(dgb_key(M, spec.cin_pad, Kph, taps))
     cfg, splits = _plan(cfg, M, spec.cin_pad, Kph, dz.device, taps)
-    if w_lo is not None:
-        splits = 1
     geom = geom + [0, 0, splits, ph, pw]
     if bnb is not None:
         _ext.ops().conv_igemm_bnb(dz, sub, dx, dx if accumulate else None, geom, cfg, bnb.z,
                                   bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
                                   bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
     else:
-        _ext.ops().conv_igemm(dz, sub, dx, dx if accumulate else None, None, None, geom, cfg, None, w_lo)
+        _ext.ops().conv_igemm(dz, sub, dx, dx if accumulate else None, None, None, geom, cfg, None, None)
+
+
+def _p3_dgrad_launch(dz: "Planes", w, w_lo, dx, accumulate: bool, geom, cfg: int, bnb: "BNBwdFuse" = None):
+    """One fp32 (Planes) data-gradient GEMM, with the consuming BN layer's backward reduction fused
+    into its epilogue when ``bnb`` is given (z fp32, the ReLU mask from the hi plane of y)."""
+    if bnb is None:
+        _ext.ops().conv_p3(dz.t, w, w_lo, dx, dx if accumulate else None, None, None, geom, cfg, None)
+        return
+    _ext.ops().conv_p3_bnb(dz.t, w, w_lo, dx, dx if accumulate else None, geom, cfg, bnb.z,
+                           _pl(bnb.y) if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean, bnb.saved.invstd,
+                           bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
 
 
 def uses_dgrad_phases(spec: ConvSpec, H: int, W: int) -> bool:
@@ -537,13 +773,18 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
                     spec.sh, spec.sw, spec.cin_pad, K, Kpad, ld(dx), 0, H, W, 1, 1,
                     1 if accumulate else 0, _f32o(dx)]
         taps = spec.kh * spec.kw
+        if dz.dtype == torch.float32:  # fp32 path: Planes operands (bf16x6 GEMM, conv_p3.hip)
+            w_lo = lo_pack(wtr)
+            assert w_lo is not None, "fp32 data gradient needs the mid / lo weight packs"
+            dz = to_planes(dz)
+            geom[4] = ld(dz)
+            cfg, splits = _plan3(cfg, M, spec.cin_pad, K, dz.device, taps)
+            _p3_dgrad_launch(dz, wtr, w_lo, dx, accumulate, geom + [0, 0, splits], cfg, bnb)
+            return dx
         if cfg is None and bnb is not None:
             cfg = _tuned.get(dgb_key(M, spec.cin_pad, K, taps))
         cfg, splits = _plan(cfg, M, spec.cin_pad, K, dz.device, taps)
         w_lo = None
-        if dz.dtype == torch.float32:
-            assert bnb is None, "no fused BN-backward epilogue on the fp32 path"
-            w_lo, splits = lo_pack(wtr), 1
         geom = geom + [0, 0, splits]
         if bnb is not None:
             _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
@@ -572,6 +813,16 @@ def conv_wgrad(dz, x, spec: ConvSpec, dw, cfg=None):
     """dw[cout, kh, kw, cin_pad] (fp32) += sum over pixels of dz (x) im2col(x)."""
     N, H, W, _ = x.shape
     _, P, Q, _ = dz.shape
+    if native(dz) and dz.dtype == torch.float32:  # fp32 path: Planes operands (conv_p3.hip)
+        dz, x = to_planes(dz), to_planes(x)
+        M = N * P * Q
+        cfg, splits = cfg if cfg is not None else wgrad_p3_plan(spec.cout, spec.K, M, spec.kh * spec.kw)
+        if _DET[0]:
+            splits = 1
+        geom = [N, H, W, spec.cin_pad, ld(x), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
+                spec.dh, spec.dw, spec.cout, ld(dz)]
+        _ext.ops().conv_wgrad_p3(dz.t, x.t, dw, geom, int(cfg), int(splits))
+        return dw
     if native(dz):
         M = N * P * Q
         cfg, splits = cfg if cfg is not None else wgrad_cfg(spec.cout, spec.K, M, spec.kh * spec.kw)
@@ -664,8 +915,8 @@ def bn_forward_acc(z, gamma, beta, running_mean, running_var, momentum, eps, out
     its normalised tensor is never written); same M, C and replica count R."""
     N, H, W, C = z.shape
     M = N * H * W
-    _ext.ops().bn_apply_acc(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0, M, C,
-                            acc, R, eps, momentum, gamma, beta, 1 if relu else 0, saved_mean, saved_invstd,
+    _ext.ops().bn_apply_acc(z, ld(z), _pl(out), ld(out), _pl(residual), ld(residual) if residual is not None else 0,
+                            M, C, acc, R, eps, momentum, gamma, beta, 1 if relu else 0, saved_mean, saved_invstd,
                             running_mean, running_var, shift, *(res_bn or ()))
     return BNSaved(saved_mean, saved_invstd)
 
@@ -677,7 +928,7 @@ def bn_relu_maxpool_acc(z, gamma, beta, running_mean, running_var, momentum, eps
     N, H, W, C = z.shape
     _, P, Q, _ = out.shape
     pt, pb, pl, pr = pads
-    _ext.ops().bn_relu_maxpool_acc(z, out, argmax, [N, H, W, C, P, Q, ld(out), kh, kw, sh, sw, pt, pl], acc, R, eps,
+    _ext.ops().bn_relu_maxpool_acc(z, _pl(out), argmax, [N, H, W, C, P, Q, ld(out), kh, kw, sh, sw, pt, pl], acc, R, eps,
                                    momentum, gamma, beta, saved_mean, saved_invstd, running_mean, running_var, shift)
     return BNSaved(saved_mean, saved_invstd)
 
@@ -694,13 +945,13 @@ def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamm
     hcb = _ext.ops()
     if pre_reduced:
         assert gres is None, "pre-reduced dy is itself the residual gradient"
-        hcb.bn_bwd_apply_acc(dy, ld(dy), None, 0, z, ld(z), dz, ld(dz), M, C, saved.mean, saved.invstd, gamma,
+        hcb.bn_bwd_apply_acc(dy, ld(dy), None, 0, z, ld(z), _pl(dz), ld(dz), M, C, saved.mean, saved.invstd, gamma,
                              beta, acc, R, dgamma, dbeta, 0, shift_out)
         return dz
-    ym = y if relu_mode == 1 else None
+    ym = _pl(y) if relu_mode == 1 else None
     hcb.bn_bwd_reduce_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), M, C, saved.mean, saved.invstd,
                           gamma, beta, relu_mode, acc, R, gres, ld(gres) if gres is not None else 0)
-    hcb.bn_bwd_apply_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), dz, ld(dz), M, C, saved.mean,
+    hcb.bn_bwd_apply_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), _pl(dz), ld(dz), M, C, saved.mean,
                          saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode, shift_out)
     return dz
 
@@ -775,6 +1026,9 @@ def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False, argmax=No
 
 def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, accumulate=False, argmax=None):
     pt, pb, pl, pr = pads
+    if is_planes(y):  # fp32 stem pool: the argmax gather reads dy and the argmax only
+        assert argmax is not None and is_max
+        y = dy
     if native(x):
         # the kernel walks x / dx with one pixel stride and y / dy with another: align views
         if ld(y) != ld(dy):
@@ -814,6 +1068,11 @@ def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, ac
 
 def gap_forward(x, out):
     N, H, W, C = x.shape
+    if is_planes(x):
+        out = out if is_planes(out) else None
+        assert out is not None, "gap_forward of Planes writes Planes"
+        _ext.ops().gap_fwd_p3(x.t, out.t, N, H * W, C)
+        return out
     if native(x):
         assert x.is_contiguous()
         _ext.ops().gap_fwd(x, out, N, H * W, C)

@@ -7,6 +7,7 @@
 // host BEFORE anything reaches the GPU (an out-of-range gather must never be launched)
 // and enqueues on the current HIP stream.
 #include <algorithm>
+#include <vector>
 
 #include <torch/library.h>
 #include <ATen/core/Tensor.h>
@@ -75,6 +76,17 @@ void check_range(const Tensor& t, int64_t need_bytes, const char* name) {
 }
 void check_align16(const void* p, const char* name) {
   TORCH_CHECK(((uintptr_t)p & 15) == 0, "hcb: ", name, " must be 16-byte aligned");
+}
+
+// fp32 path (conv_p3.hip): a plane tensor is bf16 [3, ...] (plane t = select(0, t))
+int64_t check_planes(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.dim() >= 2 && t.size(0) == 3,
+              "hcb: ", name, " must be bf16 planes [3, ...]");
+  TORCH_CHECK(t.stride(-1) == 1, "hcb: ", name, " channels must be contiguous");
+  check_align16(t.data_ptr(), name);
+  TORCH_CHECK((t.stride(0) * 2) % 16 == 0, "hcb: ", name, " plane stride must keep 16-byte alignment");
+  return t.stride(0);  // elements between planes
 }
 
 // geom = [N,H,W,C,ldx, P,Q,R,S, sh,sw,ph,pw,dh,dw,idh,idw, Nout,K,Kpad,ldy,
@@ -215,24 +227,31 @@ void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::op
 // data-grad conv whose output is the dy of a BN layer: the epilogue gates it with the
 // layer's ReLU mask (mode 1: y > 0, 2: recomputed from z, 0: none), stores g and adds
 // sum(g), sum(g*xhat) per channel into acc [R][2][Nout] (see ConvParams::bnb_*)
-void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
-                    at::IntArrayRef g, int64_t cfg, const Tensor& z, const c10::optional<Tensor>& yact,
-                    int64_t ld, const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
-                    const Tensor& acc, int64_t R, int64_t mode) {
-  hcb::ConvParams p = conv_params(x, w, y, yres, c10::nullopt, c10::nullopt, g, cfg);
-  TORCH_CHECK(!p.out_f32 && !p.relu && p.bias == nullptr, "hcb.conv_igemm_bnb: bf16 output without bias/relu");
+// the fused BN-backward fields of a data-grad GEMM; f32: the fp32 path (z fp32, y the [3, ...] bf16
+// planes of the activation -- the epilogue reads the hi plane -- output g fp32)
+void set_bnb(hcb::ConvParams& p, const Tensor& z, const c10::optional<Tensor>& yact, int64_t ld, const Tensor& mean,
+             const Tensor& invstd, const Tensor& gamma, const Tensor& beta, const Tensor& acc, int64_t R, int64_t mode,
+             bool f32) {
+  TORCH_CHECK(!p.relu && p.bias == nullptr, "hcb.conv_igemm_bnb: no bias / relu");
+  TORCH_CHECK(p.out_f32 == (f32 ? 1 : 0), "hcb.conv_igemm_bnb: 16-bit output (fp32 on the fp32 path)");
   TORCH_CHECK(mode >= 0 && mode <= 2 && R >= 1, "hcb.conv_igemm_bnb: bad mode / R");
   TORCH_CHECK(ld % 8 == 0 && ld >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm_bnb: bad ld");
   int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
-  int64_t need = (rows - 1) * ld * 2 + ((p.Nout + 7) / 8) * 8 * 2;
-  check_act(z, "z");
-  check_range(z, need, "z");
+  const int64_t zsz = f32 ? 4 : 2;
+  if (f32)
+    check_f32(z, "z");
+  else
+    check_act(z, "z");
+  check_range(z, ((rows - 1) * ld + ((p.Nout + 7) / 8) * 8) * zsz, "z");
   check_align16(z.data_ptr(), "z");
   p.bnb_y = nullptr;
   if (mode == 1) {
     TORCH_CHECK(yact.has_value(), "hcb.conv_igemm_bnb: mode 1 needs y");
-    check_act(*yact, "y");
-    check_range(*yact, need, "y");
+    if (f32)
+      check_planes(*yact, "y");
+    else
+      check_act(*yact, "y");
+    check_range(*yact, ((rows - 1) * ld + ((p.Nout + 7) / 8) * 8) * 2, "y");
     check_align16(yact->data_ptr(), "y");
     p.bnb_y = yact->data_ptr();
   }
@@ -251,6 +270,17 @@ void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10
   p.bnb_acc = acc.data_ptr<float>();
   p.bnb_mode = (int)mode;
   p.bnb_R = (int)R;
+}
+
+// data-grad conv whose output is the dy of a BN layer: the epilogue gates it with the
+// layer's ReLU mask (mode 1: y > 0, 2: recomputed from z, 0: none), stores g and adds
+// sum(g), sum(g*xhat) per channel into acc [R][2][Nout] (see ConvParams::bnb_*)
+void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
+                    at::IntArrayRef g, int64_t cfg, const Tensor& z, const c10::optional<Tensor>& yact,
+                    int64_t ld, const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
+                    const Tensor& acc, int64_t R, int64_t mode) {
+  hcb::ConvParams p = conv_params(x, w, y, yres, c10::nullopt, c10::nullopt, g, cfg);
+  set_bnb(p, z, yact, ld, mean, invstd, gamma, beta, acc, R, mode, false);
   hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
 }
 
@@ -428,14 +458,17 @@ void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, a
                          const Tensor& run_var, const c10::optional<Tensor>& shift) {
   TORCH_CHECK(g.size() == 13, "hcb.bn_relu_maxpool_acc: geom");
   const bool f32 = check_act_or_f32(z, "z");
-  same_act(z, y, "y");
+  // fp32 z with a bf16 y: y is the [3, ...] bf16 planes of the fp32 output (conv_p3 operands)
+  const bool yp3 = f32 && y.scalar_type() == at::kBFloat16;
+  const int64_t yps = yp3 ? check_planes(y, "y") : 0;
+  if (!yp3) same_act(z, y, "y");
   const int64_t e = f32 ? 4 : 2;
   check_cuda(amax, "amax");
   const int64_t N = g[0], H = g[1], W = g[2], C = g[3], P = g[4], Q = g[5], ldy = g[6];
   TORCH_CHECK(z.is_contiguous() && z.numel() == N * H * W * C, "hcb.bn_relu_maxpool_acc: z contiguous [N,H,W,C]");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldy % 8 == 0 && ldy >= C, "hcb.bn_relu_maxpool_acc: C / ldy");
   TORCH_CHECK(g[7] * g[8] <= 255, "hcb.bn_relu_maxpool_acc: window too large for the uint8 argmax");
-  check_range(y, ((N * P * Q - 1) * ldy + C) * e, "y");
+  check_range(y, yp3 ? (2 * yps + (N * P * Q - 1) * ldy + C) * 2 : ((N * P * Q - 1) * ldy + C) * e, "y");
   TORCH_CHECK(amax.scalar_type() == at::kByte && amax.is_contiguous() && amax.numel() >= N * P * Q * C,
               "hcb.bn_relu_maxpool_acc: amax uint8 [N,P,Q,C]");
   TORCH_CHECK(N * P * Q < (1ll << 31) && N * H * W < (1ll << 31), "hcb.bn_relu_maxpool_acc: 32-bit index range");
@@ -447,7 +480,7 @@ void bn_relu_maxpool_acc(const Tensor& z, const Tensor& y, const Tensor& amax, a
                                   g[10], g[11], g[12], acc.data_ptr<float>(), R, (float)eps, (float)momentum,
                                   gamma.data_ptr<float>(), beta.data_ptr<float>(), saved_mean.data_ptr<float>(),
                                   saved_invstd.data_ptr<float>(), run_mean.data_ptr<float>(),
-                                  run_var.data_ptr<float>(), opt_f32(shift, C, "shift"), cur_stream(), f32);
+                                  run_var.data_ptr<float>(), opt_f32(shift, C, "shift"), cur_stream(), f32, yps);
 }
 
 // geom = [N,H,W,C,ldx,P,Q,ldy,kh,kw,sh,sw,ph,pw,is_max,incl_pad]
@@ -633,18 +666,29 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                   const c10::optional<Tensor>& res_saved_invstd, const c10::optional<Tensor>& res_rm,
                   const c10::optional<Tensor>& res_rv, const c10::optional<Tensor>& res_shift) {
   const bool f32 = check_act_or_f32(x, "x");
-  same_act(x, y, "y");
+  // fp32 z with a bf16 y: y is written as [3, ...] bf16 planes; a bf16 residual is planes too
+  const bool yp3 = f32 && y.scalar_type() == at::kBFloat16;
+  const int64_t yps = yp3 ? check_planes(y, "y") : 0;
+  if (!yp3) same_act(x, y, "y");
+  int64_t rps = 0;
   const int64_t e = f32 ? 4 : 2;
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldy % 8 == 0 && R >= 1, "hcb.bn_apply_acc: C/ld/R");
   TORCH_CHECK(acc.numel() >= R * 2 * C && saved_mean.numel() >= C && saved_invstd.numel() >= C, "hcb.bn_apply_acc: sizes");
   check_range(x, ((M - 1) * ldx + C) * e, "x");
-  check_range(y, ((M - 1) * ldy + C) * e, "y");
+  check_range(y, yp3 ? (2 * yps + (M - 1) * ldy + C) * 2 : ((M - 1) * ldy + C) * e, "y");
   const void* rp = nullptr;
   if (res.has_value()) {
-    same_act(x, *res, "res");
     TORCH_CHECK(ldr % 8 == 0, "hcb.bn_apply_acc: ldr");
-    check_range(*res, ((M - 1) * ldr + C) * e, "res");
+    if (yp3 && res->scalar_type() == at::kBFloat16) {
+      TORCH_CHECK(!res_acc.has_value(), "hcb.bn_apply_acc: a residual BN reads the fp32 z_sc, not planes");
+      rps = check_planes(*res, "res");
+      check_range(*res, (2 * rps + (M - 1) * ldr + C) * 2, "res");
+    } else {
+      same_act(x, *res, "res");
+      check_range(*res, ((M - 1) * ldr + C) * e, "res");
+      TORCH_CHECK(!yp3 || res_acc.has_value(), "hcb.bn_apply_acc: a plain fp32-path residual must be planes");
+    }
     rp = res->data_ptr();
   }
   // residual BN (projection shortcut): the residual is that BN's raw input z_sc
@@ -667,7 +711,7 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                            beta.data_ptr<float>(), (int)relu, saved_mean.data_ptr<float>(),
                            saved_invstd.data_ptr<float>(), rm.has_value() ? rm->data_ptr<float>() : nullptr,
                            rv.has_value() ? rv->data_ptr<float>() : nullptr, opt_f32(shift, C, "shift"),
-                           res_acc.has_value() ? &rb : nullptr, cur_stream(), f32);
+                           res_acc.has_value() ? &rb : nullptr, cur_stream(), f32, yps, rps);
 }
 
 void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
@@ -682,10 +726,17 @@ void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tenso
   check_range(dy, ((M - 1) * lddy + C) * e, "dy");
   check_range(x, ((M - 1) * ldx + C) * e, "x");
   const void* yp = nullptr;
+  bool yh = false;  // fp32 path: y given as its bf16 planes, the mask read from the hi plane
   if (relu == 1) {
     TORCH_CHECK(y.has_value(), "hcb.bn_bwd_reduce_acc: relu=1 needs y");
-    same_act(dy, *y, "y");
-    check_range(*y, ((M - 1) * ldyv + C) * e, "y");
+    yh = f32 && y->scalar_type() == at::kBFloat16;
+    if (yh) {
+      check_planes(*y, "y");
+      check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    } else {
+      same_act(dy, *y, "y");
+      check_range(*y, ((M - 1) * ldyv + C) * e, "y");
+    }
     yp = y->data_ptr();
   }
   void* gp = nullptr;
@@ -697,7 +748,7 @@ void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tenso
   hcb::launch_bn_bwd_reduce_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, (int)M, (int)C,
                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
                                 beta.data_ptr<float>(), (int)relu, acc.data_ptr<float>(), (int)R, gp, (int)ldg,
-                                cur_stream(), f32);
+                                cur_stream(), f32, yh);
 }
 
 void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
@@ -707,25 +758,36 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
                       const c10::optional<Tensor>& shift_out) {
   const bool f32 = check_act_or_f32(dy, "dy");
   same_act(dy, x, "x");
-  same_act(dy, dx, "dx");
+  // fp32 dy with a bf16 dx: dx is written as [3, ...] bf16 planes (the data / weight-gradient
+  // GEMM operand format)
+  const bool dp3 = f32 && dx.scalar_type() == at::kBFloat16;
+  const int64_t dxps = dp3 ? check_planes(dx, "dx") : 0;
+  if (!dp3) same_act(dy, dx, "dx");
   const int64_t e = f32 ? 4 : 2;
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_apply_acc: C/R");
   check_range(dy, ((M - 1) * lddy + C) * e, "dy");
   check_range(x, ((M - 1) * ldx + C) * e, "x");
-  check_range(dx, ((M - 1) * lddx + C) * e, "dx");
+  check_range(dx, dp3 ? (2 * dxps + (M - 1) * lddx + C) * 2 : ((M - 1) * lddx + C) * e, "dx");
   const void* yp = nullptr;
+  bool yh = false;
   if (relu == 1) {
     TORCH_CHECK(y.has_value(), "hcb.bn_bwd_apply_acc: relu=1 needs y");
-    same_act(dy, *y, "y");
-    check_range(*y, ((M - 1) * ldyv + C) * e, "y");
+    yh = f32 && y->scalar_type() == at::kBFloat16;
+    if (yh) {
+      check_planes(*y, "y");
+      check_range(*y, ((M - 1) * ldyv + C) * 2, "y");
+    } else {
+      same_act(dy, *y, "y");
+      check_range(*y, ((M - 1) * ldyv + C) * e, "y");
+    }
     yp = y->data_ptr();
   }
   hcb::launch_bn_bwd_apply_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, dx.data_ptr(),
                                (int)lddx, (int)M, (int)C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                gamma.data_ptr<float>(), beta.data_ptr<float>(), acc.data_ptr<float>(), (int)R,
                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu,
-                               const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream(), f32);
+                               const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream(), f32, yh, dxps);
 }
 
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
@@ -885,6 +947,151 @@ void stem_wgrad_unfold(const Tensor& dwp, const Tensor& dw) {
                                 cur_stream());
 }
 
+// ---- fp32 path on bf16 planes (conv_p3.hip)
+
+// geom as conv_igemm; x: planes of the input, w: hi pack, w_lo: [2][n] mid / lo packs; y fp32
+hcb::ConvParams p3_params(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor& y,
+                          const c10::optional<Tensor>& yres, const c10::optional<Tensor>& bias,
+                          const c10::optional<Tensor>& stats, at::IntArrayRef g, int64_t cfg,
+                          const c10::optional<Tensor>& stats_shift) {
+  const int64_t xps = check_planes(x, "x");
+  TORCH_CHECK(cfg >= 0 && cfg < 7, "hcb.conv_p3: cfg 0..6");
+  // conv_params validates geometry and byte ranges on plane 0 (a bf16 tensor of this build's type);
+  // split-K is validated here against the p3 tiles
+  std::vector<int64_t> g1(g.begin(), g.end());
+  const int64_t splits = g1.size() > 30 ? g1[30] : 1;
+  if (g1.size() > 30) g1[30] = 1;
+  hcb::ConvParams p = conv_params(x.select(0, 0), w, y, yres, bias, c10::nullopt, g1, 0);
+  p.splits = (int)splits;
+  TORCH_CHECK(p.splits >= 1 && p.splits <= p.Kpad / 64, "hcb.conv_p3: 1 <= splits <= k-steps");
+  TORCH_CHECK(p.out_f32 && y.scalar_type() == at::kFloat, "hcb.conv_p3: fp32 output");
+  check_range(x, 2 * xps * 2 + (int64_t)p.x_bytes, "x planes");
+  TORCH_CHECK(2 * xps * 2 < (1ll << 32), "hcb.conv_p3: plane stride exceeds the 32-bit offset range");
+  p.x_plane = (uint32_t)(xps * 2);
+  TORCH_CHECK(w_lo.dim() == 2 && w_lo.size(0) == 2 && w_lo.stride(1) == 1 && w_lo.scalar_type() == w.scalar_type() &&
+                  w_lo.size(1) >= (int64_t)p.Nout * p.Kpad,
+              "hcb.conv_p3: w_lo must be [2][>= Nout*Kpad] of the pack's type");
+  const Tensor m = w_lo.select(0, 0), l = w_lo.select(0, 1);
+  check_align16(m.data_ptr(), "w_lo[0]");
+  check_align16(l.data_ptr(), "w_lo[1]");
+  p.w_lo = m.data_ptr();
+  p.w_lo2 = l.data_ptr();
+  p.stats = nullptr;
+  if (stats.has_value()) {
+    check_f32(*stats, "stats");
+    const int tiles_m = (p.M + hcb::p3_tile_m((int)cfg) - 1) / hcb::p3_tile_m((int)cfg);
+    const int64_t rows = p.stats_R > 0 ? p.stats_R : tiles_m;
+    TORCH_CHECK(stats->numel() >= rows * 2 * p.Nout, "hcb.conv_p3: stats buffer too small");
+    p.stats = stats->data_ptr<float>();
+  }
+  TORCH_CHECK(!stats_shift.has_value() || p.stats != nullptr, "hcb.conv_p3: stats_shift without stats");
+  p.stats_shift = opt_f32(stats_shift, p.Nout, "stats_shift");
+  if (p.splits > 1) {
+    TORCH_CHECK(g_splitk_ws != nullptr && g_splitk_cnt != nullptr, "hcb.conv_p3: split-K workspace not set");
+    const int bm = hcb::p3_tile_m((int)cfg), bn = hcb::p3_tile_n((int)cfg);
+    const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * ((p.Nout + bn - 1) / bn);
+    TORCH_CHECK(tiles * p.splits * bm * bn * 4 <= g_splitk_ws_bytes, "hcb.conv_p3: split-K workspace too small");
+    TORCH_CHECK(tiles <= g_splitk_cnt_n, "hcb.conv_p3: split-K counter array too small");
+    p.ws = g_splitk_ws;
+    p.cnt = g_splitk_cnt;
+  }
+  return p;
+}
+
+void conv_p3(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor& y, const c10::optional<Tensor>& yres,
+             const c10::optional<Tensor>& bias, const c10::optional<Tensor>& stats, at::IntArrayRef g, int64_t cfg,
+             const c10::optional<Tensor>& stats_shift) {
+  hcb::ConvParams p = p3_params(x, w, w_lo, y, yres, bias, stats, g, cfg, stats_shift);
+  hcb::launch_conv_p3(p, (int)cfg, cur_stream());
+}
+
+// fp32 data gradient with the fused BN-backward epilogue (see conv_igemm_bnb): z fp32, yact the
+// activation's planes (mode 1), output g fp32
+void conv_p3_bnb(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor& y,
+                 const c10::optional<Tensor>& yres, at::IntArrayRef g, int64_t cfg, const Tensor& z,
+                 const c10::optional<Tensor>& yact, int64_t ld, const Tensor& mean, const Tensor& invstd,
+                 const Tensor& gamma, const Tensor& beta, const Tensor& acc, int64_t R, int64_t mode) {
+  hcb::ConvParams p = p3_params(x, w, w_lo, y, yres, c10::nullopt, c10::nullopt, g, cfg, c10::nullopt);
+  set_bnb(p, z, yact, ld, mean, invstd, gamma, beta, acc, R, mode, true);
+  hcb::launch_conv_p3(p, (int)cfg, cur_stream());
+}
+
+// geom as conv_wgrad; dy / x planes
+void conv_wgrad_p3(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArrayRef g, int64_t cfg,
+                   int64_t splits) {
+  TORCH_CHECK(g.size() == 17, "hcb.conv_wgrad_p3: geom must have 17 entries");
+  const int64_t dps = check_planes(dy, "dy"), xps = check_planes(x, "x");
+  TORCH_CHECK(cfg >= 0 && cfg < 6, "hcb.conv_wgrad_p3: cfg 0..5");
+  check_f32(dw, "dw");
+  hcb::WgradParams p{};
+  p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];
+  p.P = g[5]; p.Q = g[6]; p.R = g[7]; p.S = g[8];
+  p.stride_h = g[9]; p.stride_w = g[10]; p.pad_h = g[11]; p.pad_w = g[12];
+  p.dil_h = g[13]; p.dil_w = g[14];
+  p.Nout = g[15]; p.ldy = g[16];
+  p.K = p.R * p.S * p.C;
+  p.M = p.N * p.P * p.Q;
+  TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0, "hcb.conv_wgrad_p3: C, ldx multiples of 8");
+  TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= p.Nout, "hcb.conv_wgrad_p3: bad ldy");
+  TORCH_CHECK(splits >= 1, "hcb.conv_wgrad_p3: splits >= 1");
+  const int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * 2 + (int64_t)p.C * 2;
+  const int64_t yb = ((int64_t)p.M - 1) * p.ldy * 2 + (int64_t)((p.Nout + 7) / 8) * 8 * 2;
+  TORCH_CHECK(xb < (1ll << 31) && yb < (1ll << 31), "hcb.conv_wgrad_p3: operand exceeds 2 GiB");
+  TORCH_CHECK(2 * xps * 2 < (1ll << 32) && 2 * dps * 2 < (1ll << 32), "hcb.conv_wgrad_p3: plane stride range");
+  check_range(x, 2 * xps * 2 + xb, "x planes");
+  check_range(dy, 2 * dps * 2 + yb, "dy planes");
+  check_range(dw, (int64_t)p.Nout * p.K * 4, "dw");
+  const int nkt = (p.M + 63) / 64;
+  const int per = (nkt + (int)splits - 1) / (int)splits;
+  p.ksteps_per_split = per;
+  const int eff_splits = (nkt + per - 1) / per;
+  p.fd_pq = hcb::make_fastdiv((uint32_t)(p.P * p.Q));
+  p.fd_q = hcb::make_fastdiv((uint32_t)p.Q);
+  p.fd_c = hcb::make_fastdiv((uint32_t)p.C);
+  p.fd_s = hcb::make_fastdiv((uint32_t)p.S);
+  p.dy = dy.data_ptr();
+  p.x = x.data_ptr();
+  p.dw = dw.data_ptr<float>();
+  p.dy_bytes = (uint32_t)yb;
+  p.x_bytes = (uint32_t)xb;
+  p.dy_plane = (uint32_t)(dps * 2);
+  p.x_plane = (uint32_t)(xps * 2);
+  hcb::launch_wgrad_p3(p, (int)cfg, eff_splits, cur_stream());
+}
+
+// fp32 x [rows][ldx] (first C channels) -> planes out [3][rows][ldo]
+void split_planes(const Tensor& x, int64_t ldx, int64_t rows, int64_t C, const Tensor& out, int64_t ldo) {
+  check_f32(x, "x");
+  const int64_t ps = check_planes(out, "out");
+  TORCH_CHECK(C % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0 && ldx >= C && ldo >= C, "hcb.split_planes: C / ld % 8");
+  check_align16(x.data_ptr(), "x");
+  check_range(x, ((rows - 1) * ldx + C) * 4, "x");
+  check_range(out, (2 * ps + (rows - 1) * ldo + C) * 2, "out");
+  TORCH_CHECK(ps >= (rows - 1) * ldo + C, "hcb.split_planes: planes overlap");
+  hcb::launch_split_planes(x.data_ptr<float>(), (int)ldx, rows, (int)C, (uint16_t*)out.data_ptr(), (int)ldo, ps,
+                           cur_stream());
+}
+
+void merge_planes(const Tensor& in, int64_t ldi, int64_t rows, int64_t C, const Tensor& y, int64_t ldy) {
+  const int64_t ps = check_planes(in, "in");
+  check_f32(y, "y");
+  TORCH_CHECK(C % 8 == 0 && ldi % 8 == 0 && ldy % 8 == 0, "hcb.merge_planes: C / ld % 8");
+  check_align16(y.data_ptr(), "y");
+  check_range(in, (2 * ps + (rows - 1) * ldi + C) * 2, "in");
+  check_range(y, ((rows - 1) * ldy + C) * 4, "y");
+  hcb::launch_merge_planes((const uint16_t*)in.data_ptr(), (int)ldi, ps, rows, (int)C, y.data_ptr<float>(), (int)ldy,
+                           cur_stream());
+}
+
+void gap_fwd_p3(const Tensor& x, const Tensor& y, int64_t N, int64_t HW, int64_t C) {
+  const int64_t xps = check_planes(x, "x"), yps = check_planes(y, "y");
+  TORCH_CHECK(C % 8 == 0, "hcb.gap_fwd_p3: C % 8");
+  check_range(x, (2 * xps + N * HW * C) * 2, "x");
+  check_range(y, (2 * yps + N * C) * 2, "y");
+  hcb::launch_gap_fwd_p3((const uint16_t*)x.data_ptr(), xps, (uint16_t*)y.data_ptr(), yps, (int)N, (int)HW, (int)C,
+                         cur_stream());
+}
+
 void set_deterministic(bool on) { hcb::set_deterministic(on); }
 
 }  // namespace
@@ -936,6 +1143,12 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("set_deterministic(bool on) -> ()", set_deterministic);
   m.def("stem_wfold(Tensor w, Tensor(a!) wp) -> ()");
   m.def("stem_wgrad_unfold(Tensor dwp, Tensor(a!) dw) -> ()");
+  m.def("conv_p3(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
+  m.def("conv_wgrad_p3(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
+  m.def("conv_p3_bnb(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
+  m.def("split_planes(Tensor x, int ldx, int rows, int C, Tensor(a!) out, int ldo) -> ()");
+  m.def("merge_planes(Tensor x, int ldi, int rows, int C, Tensor(a!) y, int ldy) -> ()");
+  m.def("gap_fwd_p3(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
 }
 
 HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
@@ -979,4 +1192,10 @@ HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("stem_s2d", stem_s2d);
   m.impl("stem_wfold", stem_wfold);
   m.impl("stem_wgrad_unfold", stem_wgrad_unfold);
+  m.impl("conv_p3", conv_p3);
+  m.impl("conv_wgrad_p3", conv_wgrad_p3);
+  m.impl("conv_p3_bnb", conv_p3_bnb);
+  m.impl("split_planes", split_planes);
+  m.impl("merge_planes", merge_planes);
+  m.impl("gap_fwd_p3", gap_fwd_p3);
 }

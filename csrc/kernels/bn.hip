@@ -235,20 +235,22 @@ __device__ __forceinline__ void bwd_math(const u32x4& dv, const u32x4& xvv, cons
 }
 
 // element-type generic forms (T = the build's 16-bit type or fp32) used by the finalize-free kernels
-template <typename T>
+// TY: element type of the ReLU-mask source y -- T, or (fp32 path) uint16_t: the bf16 hi plane of the
+// plane-stored activation (hi > 0 exactly when y > 0 for every normal y)
+template <typename T, typename TY = T>
 struct BwdSrcT {
   __amdgpu_buffer_rsrc_t dyr, xr, yr;
   int lddy, ldx, ldyv, cv;
-  __device__ __forceinline__ void load(int m, int M, int relu, Act8<T>& d, Act8<T>& x, Act8<T>& y) const {
+  __device__ __forceinline__ void load(int m, int M, int relu, Act8<T>& d, Act8<T>& x, Act8<TY>& y) const {
     const bool ok = m < M;
     constexpr uint32_t E = Act8<T>::ESZ;
     d.load(dyr, ok ? (uint32_t)((size_t)m * lddy + cv * 8) * E : HCB_OOB);
     x.load(xr, ok ? (uint32_t)((size_t)m * ldx + cv * 8) * E : HCB_OOB);
-    if (relu == 1) y.load(yr, ok ? (uint32_t)((size_t)m * ldyv + cv * 8) * E : HCB_OOB);
+    if (relu == 1) y.load(yr, ok ? (uint32_t)((size_t)m * ldyv + cv * 8) * Act8<TY>::ESZ : HCB_OOB);
   }
 };
-template <typename T>
-__device__ __forceinline__ void bwd_math_t(const Act8<T>& dv, const Act8<T>& xvv, const Act8<T>& yvv, int relu,
+template <typename T, typename TY = T>
+__device__ __forceinline__ void bwd_math_t(const Act8<T>& dv, const Act8<T>& xvv, const Act8<TY>& yvv, int relu,
                                            const float* mu, const float* is, const float* sc, const float* sh,
                                            float* g, float* xh) {
   float d[8], xv[8];
@@ -585,12 +587,18 @@ __device__ __forceinline__ void reduce_group_replicas(const float* acc, int R, i
 
 // RBN: the residual operand is a projection shortcut's raw conv output normalised here (ResBN);
 // its own instantiation, so the common kernel keeps its register budget
-template <bool RBN, typename T = uint16_t>
+// P3 (fp32 path): y is written as bf16 hi / mid / lo planes (plane stride yps elements) -- the
+// GEMM-operand format of the consuming convs -- and a plain residual (!RBN, the identity shortcut:
+// the block input) is read from its planes (plane stride rps); T = float (z, and an RBN residual)
+template <bool RBN, typename T = uint16_t, bool P3 = false>
 __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
-    const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, const T* __restrict__ res,
+    const T* __restrict__ x, int ldx, void* __restrict__ yv, int ldy, const void* __restrict__ resv,
     int ldr, int M, int C, int CVB, const float* __restrict__ acc, int R, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu, float* saved_mean,
-    float* saved_invstd, float* run_mean, float* run_var, const float* shift, ResBN rb) {
+    float* saved_invstd, float* run_mean, float* run_var, const float* shift, ResBN rb, int64_t yps, int64_t rps) {
+  constexpr bool RP3 = P3 && !RBN;  // residual planes
+  T* __restrict__ y = reinterpret_cast<T*>(yv);
+  const T* __restrict__ res = reinterpret_cast<const T*>(resv);
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB] (+ [2][CB] of the residual BN)
   constexpr bool rbn = RBN;
   const GroupMap gm = groupmap(CVB);
@@ -598,16 +606,29 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
   const int cl = (threadIdx.x % CVB) * 8;
   constexpr uint32_t E = Act8<T>::ESZ;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx, E));
-  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? res : x, rsrc_bytes(M, res != nullptr ? ldr : ldx, E));
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(res != nullptr ? resv : x, rsrc_bytes(M, res != nullptr ? ldr : ldx, RP3 ? 2 : E));
+  const uint16_t* r16 = reinterpret_cast<const uint16_t*>(resv);
+  const __amdgpu_buffer_rsrc_t rr1 = make_rsrc(RP3 && res != nullptr ? r16 + rps : resv, rsrc_bytes(M, ldr, 2));
+  const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(RP3 && res != nullptr ? r16 + 2 * rps : resv, rsrc_bytes(M, ldr, 2));
   const int stride = gridDim.x * gm.rows;
   int m0 = blockIdx.x * gm.rows + gm.r0;
   Act8<T> xv[BN_U], rv[BN_U];
+  u32x4 rp[RP3 ? BN_U : 1][3];
   auto load_rows = [&](int mb) {
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       int m = mb + u * stride;
       xv[u].load(xr, m < M ? (uint32_t)((size_t)m * ldx + gm.cv * 8) * E : HCB_OOB);
-      if (res != nullptr) rv[u].load(rr, m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * E : HCB_OOB);
+      if (res != nullptr) {
+        if constexpr (RP3) {
+          const uint32_t o = m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * 2u : HCB_OOB;
+          rp[u][0] = buf_load16(rr, o);
+          rp[u][1] = buf_load16(rr1, o);
+          rp[u][2] = buf_load16(rr2, o);
+        } else {
+          rv[u].load(rr, m < M ? (uint32_t)((size_t)m * ldr + gm.cv * 8) * E : HCB_OOB);
+        }
+      }
     }
   };
   // First rows and the affine parameters are in flight while the statistics are reduced.
@@ -675,7 +696,10 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
       for (int e = 0; e < 8; ++e) f[e] = f[e] * sc[e] + sh[e];
       if (res != nullptr) {
         float r[8];
-        rv[u].to_f(r);
+        if constexpr (RP3)
+          merge_p3(rp[u][0], rp[u][1], rp[u][2], r);
+        else
+          rv[u].to_f(r);
         if constexpr (RBN) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] += r[e] * sc2[e] + sh2[e];
@@ -688,14 +712,19 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
       }
-      if (m < M) Act8<T>::store(y + (size_t)m * ldy + gm.cv * 8, f);
+      if (m < M) {
+        if constexpr (P3)
+          store_p3(reinterpret_cast<uint16_t*>(yv) + (size_t)m * ldy + gm.cv * 8, yps, f);
+        else
+          Act8<T>::store(y + (size_t)m * ldy + gm.cv * 8, f);
+      }
     }
   }
 }
 
-template <typename T = uint16_t>
+template <typename T = uint16_t, typename TY = T>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
-    const T* __restrict__ dy, int lddy, const T* __restrict__ y, int ldyv,
+    const T* __restrict__ dy, int lddy, const TY* __restrict__ y, int ldyv,
     const T* __restrict__ x, int ldx, int M, int C, int CVB, const float* mean, const float* invstd,
     const float* gamma, const float* beta, int relu, float* acc, int R, T* gout, int ldg) {
   constexpr uint32_t E = Act8<T>::ESZ;
@@ -713,19 +742,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
       sc[e] = gamma[c] * is[e];
       sh[e] = beta[c] - mu[e] * sc[e];
     }
-    BwdSrcT<T> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
-                   make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx, E)), lddy, ldx, ldyv,
-                   gm.cv};
+    constexpr uint32_t EY = Act8<TY>::ESZ;
+    BwdSrcT<T, TY> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                       y != nullptr ? make_rsrc(y, rsrc_bytes(M, ldyv, EY)) : make_rsrc(x, rsrc_bytes(M, ldx, E)), lddy,
+                       ldx, ldyv, gm.cv};
     const int stride = gridDim.x * gm.rows;
     for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
-      Act8<T> dv[BN_U], xv[BN_U], yv[BN_U];
+      Act8<T> dv[BN_U], xv[BN_U];
+      Act8<TY> yv[BN_U];
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
         const int m = m0 + u * stride;
         float g[8], xh[8];
-        bwd_math_t<T>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+        bwd_math_t<T, TY>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {  // rows beyond M load zeros: g = 0 contributes nothing
           s1[e] += g[e];
@@ -757,21 +788,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
   }
 }
 
-template <typename T = uint16_t>
+// P3 (fp32 path): dx is written as bf16 hi / mid / lo planes (plane stride dxps elements), the
+// operand format of the data- and weight-gradient GEMMs that consume it
+template <typename T = uint16_t, typename TY = T, bool P3 = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
-    const T* __restrict__ dy, int lddy, const T* __restrict__ y, int ldyv,
-    const T* __restrict__ x, int ldx, T* __restrict__ dx, int lddx, int M, int C, int CVB,
+    const T* __restrict__ dy, int lddy, const TY* __restrict__ y, int ldyv,
+    const T* __restrict__ x, int ldx, void* __restrict__ dxv, int lddx, int M, int C, int CVB,
     const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
-    int R, float* dgamma, float* dbeta, int relu, float* shift_out) {
+    int R, float* dgamma, float* dbeta, int relu, float* shift_out, int64_t dxps) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]: dbeta, dgamma
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
-  constexpr uint32_t E = Act8<T>::ESZ;
-  BwdSrcT<T> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
-                 make_rsrc(y != nullptr ? y : x, rsrc_bytes(M, y != nullptr ? ldyv : ldx, E)), lddy, ldx, ldyv, gm.cv};
+  constexpr uint32_t E = Act8<T>::ESZ, EY = Act8<TY>::ESZ;
+  T* __restrict__ dx = reinterpret_cast<T*>(dxv);
+  BwdSrcT<T, TY> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                     y != nullptr ? make_rsrc(y, rsrc_bytes(M, ldyv, EY)) : make_rsrc(x, rsrc_bytes(M, ldx, E)), lddy,
+                     ldx, ldyv, gm.cv};
   const int stride = gridDim.x * gm.rows;
   const int mfirst = blockIdx.x * gm.rows + gm.r0;
-  Act8<T> dv[BN_U], xv[BN_U], yv[BN_U];
+  Act8<T> dv[BN_U], xv[BN_U];
+  Act8<TY> yv[BN_U];
   float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
   // First rows and the per-channel parameters are in flight while dgamma/dbeta are reduced.
   if (active) {
@@ -815,10 +851,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     for (int u = 0; u < BN_U; ++u) {
       const int m = m0 + u * stride;
       float g[8], xh[8], o[8];
-      bwd_math_t<T>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
+      bwd_math_t<T, TY>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
-      if (m < M) Act8<T>::store(dx + (size_t)m * lddx + gm.cv * 8, o);
+      if (m < M) {
+        if constexpr (P3)
+          store_p3(reinterpret_cast<uint16_t*>(dxv) + (size_t)m * lddx + gm.cv * 8, dxps, o);
+        else
+          Act8<T>::store(dx + (size_t)m * lddx + gm.cv * 8, o);
+      }
     }
   }
 }
@@ -830,13 +871,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
 // recomputes the ReLU mask from z (mode 2), so nothing else needs the full-size activation.
 // K3: the 3x3 window unrolled, its 9 loads in flight together (buffer loads, out-of-image taps
 // excluded by a select) instead of one dependent loop trip per tap.
-template <bool K3, typename T = uint16_t>
+// P3 (fp32 path): the pooled output is written as bf16 hi / mid / lo planes (plane stride yps)
+template <bool K3, typename T = uint16_t, bool P3 = false>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
-    const T* __restrict__ z, int H, int W, int C, int CVB, T* __restrict__ y, int P, int Q, int ldy,
+    const T* __restrict__ z, int H, int W, int C, int CVB, void* __restrict__ yv, int P, int Q, int ldy,
     uint8_t* __restrict__ amax, int kh, int kw, int sh, int sw, int ph, int pw, int Nimg, int M,
     const float* __restrict__ acc, int R, float eps, float momentum, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-    const float* shift) {
+    const float* shift, int64_t yps) {
+  T* __restrict__ y = reinterpret_cast<T*>(yv);
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
   const GroupMap gm = groupmap(CVB);
   reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
@@ -929,7 +972,10 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
         }
       }
     }
-    Act8<T>::store(y + (size_t)op * ldy + gm.cv * 8, best);
+    if constexpr (P3)
+      store_p3(reinterpret_cast<uint16_t*>(yv) + (size_t)op * ldy + gm.cv * 8, yps, best);
+    else
+      Act8<T>::store(y + (size_t)op * ldy + gm.cv * 8, best);
     u32x2 a;
     a[0] = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
     a[1] = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
@@ -959,62 +1005,71 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
   return dim3(s, groups);
 }
 
-template <typename T>
+template <typename T, bool P3 = false>
 static void bn_apply_acc_t(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                            const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                            int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                           const float* shift, const ResBN* res_bn, hipStream_t st) {
+                           const float* shift, const ResBN* res_bn, hipStream_t st, int64_t yps, int64_t rps) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   const ResBN rb = res_bn != nullptr ? *res_bn : ResBN{};
   if (res_bn != nullptr)
-    hipLaunchKernelGGL((bn_apply_acc_kernel<true, T>), grid, dim3(256), (size_t)4 * cvb * 8 * 4, st, (const T*)x, ldx,
-                       (T*)y, ldy, (const T*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta, relu, saved_mean,
-                       saved_invstd, run_mean, run_var, shift, rb);
+    hipLaunchKernelGGL((bn_apply_acc_kernel<true, T, P3>), grid, dim3(256), (size_t)4 * cvb * 8 * 4, st, (const T*)x,
+                       ldx, y, ldy, res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta, relu, saved_mean,
+                       saved_invstd, run_mean, run_var, shift, rb, yps, rps);
   else
-    hipLaunchKernelGGL((bn_apply_acc_kernel<false, T>), grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const T*)x,
-                       ldx, (T*)y, ldy, (const T*)res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta, relu,
-                       saved_mean, saved_invstd, run_mean, run_var, shift, rb);
+    hipLaunchKernelGGL((bn_apply_acc_kernel<false, T, P3>), grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const T*)x,
+                       ldx, y, ldy, res, ldr, M, C, cvb, acc, R, eps, momentum, gamma, beta, relu, saved_mean,
+                       saved_invstd, run_mean, run_var, shift, rb, yps, rps);
 }
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         const float* shift, const ResBN* res_bn, hipStream_t st, bool f32) {
-  (f32 ? bn_apply_acc_t<float> : bn_apply_acc_t<uint16_t>)(x, ldx, y, ldy, res, ldr, M, C, acc, R, eps, momentum,
-                                                           gamma, beta, relu, saved_mean, saved_invstd, run_mean,
-                                                           run_var, shift, res_bn, st);
+                         const float* shift, const ResBN* res_bn, hipStream_t st, bool f32, int64_t yps, int64_t rps) {
+  auto fn = yps > 0 ? bn_apply_acc_t<float, true> : (f32 ? bn_apply_acc_t<float> : bn_apply_acc_t<uint16_t>);
+  fn(x, ldx, y, ldy, res, ldr, M, C, acc, R, eps, momentum, gamma, beta, relu, saved_mean, saved_invstd, run_mean,
+     run_var, shift, res_bn, st, yps, rps);
 }
 
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
                                 int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
                                 float momentum, const float* gamma, const float* beta, float* saved_mean,
                                 float* saved_invstd, float* run_mean, float* run_var, const float* shift,
-                                hipStream_t st, bool f32) {
+                                hipStream_t st, bool f32, int64_t yps) {
   int cvb;
   dim3 grid = bn_grid_groups(N * P * Q, C, &cvb);
   const bool k3 = kh == 3 && kw == 3 && (long)N * H * W * C * (f32 ? 2 : 1) < (1l << 30);
-  if (f32)
-    hipLaunchKernelGGL((k3 ? bn_relu_maxpool_acc_kernel<true, float> : bn_relu_maxpool_acc_kernel<false, float>), grid,
-                       dim3(256), (size_t)2 * cvb * 8 * 4, st, (const float*)z, H, W, C, cvb, (float*)y, P, Q, ldy,
+  if (f32 && yps > 0)
+    hipLaunchKernelGGL((k3 ? bn_relu_maxpool_acc_kernel<true, float, true> : bn_relu_maxpool_acc_kernel<false, float, true>),
+                       grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const float*)z, H, W, C, cvb, y, P, Q, ldy,
                        (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps, momentum, gamma, beta,
-                       saved_mean, saved_invstd, run_mean, run_var, shift);
+                       saved_mean, saved_invstd, run_mean, run_var, shift, yps);
+  else if (f32)
+    hipLaunchKernelGGL((k3 ? bn_relu_maxpool_acc_kernel<true, float> : bn_relu_maxpool_acc_kernel<false, float>), grid,
+                       dim3(256), (size_t)2 * cvb * 8 * 4, st, (const float*)z, H, W, C, cvb, y, P, Q, ldy,
+                       (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps, momentum, gamma, beta,
+                       saved_mean, saved_invstd, run_mean, run_var, shift, (int64_t)0);
   else
     hipLaunchKernelGGL(k3 ? bn_relu_maxpool_acc_kernel<true> : bn_relu_maxpool_acc_kernel<false>, grid, dim3(256),
-                       (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W, C, cvb, (uint16_t*)y, P, Q, ldy,
+                       (size_t)2 * cvb * 8 * 4, st, (const uint16_t*)z, H, W, C, cvb, y, P, Q, ldy,
                        (uint8_t*)amax, kh, kw, sh, sw, ph, pw, N, N * H * W, acc, R, eps, momentum, gamma, beta,
-                       saved_mean, saved_invstd, run_mean, run_var, shift);
+                       saved_mean, saved_invstd, run_mean, run_var, shift, (int64_t)0);
 }
 
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
-                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32) {
+                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32, bool yh) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   // every block adds into replica blockIdx.x % R; deterministic mode: at most R row blocks, so
   // each replica slot gets one add (the kernel strides over the rows with any grid)
   if (deterministic() && (int)grid.x > R) grid.x = R;
   size_t lds = (size_t)2 * (256 / cvb) * cvb * 8 * 4;
-  if (f32)
+  if (f32 && yh)
+    hipLaunchKernelGGL((bn_bwd_reduce_acc_kernel<float, uint16_t>), grid, dim3(256), lds, st, (const float*)dy, lddy,
+                       (const uint16_t*)y, ldyv, (const float*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu, acc,
+                       R, (float*)gout, ldg);
+  else if (f32)
     hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel<float>, grid, dim3(256), lds, st, (const float*)dy, lddy,
                        (const float*)y, ldyv, (const float*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu, acc, R,
                        (float*)gout, ldg);
@@ -1027,17 +1082,28 @@ void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv,
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
-                             float* shift_out, hipStream_t st, bool f32) {
+                             float* shift_out, hipStream_t st, bool f32, bool yh, int64_t dxps) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
-  if (f32)
-    hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<float>, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st, (const float*)dy,
-                       lddy, (const float*)y, ldyv, (const float*)x, ldx, (float*)dx, lddx, M, C, cvb, mean, invstd,
-                       gamma, beta, acc, R, dgamma, dbeta, relu, shift_out);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<uint16_t>, grid, dim3(256), (size_t)2 * cvb * 8 * 4, st,
-                       (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, (uint16_t*)dx,
-                       lddx, M, C, cvb, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out);
+  const size_t lds = (size_t)2 * cvb * 8 * 4;
+  if (f32 && dxps > 0) {
+    if (yh)
+      hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, uint16_t, true>), grid, dim3(256), lds, st, (const float*)dy,
+                         lddy, (const uint16_t*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd,
+                         gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, float, true>), grid, dim3(256), lds, st, (const float*)dy,
+                         lddy, (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma,
+                         beta, acc, R, dgamma, dbeta, relu, shift_out, dxps);
+  } else if (f32) {
+    hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<float>, grid, dim3(256), lds, st, (const float*)dy, lddy,
+                       (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma, beta, acc,
+                       R, dgamma, dbeta, relu, shift_out, (int64_t)0);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<uint16_t>, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
+                       (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma,
+                       beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0);
+  }
 }
 
 }  // namespace hcb

@@ -101,6 +101,38 @@ __device__ __forceinline__ void split3_8(const u32x4& a, const u32x4& b, u32x4& 
   mid = __builtin_bit_cast(u32x4, m);
   lo = __builtin_bit_cast(u32x4, l);
 }
+// 8 bf16 values (always bf16, whatever the build's 16-bit type) -> fp32
+__device__ __forceinline__ void unpack_bf16x8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+// 8 fp32 values stored as their bf16 hi / mid / lo PLANES (the fp32 path's GEMM-operand format:
+// plane t of an [rows][ld] tensor at t * plane elements; hi + mid + lo == the fp32 value)
+__device__ __forceinline__ void store_p3(uint16_t* p, int64_t plane, const float* f) {
+  u32x4 a, b, hi, mid, lo;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = __float_as_uint(f[i]);
+    b[i] = __float_as_uint(f[4 + i]);
+  }
+  split3_8(a, b, hi, mid, lo);
+  *reinterpret_cast<u32x4*>(p) = hi;
+  *reinterpret_cast<u32x4*>(p + plane) = mid;
+  *reinterpret_cast<u32x4*>(p + 2 * plane) = lo;
+}
+// the fp32 value of 8 plane-stored elements (16-byte loads of the three planes)
+__device__ __forceinline__ void merge_p3(const u32x4& h, const u32x4& m, const u32x4& l, float* f) {
+  float a[8], b[8];
+  unpack_bf16x8(h, f);
+  unpack_bf16x8(m, a);
+  unpack_bf16x8(l, b);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] += a[e] + b[e];
+}
+
 __device__ __forceinline__ f32x4 mfma_bf16(const u32x4& a, const u32x4& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
                                                  0, 0);

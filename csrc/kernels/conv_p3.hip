@@ -1,0 +1,574 @@
+// fp32 convolutions on bf16 PLANES (the reference's precision, --compute_dtype fp32): every fp32
+// GEMM operand is held in memory as three bf16 planes hi / mid / lo (x = hi + mid + lo exactly: 8 +
+// 8 + 8 significant bits), written once by its PRODUCER (BN apply, BN backward, the plane-split
+// kernel) where the split costs nothing -- those kernels are memory bound. The GEMMs then stage
+// plain bf16 tiles: LDS-DMA (buffer_load ... lds) of 3 images per operand, no register staging, no
+// VALU split, and six MFMA products per (A, B) fragment set (bf16x6: hi*hi + hi*mid + mid*hi +
+// mid*mid + hi*lo + lo*hi, fp32 accumulation; the dropped mid*lo, lo*mid, lo*lo are ~2^-24).
+//
+// Roles (the reference's MKL-DNN fp32 Conv2D fwd / bwd-data / bwd-filter primitives, SURVEY.md
+// §2.6, driven by /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81):
+//   * conv_igemm_p3_kernel  forward and data-gradient implicit GEMMs (fp32 output, fused BN
+//                           statistics, beta-accumulate, split-K via splitk_gather)
+//   * conv_wgrad_p3_kernel  weight-gradient implicit GEMM (transposed fragment reads,
+//                           ds_read_b64_tr_b16, split-K with fp32 atomics)
+//
+// Design for CDNA4: bf16x6 does 6 MFMAs per 3+3 fragment reads, twice the MFMA work per LDS byte
+// of the bf16 GEMM, so these kernels can be MFMA bound -- the constraint is LDS CAPACITY (3 images
+// per operand): a 128x64 block tile is 72 KB per k-step, so the ring is two stages (144 KB, one
+// workgroup per CU). Each stage carries 6x the MFMA time of a bf16 k-step (1536 cycles per wave at
+// 64x32 wave tiles), which covers the next stage's DMA latency, so double buffering is enough.
+#include "common.h"
+#include "igemm_epilogue.h"
+#include "igemm_loader.h"
+#include "kernels.h"
+
+namespace hcb {
+
+// all fragment reads of both 32-deep halves first, then the 2 x MI x NI x 6 MFMAs (the compiler
+// otherwise waits on each read right before its first use)
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void p3_step(const u32x4* A, const u32x4* B, f32x4 (&acc)[TM / 16][TN / 16], int wm, int wn,
+                                        int lane) {
+  constexpr int MI = TM / 16, NI = TN / 16, BM = WM * TM, BN = WN * TN;
+  constexpr int AIMG = BM * 8, BIMG = BN * 8;  // one plane image, in u32x4
+  const int frow = lane & 15, fq = lane >> 4;
+  u32x4 a[2][3][MI], b[2][3][NI];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int ch = ks * 4 + fq;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * TM + i * 16 + frow, o = row * 8 + (ch ^ ((row >> 1) & 7));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[ks][t][i] = A[t * AIMG + o];
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wn * TN + j * 16 + frow, o = row * 8 + (ch ^ ((row >> 1) & 7));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) b[ks][t][j] = B[t * BIMG + o];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {  // small terms first
+        acc[i][j] = mfma_bf16(a[ks][2][i], b[ks][0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][2][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][0][j], acc[i][j]);
+      }
+}
+
+template <int BM, int BN>
+constexpr size_t p3_stage_bytes() {
+  return (size_t)3 * (BM + BN) * 128;
+}
+// LDS offset of the fused BN-backward parameters: above the ring and the epilogue staging
+template <int BM, int BN, int WM>
+constexpr size_t p3_param_off() {
+  const size_t a = 2 * p3_stage_bytes<BM, BN>(), b = igemm_epilogue_lds(BM, BN, WM);
+  return a > b ? a : b;
+}
+// data-grad GEMMs with at most this many 64-deep k-steps fetch their fused BN-backward epilogue
+// operands before the main loop
+constexpr int EARLY_EPI_KSTEPS_P3 = 2;
+
+// ============================================================== forward / data gradient
+// x: three bf16 planes of the NHWC input, p.x_plane bytes apart (each plane p.x_bytes long);
+// w / w_lo / w_lo2: the hi / mid / lo weight packs [Nout][Kpad]. Two-stage LDS-DMA ring.
+// BNB: the fused BN-backward epilogue (data gradient producing a BN layer's dy: ReLU gating from the
+// hi plane of y or from z, sum(g) / sum(g * xhat) into p.bnb_acc), fp32 z / beta source / output
+template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB>
+__global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p) {
+  constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int NT = WM * WN * 64, RP = NT / 8;  // threads; tile rows per load pass
+  constexpr int AV = BM / RP, BV = BN / RP;
+  constexpr int AIMG = BM * 128, BIMG = BN * 128;
+  constexpr int STAGE = (int)p3_stage_bytes<BM, BN>();
+  static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
+  static_assert(p3_param_off<BM, BN, WM>() + bnb_param_lds(BN) <= 160 * 1024, "ring + BN parameters must fit LDS");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = wave_id_uniform();
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_n = (p.Nout + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // a tile's splits are neighbours: same XCD
+  const int S = p.splits;
+  const int tile = bid / S, split = bid - tile * S;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  // lane-linear LDS image; the lane fetches the GLOBAL chunk the swizzled read expects there
+  const int chunk = (tid & 7) ^ ((tid >> 4) & 7);
+
+  const char* xb = reinterpret_cast<const char*>(p.x);
+  const __amdgpu_buffer_rsrc_t xr0 = make_rsrc(xb, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr1 = make_rsrc(xb + p.x_plane, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(xb + 2 * (size_t)p.x_plane, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr0 = make_rsrc(p.w, p.w_bytes);
+  const __amdgpu_buffer_rsrc_t wr1 = make_rsrc(p.w_lo, p.w_bytes);
+  const __amdgpu_buffer_rsrc_t wr2 = make_rsrc(p.w_lo2, p.w_bytes);
+  ALoader<AV, CBIG, LHSDIL, RP> al;
+  al.init(p, m0, tid, chunk);
+  uint32_t b_off[BV];
+#pragma unroll
+  for (int v = 0; v < BV; ++v) {
+    const int j = n0 + (tid >> 3) + RP * v;
+    b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
+  }
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = p.Kpad / BK;
+  const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's k-steps
+  auto issue = [&](int stage, int kl) {
+    const int kt = kb + kl;
+    uint32_t off[AV];
+    al.offsets(p, kt, chunk, off);  // k-steps are issued strictly in order
+    char* sa = smem + stage * STAGE + wid * 8 * 128;
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      glds16(xr0, sa + RP * v * 128, off[v]);
+      glds16(xr1, sa + AIMG + RP * v * 128, off[v]);
+      glds16(xr2, sa + 2 * AIMG + RP * v * 128, off[v]);
+    }
+    char* sb = smem + stage * STAGE + 3 * AIMG + wid * 8 * 128;
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u;
+      glds16(wr0, sb + RP * v * 128, o);
+      glds16(wr1, sb + BIMG + RP * v * 128, o);
+      glds16(wr2, sb + 2 * BIMG + RP * v * 128, o);
+    }
+  };
+  if (kb > 0) al.seek(p, kb);
+  EpiPrefetch<WM, WN, TM, TN, BNB, true> pre;
+  pre.load_shift(p, n0, wn, lane);
+  constexpr size_t PARAM_OFF = p3_param_off<BM, BN, WM>();
+  if constexpr (BNB) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
+  const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS_P3;
+  if (early) pre.load(p, 0, m0, n0, tid);
+  if (nk > 0) issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed for this thread; the barrier publishes every thread's DMA and
+    // guarantees every wave is done reading stage kt-1, which the next issue overwrites
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue((kt + 1) & 1, kt + 1);
+    const char* sb = smem + (kt & 1) * STAGE;
+    p3_step<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG), acc,
+                            wm, wn, lane);
+  }
+  __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
+  if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
+  igemm_epilogue<WM, WN, TM, TN, BNB, true>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early,
+                                            BNB ? smem + PARAM_OFF : nullptr);
+}
+
+template <typename K>
+static void p3_set_lds_once(K kern) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+template <int WM, int WN, int TM, int TN, bool BNB>
+static void launch_p3(const ConvParams& p, hipStream_t st) {
+  constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
+  const int ksteps = (p.Kpad / 64 + p.splits - 1) / p.splits;
+  const size_t lds_main = (ksteps > 1 ? 2 : 1) * p3_stage_bytes<BM, BN>();
+  const size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
+  size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+  if (BNB) lds = p3_param_off<BM, BN, WM>() + bnb_param_lds(BN);
+  const bool cbig = (p.C % 64) == 0;
+  const bool lhs = p.idil_h > 1 || p.idil_w > 1;
+  static bool once = false;
+  if (!once) {
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, true, false, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, true, true, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, false, false, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, false, true, BNB>);
+    once = true;
+  }
+  if (cbig && !lhs)
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, true, false, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+  else if (cbig && lhs)
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, true, true, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+  else if (!cbig && !lhs)
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, false, false, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+  else
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, false, true, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+}
+
+// p3 cfg: 0 128x64 (2x2 waves of 64x32), 1 64x128 (2x2 of 32x64), 2 128x64 (4x2 of 32x32),
+// 3 64x128 (2x4 of 32x32), 4 64x64 (2x2 of 32x32), 5 128x64 (4x1 of 32x64), 6 64x128 (1x4 of 64x32)
+constexpr int N_P3_CFG = 7;
+int p3_tile_m(int cfg) {
+  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64};
+  return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 128;
+}
+int p3_tile_n(int cfg) {
+  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128};
+  return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 64;
+}
+
+template <bool BNB>
+static void launch_p3_cfg(const ConvParams& p, int cfg, hipStream_t st) {
+  switch (cfg) {
+    case 1: launch_p3<2, 2, 32, 64, BNB>(p, st); break;
+    case 2: launch_p3<4, 2, 32, 32, BNB>(p, st); break;
+    case 3: launch_p3<2, 4, 32, 32, BNB>(p, st); break;
+    case 4: launch_p3<2, 2, 32, 32, BNB>(p, st); break;
+    case 5: launch_p3<4, 1, 32, 64, BNB>(p, st); break;
+    case 6: launch_p3<1, 4, 64, 32, BNB>(p, st); break;
+    default: launch_p3<2, 2, 64, 32, BNB>(p, st); break;
+  }
+}
+
+void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st) {
+  if (p.bnb_acc != nullptr)
+    launch_p3_cfg<true>(p, cfg, st);
+  else
+    launch_p3_cfg<false>(p, cfg, st);
+}
+
+// ============================================================== weight gradient
+// dW[Nout][K] += sum_m dY[m][Nout] * im2col(X)[m][K] on planes: dy planes p.dy_plane bytes apart,
+// x planes p.x_plane bytes apart. Both operands have the reduction index (pixels) as their outer
+// dimension: staged as [64 pixels][tile cols] rows and read back transposed (ds_read_b64_tr_b16),
+// 32-byte slots XOR-swizzled (wg_swz) as in conv_wgrad.hip. NST-deep LDS-DMA ring.
+template <int NSLOT>
+__device__ __forceinline__ int p3w_swz(int row) {
+  if constexpr (NSLOT >= 8) return (row & 3) | ((row >> 1) & 4);
+  else return ((row >> 1) & 1) | ((row >> 2) & 2);
+}
+
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG>
+__global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams p) {
+  constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int NW = WM * WN;
+  constexpr int ACPR = BM / 8, BCPR = BN / 8;        // 16-byte chunks per LDS row
+  constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;  // LDS rows filled by one wave instruction
+  constexpr int AI = BK / ARPI / NW, BI = BK / BRPI / NW;  // instructions per wave per plane and stage
+  constexpr int LOADS = 3 * (AI + BI);
+  constexpr int AIMG = BK * BM * 2, BIMG = BK * BN * 2;
+  constexpr int STAGE = 3 * (AIMG + BIMG);
+  static_assert(AI * ARPI * NW == BK && BI * BRPI * NW == BK && AI >= 1 && BI >= 1, "tile / wave mapping");
+  static_assert(NST >= 2 && NST <= 3 && LOADS * (NST - 2) <= 63 && NST * STAGE <= 160 * 1024, "ring");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = wave_id_uniform();
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_m = (p.Nout + BM - 1) / BM;
+  const int tiles_n = (p.K + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int i0 = tm * BM, j0 = tn * BN;
+  const int nkt = (p.M + BK - 1) / BK;
+  const int kt_begin = split * p.ksteps_per_split;
+  const int kt_end = min(kt_begin + p.ksteps_per_split, nkt);
+  if (kt_begin >= kt_end) return;  // uniform per workgroup
+
+  const char* db = reinterpret_cast<const char*>(p.dy);
+  const char* xb = reinterpret_cast<const char*>(p.x);
+  const __amdgpu_buffer_rsrc_t dyr0 = make_rsrc(db, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t dyr1 = make_rsrc(db + p.dy_plane, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t dyr2 = make_rsrc(db + 2 * (size_t)p.dy_plane, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr0 = make_rsrc(xb, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr1 = make_rsrc(xb + p.x_plane, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(xb + 2 * (size_t)p.x_plane, p.x_bytes);
+
+  int a_row[AI], a_col[AI];
+#pragma unroll
+  for (int v = 0; v < AI; ++v) {
+    const int row = (wid * AI + v) * ARPI + lane / ACPR, pos = lane % ACPR;
+    const int chunk = (((pos >> 1) ^ p3w_swz<BM / 16>(row)) << 1) | (pos & 1);
+    a_row[v] = row;
+    a_col[v] = i0 + chunk * 8;
+  }
+  int b_row[BI], b_c[BI], b_dh[BI], b_dw[BI];
+  bool b_ok[BI];
+#pragma unroll
+  for (int v = 0; v < BI; ++v) {
+    const int row = (wid * BI + v) * BRPI + lane / BCPR, pos = lane % BCPR;
+    const int chunk = (((pos >> 1) ^ p3w_swz<BN / 16>(row)) << 1) | (pos & 1);
+    const int col = j0 + chunk * 8;
+    int tap, c;
+    if constexpr (CBIG) {
+      tap = j0 / p.C;
+      c = j0 - tap * p.C + chunk * 8;
+    } else {
+      tap = (int)fdiv((uint32_t)col, p.fd_c);
+      c = col - tap * p.C;
+    }
+    const int r = (int)fdiv((uint32_t)tap, p.fd_s), s = tap - r * p.S;
+    b_row[v] = row;
+    b_c[v] = c;
+    b_dh[v] = r * p.dil_h - p.pad_h;
+    b_dw[v] = s * p.dil_w - p.pad_w;
+    b_ok[v] = col < p.K;
+  }
+
+  auto issue = [&](int stage, int kt) {
+    const int mb = kt * BK;
+    char* sA = smem + stage * STAGE;
+    char* sB = sA + 3 * AIMG;
+#pragma unroll
+    for (int v = 0; v < AI; ++v) {
+      const int m = mb + a_row[v];
+      const uint32_t off = (a_col[v] < p.Nout && m < p.M) ? (uint32_t)(m * p.ldy + a_col[v]) * 2u : HCB_OOB;
+      char* d = sA + (wid * AI + v) * ARPI * BM * 2;
+      glds16(dyr0, d, off);
+      glds16(dyr1, d + AIMG, off);
+      glds16(dyr2, d + 2 * AIMG, off);
+    }
+#pragma unroll
+    for (int v = 0; v < BI; ++v) {
+      const int m = mb + b_row[v];
+      uint32_t off = HCB_OOB;
+      if (b_ok[v] && m < p.M) {
+        const int n = (int)fdiv((uint32_t)m, p.fd_pq);
+        const int rem = m - n * p.P * p.Q;
+        const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
+        const int qq = rem - pp * p.Q;
+        const int h = pp * p.stride_h + b_dh[v], w = qq * p.stride_w + b_dw[v];
+        if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W)
+          off = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c[v]) * 2u;
+      }
+      char* d = sB + (wid * BI + v) * BRPI * BN * 2;
+      glds16(xr0, d, off);
+      glds16(xr1, d + BIMG, off);
+      glds16(xr2, d + 2 * BIMG, off);
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed fragment reads (lane supplies row + q4, columns col + 4*p4), swizzled slots
+  const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
+  auto frag = [&](const char* base, int ncols, int krow, int col) -> u32x4 {
+    short4v v[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rr = krow + 4 * h + q4, cb = (col + 4 * p4) * 2;
+      const int sw = ncols == BM ? p3w_swz<BM / 16>(rr) : p3w_swz<BN / 16>(rr);
+      const int slot = (cb >> 5) ^ sw;
+      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * ncols * 2 + slot * 32 + (cb & 31)));
+    }
+    short8 t = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
+    return __builtin_bit_cast(u32x4, t);
+  };
+
+  const int nk = kt_end - kt_begin;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, kt_begin + s);
+  for (int k = 0; k < nk; ++k) {
+    const int ahead = min(NST - 2, nk - 1 - k);
+    if (ahead >= 1)
+      wait_vmcnt<(NST >= 3 ? 1 : 0) * LOADS>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + NST - 1 < nk) issue((k + NST - 1) % NST, kt_begin + k + NST - 1);
+    const char* Ab = smem + (k % NST) * STAGE;
+    const char* Bb = Ab + 3 * AIMG;
+    u32x4 a[2][3][MI], b[2][3][NI];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) a[ks][t][i] = frag(Ab + t * AIMG, BM, ks * 32 + 8 * g, wm * TM + i * 16);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) b[ks][t][j] = frag(Bb + t * BIMG, BN, ks * 32 + 8 * g, wn * TN + j * 16);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {  // small terms first
+          acc[i][j] = mfma_bf16(a[ks][2][i], b[ks][0][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][2][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][1][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][0][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][1][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][0][j], acc[i][j]);
+        }
+  }
+  __syncthreads();  // every wave is done with the ring before the epilogue reuses LDS
+
+  constexpr int LDC = BN + 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Cs[(wm * TM + i * 16 + g * 4 + e) * LDC + wn * TN + j * 16 + li] = acc[i][j][e];
+  __syncthreads();
+  const bool sole = gridDim.x == ntiles;
+  for (int idx = tid; idx < BM * BN; idx += NW * 64) {
+    const int row = idx / BN, col = idx - row * BN;
+    const int gi = i0 + row, gj = j0 + col;
+    if (gi < p.Nout && gj < p.K) {
+      float* d = p.dw + (size_t)gi * p.K + gj;
+      if (sole)
+        *d += Cs[row * LDC + col];
+      else
+        atomicAdd(d, Cs[row * LDC + col]);
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int NST>
+static void wlaunch_p3(const WgradParams& p, int splits, hipStream_t st) {
+  constexpr int BM = WM * TM, BN = WN * TN;
+  const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
+  const size_t lds_main = (size_t)NST * 3 * 64 * (BM + BN) * 2;
+  const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
+  const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
+  static bool once = false;
+  if (!once) {
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, true>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, false>);
+    once = true;
+  }
+  const dim3 grid(tiles * splits);
+  if ((p.C % BN) == 0)
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, true>), grid, dim3(WM * WN * 64), lds, st, p);
+  else
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, false>), grid, dim3(WM * WN * 64), lds, st, p);
+}
+
+// p3 wgrad cfg: 0 128x64 (2x2 waves of 64x32), 1 64x128 (2x2 of 32x64), 2 64x64 (2x2 of 32x32, NST 3),
+// 3 128x64 (4x2 of 32x32), 4 64x128 (2x4 of 32x32), 5 64x64 (2x2 of 32x32, NST 2)
+constexpr int N_WP3_CFG = 6;
+int wgrad_p3_tile_m(int cfg) {
+  static const int t[N_WP3_CFG] = {128, 64, 64, 128, 64, 64};
+  return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
+}
+int wgrad_p3_tile_n(int cfg) {
+  static const int t[N_WP3_CFG] = {64, 128, 64, 64, 128, 64};
+  return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
+}
+
+void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st) {
+  switch (cfg) {
+    case 0: wlaunch_p3<2, 2, 64, 32, 2>(p, splits, st); break;
+    case 1: wlaunch_p3<2, 2, 32, 64, 2>(p, splits, st); break;
+    case 3: wlaunch_p3<4, 2, 32, 32, 2>(p, splits, st); break;
+    case 4: wlaunch_p3<2, 4, 32, 32, 2>(p, splits, st); break;
+    case 5: wlaunch_p3<2, 2, 32, 32, 2>(p, splits, st); break;
+    default: wlaunch_p3<2, 2, 32, 32, 3>(p, splits, st); break;
+  }
+}
+
+// ============================================================== plane split / merge
+// x fp32 [rows][ldx] (C channels used) -> three bf16 planes [3][rows][ldo] (plane stride `plane`
+// elements): hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (round to nearest even;
+// hi + mid + lo == x for every normal fp32 value)
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ x, int ldx, int C, int64_t n8,
+                                                           uint16_t* __restrict__ out, int ldo, int64_t plane) {
+  const int CV = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / CV;
+    const int cv = (int)(i - row * CV);
+    const u32x4* src = reinterpret_cast<const u32x4*>(x + row * ldx + cv * 8);
+    u32x4 hi, mid, lo;
+    split3_8(src[0], src[1], hi, mid, lo);
+    uint16_t* o = out + row * ldo + cv * 8;
+    *reinterpret_cast<u32x4*>(o) = hi;
+    *reinterpret_cast<u32x4*>(o + plane) = mid;
+    *reinterpret_cast<u32x4*>(o + 2 * plane) = lo;
+  }
+}
+
+__global__ __launch_bounds__(256) void merge_planes_kernel(const uint16_t* __restrict__ in, int ldi, int64_t plane,
+                                                           int C, int64_t n8, float* __restrict__ y, int ldy) {
+  const int CV = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / CV;
+    const int cv = (int)(i - row * CV);
+    const uint16_t* s = in + row * ldi + cv * 8;
+    float h[8], m[8], l[8];
+    unpack_bf16x8(*reinterpret_cast<const u32x4*>(s), h);
+    unpack_bf16x8(*reinterpret_cast<const u32x4*>(s + plane), m);
+    unpack_bf16x8(*reinterpret_cast<const u32x4*>(s + 2 * plane), l);
+    float* o = y + row * ldy + cv * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = h[e] + (m[e] + l[e]);
+  }
+}
+
+// global average pool on planes (the ResNet head on the fp32 path): x planes [N][HW][C] -> the
+// pooled features as planes [N][C] (the classifier GEMM's operand); fp32 sums of the exact values
+__global__ __launch_bounds__(256) void gap_fwd_p3_kernel(const uint16_t* __restrict__ x, int64_t xps,
+                                                         uint16_t* __restrict__ y, int64_t yps, int N, int HW, int C) {
+  const int CV = C >> 3;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * CV) return;
+  const int n = idx / CV, cv = idx % CV;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < HW; ++i) {
+    const uint16_t* s = x + ((size_t)n * HW + i) * C + cv * 8;
+    float f[8];
+    merge_p3(*reinterpret_cast<const u32x4*>(s), *reinterpret_cast<const u32x4*>(s + xps),
+             *reinterpret_cast<const u32x4*>(s + 2 * xps), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += f[e];
+  }
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] *= inv;
+  store_p3(y + (size_t)n * C + cv * 8, yps, acc);
+}
+
+void launch_gap_fwd_p3(const uint16_t* x, int64_t xps, uint16_t* y, int64_t yps, int N, int HW, int C, hipStream_t st) {
+  const int total = N * (C / 8);
+  hipLaunchKernelGGL(gap_fwd_p3_kernel, dim3((total + 255) / 256), dim3(256), 0, st, x, xps, y, yps, N, HW, C);
+}
+
+static int p3_grid(int64_t n8) {
+  int64_t b = (n8 + 255) / 256;
+  return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+void launch_split_planes(const float* x, int ldx, int64_t rows, int C, uint16_t* out, int ldo, int64_t plane,
+                         hipStream_t st) {
+  const int64_t n8 = rows * (C / 8);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(p3_grid(n8)), dim3(256), 0, st, x, ldx, C, n8, out, ldo, plane);
+}
+
+void launch_merge_planes(const uint16_t* in, int ldi, int64_t plane, int64_t rows, int C, float* y, int ldy,
+                         hipStream_t st) {
+  const int64_t n8 = rows * (C / 8);
+  hipLaunchKernelGGL(merge_planes_kernel, dim3(p3_grid(n8)), dim3(256), 0, st, in, ldi, plane, C, n8, y, ldy);
+}
+
+}  // namespace hcb

@@ -42,12 +42,15 @@ __device__ __forceinline__ size_t epi_out_row(const ConvParams& p, int m) {
 // chunk BEFORE its main loop, so these loads share one memory latency with the A/B tiles
 // instead of paying a second one after the MFMAs (the stage-1 data-grad GEMMs have a single
 // 64-deep k-step and are bound by exactly this latency).
-template <int WM, int WN, int TM, int TN, bool BNB>
+// F32 (the fp32 path, conv_p3.hip): z, the beta source and the output g are fp32 (two 16-byte
+// halves per 8-value segment: pr / pr2, pz / pz2), y is the bf16 hi plane of the activation
+template <int WM, int WN, int TM, int TN, bool BNB, bool F32 = false>
 struct EpiPrefetch {
   static constexpr int BM = WM * TM, BN = WN * TN, SEGS = BN / 8, NT = WM * WN * 64;
   static constexpr int ITER = BM * SEGS / NT;
   static constexpr int CH = BNB ? (ITER < BNB_PREFETCH_CH ? ITER : BNB_PREFETCH_CH) : 1;
   u32x4 pr[CH], pz[CH], py[CH];
+  u32x4 pr2[F32 ? CH : 1], pz2[F32 ? CH : 1];
   // forward GEMMs: the BN statistic shift of each of the lane's accumulator columns, loaded
   // before the main loop so the epilogue does not wait on it
   static constexpr int NKC = BNB ? 1 : TN / 16;
@@ -67,8 +70,20 @@ struct EpiPrefetch {
       const int m = m0 + (tid + (it0 + k) * NT) / SEGS;
       if (m < p.M) {
         const size_t o = epi_out_row(p, m);
-        if (p.beta) pr[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.yres) + o * p.ldy + col);
-        pz[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_z) + o * p.bnb_ld + col);
+        if constexpr (F32) {
+          if (p.beta) {
+            const u32x4* r = reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(p.yres) + o * p.ldy + col);
+            pr[k] = r[0];
+            pr2[k] = r[1];
+          }
+          const u32x4* z = reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(p.bnb_z) + o * p.bnb_ld + col);
+          pz[k] = z[0];
+          pz2[k] = z[1];
+        } else {
+          if (p.beta)
+            pr[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.yres) + o * p.ldy + col);
+          pz[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_z) + o * p.bnb_ld + col);
+        }
         if (p.bnb_mode == 1)
           py[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_y) + o * p.bnb_ld + col);
       }
@@ -134,10 +149,10 @@ __device__ __forceinline__ bool splitk_gather(const ConvParams& p, f32x4 (&acc)[
   return true;
 }
 
-template <int WM, int WN, int TM, int TN, bool BNB>
+template <int WM, int WN, int TM, int TN, bool BNB, bool F32 = false>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)[TM / 16][TN / 16], char* smem,
                                                int tm, int m0, int n0, int wm, int wn, int lane, int tid,
-                                               EpiPrefetch<WM, WN, TM, TN, BNB>& pre, bool prefetched,
+                                               EpiPrefetch<WM, WN, TM, TN, BNB, F32>& pre, bool prefetched,
                                                const char* bnb_params = nullptr) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
@@ -229,7 +244,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
 
   // fused BN-backward: the first chunk of z / y / beta-source segments is in flight before
   // the barrier (or since before the main loop); registers hold one chunk
-  constexpr int CH = EpiPrefetch<WM, WN, TM, TN, BNB>::CH;
+  constexpr int CH = EpiPrefetch<WM, WN, TM, TN, BNB, F32>::CH;
   if constexpr (BNB) {
     if (!prefetched) pre.load(p, 0, m0, n0, tid);
   }
@@ -321,7 +336,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       }
     }
   } else {
-    // bf16 output, no bias / relu (checked on the host)
+    // 16-bit (fp32 on the F32 path) output, no bias / relu (checked on the host)
     float bmu[8], bis[8], bsc[8], bsh[8], bs1[8], bs2[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -351,17 +366,33 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
         const size_t orow = out_row(m);
         float v[8];
         stage_row(row, v);
+        auto f32x8 = [](const u32x4& a, const u32x4& b, float* f) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f[e] = __uint_as_float(a[e]);
+            f[4 + e] = __uint_as_float(b[e]);
+          }
+        };
         if (p.beta) {
           float o[8];
-          unpack8(pre.pr[k], o);
+          if constexpr (F32)
+            f32x8(pre.pr[k], pre.pr2[k], o);
+          else
+            unpack8(pre.pr[k], o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += o[e];
         }
         float zf[8];
-        unpack8(pre.pz[k], zf);
+        if constexpr (F32)
+          f32x8(pre.pz[k], pre.pz2[k], zf);
+        else
+          unpack8(pre.pz[k], zf);
         if (p.bnb_mode == 1) {
           float yf[8];
-          unpack8(pre.py[k], yf);
+          if constexpr (F32)
+            unpack_bf16x8(pre.py[k], yf);  // the hi plane: > 0 exactly when y > 0
+          else
+            unpack8(pre.py[k], yf);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = yf[e] > 0.f ? v[e] : 0.f;
         } else if (p.bnb_mode == 2) {
@@ -373,7 +404,13 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
           bs1[e] += v[e];
           bs2[e] += v[e] * ((zf[e] - bmu[e]) * bis[e]);
         }
-        *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col) = pack8(v);
+        if constexpr (F32) {
+          f32x4* yo = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + orow * p.ldy + col);
+          yo[0] = f32x4{v[0], v[1], v[2], v[3]};
+          yo[1] = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col) = pack8(v);
+        }
       }
     }
     // threads sharing a column segment: LDS partials [NT/SEGS][BN] (x2), column sums, atomics

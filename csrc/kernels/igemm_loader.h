@@ -1,0 +1,161 @@
+// Shared main-loop pieces of the implicit-GEMM conv kernels (conv_igemm.hip, conv_p3.hip):
+// the division-free implicit-im2col loader, the counted LDS-DMA wait and the bf16x6 MFMA step of
+// the fp32 path.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+namespace hcb {
+
+// ---- per-thread implicit-im2col address generation, shared by both main loops.
+// k-steps are issued strictly in order (kt = 0, 1, 2, ...), so the loader keeps the current
+// filter tap / channel offset as wave-uniform state and advances it without divisions. In
+// the CBIG path (C % 64 == 0: a 64-deep k-step never straddles a tap) the per-row work is
+// two adds, two unsigned compares and a select; invalid rows carry h0 = INT_MIN/2 so the
+// bounds test rejects them without a separate flag.
+template <int AV, bool CBIG, bool LHSDIL, int RP = 32, int ESZ = 2>  // RP: rows per load pass (threads / 8)
+struct ALoader {                                                       // ESZ: bytes per element (4: fp32 x)
+  int h0[AV], w0[AV];
+  int rowoff[AV];  // byte offset of (pixel of tap (0,0)) * ldx + lane chunk, may be negative
+  int pix[AV];     // generic path: first pixel of the image, -1 = row beyond M
+  int tr, ts, tc;  // CBIG: current tap (r, s) and channel offset
+
+  __device__ __forceinline__ void init(const ConvParams& p, int m0, int tid, int chunk) {
+    const int PQ = p.P * p.Q;
+    tr = 0;
+    ts = 0;
+    tc = 0;
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      int m = m0 + (tid >> 3) + RP * v;
+      if (m < p.M) {
+        int n = m / PQ, r = m - n * PQ;
+        int pp = r / p.Q, qq = r - pp * p.Q;
+        pix[v] = n * p.H * p.W;
+        h0[v] = pp * p.stride_h - p.pad_h;
+        w0[v] = qq * p.stride_w - p.pad_w;
+        rowoff[v] = ((pix[v] + h0[v] * p.W + w0[v]) * p.ldx + chunk * 8) * ESZ;
+      } else {
+        pix[v] = -1;
+        h0[v] = -0x40000000;
+        w0[v] = 0;
+        rowoff[v] = 0;
+      }
+    }
+  }
+  // position the incremental tap state at k-step kt0 (a split-K block's first k-step)
+  __device__ __forceinline__ void seek(const ConvParams& p, int kt0) {
+    const int k0 = kt0 * 64;
+    const int tap = k0 / p.C;
+    tc = k0 - tap * p.C;
+    tr = tap / p.S;
+    ts = tap - tr * p.S;
+  }
+  // byte offsets of this thread's 16-byte vectors (row v, k-chunk `chunk`) of k-step kt
+  __device__ __forceinline__ void offsets(const ConvParams& p, int kt, int chunk, uint32_t (&off)[AV]) {
+    if constexpr (CBIG && !LHSDIL) {
+      const int dh = tr * p.dil_h, dw = ts * p.dil_w;
+      const int uoff = ((dh * p.W + dw) * p.ldx + tc) * ESZ;
+      const bool tap_ok = tr < p.R;
+#pragma unroll
+      for (int v = 0; v < AV; ++v) {
+        const int h = h0[v] + dh, w = w0[v] + dw;
+        const bool ok = tap_ok && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
+        off[v] = ok ? (uint32_t)(rowoff[v] + uoff) : HCB_OOB;
+      }
+      // advance to the next 64-channel slab
+      tc += 64;
+      if (tc >= p.C) {
+        tc = 0;
+        if (++ts == p.S) {
+          ts = 0;
+          ++tr;
+        }
+      }
+    } else {
+      const int k0 = kt * 64;
+      int tap, c, r, s;
+      if constexpr (CBIG) {
+        tap = k0 / p.C;
+        c = k0 - tap * p.C + chunk * 8;
+      } else {
+        // per-lane k (the chunk): shifts when C is a power of two (the space-to-depth stem's 16
+        // channels) instead of a VALU integer division per thread and k-step
+        const int k = k0 + chunk * 8;
+        if ((p.C & (p.C - 1)) == 0) {
+          const int lc = __builtin_ctz((unsigned)p.C);
+          tap = k >> lc;
+          c = k & (p.C - 1);
+        } else {
+          tap = k / p.C;
+          c = k - tap * p.C;
+        }
+      }
+      if ((p.S & (p.S - 1)) == 0) {
+        const int ls = __builtin_ctz((unsigned)p.S);
+        r = tap >> ls;
+        s = tap & (p.S - 1);
+      } else {
+        r = tap / p.S;
+        s = tap - r * p.S;
+      }
+      const bool tap_ok = tap < p.R * p.S;
+#pragma unroll
+      for (int v = 0; v < AV; ++v) {
+        int h = h0[v] + r * p.dil_h;
+        int w = w0[v] + s * p.dil_w;
+        bool ok = tap_ok && pix[v] >= 0 && h >= 0 && w >= 0;
+        if constexpr (LHSDIL) {
+          ok = ok && (h % p.idil_h == 0) && (w % p.idil_w == 0);
+          h /= p.idil_h;
+          w /= p.idil_w;
+        }
+        ok = ok && h < p.H && w < p.W;
+        off[v] = ok ? (uint32_t)((pix[v] + h * p.W + w) * p.ldx + c) * (uint32_t)ESZ : HCB_OOB;
+      }
+    }
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// bf16x6 step of the fp32 path: the A / B tiles staged as three bf16 images each (hi, mid, lo
+// at IMG u32x4 apart); the six products down to 2^-16 relative, small terms first
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void mfma_tile_step6(const u32x4* A, const u32x4* B, int aimg, int bimg,
+                                                f32x4 (&acc)[TM / 16][TN / 16], int wm, int wn, int lane) {
+  constexpr int MI = TM / 16, NI = TN / 16;
+  const int frow = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    u32x4 a[3][MI], b[3][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * TM + i * 16 + frow, ch = ks * 4 + fq, o = row * 8 + (ch ^ ((row >> 1) & 7));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[t][i] = A[t * aimg + o];
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wn * TN + j * 16 + frow, ch = ks * 4 + fq, o = row * 8 + (ch ^ ((row >> 1) & 7));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) b[t][j] = B[t * bimg + o];
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        acc[i][j] = mfma_bf16(a[2][i], b[0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0][i], b[2][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[1][i], b[1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[1][i], b[0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0][i], b[1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(a[0][i], b[0][j], acc[i][j]);
+      }
+  }
+}
+
+}  // namespace hcb

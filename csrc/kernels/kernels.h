@@ -83,6 +83,8 @@ struct ConvParams {
   // linear index -> (n, h', w'))
   int patch_rows;
   FastDiv fd_hw, fd_w, fd_hw2, fd_w2;
+  // bf16-plane operands (conv_p3.hip): x is three bf16 planes x_plane bytes apart, each x_bytes long
+  uint32_t x_plane;
 };
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st);
 // cfg >= CONV_PATCH_CFG0: the 3x3 / stride 1 / pad 1 kernels with the input patch resident in
@@ -109,11 +111,29 @@ struct WgradParams {
   int ksteps_per_split;
   FastDiv fd_pq, fd_q, fd_c, fd_s;
   uint32_t dy_bytes, x_bytes;
-  int f32in;  // fp32 operands, split into bf16 hi + lo while staged (register-staged cfgs only)
+  int f32in;  // fp32 operands, split into bf16 hi + mid + lo while staged (register-staged cfgs only)
+  // bf16-plane operands (conv_p3.hip): dy / x as three bf16 planes dy_plane / x_plane bytes apart
+  uint32_t dy_plane, x_plane;
 };
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st);
 int wgrad_tile_m(int cfg);
 int wgrad_tile_n(int cfg);
+
+// fp32 convolutions on bf16 hi / mid / lo planes (conv_p3.hip): forward / data-gradient GEMM (x
+// planes, weight packs w / w_lo / w_lo2, fp32 output) and weight gradient (dy and x planes)
+void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st);
+int p3_tile_m(int cfg);
+int p3_tile_n(int cfg);
+void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st);
+int wgrad_p3_tile_m(int cfg);
+int wgrad_p3_tile_n(int cfg);
+// fp32 [rows][ldx] <-> bf16 planes [3][rows][ldo] (plane stride `plane` elements)
+void launch_split_planes(const float* x, int ldx, int64_t rows, int C, uint16_t* out, int ldo, int64_t plane,
+                         hipStream_t st);
+void launch_merge_planes(const uint16_t* in, int ldi, int64_t plane, int64_t rows, int C, float* y, int ldy,
+                         hipStream_t st);
+// global average pool on planes: x planes [N][HW][C] (plane stride xps) -> y planes [N][C] (yps)
+void launch_gap_fwd_p3(const uint16_t* x, int64_t xps, uint16_t* y, int64_t yps, int N, int HW, int C, hipStream_t st);
 
 // ---------------------------------------------------------------- batch norm
 // stats slab [T][2][C] -> mean, invstd (fp32) and running stats update
@@ -165,21 +185,25 @@ struct ResBN {
 void launch_bn_apply_acc(const void* x, int ldx, void* y, int ldy, const void* res, int ldr, int M, int C,
                          const float* acc, int R, float eps, float momentum, const float* gamma, const float* beta,
                          int relu, float* saved_mean, float* saved_invstd, float* run_mean, float* run_var,
-                         const float* shift, const ResBN* res_bn, hipStream_t st, bool f32 = false);
+                         const float* shift, const ResBN* res_bn, hipStream_t st, bool f32 = false, int64_t yps = 0,
+                         int64_t rps = 0);
 // BN(acc statistics) + ReLU + max pool (NHWC, C contiguous): pooled y [N,P,Q] (row stride ldy) and
 // the uint8 window argmax [N,P,Q,C]; the BN+ReLU activation itself is not materialised
 void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void* y, int P, int Q, int ldy, void* amax,
                                 int kh, int kw, int sh, int sw, int ph, int pw, const float* acc, int R, float eps,
                                 float momentum, const float* gamma, const float* beta, float* saved_mean,
                                 float* saved_invstd, float* run_mean, float* run_var, const float* shift, hipStream_t st,
-                                bool f32 = false);
+                                bool f32 = false, int64_t yps = 0);
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
-                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32 = false);
+                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32 = false,
+                              bool yh = false);
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu, float* shift_out, hipStream_t st,
-                             bool f32 = false);
+                             bool f32 = false, bool yh = false, int64_t dxps = 0);
+// fp32 path, plane-stored tensors: (yps / rps / dxps > 0) outputs / residuals as bf16 hi / mid / lo
+// planes with that plane stride in elements; yh: the ReLU-mask source y is the bf16 hi plane
 
 // ---------------------------------------------------------------- pooling
 void launch_pool_fwd(const void* x, void* y, int N, int H, int W, int C, int ldx, int P, int Q,

@@ -1,9 +1,10 @@
 """fp32 (the reference's precision: /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81
-passes no --use_fp16) through the hand-written HIP kernels: --compute_dtype fp32 on ResNet runs
-bf16x3 GEMMs (every fp32 operand split into bf16 hi + lo while staged to LDS, hi*hi + hi*lo + lo*hi
-MFMAs, fp32 accumulation; csrc/kernels/conv_igemm.hip / conv_wgrad.hip) and the fp32
-instantiations of the BN / pool / loss kernels. Every kernel is checked against an fp64 CPU
-reference of the same fp32 operands; the full step against the fp32 CPU step."""
+passes no --use_fp16) through the hand-written HIP kernels: --compute_dtype fp32 on ResNet holds every
+GEMM operand as three bf16 planes hi / mid / lo (``Fn.Planes``, written by the producing BN / split
+kernel) and runs bf16x6 GEMMs on them (six MFMA products, fp32 accumulation;
+csrc/kernels/conv_p3.hip), with the fp32 instantiations of the BN / pool / loss kernels. Every kernel
+is checked against an fp64 CPU reference of the same fp32 operands; the full step against the fp32
+CPU step."""
 import pytest
 import torch
 
@@ -47,11 +48,12 @@ CASES = [(64, 256, 1, 1, 0, 14), (64, 64, 3, 1, 1, 14), (128, 128, 3, 2, 1, 14),
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}s{c[3]}")
-@pytest.mark.parametrize("cfg", [None, 0, 2, 12])
+@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4, 5, 6, (0, 2), (4, 3)], ids=str)
 def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
-    """bf16x6 reproduces the fp32 convolution to fp32 accuracy (~1e-6): fwd, data grad
-    (incl. the stride-phase and strided-1x1 remap forms) and weight grad (incl. split-K); an
-    LDS-DMA cfg (12) is mapped to the register-staged kernel of its tile."""
+    """bf16x6 on planes reproduces the fp32 convolution to fp32 accuracy (~1e-6): fwd, data grad
+    (incl. the stride-phase and strided-1x1 remap forms) and weight grad (incl. split-K), every
+    plane-GEMM tile config (conv_p3.hip cfg 0-6) and in-launch split-K; fp32 inputs are split into
+    planes by the ops themselves."""
     cin, cout, k, s, pad, H = case
     spec, p, pk, ps = _conv(cin, cout, k, s, pad)
     assert Fn.lo_pack(pk.pack) is not None and Fn.lo_pack(pk.tr) is not None
@@ -72,7 +74,9 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     dx = torch.zeros(N, H, H, cin, dtype=torch.float32, device=DEV)
     Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, False, cfg=cfg)
     assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 3e-6
-    for wcfg in ((2, 1), (0, 4), (10, 8)):
+    if isinstance(cfg, tuple):  # split-K case: the weight-gradient configs once
+        return
+    for wcfg in ((2, 1), (0, 4), (3, 8), (1, 2), (4, 1), (5, 2)):
         dw = torch.zeros(cout, spec.K, device=DEV)
         Fn.conv_wgrad(dz, x, spec, dw, cfg=wcfg)
         assert rel_err(dw.view(cout, k, k, cin), wr.grad.permute(0, 2, 3, 1)) < 3e-6, wcfg
@@ -138,3 +142,165 @@ def test_fp32_model_runs_the_hip_kernels():
     finally:
         Fn.set_f32_native(False)
         set_gpu_compute_dtype(torch.bfloat16)
+
+
+def test_planes_split_is_exact():
+    """x == hi + mid + lo for every fp32 value whose lo term is a normal number (random magnitudes
+    over 2^-60..2^60, signs, zeros), and the GPU split equals the CPU split bit for bit."""
+    torch.manual_seed(1)
+    x = torch.randn(1000, 64) * torch.exp2(torch.randint(-60, 60, (1000, 64)).float())
+    x[0, :8] = 0.0
+    xg = x.to(DEV)
+    pg = Fn.to_planes(xg)
+    pc = Fn.to_planes(x)
+    assert torch.equal(pg.t.cpu(), pc.t)
+    assert torch.equal(pg.float().cpu(), x)
+    y = torch.empty_like(xg)
+    Fn._ext.ops().merge_planes(pg.t, 64, 1000, 64, y, 64)
+    assert torch.equal(y.cpu(), x)
+    # strided rows (a channel window of a wider buffer)
+    wide = torch.randn(50, 96, device=DEV)
+    pw = Fn.to_planes(wide[:, 16:80])
+    assert torch.equal(pw.float(), wide[:, 16:80])
+
+
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False), (True, "bn")])
+def test_fp32_bn_planes_match_fp32_kernels(fp32_mode, relu, residual):
+    """The plane-writing BN kernels equal the fp32-output ones bit for bit after the split: forward
+    apply (plain / ReLU / planes residual / fused residual BN), the backward pair (hi-plane ReLU
+    mask, planes dz), and the stem's BN+ReLU+max-pool."""
+    torch.manual_seed(21)
+    C, N, H, R = 256, 4, 9, 8
+    spec, p, pk, ps = _conv(64, C, 3, 1, 1)
+    x = torch.randn(N, H, H, 64, device=DEV)
+    z = torch.empty(N, H, H, C, device=DEV)
+    acc_f = torch.zeros(R * 2 * C, device=DEV)
+    Fn.conv_forward(x, spec, pk.pack, p.data, z, stats=acc_f, stats_R=R)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    res = res_bn = None
+    if residual is True:
+        res = torch.randn(N, H, H, C, device=DEV)
+    elif residual == "bn":
+        res = torch.randn(N, H, H, C, device=DEV) * 3 + 1
+        racc = torch.zeros(R, 2, C, device=DEV)
+        rf = res.view(-1, C)
+        racc[0, 0] = rf.sum(0)
+        racc[0, 1] = (rf * rf).sum(0)
+
+        def res_bn():
+            return (racc, torch.ones(C, device=DEV), torch.zeros(C, device=DEV), torch.empty(C, device=DEV),
+                    torch.empty(C, device=DEV), None, None, None)
+    outs = []
+    for planes in (False, True):
+        y = Fn.Planes.empty((N, H, H, C), DEV) if planes else torch.empty_like(z)
+        r = Fn.to_planes(res) if (planes and residual is True) else res
+        mean, invstd = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        Fn.bn_forward_acc(z, gamma, beta, None, None, 0.9, 1e-5, y, relu, acc_f, R, mean, invstd, residual=r,
+                          res_bn=res_bn() if res_bn else None)
+        outs.append((y, Fn.BNSaved(mean, invstd)))
+    (y32, sv), (yp, _) = outs
+    assert torch.equal(yp.t, Fn.to_planes(y32).t)
+    dy = torch.randn(N, H, H, C, device=DEV)
+    mode = (1 if residual else 2) if relu else 0
+    dzs = []
+    Fn.set_deterministic(True)  # one add per accumulator slot: the two backward runs sum identically
+    for planes in (False, True):
+        dz = Fn.Planes.empty((N, H, H, C), DEV) if planes else torch.empty_like(z)
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        acc_b = torch.zeros(R * 2 * C, device=DEV)
+        Fn.bn_backward_acc(dy, yp if planes else y32, z, sv, gamma, beta, mode, dg, db, dz, acc_b, R)
+        dzs.append((dz, dg, db))
+    Fn.set_deterministic(False)
+    # the two kernel instantiations may contract one FMA differently: 1 ulp
+    assert torch.allclose(dzs[1][0].float(), dzs[0][0], rtol=3e-7, atol=1e-7 * float(dzs[0][0].abs().max()))
+    assert torch.equal(dzs[1][1], dzs[0][1]) and torch.equal(dzs[1][2], dzs[0][2])
+    # stem: BN + ReLU + 3x3/2 max pool into planes
+    Pp = (H + 1) // 2
+    pooled = []
+    for planes in (False, True):
+        out = Fn.Planes.empty((N, Pp, Pp, C), DEV) if planes else torch.empty(N, Pp, Pp, C, device=DEV)
+        amax = torch.empty(N, Pp, Pp, C, dtype=torch.uint8, device=DEV)
+        Fn.bn_relu_maxpool_acc(z, gamma, beta, torch.zeros(C, device=DEV), torch.ones(C, device=DEV), 0.9, 1e-5,
+                               acc_f, R, torch.empty(C, device=DEV), torch.empty(C, device=DEV), out, amax, 3, 3, 2,
+                               2, (1, 1, 1, 1))
+        pooled.append((out, amax))
+    assert torch.equal(pooled[1][0].t, Fn.to_planes(pooled[0][0]).t) and torch.equal(pooled[1][1], pooled[0][1])
+
+
+def test_fp32_gap_planes():
+    torch.manual_seed(2)
+    x = torch.randn(4, 7, 7, 2048, device=DEV)
+    xp = Fn.to_planes(x)
+    y = Fn.Planes.empty((4, 2048), DEV)
+    Fn.gap_forward(xp, y)
+    assert rel_err(y.float(), x.double().mean(dim=(1, 2))) < 2e-7
+
+
+def test_fp32_model_activations_are_planes():
+    """The ResNet fp32 step keeps its GEMM operands as planes end to end: no fp32 -> plane split
+    launch inside the step except the input image's (the producers write planes)."""
+    m = create_model("resnet50", image_size=64, device=DEV, compute_dtype="fp32", seed=3)
+    try:
+        img, lab = synthetic_batch(m, 4)
+        calls = []
+        real = Fn.to_planes
+
+        def spy(t):
+            if not Fn.is_planes(t):
+                calls.append(tuple(t.shape))
+            return real(t)
+
+        Fn.to_planes = spy
+        try:
+            t = Trainer(m, 4, constant_lr(0.01), use_graph=False)
+            t.step(img, lab)
+        finally:
+            Fn.to_planes = real
+        # the stem image and the classifier's dlogits (tiny) are the only splits
+        assert sorted(calls) == sorted([tuple(img.shape), (4, m.fc.ld)]), calls
+    finally:
+        Fn.set_f32_native(False)
+        set_gpu_compute_dtype(torch.bfloat16)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+# (a strided 1x1 data gradient visits only the strided pixels: the models never fuse into it)
+@pytest.mark.parametrize("case", [(256, 64, 1, 1, 0, 14, False), (64, 64, 3, 1, 1, 14, True),
+                                  (128, 256, 1, 1, 0, 7, True), (128, 128, 3, 2, 1, 14, False)],
+                         ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}s{c[3]}acc{int(c[6])}")
+def test_fp32_fused_bn_backward_matches_unfused(fp32_mode, case, mode):
+    """conv_p3_bnb: the fp32 data-grad GEMM with the consuming BN's backward reduction fused into its
+    epilogue stores g = dx * relu_mask (mask from the hi plane of y, or recomputed from z) and adds
+    sum(g), sum(g * xhat) -- against the unfused GEMM plus an fp64 reduction."""
+    cin, cout, k, s, pad, H, accumulate = case
+    spec, p, pk, ps = _conv(cin, cout, k, s, pad)
+    torch.manual_seed(7)
+    N = 4
+    P, Q = spec.out_hw(H, H)
+    dz = Fn.to_planes(torch.randn(N, P, Q, cout, device=DEV))
+    z = torch.randn(N, H, H, cin, device=DEV) * 1.5 + 0.2
+    mean, invstd = torch.randn(cin, device=DEV) * 0.1, torch.rand(cin, device=DEV) + 0.5
+    gamma, beta = torch.rand(cin, device=DEV) + 0.5, torch.randn(cin, device=DEV) * 0.1
+    yf = torch.relu(torch.randn(N, H, H, cin, device=DEV))
+    y = Fn.to_planes(yf)
+    base = torch.randn(N, H, H, cin, device=DEV) if accumulate else None
+    dx_u = base.clone() if accumulate else torch.zeros(N, H, H, cin, device=DEV)
+    Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx_u, accumulate)
+    R = 8
+    acc = torch.zeros(R, 2, cin, device=DEV)
+    dx_f = base.clone() if accumulate else torch.zeros(N, H, H, cin, device=DEV)
+    bnb = Fn.BNBwdFuse(z, y, Fn.BNSaved(mean, invstd), gamma, beta, mode, acc, R)
+    Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx_f, accumulate, bnb=bnb)
+    g = dx_u.double()
+    if mode == 1:
+        g = g * (yf > 0).double()
+    elif mode == 2:
+        xh = (z.double() - mean.double()) * invstd.double()
+        g = g * ((xh * gamma.double() + beta.double()) > 0).double()
+    assert rel_err(dx_f, g) < 1e-6
+    xhat = ((z.double() - mean.double()) * invstd.double()).view(-1, cin)
+    s1 = g.view(-1, cin).sum(0)
+    s2 = (g.view(-1, cin) * xhat).sum(0)
+    a = acc.double().sum(0)
+    assert rel_err(a[0], s1) < 1e-5 and rel_err(a[1], s2) < 1e-5
