@@ -25,15 +25,19 @@
 
 namespace hcb {
 
-// all fragment reads of both 32-deep halves first, then the 2 x MI x NI x 6 MFMAs (the compiler
-// otherwise waits on each read right before its first use)
+// the fragments of one 64-deep k-step (both 32-deep halves, three planes of each operand) in registers
+template <int TM, int TN>
+struct P3Frags {
+  static constexpr int MI = TM / 16, NI = TN / 16;
+  u32x4 a[2][3][MI], b[2][3][NI];
+};
+
+// every fragment read of the k-step (LDS -> registers), issued back to back
 template <int WM, int WN, int TM, int TN>
-__device__ __forceinline__ void p3_step(const u32x4* A, const u32x4* B, f32x4 (&acc)[TM / 16][TN / 16], int wm, int wn,
-                                        int lane) {
+__device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<TM, TN>& f, int wm, int wn, int lane) {
   constexpr int MI = TM / 16, NI = TN / 16, BM = WM * TM, BN = WN * TN;
   constexpr int AIMG = BM * 8, BIMG = BN * 8;  // one plane image, in u32x4
   const int frow = lane & 15, fq = lane >> 4;
-  u32x4 a[2][3][MI], b[2][3][NI];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int ch = ks * 4 + fq;
@@ -41,28 +45,33 @@ __device__ __forceinline__ void p3_step(const u32x4* A, const u32x4* B, f32x4 (&
     for (int i = 0; i < MI; ++i) {
       const int row = wm * TM + i * 16 + frow, o = row * 8 + (ch ^ ((row >> 1) & 7));
 #pragma unroll
-      for (int t = 0; t < 3; ++t) a[ks][t][i] = A[t * AIMG + o];
+      for (int t = 0; t < 3; ++t) f.a[ks][t][i] = A[t * AIMG + o];
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int row = wn * TN + j * 16 + frow, o = row * 8 + (ch ^ ((row >> 1) & 7));
 #pragma unroll
-      for (int t = 0; t < 3; ++t) b[ks][t][j] = B[t * BIMG + o];
+      for (int t = 0; t < 3; ++t) f.b[ks][t][j] = B[t * BIMG + o];
     }
   }
-  __builtin_amdgcn_sched_barrier(0);
+}
+
+// the 2 x MI x NI x 6 MFMAs of the k-step on register fragments
+template <int TM, int TN>
+__device__ __forceinline__ void p3_mma(const P3Frags<TM, TN>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
+  constexpr int MI = TM / 16, NI = TN / 16;
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {  // small terms first
-        acc[i][j] = mfma_bf16(a[ks][2][i], b[ks][0][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][2][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][1][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][0][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][1][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(f.a[ks][2][i], f.b[ks][0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][2][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(f.a[ks][1][i], f.b[ks][1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(f.a[ks][1][i], f.b[ks][0][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][1][j], acc[i][j]);
+        acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][0][j], acc[i][j]);
       }
 }
 
@@ -91,8 +100,10 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, RP = NT / 8;  // threads; tile rows per load pass
   constexpr int AV = BM / RP, BV = BN / RP;
+  constexpr int LOADS = 3 * (AV + BV);  // LDS-DMA instructions per thread per slot
   constexpr int AIMG = BM * 128, BIMG = BN * 128;
   constexpr int STAGE = (int)p3_stage_bytes<BM, BN>();
+  static_assert(LOADS <= 63, "vmcnt range");
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(p3_param_off<BM, BN, WM>() + bnb_param_lds(BN) <= 160 * 1024, "ring + BN parameters must fit LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -159,17 +170,32 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
   if constexpr (BNB) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
   const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS_P3;
   if (early) pre.load(p, 0, m0, n0, tid);
+  // Two-slot ring with EARLY RELEASE: a slot is refilled as soon as every wave holds its fragments
+  // in registers (second barrier), not after the MFMAs, so during the k-step's MFMAs the DMA of
+  // the next TWO k-steps is in flight (the 6x MFMA time of two stages covers the L2 / HBM latency
+  // that one stage does not).
   if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  P3Frags<TM, TN> fr;
   for (int kt = 0; kt < nk; ++kt) {
-    // stage kt has landed for this thread; the barrier publishes every thread's DMA and
-    // guarantees every wave is done reading stage kt-1, which the next issue overwrites
-    wait_vmcnt<0>();
+    // slot kt has landed for this thread once at most the next slot's loads are outstanding;
+    // the barrier publishes every thread's DMA
+    if (kt + 1 < nk)
+      wait_vmcnt<LOADS>();
+    else
+      wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 1 < nk) issue((kt + 1) & 1, kt + 1);
     const char* sb = smem + (kt & 1) * STAGE;
-    p3_step<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG), acc,
-                            wm, wn, lane);
+    p3_read<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG), fr, wm,
+                            wn, lane);
+    if (kt + 2 < nk) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+      __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+      asm volatile("" ::: "memory");
+      issue(kt & 1, kt + 2);
+    }
+    p3_mma<TM, TN>(fr, acc);
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
   if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
@@ -266,7 +292,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
   constexpr int AIMG = BK * BM * 2, BIMG = BK * BN * 2;
   constexpr int STAGE = 3 * (AIMG + BIMG);
   static_assert(AI * ARPI * NW == BK && BI * BRPI * NW == BK && AI >= 1 && BI >= 1, "tile / wave mapping");
-  static_assert(NST >= 2 && NST <= 3 && LOADS * (NST - 2) <= 63 && NST * STAGE <= 160 * 1024, "ring");
+  static_assert(NST >= 2 && NST <= 3 && LOADS * (NST - 1) <= 63 && NST * STAGE <= 160 * 1024, "ring");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -378,22 +404,25 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
     return __builtin_bit_cast(u32x4, t);
   };
 
+  // NST-slot ring with early release (see conv_igemm_p3_kernel): a slot is refilled once every wave
+  // holds its fragments in registers, so NST k-steps of DMA are in flight during the MFMAs
   const int nk = kt_end - kt_begin;
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
+  for (int s = 0; s < NST; ++s)
     if (s < nk) issue(s, kt_begin + s);
+  u32x4 a[2][3][MI], b[2][3][NI];
   for (int k = 0; k < nk; ++k) {
-    const int ahead = min(NST - 2, nk - 1 - k);
-    if (ahead >= 1)
-      wait_vmcnt<(NST >= 3 ? 1 : 0) * LOADS>();
+    const int ahead = min(NST - 1, nk - 1 - k);  // later slots still in flight
+    if (ahead >= 2)
+      wait_vmcnt<(NST >= 3 ? 2 : 0) * LOADS>();
+    else if (ahead == 1)
+      wait_vmcnt<LOADS>();
     else
       wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (k + NST - 1 < nk) issue((k + NST - 1) % NST, kt_begin + k + NST - 1);
     const char* Ab = smem + (k % NST) * STAGE;
     const char* Bb = Ab + 3 * AIMG;
-    u32x4 a[2][3][MI], b[2][3][NI];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -405,7 +434,12 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
 #pragma unroll
         for (int t = 0; t < 3; ++t) b[ks][t][j] = frag(Bb + t * BIMG, BN, ks * 32 + 8 * g, wn * TN + j * 16);
     }
-    __builtin_amdgcn_sched_barrier(0);
+    if (k + NST < nk) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+      __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+      asm volatile("" ::: "memory");
+      issue(k % NST, kt_begin + k + NST);
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
