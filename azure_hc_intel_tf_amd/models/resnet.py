@@ -87,7 +87,7 @@ class ResNet(CNNModel):
         ps = self.ps
         S = self.image_size
         v15 = self.version == "v1.5"
-        if self.native and L.STEM_S2D and self.compute_dtype != "fp32":  # the fold kernels are 16-bit
+        if self.native and L.STEM_S2D:  # fp32: the fold runs on the image's bf16 planes
             self.stem = StemS2D(ps, "conv0", (S, S, self.image_channels), 64, relu=True, need_dx=False,
                                 logical_cin=3)
         else:

@@ -384,19 +384,38 @@ class StemS2D(ConvBN):
         self.fold_shape = (P + 3, Q + 3, 16)
         self.fold_spec = ConvSpec(cin=16, cin_pad=16, cout=cout, kh=4, kw=4, sh=1, sw=1, pt=0, pl=0, pb=0, pr=0)
         self._wfold = None
+        self._wpack = None
         self._dwfold = None
 
     def _folded_weight(self, dev):
-        if self._wfold is None or self._wfold.device != dev:
-            self._wfold = torch.empty((self.spec.cout, 256), dtype=act_dtype(dev), device=dev)
+        """The folded GEMM weight [cout][256]: the 16-bit pack, or on the fp32 path the hi pack of
+        its three planes (mid / lo attached as the pack's ``hcb_lo``, ops.functional.lo_pack)."""
         from ..ops import _ext
 
+        p3 = Fn.lo_pack(self.pack.pack) is not None  # this model's packs carry planes: the fp32 path
+        if self._wfold is None or self._wfold.device != dev or (self._wfold.dim() == 3) != p3:
+            if p3:
+                self._wfold = torch.empty((3, self.spec.cout, 256), dtype=torch.bfloat16, device=dev)
+                self._wpack = self._wfold[0]
+                Fn.register_lo(self._wpack, self._wfold[1:].reshape(2, -1))
+            else:
+                self._wfold = torch.empty((self.spec.cout, 256), dtype=act_dtype(dev), device=dev)
+                self._wpack = self._wfold
         _ext.ops().stem_wfold(self.w.data, self._wfold)
-        return self._wfold
+        return self._wpack
 
     def fold_input(self, x):
+        """2x2 space-to-depth fold of the padded image; on the fp32 path the image is split into its
+        bf16 planes first and the three planes are folded as one batch of 3N images."""
         from ..ops import _ext
 
+        if Fn.is_planes(x) or (x.is_cuda and x.dtype == torch.float32):
+            xp = Fn.to_planes(x)
+            N = x.shape[0]
+            xf = Fn.Planes.empty((N,) + self.fold_shape, x.device)
+            _ext.ops().stem_s2d(xp.t.view((3 * N,) + tuple(xp.shape[1:])), xf.t.view((3 * N,) + self.fold_shape),
+                                self.PAD)
+            return xf
         xf = torch.empty((x.shape[0],) + self.fold_shape, dtype=x.dtype, device=x.device)
         _ext.ops().stem_s2d(x, xf, self.PAD)
         return xf

@@ -237,10 +237,15 @@ class ParamStore:
             # the pack kernel moves 8-channel vectors (fp32 float4 pairs -> one 16-byte bf16 store)
             for pk in self.packs:
                 assert pk.C % 8 == 0 and pk.Kpad % 64 == 0, f"pack of {pk.param.name}: C % 8, Kpad % 64"
-            self.pack_buf = torch.zeros(max(poff, ALIGN), dtype=dtype_pack, device=device)
             self.pack_table = torch.tensor(rows, dtype=torch.int64, device=device)
-            self.pack_buf_lo = (torch.zeros((2, self.pack_buf.numel()), dtype=dtype_pack, device=device)
-                                if pack_lo else None)
+            if pack_lo:  # fp32 path: the hi / mid / lo planes of every pack in one [3][n] buffer
+                self.pack_planes = torch.zeros((3, max(poff, ALIGN)), dtype=dtype_pack, device=device)
+                self.pack_buf = self.pack_planes[0]
+                self.pack_buf_lo = self.pack_planes[1:]
+            else:
+                self.pack_planes = None
+                self.pack_buf = torch.zeros(max(poff, ALIGN), dtype=dtype_pack, device=device)
+                self.pack_buf_lo = None
             from ..ops import functional as Fn
 
             for pk in self.packs:
@@ -256,6 +261,7 @@ class ParamStore:
         else:
             self.pack_buf = None
             self.pack_buf_lo = None
+            self.pack_planes = None
             self.pack_table = None
         self.finalized = True
         return self
@@ -267,10 +273,10 @@ class ParamStore:
             return
         from ..ops import _ext
 
+        if self.pack_planes is not None:  # fp32 path: hi / mid / lo planes in one launch
+            _ext.ops().weight_pack(self.master, self.pack_planes, self.pack_table, self.pack_max_work, 3)
+            return
         _ext.ops().weight_pack(self.master, self.pack_buf, self.pack_table, self.pack_max_work)
-        if self.pack_buf_lo is not None:  # fp32 path: the mid and lo packs
-            _ext.ops().weight_pack(self.master, self.pack_buf_lo[0], self.pack_table, self.pack_max_work, 1)
-            _ext.ops().weight_pack(self.master, self.pack_buf_lo[1], self.pack_table, self.pack_max_work, 2)
 
     def zero_grad(self):
         self.grad.zero_()

@@ -433,7 +433,10 @@ def set_tuned(table: dict) -> None:
 
 
 # ---- fp32 path (Planes operands, conv_p3.hip): its own tile sets and tuning keys
-_P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128)}
+# cfg -> block tile (conv_p3.hip): 0-6 64-deep two-slot rings, 7-13 32-deep slots (bigger tiles per CU)
+_P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
+             7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
+             13: (128, 64)}
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64)}
 
 
@@ -452,7 +455,7 @@ def p3_candidates(M: int, N: int, K: int):
     out = []
     ksteps = math.ceil(K / 64)
     for c, (bm, bn) in _P3_TILES.items():
-        if N <= 64 and bn > 64:
+        if (N <= 64 and bn > 64) or (N <= 128 and bn > 128) or (M <= 4096 and bm > 128):
             continue
         tiles = math.ceil(M / bm) * math.ceil(N / bn)
         out.append((c, 1))
@@ -470,7 +473,7 @@ def p3_plan(M: int, N: int, K: int, taps: int = 1):
     if key in _tuned:
         c = _tuned[key]
         return (int(c[0]), int(c[1])) if isinstance(c, (tuple, list)) else (int(c), 1)
-    cfg = 1 if N >= 128 and M < 4096 else 0
+    cfg = 7 if N >= 128 else 13
     bm, bn = _P3_TILES[cfg]
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
     ksteps = math.ceil(K / 64)

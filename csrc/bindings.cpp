@@ -631,13 +631,20 @@ void sgd_momentum(const Tensor& w, const Tensor& mom, const Tensor& g, int64_t n
 
 void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, int64_t max_work, int64_t lo) {
   check_f32(master, "master");
-  check_act(pack, "pack");
+  int64_t pstride = 0;
+  if (lo == 3) {  // all three planes: pack is [3][n] bf16 (plane t at t * stride(0))
+    pstride = check_planes(pack, "pack");
+    TORCH_CHECK(pack.dim() == 2, "hcb.weight_pack: planes [3][n]");
+  } else {
+    TORCH_CHECK(lo >= 0 && lo <= 2, "hcb.weight_pack: lo 0..3");
+    check_act(pack, "pack");
+  }
   check_cuda(table, "table");
   TORCH_CHECK(table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 9, "hcb.weight_pack: table [n][9] int64");
   TORCH_CHECK(table.is_contiguous(), "hcb.weight_pack: table contiguous");
   hcb::launch_weight_pack(master.data_ptr<float>(), (uint16_t*)pack.data_ptr(),
                           reinterpret_cast<const hcb::WPackEntry*>(table.data_ptr<int64_t>()),
-                          (int)table.size(0), max_work, cur_stream(), (int)lo);
+                          (int)table.size(0), max_work, cur_stream(), (int)lo, pstride);
 }
 
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {
@@ -931,10 +938,12 @@ void stem_wfold(const Tensor& w, const Tensor& wp) {
   check_cuda(wp, "wp");
   TORCH_CHECK(w.dim() == 4 && w.size(1) == 7 && w.size(2) == 7 && w.size(3) >= 3 && w.is_contiguous(),
               "hcb.stem_wfold: w [cout][7][7][>=3] fp32");
-  TORCH_CHECK(wp.scalar_type() == kAct && wp.is_contiguous() && wp.numel() == w.size(0) * 256,
-              "hcb.stem_wfold: wp bf16 [cout][256]");
+  // wp: the bf16 pack [cout][256], or (fp32 path) its hi / mid / lo planes [3][cout][256]
+  const bool p3 = wp.dim() == 3 && wp.size(0) == 3 && wp.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((p3 || wp.scalar_type() == kAct) && wp.is_contiguous() && wp.numel() == (p3 ? 3 : 1) * w.size(0) * 256,
+              "hcb.stem_wfold: wp bf16 [cout][256] or planes [3][cout][256]");
   hcb::launch_stem_wfold(w.data_ptr<float>(), (int)w.size(0), (int)w.size(3),
-                         reinterpret_cast<uint16_t*>(wp.data_ptr()), cur_stream());
+                         reinterpret_cast<uint16_t*>(wp.data_ptr()), cur_stream(), p3);
 }
 
 void stem_wgrad_unfold(const Tensor& dwp, const Tensor& dw) {
@@ -955,7 +964,7 @@ hcb::ConvParams p3_params(const Tensor& x, const Tensor& w, const Tensor& w_lo, 
                           const c10::optional<Tensor>& stats, at::IntArrayRef g, int64_t cfg,
                           const c10::optional<Tensor>& stats_shift) {
   const int64_t xps = check_planes(x, "x");
-  TORCH_CHECK(cfg >= 0 && cfg < 7, "hcb.conv_p3: cfg 0..6");
+  TORCH_CHECK(cfg >= 0 && cfg < 14, "hcb.conv_p3: cfg 0..13");
   // conv_params validates geometry and byte ranges on plane 0 (a bf16 tensor of this build's type);
   // split-K is validated here against the p3 tiles
   std::vector<int64_t> g1(g.begin(), g.end());

@@ -129,7 +129,9 @@ struct Comm {
   // debug (HCB_COMM_DEBUG_SLEEP_MS): a bounded device sleep on the comm stream at every fork, so a
   // stalled collective can be staged on one GPU (it is captured into the step graph like the rest)
   int debug_sleep_ms = 0;
-  hipEvent_t watch_ev = nullptr;
+  // one event per watched cycle (WatchState::pending), recycled through a free list
+  std::vector<hipEvent_t> watch_evs;
+  std::vector<int64_t> watch_free;
   std::atomic<bool> aborted{false};
 
   hipEvent_t get_event() {
@@ -139,7 +141,27 @@ struct Comm {
       return e;
     });
   }
-  bool watch_done() { return hipEventQuery(watch_ev) == hipSuccess; }
+  // an event recorded behind the work just enqueued on `s`; its token for WatchState::enqueue
+  int64_t record_watch(hipStream_t s) {
+    int64_t t;
+    if (!watch_free.empty()) {
+      t = watch_free.back();
+      watch_free.pop_back();
+    } else {
+      hipEvent_t e;
+      HCB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      watch_evs.push_back(e);
+      t = (int64_t)watch_evs.size() - 1;
+    }
+    HCB_HIP(hipEventRecord(watch_evs[t], s));
+    return t;
+  }
+  auto watch_done() {
+    return [this](int64_t t) { return hipEventQuery(watch_evs[t]) == hipSuccess; };
+  }
+  auto watch_release() {
+    return [this](int64_t t) { watch_free.push_back(t); };
+  }
   void flush_timeline(bool block) {
     timeline.flush(
         block, events, [](hipEvent_t e) { return hipEventQuery(e) == hipSuccess; },
@@ -190,7 +212,7 @@ void watchdog_loop(Comm* c) {
     auto now = std::chrono::steady_clock::now();
     {
       std::lock_guard<std::mutex> lk(c->mu);
-      c->ws.poll_quiet(now, 1.0, [c] { return c->watch_done(); });
+      c->ws.poll_quiet(now, 1.0, c->watch_done(), c->watch_release());
     }
     double waited = 0;
     const StallWatch::Action act = c->ws.watch.evaluate(now, &waited);
@@ -305,7 +327,6 @@ int64_t create(const Tensor& uid, int64_t rank, int64_t world, int64_t device) {
   HCB_HIP(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
   HCB_HIP(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
   HCB_HIP(hipEventCreate(&c->base_ev));
-  HCB_HIP(hipEventCreateWithFlags(&c->watch_ev, hipEventDisableTiming));
   HCB_HIP(hipEventRecord(c->base_ev, c->stream));
   if (const char* tl = std::getenv("HOROVOD_TIMELINE")) {
     if (*tl) {
@@ -342,7 +363,7 @@ void destroy(int64_t h) {
   hipEventDestroy(c->fork_ev);
   hipEventDestroy(c->join_ev);
   hipEventDestroy(c->base_ev);
-  hipEventDestroy(c->watch_ev);
+  for (hipEvent_t e : c->watch_evs) hipEventDestroy(e);
   if (c->cbuf) hipFree(c->cbuf);
   hipStreamDestroy(c->stream);
 }
@@ -422,7 +443,7 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
   const bool cap = capturing(cur);
   if (!cap) c->flush_timeline(false);
   if (!cap && c->wd.joinable())
-    c->ws.enter([c] { return c->watch_done(); });
+    c->ws.enter(c->watch_done(), c->watch_release());
   else
     c->ws.last_call = std::chrono::steady_clock::now();
   if (const size_t grow = hcb::comm::scratch_bytes(c->cbuf_bytes, n, (hcb::comm::Wire)compress)) {
@@ -445,10 +466,7 @@ void bucket_impl(int64_t h, const Tensor& flat, const Tensor& buckets, int64_t c
       c->engine->submit(flat.data_ptr<float>(), n, bk, nb, (hcb::comm::Wire)compress, average,
                  fusion_bytes > 0 ? fusion_bytes : c->fusion_bytes, do_join);
   c->buckets_issued += (int64_t)issued.size();
-  if (!cap && c->wd.joinable()) {
-    HCB_HIP(hipEventRecord(c->watch_ev, c->stream));
-    c->ws.enqueue(c->buckets_issued - 1, false);
-  }
+  if (!cap && c->wd.joinable()) c->ws.enqueue(c->buckets_issued - 1, false, c->record_watch(c->stream));
   c->cycle++;
 }
 
@@ -469,11 +487,11 @@ void bucket_allreduce_async_(int64_t h, const Tensor& flat, const Tensor& bucket
 // Per-step heartbeat of the graph-replayed data-parallel step (call right after the replay, on
 // the stream it was launched on, never inside a capture). The collectives of a captured step
 // make no host call when replayed, so without this the watchdog would never learn about them:
-// record the watch event behind the step (the graph's comm branch joins the capture stream
-// before the graph ends, so the event completes only once every reduction of the step has)
-// and enqueue one watch cycle. As for eager reductions, completion is observed without
-// blocking on the CALLER's thread (the previous mark's event) or, once the caller has been
-// quiet for > 1 s (blocked on a hung step), by the watchdog thread itself.
+// record a watch event of this step's own behind it (the graph's comm branch joins the capture
+// stream before the graph ends, so the event completes only once every reduction of the step
+// has) and enqueue one watch cycle. As for eager reductions, completion is observed without
+// blocking on the CALLER's thread (every earlier mark whose event has finished, oldest first) or,
+// once the caller has been quiet for > 1 s (blocked on a hung step), by the watchdog thread.
 void step_mark(int64_t h) {
   Comm* c = get(h);
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
@@ -484,9 +502,8 @@ void step_mark(int64_t h) {
     c->ws.marks++;
     return;
   }
-  c->ws.enter([c] { return c->watch_done(); });
-  HCB_HIP(hipEventRecord(c->watch_ev, cur));
-  c->ws.enqueue(c->buckets_issued - 1, true);
+  c->ws.enter(c->watch_done(), c->watch_release());
+  c->ws.enqueue(c->buckets_issued - 1, true, c->record_watch(cur));
 }
 int64_t steps_marked(int64_t h) {
   Comm* c = get(h);

@@ -12,6 +12,7 @@
 // The device side (events, streams) enters only through the functors the callers pass in.
 #pragma once
 #include <chrono>
+#include <deque>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -176,21 +177,36 @@ inline size_t scratch_bytes(size_t have, int64_t numel, Wire w) {
 struct WatchState {
   using clock = std::chrono::steady_clock;
   StallWatch watch;
-  int64_t cycle = 0;         // the cycle the watch event currently stands for
+  int64_t cycle = 0;         // the newest enqueued cycle
   int64_t first_mark = -1;   // first cycle enqueued by a step mark (graph-replayed steps)
   int64_t marks = 0;         // step marks seen
   clock::time_point last_call = clock::now();
+  // every enqueued cycle with the token of the event recorded behind it, oldest first: each
+  // cycle has an event of its own, so a caller that runs several steps ahead of the device (graph
+  // replays never sync) still sees every one of them complete -- one re-recorded event would be
+  // overwritten before it completed and the watchdog would report a stall of a healthy run
+  std::deque<std::pair<int64_t, int64_t>> pending;
 
-  // the caller enters (a reduction or a step mark): note the time, and retire the previous
-  // cycle if its event has completed
-  template <class Done>
-  void enter(Done&& done) {
-    last_call = clock::now();
-    if (watch.completed() < cycle && done()) watch.complete(cycle);
+  // complete, oldest first, every pending cycle whose event has finished (done(token): a
+  // non-blocking query); release(token) hands the event back to the owner's pool
+  template <class Done, class Release>
+  void retire(Done&& done, Release&& release) {
+    while (!pending.empty() && done(pending.front().second)) {
+      watch.complete(pending.front().first);
+      release(pending.front().second);
+      pending.pop_front();
+    }
   }
-  // after the watch event was re-recorded behind the new work: one more cycle to watch
-  int64_t enqueue(int64_t last_bucket, bool step_mark) {
+  // the caller enters (a reduction or a step mark): note the time, retire finished cycles
+  template <class Done, class Release>
+  void enter(Done&& done, Release&& release) {
+    last_call = clock::now();
+    retire(done, release);
+  }
+  // after an event (token) was recorded behind the new work: one more cycle to watch
+  int64_t enqueue(int64_t last_bucket, bool step_mark, int64_t token) {
     cycle = watch.enqueue(last_bucket);
+    pending.emplace_back(cycle, token);
     if (step_mark) {
       ++marks;
       if (first_mark < 0) first_mark = cycle;
@@ -198,11 +214,10 @@ struct WatchState {
     return cycle;
   }
   // the watchdog thread, when the caller has been quiet for > quiet_s (blocked on a hung
-  // collective or idle): it may query the event itself
-  template <class Done>
-  void poll_quiet(clock::time_point now, double quiet_s, Done&& done) {
-    if (watch.completed() < cycle && std::chrono::duration<double>(now - last_call).count() > quiet_s && done())
-      watch.complete(cycle);
+  // collective or idle): it may query the events itself
+  template <class Done, class Release>
+  void poll_quiet(clock::time_point now, double quiet_s, Done&& done, Release&& release) {
+    if (!pending.empty() && std::chrono::duration<double>(now - last_call).count() > quiet_s) retire(done, release);
   }
   bool is_graph_cycle(int64_t c) const { return first_mark >= 0 && c >= first_mark; }
 };

@@ -25,43 +25,57 @@
 
 namespace hcb {
 
-// the fragments of one 64-deep k-step (both 32-deep halves, three planes of each operand) in registers
-template <int TM, int TN>
+// Tile geometry of the plane GEMMs. KW: channels per ring slot (k-depth): 64 (128-byte LDS rows, the
+// bf16 kernels' layout) or 32 (64-byte rows: half the LDS per slot, so a 128x128 or 256x128 block
+// tile fits a 3- or 2-slot ring and each loaded byte feeds twice the MFMAs of a 64x128 tile -- the
+// per-CU L2 -> LDS fill rate, not the MFMA, is what bounds the smaller tiles).
+template <int KW>
+__device__ __forceinline__ int p3_swz(int row) {
+  // 16-byte chunk XOR per row, conflict-free ds_read_b128 fragment reads: 128-byte rows: the
+  // generic kernels' (row >> 1) & 7; 64-byte rows: (row >> 2) & 2 (each lane group of the read
+  // then covers the 16 distinct 16-byte bank quads of a 256-byte bank row)
+  if constexpr (KW == 64) return (row >> 1) & 7;
+  else return (row >> 2) & 2;
+}
+
+// the fragments of one slot (KS = KW / 32 halves of 32, three planes of each operand) in registers
+template <int TM, int TN, int KS>
 struct P3Frags {
   static constexpr int MI = TM / 16, NI = TN / 16;
-  u32x4 a[2][3][MI], b[2][3][NI];
+  u32x4 a[KS][3][MI], b[KS][3][NI];
 };
 
-// every fragment read of the k-step (LDS -> registers), issued back to back
-template <int WM, int WN, int TM, int TN>
-__device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<TM, TN>& f, int wm, int wn, int lane) {
-  constexpr int MI = TM / 16, NI = TN / 16, BM = WM * TM, BN = WN * TN;
-  constexpr int AIMG = BM * 8, BIMG = BN * 8;  // one plane image, in u32x4
+// every fragment read of the slot (LDS -> registers), issued back to back
+template <int WM, int WN, int TM, int TN, int KW>
+__device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<TM, TN, KW / 32>& f, int wm, int wn,
+                                        int lane) {
+  constexpr int MI = TM / 16, NI = TN / 16, BM = WM * TM, BN = WN * TN, CPR = KW / 8;
+  constexpr int AIMG = BM * CPR, BIMG = BN * CPR;  // one plane image, in u32x4
   const int frow = lane & 15, fq = lane >> 4;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
+  for (int ks = 0; ks < KW / 32; ++ks) {
     const int ch = ks * 4 + fq;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const int row = wm * TM + i * 16 + frow, o = row * 8 + (ch ^ ((row >> 1) & 7));
+      const int row = wm * TM + i * 16 + frow, o = row * CPR + (ch ^ p3_swz<KW>(row));
 #pragma unroll
       for (int t = 0; t < 3; ++t) f.a[ks][t][i] = A[t * AIMG + o];
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int row = wn * TN + j * 16 + frow, o = row * 8 + (ch ^ ((row >> 1) & 7));
+      const int row = wn * TN + j * 16 + frow, o = row * CPR + (ch ^ p3_swz<KW>(row));
 #pragma unroll
       for (int t = 0; t < 3; ++t) f.b[ks][t][j] = B[t * BIMG + o];
     }
   }
 }
 
-// the 2 x MI x NI x 6 MFMAs of the k-step on register fragments
-template <int TM, int TN>
-__device__ __forceinline__ void p3_mma(const P3Frags<TM, TN>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
+// the KS x MI x NI x 6 MFMAs of the slot on register fragments
+template <int TM, int TN, int KS>
+__device__ __forceinline__ void p3_mma(const P3Frags<TM, TN, KS>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
   constexpr int MI = TM / 16, NI = TN / 16;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -75,14 +89,14 @@ __device__ __forceinline__ void p3_mma(const P3Frags<TM, TN>& f, f32x4 (&acc)[TM
       }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int KW>
 constexpr size_t p3_stage_bytes() {
-  return (size_t)3 * (BM + BN) * 128;
+  return (size_t)3 * (BM + BN) * KW * 2;
 }
 // LDS offset of the fused BN-backward parameters: above the ring and the epilogue staging
-template <int BM, int BN, int WM>
+template <int BM, int BN, int WM, int KW, int NST>
 constexpr size_t p3_param_off() {
-  const size_t a = 2 * p3_stage_bytes<BM, BN>(), b = igemm_epilogue_lds(BM, BN, WM);
+  const size_t a = NST * p3_stage_bytes<BM, BN, KW>(), b = igemm_epilogue_lds(BM, BN, WM);
   return a > b ? a : b;
 }
 // data-grad GEMMs with at most this many 64-deep k-steps fetch their fused BN-backward epilogue
@@ -91,21 +105,26 @@ constexpr int EARLY_EPI_KSTEPS_P3 = 2;
 
 // ============================================================== forward / data gradient
 // x: three bf16 planes of the NHWC input, p.x_plane bytes apart (each plane p.x_bytes long);
-// w / w_lo / w_lo2: the hi / mid / lo weight packs [Nout][Kpad]. Two-stage LDS-DMA ring.
+// w / w_lo / w_lo2: the hi / mid / lo weight packs [Nout][Kpad]. NST-slot LDS-DMA ring of KW-deep
+// slots with EARLY RELEASE: a slot is refilled as soon as every wave holds its fragments in
+// registers (second barrier), not after the MFMAs, so NST slots of DMA are in flight during a
+// slot's MFMAs.
 // BNB: the fused BN-backward epilogue (data gradient producing a BN layer's dy: ReLU gating from the
 // hi plane of y or from z, sum(g) / sum(g * xhat) into p.bnb_acc), fp32 z / beta source / output
-template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB>
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool LHSDIL, bool BNB>
 __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p) {
-  constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
+  constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
-  constexpr int NT = WM * WN * 64, RP = NT / 8;  // threads; tile rows per load pass
+  constexpr int NT = WM * WN * 64, CPR = KW / 8, RB = KW * 2;  // threads; chunks and bytes per LDS row
+  constexpr int RP = NT / CPR;                                    // tile rows per load pass
   constexpr int AV = BM / RP, BV = BN / RP;
   constexpr int LOADS = 3 * (AV + BV);  // LDS-DMA instructions per thread per slot
-  constexpr int AIMG = BM * 128, BIMG = BN * 128;
-  constexpr int STAGE = (int)p3_stage_bytes<BM, BN>();
-  static_assert(LOADS <= 63, "vmcnt range");
+  constexpr int AIMG = BM * RB, BIMG = BN * RB;
+  constexpr int STAGE = (int)p3_stage_bytes<BM, BN, KW>();
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
-  static_assert(p3_param_off<BM, BN, WM>() + bnb_param_lds(BN) <= 160 * 1024, "ring + BN parameters must fit LDS");
+  static_assert(LOADS * (NST - 1) <= 63 && NST >= 2 && NST <= 4, "vmcnt range");
+  static_assert(p3_param_off<BM, BN, WM, KW, NST>() + bnb_param_lds(BN) <= 160 * 1024,
+                "ring + BN parameters must fit LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -117,8 +136,10 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
   const int tile = bid / S, split = bid - tile * S;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  // lane-linear LDS image; the lane fetches the GLOBAL chunk the swizzled read expects there
-  const int chunk = (tid & 7) ^ ((tid >> 4) & 7);
+  // lane-linear LDS image (row tid / CPR of the pass, position tid % CPR); the lane fetches the
+  // GLOBAL chunk the swizzled read expects there (the XOR is an involution; RP * v and a wave's
+  // row base are multiples of 16, so the row's swizzle is a function of tid)
+  const int chunk = (tid % CPR) ^ p3_swz<KW>(tid / CPR);
 
   const char* xb = reinterpret_cast<const char*>(p.x);
   const __amdgpu_buffer_rsrc_t xr0 = make_rsrc(xb, p.x_bytes);
@@ -127,12 +148,12 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
   const __amdgpu_buffer_rsrc_t wr0 = make_rsrc(p.w, p.w_bytes);
   const __amdgpu_buffer_rsrc_t wr1 = make_rsrc(p.w_lo, p.w_bytes);
   const __amdgpu_buffer_rsrc_t wr2 = make_rsrc(p.w_lo2, p.w_bytes);
-  ALoader<AV, CBIG, LHSDIL, RP> al;
+  ALoader<AV, CBIG, LHSDIL, RP, 2, KW> al;
   al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
 #pragma unroll
   for (int v = 0; v < BV; ++v) {
-    const int j = n0 + (tid >> 3) + RP * v;
+    const int j = n0 + tid / CPR + RP * v;
     b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
   }
   f32x4 acc[MI][NI];
@@ -141,61 +162,64 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk_all = p.Kpad / BK;
-  const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's k-steps
+  const int nk_all = p.Kpad / KW;
+  const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's slots
+  constexpr int WROWS = 64 / CPR;  // LDS rows one wave instruction fills
   auto issue = [&](int stage, int kl) {
     const int kt = kb + kl;
     uint32_t off[AV];
     al.offsets(p, kt, chunk, off);  // k-steps are issued strictly in order
-    char* sa = smem + stage * STAGE + wid * 8 * 128;
+    char* sa = smem + stage * STAGE + wid * WROWS * RB;
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
-      glds16(xr0, sa + RP * v * 128, off[v]);
-      glds16(xr1, sa + AIMG + RP * v * 128, off[v]);
-      glds16(xr2, sa + 2 * AIMG + RP * v * 128, off[v]);
+      glds16(xr0, sa + RP * v * RB, off[v]);
+      glds16(xr1, sa + AIMG + RP * v * RB, off[v]);
+      glds16(xr2, sa + 2 * AIMG + RP * v * RB, off[v]);
     }
-    char* sb = smem + stage * STAGE + 3 * AIMG + wid * 8 * 128;
+    char* sb = smem + stage * STAGE + 3 * AIMG + wid * WROWS * RB;
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
-      const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u;
-      glds16(wr0, sb + RP * v * 128, o);
-      glds16(wr1, sb + BIMG + RP * v * 128, o);
-      glds16(wr2, sb + 2 * BIMG + RP * v * 128, o);
+      const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * (uint32_t)RB;
+      glds16(wr0, sb + RP * v * RB, o);
+      glds16(wr1, sb + BIMG + RP * v * RB, o);
+      glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
     }
   };
   if (kb > 0) al.seek(p, kb);
   EpiPrefetch<WM, WN, TM, TN, BNB, true> pre;
   pre.load_shift(p, n0, wn, lane);
-  constexpr size_t PARAM_OFF = p3_param_off<BM, BN, WM>();
+  constexpr size_t PARAM_OFF = p3_param_off<BM, BN, WM, KW, NST>();
   if constexpr (BNB) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
-  const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS_P3;
+  const bool early = BNB && S == 1 && nk * KW <= EARLY_EPI_KSTEPS_P3 * 64;
   if (early) pre.load(p, 0, m0, n0, tid);
-  // Two-slot ring with EARLY RELEASE: a slot is refilled as soon as every wave holds its fragments
-  // in registers (second barrier), not after the MFMAs, so during the k-step's MFMAs the DMA of
-  // the next TWO k-steps is in flight (the 6x MFMA time of two stages covers the L2 / HBM latency
-  // that one stage does not).
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  P3Frags<TM, TN> fr;
+#pragma unroll
+  for (int s = 0; s < NST; ++s)
+    if (s < nk) issue(s, s);
+  P3Frags<TM, TN, KW / 32> fr;
   for (int kt = 0; kt < nk; ++kt) {
-    // slot kt has landed for this thread once at most the next slot's loads are outstanding;
+    // slot kt has landed for this thread once at most the later slots' loads are outstanding;
     // the barrier publishes every thread's DMA
-    if (kt + 1 < nk)
+    const int ahead = min(NST - 1, nk - 1 - kt);
+    if (ahead >= 3)
+      wait_vmcnt<(NST >= 4 ? 3 : 0) * LOADS>();
+    else if (ahead == 2)
+      wait_vmcnt<(NST >= 3 ? 2 : 0) * LOADS>();
+    else if (ahead == 1)
       wait_vmcnt<LOADS>();
     else
       wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const char* sb = smem + (kt & 1) * STAGE;
-    p3_read<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG), fr, wm,
-                            wn, lane);
-    if (kt + 2 < nk) {
+    const char* sb = smem + (kt % NST) * STAGE;
+    p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG),
+                                fr, wm, wn, lane);
+    if (kt + NST < nk) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
       __builtin_amdgcn_s_barrier();                        // ... and every other wave's
       asm volatile("" ::: "memory");
-      issue(kt & 1, kt + 2);
+      issue(kt % NST, kt + NST);
     }
-    p3_mma<TM, TN>(fr, acc);
+    p3_mma<TM, TN, KW / 32>(fr, acc);
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
   if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
@@ -208,57 +232,74 @@ static void p3_set_lds_once(K kern) {
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-template <int WM, int WN, int TM, int TN, bool BNB>
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool BNB>
 static void launch_p3(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   const int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
-  const int ksteps = (p.Kpad / 64 + p.splits - 1) / p.splits;
-  const size_t lds_main = (ksteps > 1 ? 2 : 1) * p3_stage_bytes<BM, BN>();
+  const int slots = (p.Kpad / KW + p.splits - 1) / p.splits;
+  const size_t lds_main = (size_t)(slots < NST ? slots : NST) * p3_stage_bytes<BM, BN, KW>();
   const size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-  if (BNB) lds = p3_param_off<BM, BN, WM>() + bnb_param_lds(BN);
+  if (BNB) lds = p3_param_off<BM, BN, WM, KW, NST>() + bnb_param_lds(BN);
   const bool cbig = (p.C % 64) == 0;
   const bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, true, false, BNB>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, true, true, BNB>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, false, false, BNB>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, false, true, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, true, false, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB>), dim3(tiles), dim3(NT), lds,
+                       st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, true, true, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB>), dim3(tiles), dim3(NT), lds,
+                       st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, false, false, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB>), dim3(tiles), dim3(NT), lds,
+                       st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, false, true, BNB>), dim3(tiles), dim3(NT), lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB>), dim3(tiles), dim3(NT), lds,
+                       st, p);
 }
 
-// p3 cfg: 0 128x64 (2x2 waves of 64x32), 1 64x128 (2x2 of 32x64), 2 128x64 (4x2 of 32x32),
-// 3 64x128 (2x4 of 32x32), 4 64x64 (2x2 of 32x32), 5 128x64 (4x1 of 32x64), 6 64x128 (1x4 of 64x32)
-constexpr int N_P3_CFG = 7;
+// p3 cfg (block tile, waves x wave tile, slot depth, ring slots):
+//   64-deep slots, 2 slots:  0 128x64 (2x2 of 64x32), 1 64x128 (2x2 of 32x64), 2 128x64 (4x2 of 32x32),
+//                            3 64x128 (2x4 of 32x32), 4 64x64 (2x2 of 32x32), 5 128x64 (4x1 of 32x64),
+//                            6 64x128 (1x4 of 64x32)
+//   32-deep slots:           7 128x128 (2x4 of 64x32, 3 slots), 8 128x128 (4x2 of 32x64, 3 slots),
+//                            9 128x128 (2x2 of 64x64, 3 slots), 10 256x128 (4x2 of 64x64, 2 slots),
+//                            11 128x256 (2x4 of 64x64, 2 slots), 12 64x128 (2x2 of 32x64, 4 slots),
+//                            13 128x64 (2x2 of 64x32, 4 slots)
+constexpr int N_P3_CFG = 14;
 int p3_tile_m(int cfg) {
-  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64};
+  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 128};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 128;
 }
 int p3_tile_n(int cfg) {
-  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128};
+  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256, 128, 64};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 64;
 }
 
 template <bool BNB>
 static void launch_p3_cfg(const ConvParams& p, int cfg, hipStream_t st) {
   switch (cfg) {
-    case 1: launch_p3<2, 2, 32, 64, BNB>(p, st); break;
-    case 2: launch_p3<4, 2, 32, 32, BNB>(p, st); break;
-    case 3: launch_p3<2, 4, 32, 32, BNB>(p, st); break;
-    case 4: launch_p3<2, 2, 32, 32, BNB>(p, st); break;
-    case 5: launch_p3<4, 1, 32, 64, BNB>(p, st); break;
-    case 6: launch_p3<1, 4, 64, 32, BNB>(p, st); break;
-    default: launch_p3<2, 2, 64, 32, BNB>(p, st); break;
+    case 1: launch_p3<2, 2, 32, 64, 64, 2, BNB>(p, st); break;
+    case 2: launch_p3<4, 2, 32, 32, 64, 2, BNB>(p, st); break;
+    case 3: launch_p3<2, 4, 32, 32, 64, 2, BNB>(p, st); break;
+    case 4: launch_p3<2, 2, 32, 32, 64, 2, BNB>(p, st); break;
+    case 5: launch_p3<4, 1, 32, 64, 64, 2, BNB>(p, st); break;
+    case 6: launch_p3<1, 4, 64, 32, 64, 2, BNB>(p, st); break;
+    case 7: launch_p3<2, 4, 64, 32, 32, 3, BNB>(p, st); break;
+    case 8: launch_p3<4, 2, 32, 64, 32, 3, BNB>(p, st); break;
+    case 9: launch_p3<2, 2, 64, 64, 32, 3, BNB>(p, st); break;
+    case 10: launch_p3<4, 2, 64, 64, 32, 2, BNB>(p, st); break;
+    case 11: launch_p3<2, 4, 64, 64, 32, 2, BNB>(p, st); break;
+    case 12: launch_p3<2, 2, 32, 64, 32, 4, BNB>(p, st); break;
+    case 13: launch_p3<2, 2, 64, 32, 32, 4, BNB>(p, st); break;
+    default: launch_p3<2, 2, 64, 32, 64, 2, BNB>(p, st); break;
   }
 }
 

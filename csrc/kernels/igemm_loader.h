@@ -13,8 +13,11 @@ namespace hcb {
 // the CBIG path (C % 64 == 0: a 64-deep k-step never straddles a tap) the per-row work is
 // two adds, two unsigned compares and a select; invalid rows carry h0 = INT_MIN/2 so the
 // bounds test rejects them without a separate flag.
-template <int AV, bool CBIG, bool LHSDIL, int RP = 32, int ESZ = 2>  // RP: rows per load pass (threads / 8)
-struct ALoader {                                                       // ESZ: bytes per element (4: fp32 x)
+// RP: rows per load pass (threads / (KW / 8)); ESZ: bytes per element (4: fp32 x); KW: channels per
+// k-step (64, or 32 for the half-depth stages of the plane GEMMs, conv_p3.hip)
+template <int AV, bool CBIG, bool LHSDIL, int RP = 32, int ESZ = 2, int KW = 64>
+struct ALoader {
+  static constexpr int LPR = KW / 8;  // lanes per tile row
   int h0[AV], w0[AV];
   int rowoff[AV];  // byte offset of (pixel of tap (0,0)) * ldx + lane chunk, may be negative
   int pix[AV];     // generic path: first pixel of the image, -1 = row beyond M
@@ -27,7 +30,7 @@ struct ALoader {                                                       // ESZ: b
     tc = 0;
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
-      int m = m0 + (tid >> 3) + RP * v;
+      int m = m0 + tid / LPR + RP * v;
       if (m < p.M) {
         int n = m / PQ, r = m - n * PQ;
         int pp = r / p.Q, qq = r - pp * p.Q;
@@ -45,7 +48,7 @@ struct ALoader {                                                       // ESZ: b
   }
   // position the incremental tap state at k-step kt0 (a split-K block's first k-step)
   __device__ __forceinline__ void seek(const ConvParams& p, int kt0) {
-    const int k0 = kt0 * 64;
+    const int k0 = kt0 * KW;
     const int tap = k0 / p.C;
     tc = k0 - tap * p.C;
     tr = tap / p.S;
@@ -63,8 +66,8 @@ struct ALoader {                                                       // ESZ: b
         const bool ok = tap_ok && (unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W;
         off[v] = ok ? (uint32_t)(rowoff[v] + uoff) : HCB_OOB;
       }
-      // advance to the next 64-channel slab
-      tc += 64;
+      // advance to the next KW-channel slab
+      tc += KW;
       if (tc >= p.C) {
         tc = 0;
         if (++ts == p.S) {
@@ -73,7 +76,7 @@ struct ALoader {                                                       // ESZ: b
         }
       }
     } else {
-      const int k0 = kt * 64;
+      const int k0 = kt * KW;
       int tap, c, r, s;
       if constexpr (CBIG) {
         tap = k0 / p.C;

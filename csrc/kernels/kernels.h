@@ -237,8 +237,10 @@ struct WPackEntry {  // all int64 so the table is a plain int64 tensor [n][9]
   int64_t tr_off;    // bf16 transposed-flipped [C][Kpad_t] offset, -1 = skip
   int64_t Nout, R, S, C, Kpad, Kpad_t;
 };
+// lo: 0 the bf16 pack (the hi plane), 1 / 2 the mid / lo plane alone, 3 all three planes (plane
+// stride pstride elements: the fp32 path's pack planes in one pass)
 void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
-                        int n_entries, int64_t max_work, hipStream_t st, int lo = 0);
+                        int n_entries, int64_t max_work, hipStream_t st, int lo = 0, int64_t pstride = 0);
 // dropout on bf16 activations (n % 8 == 0): mask = 1 bit per element packed 8 per byte
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
                         const int64_t* step, hipStream_t st);
@@ -262,7 +264,7 @@ void launch_preprocess_images(const uint8_t* src, const int64_t* desc, int B, vo
 // ---------------------------------------------------------------- space-to-depth stem (stem.hip)
 void launch_stem_s2d(const uint16_t* x, int N, int H, int W, int ldx, uint16_t* out, int Hs, int Ws, int pad,
                      hipStream_t st);
-void launch_stem_wfold(const float* w, int cout, int cs, uint16_t* wp, hipStream_t st);
+void launch_stem_wfold(const float* w, int cout, int cs, uint16_t* wp, hipStream_t st, bool p3 = false);
 void launch_stem_wgrad_unfold(const float* dwp, int cout, int cs, float* dw, hipStream_t st);
 
 // ---------------------------------------------------------------- gradient buckets

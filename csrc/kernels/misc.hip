@@ -180,9 +180,14 @@ __device__ __forceinline__ float wp_val(float v, int lo) {
   const float r = v - bf2f(f2bf(v));
   return lo == 1 ? r : r - bf2f(f2bf(r));
 }
+// P3 (the fp32 path): all three bf16 planes hi / mid / lo of every pack in one pass over the
+// masters, plane t at pack + t * pstride
+template <bool P3>
 __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restrict__ master,
                                                           uint16_t* __restrict__ pack,
-                                                          const WPackEntry* __restrict__ ents, int lo) {
+                                                          const WPackEntry* __restrict__ ents, int lo,
+                                                          int64_t pstride) {
+  constexpr int NPL = P3 ? 3 : 1;
   __shared__ float tile[64][65];
   const WPackEntry e = ents[blockIdx.y];
   const int R = (int)e.R, S = (int)e.S, C = (int)e.C, Nout = (int)e.Nout;
@@ -200,12 +205,16 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
         const int j = i / K8, k8 = i - j * K8;
         const float4* s4 = reinterpret_cast<const float4*>(src + (size_t)j * K + k8 * 8);
         const float4 a = s4[0], b = s4[1];
-        u32x4 v;
-        v[0] = pack2(wp_val(a.x, lo), wp_val(a.y, lo));
-        v[1] = pack2(wp_val(a.z, lo), wp_val(a.w, lo));
-        v[2] = pack2(wp_val(b.x, lo), wp_val(b.y, lo));
-        v[3] = pack2(wp_val(b.z, lo), wp_val(b.w, lo));
-        *reinterpret_cast<u32x4*>(pack + e.pack_off + (size_t)j * Kpad + k8 * 8) = v;
+#pragma unroll
+        for (int t = 0; t < NPL; ++t) {
+          const int l = P3 ? t : lo;
+          u32x4 v;
+          v[0] = pack2(wp_val(a.x, l), wp_val(a.y, l));
+          v[1] = pack2(wp_val(a.z, l), wp_val(a.w, l));
+          v[2] = pack2(wp_val(b.x, l), wp_val(b.y, l));
+          v[3] = pack2(wp_val(b.z, l), wp_val(b.w, l));
+          *reinterpret_cast<u32x4*>(pack + t * pstride + e.pack_off + (size_t)j * Kpad + k8 * 8) = v;
+        }
       }
       continue;
     }
@@ -224,27 +233,32 @@ __global__ __launch_bounds__(256) void weight_pack_kernel(const float* __restric
       if (kk0 + row < Nout && c0 + c4 < C)
         v = *reinterpret_cast<const float4*>(src + ((size_t)((kk0 + row) * R + (R - 1 - rr)) * S + (S - 1 - ss)) * C +
                                              c0 + c4);
-      tile[row][c4] = wp_val(v.x, lo);
-      tile[row][c4 + 1] = wp_val(v.y, lo);
-      tile[row][c4 + 2] = wp_val(v.z, lo);
-      tile[row][c4 + 3] = wp_val(v.w, lo);
+      tile[row][c4] = P3 ? v.x : wp_val(v.x, lo);  // P3: the raw value, split at the pack stage
+      tile[row][c4 + 1] = P3 ? v.y : wp_val(v.y, lo);
+      tile[row][c4 + 2] = P3 ? v.z : wp_val(v.z, lo);
+      tile[row][c4 + 3] = P3 ? v.w : wp_val(v.w, lo);
     }
     __syncthreads();
     {
       const int c = tid >> 2, k16 = (tid & 3) * 16;
       if (c0 + c < C) {
         const size_t o = (size_t)e.tr_off + (size_t)(c0 + c) * Kpad_t + (size_t)tap * Nout + kk0 + k16;
-        if (kk0 + k16 + 16 <= Nout && (o & 7) == 0) {
-          u32x4 v0, v1;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v0[q] = pack2(tile[k16 + 2 * q][c], tile[k16 + 2 * q + 1][c]);
-            v1[q] = pack2(tile[k16 + 8 + 2 * q][c], tile[k16 + 9 + 2 * q][c]);
+        for (int t = 0; t < NPL; ++t) {
+          auto tv = [&](int k) { return P3 ? wp_val(tile[k][c], t) : tile[k][c]; };
+          uint16_t* pk = pack + t * pstride;
+          if (kk0 + k16 + 16 <= Nout && (o & 7) == 0) {
+            u32x4 v0, v1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v0[q] = pack2(tv(k16 + 2 * q), tv(k16 + 2 * q + 1));
+              v1[q] = pack2(tv(k16 + 8 + 2 * q), tv(k16 + 9 + 2 * q));
+            }
+            reinterpret_cast<u32x4*>(pk + o)[0] = v0;
+            reinterpret_cast<u32x4*>(pk + o)[1] = v1;
+          } else {
+            for (int q = 0; q < 16 && kk0 + k16 + q < Nout; ++q) pk[o + q] = f2act(tv(k16 + q));
           }
-          reinterpret_cast<u32x4*>(pack + o)[0] = v0;
-          reinterpret_cast<u32x4*>(pack + o)[1] = v1;
-        } else {
-          for (int q = 0; q < 16 && kk0 + k16 + q < Nout; ++q) pack[o + q] = f2act(tile[k16 + q][c]);
         }
       }
     }
@@ -545,11 +559,15 @@ void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st) {
   hipLaunchKernelGGL(l2norm_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, out);
 }
 void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* entries_dev,
-                        int n_entries, int64_t max_work, hipStream_t st, int lo) {
+                        int n_entries, int64_t max_work, hipStream_t st, int lo, int64_t pstride) {
   int64_t units = max_work / 2048 + 2;  // A chunks are 2048 elements, B tiles 4096
   int gx = units > 1024 ? 1024 : (int)units;
-  hipLaunchKernelGGL(weight_pack_kernel, dim3(gx, n_entries), dim3(256), 0, st, master, pack,
-                     entries_dev, lo);
+  if (lo == 3)  // all three planes, plane stride pstride
+    hipLaunchKernelGGL(weight_pack_kernel<true>, dim3(gx, n_entries), dim3(256), 0, st, master, pack, entries_dev, 0,
+                       pstride);
+  else
+    hipLaunchKernelGGL(weight_pack_kernel<false>, dim3(gx, n_entries), dim3(256), 0, st, master, pack, entries_dev,
+                       lo, (int64_t)0);
 }
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
                         const int64_t* step, hipStream_t st) {

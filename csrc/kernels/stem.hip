@@ -44,6 +44,8 @@ __global__ __launch_bounds__(256) void stem_s2d_kernel(const uint16_t* __restric
 
 // folded bf16 GEMM operand W'[cout][256] from the fp32 master w[cout][7][7][cs] (cs = stored
 // channels, the first 3 real)
+// P3 (fp32 path): the folded weight as bf16 hi / mid / lo planes (plane stride cout * 256)
+template <bool P3>
 __global__ __launch_bounds__(256) void stem_wfold_kernel(const float* __restrict__ w, int cout, int cs,
                                                          uint16_t* __restrict__ wp) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -54,7 +56,15 @@ __global__ __launch_bounds__(256) void stem_wfold_kernel(const float* __restrict
   const int r = 2 * i + a - 1, s = 2 * j + b - 1;
   float v = 0.f;
   if ((unsigned)r < 7u && (unsigned)s < 7u && c < 3) v = w[((k * 7 + r) * 7 + s) * cs + c];
-  wp[t] = f2act(v);
+  if constexpr (P3) {
+    const int n = cout * 256;
+    const float h = bf2f(f2bf(v)), rr = v - h, m = bf2f(f2bf(rr));
+    wp[t] = f2bf(v);
+    wp[n + t] = f2bf(rr);
+    wp[2 * n + t] = f2bf(rr - m);
+  } else {
+    wp[t] = f2act(v);
+  }
 }
 
 // dw[cout][7][7][cs] += dW'[cout][256] mapped back (each real weight has exactly one folded slot)
@@ -75,8 +85,11 @@ void launch_stem_s2d(const uint16_t* x, int N, int H, int W, int ldx, uint16_t* 
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(stem_s2d_kernel, dim3((int)g), dim3(256), 0, st, x, N, H, W, ldx, out, Hs, Ws, pad);
 }
-void launch_stem_wfold(const float* w, int cout, int cs, uint16_t* wp, hipStream_t st) {
-  hipLaunchKernelGGL(stem_wfold_kernel, dim3((cout * 256 + 255) / 256), dim3(256), 0, st, w, cout, cs, wp);
+void launch_stem_wfold(const float* w, int cout, int cs, uint16_t* wp, hipStream_t st, bool p3) {
+  if (p3)
+    hipLaunchKernelGGL(stem_wfold_kernel<true>, dim3((cout * 256 + 255) / 256), dim3(256), 0, st, w, cout, cs, wp);
+  else
+    hipLaunchKernelGGL(stem_wfold_kernel<false>, dim3((cout * 256 + 255) / 256), dim3(256), 0, st, w, cout, cs, wp);
 }
 void launch_stem_wgrad_unfold(const float* dwp, int cout, int cs, float* dw, hipStream_t st) {
   hipLaunchKernelGGL(stem_wgrad_unfold_kernel, dim3((cout * 147 + 255) / 256), dim3(256), 0, st, dwp, cout, cs, dw);

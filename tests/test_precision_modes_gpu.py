@@ -21,7 +21,7 @@ def test_fp32_gpu_matches_fp32_cpu_step():
     assert mg.native and mg.image_channels == 8
     assert torch.equal(mg.ps.master.cpu(), mc.ps.master)
     img_c, lab_c = synthetic_batch(mc, 4, seed=3)
-    img_c = (img_c - 127.0) / 60.0
+    img_c[..., :3] = (img_c[..., :3] - 127.0) / 60.0  # the padded channels stay zero (the S2D stem's contract)
     tg = Trainer(mg, 4, constant_lr(0.05))
     tc = Trainer(mc, 4, constant_lr(0.05))
     lg = float(tg.step(img_c.cuda(), lab_c.cuda()))
@@ -29,7 +29,9 @@ def test_fp32_gpu_matches_fp32_cpu_step():
     torch.cuda.synchronize()
     assert abs(lg - lc) <= 1e-4 * abs(lc), (lg, lc)
     # whole-network gradients of a random-init BN net are chaotic in the rounding order
-    # (bf16x6 MFMA vs oneDNN accumulation): compared as a whole, not elementwise
+    # (bf16x6 MFMA vs oneDNN accumulation): compared as a whole, not elementwise. Measured floor of
+    # this configuration on the CPU alone: fp32 vs fp64 2.9%, fp32 vs fp32 with the input scaled by
+    # (1 + 1e-7) 2.7% (the GPU step lands at ~3.6%)
     gg, gc = mg.ps.grad.cpu(), mc.ps.grad
     assert (gg - gc).norm() / gc.norm() < 5e-2
     assert float(gg @ gc / (gg.norm() * gc.norm())) > 0.999

@@ -58,6 +58,51 @@ def test_s2d_weight_gradient_maps_back_to_7x7():
     assert torch.all(st.w.grad[..., 3:] == 0), "padded input channels must get no gradient"
 
 
+@pytest.fixture
+def fp32_stem():
+    from azure_hc_intel_tf_amd.nn.layers import StemS2D, set_gpu_compute_dtype
+    from azure_hc_intel_tf_amd.nn.params import ParamStore
+    import azure_hc_intel_tf_amd.ops.functional as Fn
+
+    set_gpu_compute_dtype(torch.float32)
+    Fn.set_f32_native(True)
+    ps = ParamStore(seed=3)
+    st = StemS2D(ps, "conv0", (64, 64, 8), 64, relu=True, need_dx=False, logical_cin=3)
+    ps.finalize(torch.device("cuda"), pack_lo=True)
+    ps.repack()
+    yield st
+    Fn.set_f32_native(False)
+    set_gpu_compute_dtype(torch.bfloat16)
+
+
+def test_s2d_fp32_planes_match_fp64(fp32_stem):
+    """fp32 path: the image split into planes and folded (three planes as one 3N batch), the folded
+    weight as planes, the bf16x6 plane GEMM -- forward and weight gradient to fp32 accuracy."""
+    import azure_hc_intel_tf_amd.ops.functional as Fn
+
+    st = fp32_stem
+    torch.manual_seed(2)
+    x = torch.zeros(2, 64, 64, 8, device="cuda")
+    x[..., :3] = torch.randn(2, 64, 64, 3, device="cuda")
+    P, Q, C = st.out_shape
+    xf = st.fold_input(x)
+    assert Fn.is_planes(xf)
+    z = torch.empty(2, P, Q, C, device="cuda")
+    Fn.conv_forward(xf, st.fold_spec, st._folded_weight(x.device), st.w.data, z)
+    xd = x[..., :3].permute(0, 3, 1, 2).double().cpu()
+    wd = st.w.data[..., :3].permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(xd, wd, stride=2, padding=3)
+    got = z.permute(0, 3, 1, 2).double().cpu()
+    assert ((got - ref).norm() / ref.norm()).item() < 3e-6
+    dz = torch.randn(2, P, Q, C, device="cuda")
+    st.w.grad.zero_()
+    st._wgrad(Fn.to_planes(dz), xf)
+    torch.cuda.synchronize()
+    gref = torch.nn.grad.conv2d_weight(xd, (64, 3, 7, 7), dz.permute(0, 3, 1, 2).double().cpu(), stride=2, padding=3)
+    g = st.w.grad[..., :3].permute(0, 3, 1, 2).double().cpu()
+    assert ((g - gref).norm() / gref.norm()).item() < 3e-6
+
+
 def test_resnet_uses_s2d_stem_and_trains():
     from azure_hc_intel_tf_amd.models import create_model
     from azure_hc_intel_tf_amd.nn.layers import StemS2D

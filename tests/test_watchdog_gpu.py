@@ -17,13 +17,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
-def _run(extra):
+def _run(extra, steps=3):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
     env.update(HOROVOD_STALL_CHECK_TIME_SECONDS="1", HCB_COMM_DEBUG_SLEEP_MS="2500", HCB_BENCH_COMM_PROFILE="0")
     env.update(extra)
     return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "trivial", "--batch_size", "8",
-                           "--force_dp_path", "--steps", "3", "--warmup", "3", "--no_tune"],
-                          env=env, capture_output=True, text=True, timeout=150)
+                           "--compute_dtype", "bf16", "--force_dp_path", "--steps", str(steps), "--warmup", "3",
+                           "--no_tune"], env=env, capture_output=True, text=True, timeout=150)
 
 
 def test_watchdog_warns_on_a_stalled_replayed_step():
@@ -38,3 +38,14 @@ def test_stall_abort_exits_nonzero_on_the_graph_path():
     assert r.returncode != 0, r.stderr[-3000:]
     assert "aborting" in r.stderr, r.stderr[-3000:]
     assert '"n_gpus"' not in r.stdout  # no result line from an aborted run
+
+
+def test_no_false_stall_when_the_host_runs_ahead():
+    """Healthy but slow replayed steps queued without any host sync (the host runs many steps ahead
+    of the device) for longer than the stall threshold: every step's own watch event completes in
+    turn, so the watchdog sees progress and neither warns nor aborts (one re-recorded event would be
+    overwritten before completing and report a stall of a healthy job)."""
+    r = _run({"HOROVOD_STALL_CHECK_TIME_SECONDS": "3", "HCB_STALL_ABORT_SECONDS": "4", "HCB_COMM_DEBUG_SLEEP_MS": "500"},
+             steps=12)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "[hcb watchdog]" not in r.stderr, r.stderr[-3000:]

@@ -2,7 +2,11 @@
 """Per-layer timing of the hand-written conv kernels (fwd / dgrad / wgrad) of a model, with
 MIOpen (torch conv, channels_last bf16) timed on the same shapes as a comparison point.
 
-    python tools/conv_bench.py --model resnet50 --batch 64 [--no_miopen] [--tune]
+    python tools/conv_bench.py --model resnet50 --batch 64 [--no_miopen] [--tune] [--fp32]
+
+--fp32: the reference-precision kernels (bf16-plane operands, bf16x6 GEMMs, conv_p3.hip) at their
+tuned configs; TF columns are fp32 FLOP/s and "mfma%" the share of the 2.5 PF bf16 dense peak the
+six MFMA products run at.
 """
 import argparse
 import json
@@ -39,9 +43,12 @@ def main():
     ap.add_argument("--no_miopen", action="store_true")
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--fp32", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda")
-    m = create_model(a.model, device=dev)
+    m = create_model(a.model, device=dev, compute_dtype="fp32" if a.fp32 else None)
+    if a.fp32:
+        a.no_miopen = True
     m.ps.repack()
     autotune.load_cache()
     if a.tune:
@@ -65,9 +72,15 @@ def main():
         N = a.batch
         H, W, C = l.in_shape
         P, Q, K = l.out_shape
-        x = torch.randn(N, H, W, C, device=dev).bfloat16()
-        dz = torch.randn(N, P, Q, K, device=dev).bfloat16()
-        y = torch.empty(N, P, Q, K, device=dev, dtype=torch.bfloat16)
+        if a.fp32:
+            m.activate()
+            x = Fn.to_planes(torch.randn(N, H, W, C, device=dev))
+            dz = Fn.to_planes(torch.randn(N, P, Q, K, device=dev))
+            y = torch.empty(N, P, Q, K, device=dev)
+        else:
+            x = torch.randn(N, H, W, C, device=dev).bfloat16()
+            dz = torch.randn(N, P, Q, K, device=dev).bfloat16()
+            y = torch.empty(N, P, Q, K, device=dev, dtype=torch.bfloat16)
         slab, T, cfg = Fn.conv_stats_slab(x.shape, s, dev)
         r = {"layer": l.name, "in": list(l.in_shape), "out": list(l.out_shape), "k": [s.kh, s.kw], "stride": s.sh,
              "count": 1}
@@ -76,7 +89,7 @@ def main():
         dw = torch.zeros(K, s.K, device=dev)
         r["wgrad"] = tm(lambda: Fn.conv_wgrad(dz, x, s, dw))
         if l.need_dx:
-            dx = torch.zeros(N, H, W, C, device=dev, dtype=torch.bfloat16)
+            dx = torch.zeros(N, H, W, C, device=dev, dtype=torch.float32 if a.fp32 else torch.bfloat16)
             r["dgrad"] = tm(lambda: Fn.conv_dgrad(dz, s, l.pack.tr, None, dx, False))
         else:
             r["dgrad"] = 0.0
@@ -105,11 +118,20 @@ def main():
             tot[k] += r[k]
         seen[key] = r
         rows.append(r)
-        mi = lambda k: f"{r.get('mi_' + k, 0) or 0:7.1f}"
-        print(f"{l.name:28s} {str(l.in_shape):16s}->{str(l.out_shape):16s} k{s.kh}x{s.kw}/{s.sh} "
-              f"fwd {r['fwd']:7.1f}us ({r['tf_fwd']:5.0f}TF) mi {mi('fwd')} | "
-              f"dgrad {r['dgrad']:7.1f} mi {mi('dgrad')} | wgrad {r['wgrad']:7.1f}us ({r['tf_wgrad']:5.0f}TF) "
-              f"mi {mi('wgrad')}", flush=True)
+        if a.fp32:
+            M = N * P * Q
+            r["cfg"] = [Fn.p3_plan(M, K, s.K, s.kh * s.kw), Fn.wgrad_p3_plan(K, s.K, M, s.kh * s.kw)]
+            pk = lambda t: f"{6 * flops / t / 1e6 / 2500 * 100:4.0f}%" if t else "   -"
+            print(f"{l.name:28s} {str(l.in_shape):16s}->{str(l.out_shape):16s} k{s.kh}x{s.kw}/{s.sh} "
+                  f"fwd {r['fwd']:7.1f}us ({r['tf_fwd']:4.0f}TF {pk(r['fwd'])}) | dgrad {r['dgrad']:7.1f}us "
+                  f"({pk(r['dgrad'])}) | wgrad {r['wgrad']:7.1f}us ({r['tf_wgrad']:4.0f}TF {pk(r['wgrad'])}) "
+                  f"cfg {r['cfg']}", flush=True)
+        else:
+            mi = lambda k: f"{r.get('mi_' + k, 0) or 0:7.1f}"
+            print(f"{l.name:28s} {str(l.in_shape):16s}->{str(l.out_shape):16s} k{s.kh}x{s.kw}/{s.sh} "
+                  f"fwd {r['fwd']:7.1f}us ({r['tf_fwd']:5.0f}TF) mi {mi('fwd')} | "
+                  f"dgrad {r['dgrad']:7.1f} mi {mi('dgrad')} | wgrad {r['wgrad']:7.1f}us ({r['tf_wgrad']:5.0f}TF) "
+                  f"mi {mi('wgrad')}", flush=True)
     print("TOTAL per step (us): " + json.dumps({k: round(v, 1) for k, v in tot.items()}))
     if a.json:
         with open(a.json, "w") as f:

@@ -128,20 +128,36 @@ static void timeline_and_pool() {
   CHECK(destroyed == (int)pool.created() && pool.free_count() == 0);
 }
 
-// submitter (caller's thread) + fake device + watchdog, sharing one WatchState under a mutex
+// submitter (caller's thread) + fake device + watchdog, sharing one WatchState under a mutex; each
+// enqueued cycle records its own fake event (the device sequence number it completes at)
 static void watch_protocol() {
   WatchState ws;
   ws.watch.configure(0.25, 0.8);
   std::mutex mu;
   FakeDevice dev;
-  std::atomic<int64_t> watch_ev{0};  // the device sequence the single watch event stands for
+  std::vector<int64_t> ev_target;  // token -> device sequence (guarded by mu)
+  std::vector<int64_t> ev_free;
   std::atomic<int64_t> dev_target{0};
   std::atomic<bool> stop{false}, warned{false}, aborted{false};
-  auto done = [&] { return dev.reached.load() >= watch_ev.load(); };
+  auto done = [&](int64_t t) { return dev.reached.load() >= ev_target[t]; };
+  auto release = [&](int64_t t) { ev_free.push_back(t); };
+  auto record = [&](int64_t seq) {
+    int64_t t;
+    if (!ev_free.empty()) {
+      t = ev_free.back();
+      ev_free.pop_back();
+      ev_target[t] = seq;
+    } else {
+      ev_target.push_back(seq);
+      t = (int64_t)ev_target.size() - 1;
+    }
+    return t;
+  };
+  std::atomic<int> dev_delay_us{20};
   std::thread device([&] {
     while (!stop.load()) {
       if (!dev.stalled.load() && dev.reached.load() < dev_target.load()) dev.reached.fetch_add(1);
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      std::this_thread::sleep_for(std::chrono::microseconds(dev_delay_us.load()));
     }
   });
   std::thread watchdog([&] {
@@ -150,7 +166,7 @@ static void watch_protocol() {
       const auto now = clk::now();
       {
         std::lock_guard<std::mutex> lk(mu);
-        ws.poll_quiet(now, 0.05, done);
+        ws.poll_quiet(now, 0.05, done, release);
       }
       double waited = 0;
       const StallWatch::Action a = ws.watch.evaluate(now, &waited);
@@ -161,31 +177,52 @@ static void watch_protocol() {
   // healthy phase: 400 cycles (eager reductions and step marks alternately)
   for (int i = 0; i < 400; ++i) {
     std::lock_guard<std::mutex> lk(mu);
-    ws.enter(done);
+    ws.enter(done, release);
     const int64_t t = dev_target.fetch_add(1) + 1;  // the work of this cycle
-    watch_ev = t;                                    // the watch event recorded behind it
-    ws.enqueue(i, i % 2 == 1);
+    ws.enqueue(i, i % 2 == 1, record(t));            // its own event recorded behind it
     if (i % 50 == 0) {
       std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
   }
-  // drain: the watchdog completes the last cycle once the caller is quiet
-  const auto t0 = clk::now();
-  while (ws.watch.completed() < ws.watch.enqueued() && clk::now() - t0 < std::chrono::seconds(5))
-    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  // drain: the watchdog completes the last cycles once the caller is quiet
+  auto drain = [&] {
+    const auto t0 = clk::now();
+    while (ws.watch.completed() < ws.watch.enqueued() && clk::now() - t0 < std::chrono::seconds(5))
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  };
+  drain();
   CHECK(ws.watch.completed() == ws.watch.enqueued());
   CHECK(!warned.load() && !aborted.load());
   {
     std::lock_guard<std::mutex> lk(mu);
     CHECK(ws.marks == 200 && ws.first_mark == 2 && ws.is_graph_cycle(400) && !ws.is_graph_cycle(1));
+    CHECK(ws.pending.empty() && ev_free.size() == ev_target.size());
   }
+  // the caller runs far ahead of a slow device (graph replays never sync) for longer than the warn
+  // threshold: the device keeps completing cycles, so no stall may be reported (with one
+  // re-recorded event the earlier cycles were never seen completing)
+  dev_delay_us = 2000;
+  const auto ta = clk::now();
+  for (int i = 0; clk::now() - ta < std::chrono::milliseconds(600); ++i) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      ws.enter(done, release);
+      const int64_t t = dev_target.fetch_add(1) + 1;
+      ws.enqueue(400 + i, true, record(t));
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(300));  // 6-7x faster than the device
+  }
+  CHECK(!warned.load() && !aborted.load());
+  dev_delay_us = 20;
+  drain();
+  CHECK(ws.watch.completed() == ws.watch.enqueued());
+  CHECK(!warned.load() && !aborted.load());
   // stall phase: the device stops; one more cycle must warn, then abort
   dev.stalled = true;
   {
     std::lock_guard<std::mutex> lk(mu);
-    ws.enter(done);
-    watch_ev = dev_target.fetch_add(1) + 1;
-    ws.enqueue(400, true);
+    ws.enter(done, release);
+    ws.enqueue(100000, true, record(dev_target.fetch_add(1) + 1));
   }
   const auto t1 = clk::now();
   while (!aborted.load() && clk::now() - t1 < std::chrono::seconds(5))
