@@ -437,7 +437,9 @@ def set_tuned(table: dict) -> None:
 _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
              7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
              13: (128, 64)}
-_WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64)}
+# wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles)
+_WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),
+              6: (128, 128), 7: (128, 128), 8: (256, 128), 9: (128, 256), 10: (128, 128), 11: (128, 64)}
 
 
 def fwd3_key(M: int, N: int, K: int, taps: int = 1):
@@ -449,9 +451,10 @@ def wgrad3_key(Nout: int, K: int, M: int, taps: int = 1):
 
 
 def p3_candidates(M: int, N: int, K: int):
-    """(cfg, splits) worth timing for an fp32 (Planes) forward / data-grad GEMM: every tile, and
-    split-K while the grid is below ~1 workgroup per CU (one fits per CU: 144 KB of LDS) and every
-    split keeps >= 3 k-steps."""
+    """(cfg, splits) worth timing for an fp32 (Planes) forward / data-grad GEMM: every tile, with
+    split-K factors that bring the grid close to whole rounds of the 256 CUs (one workgroup fits per
+    CU: 144 KB of LDS) -- a 196-tile layer leaves 60 CUs idle, 4 splits run it in 3.06 rounds --
+    while every split keeps >= 2 64-deep k-steps."""
     out = []
     ksteps = math.ceil(K / 64)
     for c, (bm, bn) in _P3_TILES.items():
@@ -459,8 +462,8 @@ def p3_candidates(M: int, N: int, K: int):
             continue
         tiles = math.ceil(M / bm) * math.ceil(N / bn)
         out.append((c, 1))
-        for s in (2, 3, 4, 6, 8):
-            if tiles * (s - 1) >= N_CU or ksteps // s < 3 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
+        for s in (2, 3, 4, 5, 6, 8, 12, 16):
+            if tiles * s > 6 * N_CU or ksteps // s < 2 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
                 break
             out.append((c, s))
     return out
@@ -487,6 +490,9 @@ def wgrad_p3_candidates(Nout: int, K: int, M: int):
     ksteps = math.ceil(M / 64)
     out = []
     for c, (bm, bn) in _WP3_TILES.items():
+        if (Nout <= 64 and bm > 64) or (K <= 64 and bn > 64) or (Nout < 256 and bm > 128) \
+                or (K < 256 and bn > 128):
+            continue
         tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
         for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
             if s > 1 and ksteps // s < 2:

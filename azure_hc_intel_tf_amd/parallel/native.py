@@ -136,6 +136,41 @@ class Communicator:
             pass
 
 
+def xgmi_probe(n: int, rank: int) -> torch.Tensor:
+    """Rank-dependent probe values whose fp32 sums are exact in any order (small integers / 2)."""
+    i = torch.arange(n, dtype=torch.float32)
+    return ((i % 97) + 7 * (rank + 1) + (i % 5) * rank) * 0.5
+
+
+def validate_xgmi(one_shot, rccl, agree_min, n: int, rank: int, device=None) -> str:
+    """Startup cross-check of the one-shot xGMI allreduce against RCCL (every rank, collectively):
+    reduce the same probe with both; the sums are exact, so they must match bitwise. Returns
+    "on", or "disabled(<reason>)" when ANY rank saw a mismatch, a peer time-out (the kernel's
+    bounded wait poisons with NaN and raises the error flag) or an exception. ``one_shot(t)`` /
+    ``rccl(t)`` reduce in place (and for one_shot: return nonzero on a device error);
+    ``agree_min(int) -> int`` is the MIN over ranks, so every rank takes the same decision."""
+    reason = ""
+    a = xgmi_probe(n, rank)
+    if device is not None:
+        a = a.to(device)
+    b = a.clone()
+    try:
+        if one_shot(a):
+            reason = "peer timeout"
+    except Exception as e:  # noqa: BLE001 -- any failure disables the path, never the job
+        reason = f"{type(e).__name__}: {e}"[:120]
+    rccl(b)  # every rank takes part in the RCCL reduction whatever its one-shot did
+    if device is not None:
+        torch.cuda.synchronize(device)
+    if not reason and not torch.equal(a.cpu(), b.cpu()):
+        bad = int((a.cpu() != b.cpu()).sum())
+        reason = f"mismatch vs RCCL in {bad}/{n} probe elements"
+    ok = agree_min(0 if reason else 1)
+    if ok:
+        return "on"
+    return f"disabled({reason or 'failed on another rank'})"
+
+
 class NativeReducer:
     """Flat-buffer gradient allreduce on the C++ RCCL engine."""
 
@@ -155,13 +190,52 @@ class NativeReducer:
         self.graph_safe = os.environ.get("HCB_GRAPH_COMM", "1") == "1"
         self.force = force
         self._buckets = None
-        # opt-in one-shot xGMI allreduce for small fp32 ranges (single node only)
+        # opt-in one-shot xGMI allreduce for small fp32 ranges (single node only), validated
+        # against RCCL at startup; ``xgmi_status`` ("off" | "on" | "disabled(reason)") goes into
+        # the bench JSON's comm block
         self.xgmi, self.xgmi_bytes = None, int(os.environ.get("HCB_XGMI_BYTES", "0"))
+        self.xgmi_status = "off"
         local = int(os.environ.get("LOCAL_WORLD_SIZE", self.comm.world))
-        if self.xgmi_bytes > 0 and not self.compress and 1 < self.comm.world == local:
-            from .xgmi import XgmiAllreduce
+        if self.xgmi_bytes > 0:
+            if self.compress:
+                self.xgmi_status = "disabled(compressed wire: the one-shot sums fp32 only)"
+            elif self.comm.world == 1:
+                self.xgmi_status = "disabled(single rank)"
+            elif self.comm.world != local:
+                self.xgmi_status = "disabled(multi-node: xGMI peers are node-local)"
+            else:
+                self._enable_xgmi()
 
-            self.xgmi = XgmiAllreduce(capacity_bytes=self.xgmi_bytes)
+    def _enable_xgmi(self):
+        from .xgmi import XgmiAllreduce
+
+        def agree_min(v: int) -> int:
+            t = torch.tensor([v], dtype=torch.int32, device=torch.cuda.current_device())
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return int(t.item())
+
+        xg = None
+        try:
+            xg = XgmiAllreduce(capacity_bytes=self.xgmi_bytes)
+            one_shot = lambda t: (xg.allreduce_(t), xg.error())[1]  # noqa: E731
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"[:120]
+
+            def one_shot(t):
+                raise RuntimeError(err)
+        n = max(64, min(self.xgmi_bytes // 4, 1 << 18))
+        self.xgmi_status = validate_xgmi(one_shot, self.comm.allreduce_, agree_min, n, self.comm.rank,
+                                         device=torch.cuda.current_device())
+        if self.xgmi_status == "on":
+            self.xgmi = xg
+        else:
+            if xg is not None:
+                xg.close()
+            if self.comm.rank == 0:
+                import sys
+
+                print(f"[hcb] HCB_XGMI_BYTES={self.xgmi_bytes}: one-shot xGMI allreduce {self.xgmi_status}; "
+                      "all ranges go through RCCL", file=sys.stderr)
 
     def _bucket_table(self, numel):
         # whole-buffer form: buckets from the END of the buffer first (the engine cuts each

@@ -226,28 +226,56 @@ class Trainer:
             self._check_ranges.append((off, n))
 
     def _check_verify(self):
-        """comm_check: blocking reference allreduce of the snapshots vs the engine's result."""
+        """comm_check: blocking reference allreduce of the snapshots vs the engine's result.
+
+        fp32 wire: every element within 1e-5 of its range's max |value| (summation order only).
+        16-bit wire (bf16 / fp16 compression): each rank's input and each of RCCL's world - 1
+        partial sums is rounded to the wire format, i.e. by at most ``ulp`` (bf16 2^-8, fp16 2^-11)
+        of sum_r |g_r| -- and the engine (cut per segment) and the reference (whole buffer) may sum
+        in different orders. So the bound is per ELEMENT: |engine - ref| <= 2 * ulp * world *
+        S_i, S_i = sum over ranks of |g_r,i| (an exact fp32 allreduce of |snapshot|). A range whose
+        reduction missed or doubled one rank's contribution is off by |g_r,i| ~ S_i / world for
+        most elements, far above that bound."""
         ref = self._check
-        self.reducer.allreduce_(ref)
-        g = self.ps.grad
-        worst = 0.0
-        # tolerance relative to the range's max |value|: fp32 on the wire -> 1e-5; a 16-bit wire
-        # format rounds every partial sum, and the engine (cut per segment) and the reference
-        # (whole buffer) may split buckets differently, so RCCL's summation order differs: a few
-        # 16-bit ulps per rank (bf16 2^-8, fp16 2^-11)
         wire = getattr(self.reducer, "compression", None) or {1: "bf16", 2: "fp16"}.get(
             getattr(self.reducer, "compress", 0))
         ulp = {"bf16": 2.0 ** -8, "fp16": 2.0 ** -11}.get(wire)
-        tol = 1e-5 if ulp is None else 4.0 * ulp * max(self.world, 2)
+        mag = None
+        if ulp is not None:
+            mag = ref.abs()
+            if self.world > 1:
+                import torch.distributed as dist
+
+                if not dist.is_initialized():
+                    raise RuntimeError("comm check with a compressed wire needs torch.distributed for the "
+                                       "per-element bound (sum over ranks of |g|)")
+                dist.all_reduce(mag)
+        self.reducer.allreduce_(ref)
+        g = self.ps.grad
+        worst = 0.0
         for off, n in self._check_ranges:
+            if n == 0:
+                continue
             a, b = g[off:off + n], ref[off:off + n]
-            scale = float(b.abs().max()) if n else 0.0
-            err = float((a - b).abs().max()) if n else 0.0
-            worst = max(worst, err / (scale + 1e-30))
-            if err > tol * scale + 1e-20:
+            d = (a - b).abs()
+            if mag is None:
+                scale = float(b.abs().max())
+                err = float(d.max())
+                rel, bad = err / (scale + 1e-30), err > 1e-5 * scale + 1e-20
+            else:
+                # fp16 also flushes what underflows its range: 2^-24 per rank, absolute
+                floor = self.world * 2.0 ** -24 if wire == "fp16" else 1e-30
+                bound = 2.0 * ulp * max(self.world, 1) * mag[off:off + n] + floor
+                ratio = d / bound
+                i = int(ratio.argmax())
+                rel, bad = float(ratio[i]) * 2.0 * ulp * max(self.world, 1), bool(ratio[i] > 1.0)
+                err, scale = float(d[i]), float(mag[off + i])
+            worst = max(worst, rel)
+            if bad:
                 raise RuntimeError(f"comm check: reduced gradient range [{off}, {off + n}) differs from the blocking "
-                                   f"reference allreduce by {err:.3e} (max |ref| {scale:.3e}): the overlapped "
-                                   "reduction read the gradients before backward had finished writing them")
+                                   f"reference allreduce by {err:.3e} (reference magnitude {scale:.3e}): the "
+                                   "overlapped reduction read the gradients before backward had finished writing "
+                                   "them")
         self.comm_check_errs.append(worst)
         self._check_ranges = []
 

@@ -353,6 +353,9 @@ def main(argv=None):
             "world": world,
             "rccl_nranks": rccl_nranks,
             "comm": main_r["comm"],
+            # one-shot xGMI allreduce (HCB_XGMI_BYTES): "off" | "on" (passed the startup cross-check
+            # against RCCL) | "disabled(reason)"
+            "xgmi": getattr(reducer, "xgmi_status", "off"),
         }
         for r in results[1:]:
             d = r["dtype"]

@@ -195,11 +195,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
 #pragma unroll
   for (int s = 0; s < NST; ++s)
     if (s < nk) issue(s, s);
-  P3Frags<TM, TN, KW / 32> fr;
-  for (int kt = 0; kt < nk; ++kt) {
-    // slot kt has landed for this thread once at most the later slots' loads are outstanding;
-    // the barrier publishes every thread's DMA
-    const int ahead = min(NST - 1, nk - 1 - kt);
+  // wait until at most `ahead` later slots' DMA is outstanding for this thread
+  auto wait_ahead = [&](int ahead) {
     if (ahead >= 3)
       wait_vmcnt<(NST >= 4 ? 3 : 0) * LOADS>();
     else if (ahead == 2)
@@ -208,18 +205,57 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
       wait_vmcnt<LOADS>();
     else
       wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* sb = smem + (kt % NST) * STAGE;
-    p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG),
-                                fr, wm, wn, lane);
-    if (kt + NST < nk) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
-      __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+  };
+  auto read = [&](int k, P3Frags<TM, TN, KW / 32>& f) {
+    const char* sb = smem + (k % NST) * STAGE;
+    p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG), f,
+                                wm, wn, lane);
+  };
+  // two register fragment sets when they fit (PIPE): slot k+1's fragment reads are in flight
+  // while slot k's MFMAs run, and ONE barrier per slot both publishes slot k+1's DMA and retires
+  // every wave's reads of slot k (which is refilled right after it); otherwise one set, read,
+  // then a second barrier before the refill
+  constexpr int FREGS = (MI + NI) * 3 * 4 * (KW / 32), AREGS = MI * NI * 4;
+  constexpr bool PIPE = 2 * FREGS + AREGS <= (NT == 512 ? 200 : 400) && !(BNB && NT == 512);
+  if constexpr (PIPE) {
+    P3Frags<TM, TN, KW / 32> fr[2];
+    if (nk > 0) {
+      wait_ahead(min(NST - 1, nk - 1));
+      __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      issue(kt % NST, kt + NST);
+      read(0, fr[0]);
     }
-    p3_mma<TM, TN, KW / 32>(fr, acc);
+    auto body = [&](int k, P3Frags<TM, TN, KW / 32>& cur, P3Frags<TM, TN, KW / 32>& nxt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot k are done
+      if (k + 1 < nk) wait_ahead(min(NST - 2, nk - 2 - k));  // slot k+1 landed for this thread
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (k + NST < nk) issue(k % NST, k + NST);
+      if (k + 1 < nk) read(k + 1, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      p3_mma<TM, TN, KW / 32>(cur, acc);
+    };
+    for (int k = 0; k < nk; k += 2) {
+      body(k, fr[0], fr[1]);
+      if (k + 1 < nk) body(k + 1, fr[1], fr[0]);
+    }
+  } else {
+    P3Frags<TM, TN, KW / 32> fr;
+    for (int kt = 0; kt < nk; ++kt) {
+      // slot kt has landed for this thread once at most the later slots' loads are outstanding;
+      // the barrier publishes every thread's DMA
+      wait_ahead(min(NST - 1, nk - 1 - kt));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read(kt, fr);
+      if (kt + NST < nk) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+        __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+        asm volatile("" ::: "memory");
+        issue(kt % NST, kt + NST);
+      }
+      p3_mma<TM, TN, KW / 32>(fr, acc);
+    }
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
   if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
@@ -321,14 +357,18 @@ __device__ __forceinline__ int p3w_swz(int row) {
   else return ((row >> 1) & 1) | ((row >> 2) & 2);
 }
 
-template <int WM, int WN, int TM, int TN, int NST, bool CBIG>
+// BK: pixel rows (reduction depth) per ring slot, 64 or 32 (32: half the LDS per slot, so 128x128 /
+// 256x128 block tiles fit); NST slots with early release; PIPE (when two fragment sets fit the
+// register budget): slot k+1's transposed fragment reads in flight during slot k's MFMAs, one
+// barrier per slot.
+template <int WM, int WN, int TM, int TN, int NST, int BK, bool CBIG>
 __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams p) {
-  constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
-  constexpr int MI = TM / 16, NI = TN / 16;
-  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM, BN = WN * TN;
+  constexpr int MI = TM / 16, NI = TN / 16, KS = BK / 32;
+  constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int ACPR = BM / 8, BCPR = BN / 8;        // 16-byte chunks per LDS row
   constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;  // LDS rows filled by one wave instruction
-  constexpr int AI = BK / ARPI / NW, BI = BK / BRPI / NW;  // instructions per wave per plane and stage
+  constexpr int AI = BK / ARPI / NW, BI = BK / BRPI / NW;  // instructions per wave per plane and slot
   constexpr int LOADS = 3 * (AI + BI);
   constexpr int AIMG = BK * BM * 2, BIMG = BK * BN * 2;
   constexpr int STAGE = 3 * (AIMG + BIMG);
@@ -346,10 +386,10 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
   const int tile = bid % ntiles, split = bid / ntiles;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int i0 = tm * BM, j0 = tn * BN;
-  const int nkt = (p.M + BK - 1) / BK;
-  const int kt_begin = split * p.ksteps_per_split;
-  const int kt_end = min(kt_begin + p.ksteps_per_split, nkt);
-  if (kt_begin >= kt_end) return;  // uniform per workgroup
+  // the host plans splits in 64-row k-steps; this block's pixel rows [mbeg, mend)
+  const int mbeg = split * p.ksteps_per_split * 64;
+  const int mend = min(mbeg + p.ksteps_per_split * 64, p.M);
+  if (mbeg >= mend) return;  // uniform per workgroup
 
   const char* db = reinterpret_cast<const char*>(p.dy);
   const char* xb = reinterpret_cast<const char*>(p.x);
@@ -391,14 +431,14 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
     b_ok[v] = col < p.K;
   }
 
-  auto issue = [&](int stage, int kt) {
-    const int mb = kt * BK;
+  auto issue = [&](int stage, int kl) {
+    const int mb = mbeg + kl * BK;
     char* sA = smem + stage * STAGE;
     char* sB = sA + 3 * AIMG;
 #pragma unroll
     for (int v = 0; v < AI; ++v) {
       const int m = mb + a_row[v];
-      const uint32_t off = (a_col[v] < p.Nout && m < p.M) ? (uint32_t)(m * p.ldy + a_col[v]) * 2u : HCB_OOB;
+      const uint32_t off = (a_col[v] < p.Nout && m < mend) ? (uint32_t)(m * p.ldy + a_col[v]) * 2u : HCB_OOB;
       char* d = sA + (wid * AI + v) * ARPI * BM * 2;
       glds16(dyr0, d, off);
       glds16(dyr1, d + AIMG, off);
@@ -408,7 +448,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
     for (int v = 0; v < BI; ++v) {
       const int m = mb + b_row[v];
       uint32_t off = HCB_OOB;
-      if (b_ok[v] && m < p.M) {
+      if (b_ok[v] && m < mend) {
         const int n = (int)fdiv((uint32_t)m, p.fd_pq);
         const int rem = m - n * p.P * p.Q;
         const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
@@ -444,56 +484,74 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
     short8 t = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
     return __builtin_bit_cast(u32x4, t);
   };
-
-  // NST-slot ring with early release (see conv_igemm_p3_kernel): a slot is refilled once every wave
-  // holds its fragments in registers, so NST k-steps of DMA are in flight during the MFMAs
-  const int nk = kt_end - kt_begin;
+  using Fr = P3Frags<TM, TN, KS>;
+  auto read = [&](int k, Fr& f) {
+    const char* Ab = smem + (k % NST) * STAGE;
+    const char* Bb = Ab + 3 * AIMG;
 #pragma unroll
-  for (int s = 0; s < NST; ++s)
-    if (s < nk) issue(s, kt_begin + s);
-  u32x4 a[2][3][MI], b[2][3][NI];
-  for (int k = 0; k < nk; ++k) {
-    const int ahead = min(NST - 1, nk - 1 - k);  // later slots still in flight
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) f.a[ks][t][i] = frag(Ab + t * AIMG, BM, ks * 32 + 8 * g, wm * TM + i * 16);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) f.b[ks][t][j] = frag(Bb + t * BIMG, BN, ks * 32 + 8 * g, wn * TN + j * 16);
+    }
+  };
+  auto wait_ahead = [&](int ahead) {
     if (ahead >= 2)
       wait_vmcnt<(NST >= 3 ? 2 : 0) * LOADS>();
     else if (ahead == 1)
       wait_vmcnt<LOADS>();
     else
       wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* Ab = smem + (k % NST) * STAGE;
-    const char* Bb = Ab + 3 * AIMG;
+  };
+
+  const int nk = (mend - mbeg + BK - 1) / BK;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) a[ks][t][i] = frag(Ab + t * AIMG, BM, ks * 32 + 8 * g, wm * TM + i * 16);
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) b[ks][t][j] = frag(Bb + t * BIMG, BN, ks * 32 + 8 * g, wn * TN + j * 16);
-    }
-    if (k + NST < nk) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
-      __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+  for (int s = 0; s < NST; ++s)
+    if (s < nk) issue(s, s);
+  constexpr int FREGS = (MI + NI) * 3 * 4 * KS, AREGS = MI * NI * 4;
+  constexpr bool PIPE = 2 * FREGS + AREGS <= (NT == 512 ? 168 : 400);
+  if constexpr (PIPE) {
+    Fr fr[2];
+    if (nk > 0) {
+      wait_ahead(min(NST - 1, nk - 1));
+      __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      issue(k % NST, kt_begin + k + NST);
+      read(0, fr[0]);
     }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {  // small terms first
-          acc[i][j] = mfma_bf16(a[ks][2][i], b[ks][0][j], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][2][j], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][1][j], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[ks][1][i], b[ks][0][j], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][1][j], acc[i][j]);
-          acc[i][j] = mfma_bf16(a[ks][0][i], b[ks][0][j], acc[i][j]);
-        }
+    auto body = [&](int k, Fr& cur, Fr& nxt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot k are done
+      if (k + 1 < nk) wait_ahead(min(NST - 2, nk - 2 - k));  // slot k+1 landed for this thread
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (k + NST < nk) issue(k % NST, k + NST);
+      if (k + 1 < nk) read(k + 1, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      p3_mma<TM, TN, KS>(cur, acc);
+    };
+    for (int k = 0; k < nk; k += 2) {
+      body(k, fr[0], fr[1]);
+      if (k + 1 < nk) body(k + 1, fr[1], fr[0]);
+    }
+  } else {
+    Fr fr;
+    for (int k = 0; k < nk; ++k) {
+      wait_ahead(min(NST - 1, nk - 1 - k));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read(k, fr);
+      if (k + NST < nk) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+        __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+        asm volatile("" ::: "memory");
+        issue(k % NST, k + NST);
+      }
+      p3_mma<TM, TN, KS>(fr, acc);
+    }
   }
   __syncthreads();  // every wave is done with the ring before the epilogue reuses LDS
 
@@ -508,7 +566,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
         Cs[(wm * TM + i * 16 + g * 4 + e) * LDC + wn * TN + j * 16 + li] = acc[i][j][e];
   __syncthreads();
   const bool sole = gridDim.x == ntiles;
-  for (int idx = tid; idx < BM * BN; idx += NW * 64) {
+  for (int idx = tid; idx < BM * BN; idx += NT) {
     const int row = idx / BN, col = idx - row * BN;
     const int gi = i0 + row, gj = j0 + col;
     if (gi < p.Nout && gj < p.K) {
@@ -521,46 +579,55 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
   }
 }
 
-template <int WM, int WN, int TM, int TN, int NST>
+template <int WM, int WN, int TM, int TN, int NST, int BK>
 static void wlaunch_p3(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
-  const size_t lds_main = (size_t)NST * 3 * 64 * (BM + BN) * 2;
+  const size_t lds_main = (size_t)NST * 3 * BK * (BM + BN) * 2;
   const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   static bool once = false;
   if (!once) {
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, true>);
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, false>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false>);
     once = true;
   }
   const dim3 grid(tiles * splits);
   if ((p.C % BN) == 0)
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, true>), grid, dim3(WM * WN * 64), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true>), grid, dim3(WM * WN * 64), lds, st, p);
   else
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, false>), grid, dim3(WM * WN * 64), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false>), grid, dim3(WM * WN * 64), lds, st, p);
 }
 
-// p3 wgrad cfg: 0 128x64 (2x2 waves of 64x32), 1 64x128 (2x2 of 32x64), 2 64x64 (2x2 of 32x32, NST 3),
-// 3 128x64 (4x2 of 32x32), 4 64x128 (2x4 of 32x32), 5 64x64 (2x2 of 32x32, NST 2)
-constexpr int N_WP3_CFG = 6;
+// p3 wgrad cfg (block tile, waves x wave tile, slots x pixel rows):
+//   0 128x64 (2x2 of 64x32, 2x64), 1 64x128 (2x2 of 32x64, 2x64), 2 64x64 (2x2 of 32x32, 3x64),
+//   3 128x64 (4x2 of 32x32, 2x64), 4 64x128 (2x4 of 32x32, 2x64), 5 64x64 (2x2 of 32x32, 2x64),
+//   6 128x128 (2x4 of 64x32, 3x32), 7 128x128 (4x2 of 32x64, 3x32), 8 256x128 (4x2 of 64x64, 2x32),
+//   9 128x256 (2x4 of 64x64, 2x32), 10 128x128 (2x2 of 64x64, 3x32), 11 128x64 (2x2 of 64x32, 3x32)
+constexpr int N_WP3_CFG = 12;
 int wgrad_p3_tile_m(int cfg) {
-  static const int t[N_WP3_CFG] = {128, 64, 64, 128, 64, 64};
+  static const int t[N_WP3_CFG] = {128, 64, 64, 128, 64, 64, 128, 128, 256, 128, 128, 128};
   return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
 }
 int wgrad_p3_tile_n(int cfg) {
-  static const int t[N_WP3_CFG] = {64, 128, 64, 64, 128, 64};
+  static const int t[N_WP3_CFG] = {64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64};
   return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
 }
 
 void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st) {
   switch (cfg) {
-    case 0: wlaunch_p3<2, 2, 64, 32, 2>(p, splits, st); break;
-    case 1: wlaunch_p3<2, 2, 32, 64, 2>(p, splits, st); break;
-    case 3: wlaunch_p3<4, 2, 32, 32, 2>(p, splits, st); break;
-    case 4: wlaunch_p3<2, 4, 32, 32, 2>(p, splits, st); break;
-    case 5: wlaunch_p3<2, 2, 32, 32, 2>(p, splits, st); break;
-    default: wlaunch_p3<2, 2, 32, 32, 3>(p, splits, st); break;
+    case 0: wlaunch_p3<2, 2, 64, 32, 2, 64>(p, splits, st); break;
+    case 1: wlaunch_p3<2, 2, 32, 64, 2, 64>(p, splits, st); break;
+    case 3: wlaunch_p3<4, 2, 32, 32, 2, 64>(p, splits, st); break;
+    case 4: wlaunch_p3<2, 4, 32, 32, 2, 64>(p, splits, st); break;
+    case 5: wlaunch_p3<2, 2, 32, 32, 2, 64>(p, splits, st); break;
+    case 6: wlaunch_p3<2, 4, 64, 32, 3, 32>(p, splits, st); break;
+    case 7: wlaunch_p3<4, 2, 32, 64, 3, 32>(p, splits, st); break;
+    case 8: wlaunch_p3<4, 2, 64, 64, 2, 32>(p, splits, st); break;
+    case 9: wlaunch_p3<2, 4, 64, 64, 2, 32>(p, splits, st); break;
+    case 10: wlaunch_p3<2, 2, 64, 64, 3, 32>(p, splits, st); break;
+    case 11: wlaunch_p3<2, 2, 64, 32, 3, 32>(p, splits, st); break;
+    default: wlaunch_p3<2, 2, 32, 32, 3, 64>(p, splits, st); break;
   }
 }
 

@@ -48,7 +48,9 @@ template <int WM, int WN, int TM, int TN, bool BNB, bool F32 = false>
 struct EpiPrefetch {
   static constexpr int BM = WM * TM, BN = WN * TN, SEGS = BN / 8, NT = WM * WN * 64;
   static constexpr int ITER = BM * SEGS / NT;
-  static constexpr int CH = BNB ? (ITER < BNB_PREFETCH_CH ? ITER : BNB_PREFETCH_CH) : 1;
+  // (fp32: two segments per chunk -- its operands are twice the registers)
+  static constexpr int CHMAX = F32 ? BNB_PREFETCH_CH / 2 : BNB_PREFETCH_CH;
+  static constexpr int CH = BNB ? (ITER < CHMAX ? ITER : CHMAX) : 1;
   u32x4 pr[CH], pz[CH], py[CH];
   u32x4 pr2[F32 ? CH : 1], pz2[F32 ? CH : 1];
   // forward GEMMs: the BN statistic shift of each of the lane's accumulator columns, loaded

@@ -55,7 +55,7 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     (incl. the stride-phase and strided-1x1 remap forms) and weight grad (incl. split-K), every
     plane-GEMM tile config (conv_p3.hip cfg 0-6) and in-launch split-K; fp32 inputs are split into
     planes by the ops themselves. cfg 7-13: 32-deep slots (64-byte LDS rows) and 128x128 / 256x128
-    block tiles."""
+    block tiles; weight-grad cfg 6-11: 32-deep slots, up to 256x128 / 128x256."""
     cin, cout, k, s, pad, H = case
     spec, p, pk, ps = _conv(cin, cout, k, s, pad)
     assert Fn.lo_pack(pk.pack) is not None and Fn.lo_pack(pk.tr) is not None
@@ -78,7 +78,7 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 3e-6
     if isinstance(cfg, tuple):  # split-K case: the weight-gradient configs once
         return
-    for wcfg in ((2, 1), (0, 4), (3, 8), (1, 2), (4, 1), (5, 2)):
+    for wcfg in ((2, 1), (0, 4), (3, 8), (1, 2), (4, 1), (5, 2), (6, 1), (7, 2), (8, 1), (9, 3), (10, 4), (11, 2)):
         dw = torch.zeros(cout, spec.K, device=DEV)
         Fn.conv_wgrad(dz, x, spec, dw, cfg=wcfg)
         assert rel_err(dw.view(cout, k, k, cin), wr.grad.permute(0, 2, 3, 1)) < 3e-6, wcfg

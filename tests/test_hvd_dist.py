@@ -385,9 +385,10 @@ def test_rccl_env_plumbing(monkeypatch):
     assert w["NCCL_ALGO"] == "Ring" and w["NCCL_MIN_NCHANNELS"] == "16" and w["RANK"] == "1"
 
 
-def _comm_check(hvd):
+def _comm_check(hvd, compression=None):
     """The overlapped-allreduce race detector (Trainer comm_check) passes on a correct engine and
-    fails loudly when a reduction reads gradients that are not final."""
+    fails loudly when a reduction reads gradients that are not final -- also with a 16-bit wire,
+    whose bound is per element (2 ulp * world * sum_r |g_r|), not relative to a range's max."""
     from azure_hc_intel_tf_amd.models import create_model
     from azure_hc_intel_tf_amd.parallel import make_reducer
     from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
@@ -396,17 +397,20 @@ def _comm_check(hvd):
     hvd.broadcast_global_variables(m, 0)
     img, lab = synthetic_batch(m, 2, seed=hvd.rank())
     img = (img - 127) / 60
-    red = make_reducer("torch", bucket_bytes=1 << 20)
+    red = make_reducer("torch", compression=compression, bucket_bytes=1 << 20)
     t = Trainer(m, 2, constant_lr(0.01), reducer=red, world_size=hvd.size(), comm_check=True)
     assert t.overlap and not t.use_graph
     t.step(img, lab)
-    assert len(t.comm_check_errs) == 1 and t.comm_check_errs[0] < 1e-6
-    # a broken engine: every async range reduction sees this rank's gradients scaled by 2
+    assert len(t.comm_check_errs) == 1 and t.comm_check_errs[0] < (1e-6 if compression is None else 0.05)
+    # a broken engine: one range reduction per segment sees this rank's gradients scaled by 1.25
+    # (on rank 0 only, a quarter of one contribution: under the old range-max bound a bf16 wire let
+    # this through)
     real = red.allreduce_ranges_async_
 
     def stale(flat, ranges):
-        for off, n in ranges:
-            flat[off:off + n].mul_(2.0)
+        if hvd.rank() == 0:
+            off, n = ranges[0]
+            flat[off:off + n].mul_(1.25)
         return real(flat, ranges)
 
     red.allreduce_ranges_async_ = stale
@@ -420,3 +424,58 @@ def _comm_check(hvd):
 
 def test_comm_check_race_detector():
     run(2, _comm_check)
+
+
+def _comm_check_bf16(hvd):
+    _comm_check(hvd, "bf16")
+
+
+def test_comm_check_race_detector_bf16_wire():
+    run(2, _comm_check_bf16)
+
+
+def _xgmi_validation(hvd):
+    """The one-shot xGMI allreduce's startup cross-check (parallel/native.py validate_xgmi), with a
+    fake one-shot on gloo: a correct one-shot is turned on; a mismatch, a peer time-out or an
+    exception on ANY rank disables it on EVERY rank, with the reason."""
+    from azure_hc_intel_tf_amd.parallel.native import validate_xgmi, xgmi_probe
+
+    def agree_min(v):
+        t = torch.tensor([v], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item())
+
+    def rccl(t):
+        dist.all_reduce(t)
+
+    def exact(t):  # what a working one-shot computes, without a gloo collective of its own
+        t.copy_(sum(xgmi_probe(t.numel(), r) for r in range(hvd.size())))
+
+    good = lambda t: (exact(t), 0)[1]  # noqa: E731
+    assert validate_xgmi(good, rccl, agree_min, 4096, hvd.rank()) == "on"
+
+    def wrong_on_rank1(t):
+        exact(t)
+        if hvd.rank() == 1:
+            t[7] += 1.0
+        return 0
+
+    st = validate_xgmi(wrong_on_rank1, rccl, agree_min, 4096, hvd.rank())
+    assert st.startswith("disabled("), st
+    assert ("mismatch" in st) if hvd.rank() == 1 else ("another rank" in st), st
+    timeout = lambda t: (exact(t), 1)[1]  # noqa: E731
+    assert validate_xgmi(timeout, rccl, agree_min, 256, hvd.rank()) == "disabled(peer timeout)"
+
+    def boom_on_rank0(t):
+        if hvd.rank() == 0:
+            raise RuntimeError("hipIpcOpenMemHandle failed")
+        exact(t)
+        return 0
+
+    st = validate_xgmi(boom_on_rank0, rccl, agree_min, 256, hvd.rank())
+    assert st.startswith("disabled(RuntimeError: hipIpcOpenMemHandle" if hvd.rank() == 0 else
+                         "disabled(failed on another rank"), st
+
+
+def test_xgmi_startup_validation_disables_on_any_rank_failure():
+    run(2, _xgmi_validation)
