@@ -433,13 +433,16 @@ def set_tuned(table: dict) -> None:
 
 
 # ---- fp32 path (Planes operands, conv_p3.hip): its own tile sets and tuning keys
-# cfg -> block tile (conv_p3.hip): 0-6 64-deep two-slot rings, 7-13 32-deep slots (bigger tiles per CU)
+# cfg -> block tile (conv_p3.hip): 0-6 64-deep two-slot rings, 7-13 32-deep slots (bigger tiles per CU),
+# 14-17 32-deep slots sized for two / three workgroups per CU
 _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
              7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
-             13: (128, 64)}
-# wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles)
+             13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64)}
+# wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles),
+# 12-15 32-deep slots, two / three workgroups per CU
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),
-              6: (128, 128), 7: (128, 128), 8: (256, 128), 9: (128, 256), 10: (128, 128), 11: (128, 64)}
+              6: (128, 128), 7: (128, 128), 8: (256, 128), 9: (128, 256), 10: (128, 128), 11: (128, 64),
+              12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (64, 64)}
 
 
 def fwd3_key(M: int, N: int, K: int, taps: int = 1):

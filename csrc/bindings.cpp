@@ -964,7 +964,7 @@ hcb::ConvParams p3_params(const Tensor& x, const Tensor& w, const Tensor& w_lo, 
                           const c10::optional<Tensor>& stats, at::IntArrayRef g, int64_t cfg,
                           const c10::optional<Tensor>& stats_shift) {
   const int64_t xps = check_planes(x, "x");
-  TORCH_CHECK(cfg >= 0 && cfg < 14, "hcb.conv_p3: cfg 0..13");
+  TORCH_CHECK(cfg >= 0 && cfg < 18, "hcb.conv_p3: cfg 0..17");
   // conv_params validates geometry and byte ranges on plane 0 (a bf16 tensor of this build's type);
   // split-K is validated here against the p3 tiles
   std::vector<int64_t> g1(g.begin(), g.end());
@@ -1030,7 +1030,7 @@ void conv_wgrad_p3(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntA
                    int64_t splits) {
   TORCH_CHECK(g.size() == 17, "hcb.conv_wgrad_p3: geom must have 17 entries");
   const int64_t dps = check_planes(dy, "dy"), xps = check_planes(x, "x");
-  TORCH_CHECK(cfg >= 0 && cfg < 12, "hcb.conv_wgrad_p3: cfg 0..11");
+  TORCH_CHECK(cfg >= 0 && cfg < 16, "hcb.conv_wgrad_p3: cfg 0..15");
   check_f32(dw, "dw");
   hcb::WgradParams p{};
   p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];

@@ -111,8 +111,14 @@ constexpr int EARLY_EPI_KSTEPS_P3 = 2;
 // slot's MFMAs.
 // BNB: the fused BN-backward epilogue (data gradient producing a BN layer's dy: ReLU gating from the
 // hi plane of y or from z, sum(g) / sum(g * xhat) into p.bnb_acc), fp32 z / beta source / output
-template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool LHSDIL, bool BNB>
-__global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p) {
+// OCC: workgroups per CU the tile is built for (2: <= 80 KB of LDS and <= 512 / (2 * waves per SIMD)
+// registers per wave, so one workgroup's barrier / DMA waits are covered by the other's MFMAs)
+template <int OCC, int NW>
+constexpr int p3_regs_per_wave() {
+  return 512 / (OCC * NW / 4 > 0 ? OCC * NW / 4 : 1);
+}
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool LHSDIL, bool BNB, int OCC = 1>
+__global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, CPR = KW / 8, RB = KW * 2;  // threads; chunks and bytes per LDS row
@@ -216,7 +222,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_igemm_p3_kernel(ConvParams p
   // every wave's reads of slot k (which is refilled right after it); otherwise one set, read,
   // then a second barrier before the refill
   constexpr int FREGS = (MI + NI) * 3 * 4 * (KW / 32), AREGS = MI * NI * 4;
-  constexpr bool PIPE = 2 * FREGS + AREGS <= (NT == 512 ? 200 : 400) && !(BNB && NT == 512);
+  constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 56 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 56 : 400;
+  constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET && !(BNB && RBUDGET < 400);
   if constexpr (PIPE) {
     P3Frags<TM, TN, KW / 32> fr[2];
     if (nk > 0) {
@@ -268,7 +275,7 @@ static void p3_set_lds_once(K kern) {
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-template <int WM, int WN, int TM, int TN, int KW, int NST, bool BNB>
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool BNB, int OCC = 1>
 static void launch_p3(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   const int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
@@ -281,23 +288,23 @@ static void launch_p3(const ConvParams& p, hipStream_t st) {
   const bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB, OCC>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB, OCC>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB, OCC>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB, OCC>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB, OCC>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB, OCC>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB, OCC>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB, OCC>), dim3(tiles), dim3(NT), lds,
                        st, p);
 }
 
@@ -309,13 +316,16 @@ static void launch_p3(const ConvParams& p, hipStream_t st) {
 //                            9 128x128 (2x2 of 64x64, 3 slots), 10 256x128 (4x2 of 64x64, 2 slots),
 //                            11 128x256 (2x4 of 64x64, 2 slots), 12 64x128 (2x2 of 32x64, 4 slots),
 //                            13 128x64 (2x2 of 64x32, 4 slots)
-constexpr int N_P3_CFG = 14;
+//   32-deep, two per CU:     14 128x64 (2x2 of 64x32, 2 slots), 15 64x128 (2x2 of 32x64, 2 slots),
+//                            16 64x64 (2x2 of 32x32, 3 slots)
+//   32-deep, three per CU:   17 64x64 (2x2 of 32x32, 2 slots)
+constexpr int N_P3_CFG = 18;
 int p3_tile_m(int cfg) {
-  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 128};
+  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 128, 128, 64, 64, 64};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 128;
 }
 int p3_tile_n(int cfg) {
-  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256, 128, 64};
+  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256, 128, 64, 64, 128, 64, 64};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 64;
 }
 
@@ -335,6 +345,10 @@ static void launch_p3_cfg(const ConvParams& p, int cfg, hipStream_t st) {
     case 11: launch_p3<2, 4, 64, 64, 32, 2, BNB>(p, st); break;
     case 12: launch_p3<2, 2, 32, 64, 32, 4, BNB>(p, st); break;
     case 13: launch_p3<2, 2, 64, 32, 32, 4, BNB>(p, st); break;
+    case 14: launch_p3<2, 2, 64, 32, 32, 2, BNB, 2>(p, st); break;
+    case 15: launch_p3<2, 2, 32, 64, 32, 2, BNB, 2>(p, st); break;
+    case 16: launch_p3<2, 2, 32, 32, 32, 3, BNB, 2>(p, st); break;
+    case 17: launch_p3<2, 2, 32, 32, 32, 2, BNB, 3>(p, st); break;
     default: launch_p3<2, 2, 64, 32, 64, 2, BNB>(p, st); break;
   }
 }
@@ -361,8 +375,8 @@ __device__ __forceinline__ int p3w_swz(int row) {
 // 256x128 block tiles fit); NST slots with early release; PIPE (when two fragment sets fit the
 // register budget): slot k+1's transposed fragment reads in flight during slot k's MFMAs, one
 // barrier per slot.
-template <int WM, int WN, int TM, int TN, int NST, int BK, bool CBIG>
-__global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams p) {
+template <int WM, int WN, int TM, int TN, int NST, int BK, bool CBIG, int OCC = 1>
+__global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_kernel(WgradParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16, KS = BK / 32;
   constexpr int NW = WM * WN, NT = NW * 64;
@@ -514,7 +528,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
   for (int s = 0; s < NST; ++s)
     if (s < nk) issue(s, s);
   constexpr int FREGS = (MI + NI) * 3 * 4 * KS, AREGS = MI * NI * 4;
-  constexpr bool PIPE = 2 * FREGS + AREGS <= (NT == 512 ? 168 : 400);
+  constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 88 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 88 : 400;
+  constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET;
   if constexpr (PIPE) {
     Fr fr[2];
     if (nk > 0) {
@@ -579,7 +594,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_wgrad_p3_kernel(WgradParams 
   }
 }
 
-template <int WM, int WN, int TM, int TN, int NST, int BK>
+template <int WM, int WN, int TM, int TN, int NST, int BK, int OCC = 1>
 static void wlaunch_p3(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
@@ -588,29 +603,31 @@ static void wlaunch_p3(const WgradParams& p, int splits, hipStream_t st) {
   const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   static bool once = false;
   if (!once) {
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true>);
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC>);
     once = true;
   }
   const dim3 grid(tiles * splits);
   if ((p.C % BN) == 0)
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true>), grid, dim3(WM * WN * 64), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC>), grid, dim3(WM * WN * 64), lds, st, p);
   else
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false>), grid, dim3(WM * WN * 64), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC>), grid, dim3(WM * WN * 64), lds, st, p);
 }
 
 // p3 wgrad cfg (block tile, waves x wave tile, slots x pixel rows):
 //   0 128x64 (2x2 of 64x32, 2x64), 1 64x128 (2x2 of 32x64, 2x64), 2 64x64 (2x2 of 32x32, 3x64),
 //   3 128x64 (4x2 of 32x32, 2x64), 4 64x128 (2x4 of 32x32, 2x64), 5 64x64 (2x2 of 32x32, 2x64),
 //   6 128x128 (2x4 of 64x32, 3x32), 7 128x128 (4x2 of 32x64, 3x32), 8 256x128 (4x2 of 64x64, 2x32),
-//   9 128x256 (2x4 of 64x64, 2x32), 10 128x128 (2x2 of 64x64, 3x32), 11 128x64 (2x2 of 64x32, 3x32)
-constexpr int N_WP3_CFG = 12;
+//   9 128x256 (2x4 of 64x64, 2x32), 10 128x128 (2x2 of 64x64, 3x32), 11 128x64 (2x2 of 64x32, 3x32),
+//   two per CU: 12 128x64 (2x2 of 64x32, 2x32), 13 64x128 (2x2 of 32x64, 2x32), 14 64x64 (2x2 of 32x32, 3x32),
+//   three per CU: 15 64x64 (2x2 of 32x32, 2x32)
+constexpr int N_WP3_CFG = 16;
 int wgrad_p3_tile_m(int cfg) {
-  static const int t[N_WP3_CFG] = {128, 64, 64, 128, 64, 64, 128, 128, 256, 128, 128, 128};
+  static const int t[N_WP3_CFG] = {128, 64, 64, 128, 64, 64, 128, 128, 256, 128, 128, 128, 128, 64, 64, 64};
   return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
 }
 int wgrad_p3_tile_n(int cfg) {
-  static const int t[N_WP3_CFG] = {64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64};
+  static const int t[N_WP3_CFG] = {64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 64, 128, 64, 64};
   return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
 }
 
@@ -627,6 +644,10 @@ void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st) 
     case 9: wlaunch_p3<2, 4, 64, 64, 2, 32>(p, splits, st); break;
     case 10: wlaunch_p3<2, 2, 64, 64, 3, 32>(p, splits, st); break;
     case 11: wlaunch_p3<2, 2, 64, 32, 3, 32>(p, splits, st); break;
+    case 12: wlaunch_p3<2, 2, 64, 32, 2, 32, 2>(p, splits, st); break;
+    case 13: wlaunch_p3<2, 2, 32, 64, 2, 32, 2>(p, splits, st); break;
+    case 14: wlaunch_p3<2, 2, 32, 32, 3, 32, 2>(p, splits, st); break;
+    case 15: wlaunch_p3<2, 2, 32, 32, 2, 32, 3>(p, splits, st); break;
     default: wlaunch_p3<2, 2, 32, 32, 3, 64>(p, splits, st); break;
   }
 }

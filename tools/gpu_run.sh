@@ -13,6 +13,8 @@
 #   benchab:ENV      bench.py with and without ENV (e.g. benchab:HCB_X=0), interleaved 2 rounds
 #   prof[:args]      rocprofv3 --kernel-trace --stats of bench.py, summarised by tools/kstats.py
 #   pmc:COUNTERS     one rocprofv3 --pmc pass (counters comma-separated) over bench.py --steps 3
+#   dpsweep[:dtype]  forced 1-rank DP path (native RCCL engine): backward_segments stage|block x
+#                    HOROVOD_FUSION_THRESHOLD 32/64/128 MiB, against the single-graph step
 #   readme           tools/gpu_readme_numbers.sh
 #   race             tools/race_full.py (serialised vs async bitwise race check at full size)
 #   py:SCRIPT[,args] python SCRIPT args (a probe / diagnostic)
@@ -60,6 +62,17 @@ for step in "$@"; do
       (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $args --kernel-trace --output-format csv -d ${O}_pmc -o run \
         -- python $R/bench.py --steps 3 --warmup 2 > ${O}_pmc.log 2>&1) || fail pmc ${O}_pmc.log
       echo "pmc done: ${O}_pmc" ;;
+    dpsweep)
+      dt=${args:-fp32}
+      common="--compute_dtype $dt --secondary none --steps 40 --warmup 10"
+      timeout -k 10 400 python bench.py $common > ${O}_dp.json 2> ${O}_dp.err || fail dpsweep ${O}_dp.err
+      echo "single-graph $(python tools/jfield.py ${O}_dp.json value ms_per_step)" | tee ${O}_dpsweep.txt
+      for seg in stage block; do for mb in 32 64 128; do
+        HOROVOD_FUSION_THRESHOLD=$((mb << 20)) timeout -k 10 400 python bench.py $common --force_dp_path \
+          --backward_segments $seg > ${O}_dp.json 2> ${O}_dp.err || fail dpsweep ${O}_dp.err
+        echo "dp seg=$seg bucket=${mb}MiB $(python tools/jfield.py ${O}_dp.json value ms_per_step comm)" \
+          | tee -a ${O}_dpsweep.txt
+      done; done ;;
     readme)
       bash tools/gpu_readme_numbers.sh || fail readme ;;
     race)
