@@ -1,25 +1,13 @@
 """MI355X-native re-design of md-k-sarker/azure-hc-intel-tf (tf_cnn_benchmarks + Horovod on
 Azure HC): hand-written HIP/CDNA4 kernels, HIP-graph captured training steps and RCCL over xGMI.
 
-Importing the package sets HIP runtime defaults that must be in place before the GPU is first
-touched (the HIP runtime reads them once, at initialisation):
-
-* ``DEBUG_CLR_GRAPH_PACKET_CAPTURE=0`` (FORCED): with the runtime's default pre-recorded graph
-  packets the captured training step replays inexactly on MI355X -- the single-graph step (no
-  comm fork) diverges from its kernel-serialised run, and the data-parallel overlap step blows up
-  to inf/NaN in 4 of 6 runs -- while every API-level shape of that graph (forks, re-recorded join
-  events, memset nodes, cross-XCD and scalar-cache producer/consumer chains) replays exactly in
-  ``tools/graph_fork_repro.hip`` and no fusion switch removes it; no trigger smaller than the full
-  step was found (profiles/r2f_graph_packet_capture.txt, profiles/r3_packet_capture_recheck.txt).
-  With packet capture off every graph is exact and the step time is unchanged. A value of 1 set
-  by the user is overridden (with a warning): it would silently corrupt training. (Investigation
-  tools re-set it in os.environ after this import and before the GPU is first touched.)
+HIP graph packet capture (``DEBUG_CLR_GRAPH_PACKET_CAPTURE``, the runtime's default) is left as
+the runtime sets it. Rounds 2-3 forced it off: with it on, the captured step replayed inexactly.
+The round-4 buffer-level bisection (tools/pc_buffer_bisect.py: every buffer of the step hashed
+after each replay, capture on vs off, in separate processes) found the first differing producer:
+the fc-bias gradient's column sum, whose zeroing was a ``hipMemsetAsync`` node inside the graph
+(every activation, statistic and other gradient equal; that one slice garbage, ~1e37-1e38, at the
+third replay). Its zeroing is now part of the kernel (csrc/kernels/misc.hip launch_colsum2) and
+the step graph contains no memset node: with capture on, single-graph and data-parallel replays
+are bitwise equal to capture off (profiles/r4_packet_capture_root_cause.txt).
 """
-import os as _os
-import warnings as _warnings
-
-if _os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0") != "0":
-    _warnings.warn("azure_hc_intel_tf_amd: DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 makes the captured training step "
-                   "replay inexactly on MI355X (profiles/r3_packet_capture_recheck.txt); forcing it to 0",
-                   RuntimeWarning, stacklevel=2)
-_os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = "0"

@@ -15,6 +15,8 @@
 //     generated once on device) + uniform labels.
 //   * bucket pack/unpack: Horovod fusion-buffer memcpy-in/out role with scale and
 //     optional bf16 compression.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -60,12 +62,19 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   }
 }
 
-// column sums: out[n] += sum_m g[m][n] (bf16 or fp32 input, fp32 out; `out` is zeroed by the
-// caller). A block covers 256 columns (32 lanes x 8-column vectors) and 8 row lanes that
-// stride over M; the 8 row partials meet in LDS and one fp32 atomic per column and block
-// publishes them. (The bias gradient of a conv over a 224x224 map reduces 3.2 M rows.)
+// column sums: out[n] = sum_m g[m][n] (bf16 or fp32 input, fp32 out). A block covers 256 columns
+// (32 lanes x 8-column vectors) and 8 row lanes that stride over M; the 8 row partials meet in
+// LDS. One block row (gridDim.x == 1, `direct`): the block is the column's only writer and
+// stores the sum; otherwise one fp32 atomic per column and block into `out` zeroed by
+// zero_f32_kernel just before. (The bias gradient of a conv over a 224x224 map reduces 3.2 M
+// rows.) No hipMemsetAsync: inside a captured step graph with the runtime's packet capture on,
+// the memset node of the 1001-float fc-bias gradient left non-zero garbage (tools/pc_buffer_bisect.py,
+// tools/graph_fork_repro.hip mode 10, profiles/r4_packet_capture_root_cause.txt).
+__global__ void zero_f32_kernel(float* out, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = 0.f;
+}
 __global__ __launch_bounds__(256) void colsum_kernel(const void* g, int ld, int M, int N, int is_f32,
-                                                     float* out) {
+                                                     float* out, int direct) {
   __shared__ float part[8][257];
   const int lane = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int c0 = (blockIdx.y * 32 + lane) * 8;
@@ -96,7 +105,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* g, int ld, int 
     float s = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) s += part[r][threadIdx.x];
-    atomicAdd(out + c, s);
+    if (direct)
+      out[c] = s;
+    else
+      atomicAdd(out + c, s);
   }
 }
 
@@ -547,8 +559,19 @@ void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out,
   const int cap = (2048 + gy - 1) / gy;
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
-  (void)hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
-  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, st, g, ld, M, N, is_f32, out);
+  // HCB_COLSUM_MEMSET=1: the round-3 form (memset node + atomics), kept only to reproduce the
+  // packet-capture finding (tools/pc_buffer_bisect.py)
+  static const bool legacy = [] {
+    const char* e = std::getenv("HCB_COLSUM_MEMSET");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (legacy) {
+    (void)hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
+    hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, st, g, ld, M, N, is_f32, out, 0);
+    return;
+  }
+  if (gx > 1) hipLaunchKernelGGL(zero_f32_kernel, dim3((N + 255) / 256), dim3(256), 0, st, out, N);
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, st, g, ld, M, N, is_f32, out, gx == 1 ? 1 : 0);
 }
 void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
                          const float* hyper, float* l2_out, int nesterov, int hyper_n, hipStream_t st) {

@@ -23,6 +23,17 @@
 // mode 9: a chain through a SCALAR value: link k reads s_k with a wave-uniform load (an s_load
 //   through the scalar cache) that link k-1 wrote, fills x with it and writes s_{k+1} = s_k + 1;
 //   a scalar cache left uninvalidated between two graph kernels reads a stale s_k.
+// mode 10 / 11: the training step's bias-gradient pattern (launch_colsum2, csrc/kernels/misc.hip):
+//   a kernel dirties a float region, hipMemsetAsync(region, 0, bytes) zeroes it, a consumer
+//   counts the elements that are not zero -- mode 10 with 1001 floats (4004 bytes, not a multiple
+//   of 8 / 16: the fc bias of a 1001-class head), mode 11 with 1024 floats (4096 bytes). The
+//   region sits 256-byte aligned inside a larger allocation, as the bias slice of the flat
+//   gradient buffer does. mode 12: mode 10 with EAGER work between the replays (a kernel and a
+//   hipMemsetAsync with another destination, size and value on the same stream -- what a training
+//   loop does between two step graphs: loss copies, statistics); mode 13: eager kernels only;
+//   mode 14: eager memsets only. mode 15: the step graph's SIZE around the memset: 320 kernel
+//   nodes with 512-byte kernel arguments (the conv kernels pass a ~0.5 KB ConvParams by value)
+//   before and after one dirty / memset / check link, per replay.
 // Any ordering violation (a kernel started before its predecessor finished) or cross-XCD
 // visibility gap shows up as a nonzero error count.
 #include <hip/hip_runtime.h>
@@ -64,6 +75,24 @@ __global__ void k_scalar_link(const float* s_in, float* s_out, float* x, int n) 
 }
 __global__ void k_accum(const float* a, float* acc, int n) {  // acc = 0 (memset) + a + 1
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) acc[i] += a[i] + 1.f;
+}
+__global__ void k_dirty(float* r, int n, const unsigned* epoch) {  // any non-zero pattern
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    r[i] = 1.0e30f + (float)(*epoch & 0xff) + (float)i;
+}
+struct BigArgs {
+  float* dst;
+  int n;
+  int pad[125];  // 512 bytes of kernel arguments
+};
+__global__ void k_big(BigArgs a) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x)
+    a.dst[i] += (float)a.pad[i & 63];
+}
+__global__ void k_count_nonzero(const float* r, int n, unsigned* errors) {
+  unsigned bad = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) bad += r[i] != 0.f;
+  if (bad) atomicAdd(errors, bad);
 }
 __global__ void k_check(const unsigned* epoch, const float* y, float yadd, const float* z, float zmul, int n,
                         unsigned* errors) {
@@ -109,7 +138,27 @@ int main(int argc, char** argv) {
   CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
   hipLaunchKernelGGL(k_seed, g, b, 0, s, epoch, x, n);
   hipLaunchKernelGGL(k_bump, dim3(1), dim3(1), 0, s, epoch);
-  if (mode == 0) {
+  if (mode == 15) {
+    const int nf = 1001;
+    float* region = z + 4096;
+    BigArgs ba{};
+    ba.dst = t1;
+    ba.n = 4096;
+    for (int k = 0; k < 125; ++k) ba.pad[k] = k;
+    for (int k = 0; k < 320; ++k) hipLaunchKernelGGL(k_big, dim3(16), dim3(256), 0, s, ba);
+    hipLaunchKernelGGL(k_dirty, dim3(4), dim3(256), 0, s, region, nf, epoch);
+    CK(hipMemsetAsync(region, 0, (size_t)nf * 4, s));
+    hipLaunchKernelGGL(k_count_nonzero, dim3(4), dim3(256), 0, s, region, nf, errors);
+    for (int k = 0; k < 320; ++k) hipLaunchKernelGGL(k_big, dim3(16), dim3(256), 0, s, ba);
+  } else if (mode >= 10 && mode <= 14) {
+    const int nf = mode == 11 ? 1024 : 1001;
+    float* region = z + 4096;  // 16 KiB into the allocation: 256-byte aligned
+    for (int k = 0; k < 64; ++k) {  // 64 dirty / zero / check links per replay
+      hipLaunchKernelGGL(k_dirty, dim3(4), dim3(256), 0, s, region, nf, epoch);
+      CK(hipMemsetAsync(region, 0, (size_t)nf * 4, s));
+      hipLaunchKernelGGL(k_count_nonzero, dim3(4), dim3(256), 0, s, region, nf, errors);
+    }
+  } else if (mode == 0) {
     CK(hipEventRecord(fork, s));
     CK(hipStreamWaitEvent(c, fork, 0));
     hipLaunchKernelGGL(k_copy_add, g, b, 0, c, x, t0, n, 0.25f);
@@ -164,7 +213,12 @@ int main(int argc, char** argv) {
   hipGraphExec_t exec;
   CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
 
-  for (int it = 0; it < iters; ++it) CK(hipGraphLaunch(exec, s));
+  const bool eager_k = mode == 12 || mode == 13, eager_m = mode == 12 || mode == 14;
+  for (int it = 0; it < iters; ++it) {
+    CK(hipGraphLaunch(exec, s));
+    if (eager_k) hipLaunchKernelGGL(k_dirty, dim3(8), dim3(256), 0, s, t1, 2048 + (it & 7), epoch);
+    if (eager_m) CK(hipMemsetAsync(t0 + 64 * (it & 15), 0x5a, (size_t)(3000 + 4 * (it & 31)), s));
+  }
   CK(hipStreamSynchronize(s));
   unsigned host_err = 0, host_epoch = 0;
   CK(hipMemcpy(&host_err, errors, 4, hipMemcpyDeviceToHost));
