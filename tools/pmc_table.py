@@ -35,6 +35,12 @@ def main(root, filt=""):
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
                 if c in cs:
                     d[c.replace("SQ_", "").lower()] = cs[c] / wc
+        if cs.get("TCC_HIT_sum") or cs.get("TCC_MISS_sum"):
+            h, mi = cs.get("TCC_HIT_sum", 0.0), cs.get("TCC_MISS_sum", 0.0)
+            d["l2_hit"] = h / max(h + mi, 1.0)
+            d["l2_req_per_call"] = (h + mi) / n
+        if cs.get("TCP_TCC_READ_REQ_sum"):
+            d["l1_l2_rd_req_per_call"] = cs["TCP_TCC_READ_REQ_sum"] / n
         if cs.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_conflict"] = cs.get("SQ_LDS_BANK_CONFLICT", 0.0) / cs["SQ_LDS_IDX_ACTIVE"]
         rows.append((g, k, d))
