@@ -438,6 +438,8 @@ def set_tuned(table: dict) -> None:
 _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
              7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
              13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64)}
+# workgroups per CU each plane-GEMM cfg is built for (its stream-K grid: N_CU x occupancy)
+_P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3}
 # wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles),
 # 12-15 32-deep slots, two / three workgroups per CU
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),
@@ -469,6 +471,19 @@ def p3_candidates(M: int, N: int, K: int):
             if tiles * s > 6 * N_CU or ksteps // s < 2 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
                 break
             out.append((c, s))
+        # stream-K: one or two rounds of the resident workgroups, each an even share of every
+        # (tile, k-slot) iteration (no quantization of e.g. 196 tiles on 256 CUs)
+        nk = ksteps * 64 // (64 if c <= 6 else 32)
+        if tiles % N_CU == 0:
+            continue
+        for rounds in (1, 2):
+            G = N_CU * _P3_OCC.get(c, 1) * rounds
+            q = tiles * nk // G
+            if G >= tiles * nk or q < 4:
+                continue
+            smax = min(G, -(-nk // q) + 1)
+            if tiles * smax * bm * bn <= SPLITK_WS_FLOATS:
+                out.append((c, -G))
     return out
 
 
@@ -526,10 +541,12 @@ def _plan3(cfg, M, N, K, device, taps: int = 1):
         cfg, splits = cfg
     else:
         splits = 1
-    splits = max(1, min(int(splits), max(K // 64, 1)))
+    splits = int(splits)
+    if splits >= 0:
+        splits = max(1, min(splits, max(K // 64, 1)))
     if _DET[0]:
         splits = 1
-    if splits > 1:
+    if splits != 1:  # split-K, or stream-K (splits = -G workgroups)
         ensure_splitk_workspace(device)
     return int(cfg), int(splits)
 

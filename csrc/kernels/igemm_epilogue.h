@@ -113,11 +113,12 @@ __device__ __forceinline__ void stage_bnb_params(const ConvParams& p, int n0, ch
 // agent-scope release + ticket; the last arriver acquires and sums the others into acc and
 // returns true (it then runs the epilogue), the others return false. Call after the main
 // loop's final barrier (smem word 0 is used as the broadcast flag).
+// sstride: slabs reserved per tile (S for split-K; the maximum share count for stream-K).
 template <int MI, int NI, int NT>
 __device__ __forceinline__ bool splitk_gather(const ConvParams& p, f32x4 (&acc)[MI][NI], char* smem, int tile,
-                                              int split, int S, int tid) {
+                                              int split, int S, int tid, int sstride = 0) {
   constexpr int FR = MI * NI;  // f32x4 fragments per thread
-  f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)tile * S * FR * NT;
+  f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)tile * (sstride > 0 ? sstride : S) * FR * NT;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll

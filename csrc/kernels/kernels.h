@@ -70,6 +70,9 @@ struct ConvParams {
   int splits;
   float* ws;
   unsigned* cnt;
+  // stream-K (plane GEMMs): sk_grid > 0 workgroups each take an even share of all (tile, k-slot)
+  // iterations; a tile's shares meet in ws slabs [tile][sk_smax][tile elems] (splits == 1)
+  int sk_grid, sk_smax;
   // fp32 activations (the reference's precision, --compute_dtype fp32): x is fp32 NHWC and the
   // weights come as three bf16 packs, w (high part), w_lo (bf16 of the residual) and w_lo2 (bf16
   // of what is left); the register-staged loop splits every loaded fp32 value into bf16
@@ -124,6 +127,8 @@ int wgrad_tile_n(int cfg);
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st);
 int p3_tile_m(int cfg);
 int p3_tile_n(int cfg);
+int p3_slot_k(int cfg);
+void launch_conv_p3_sk(const ConvParams& p, int cfg, hipStream_t st);
 void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st);
 int wgrad_p3_tile_m(int cfg);
 int wgrad_p3_tile_n(int cfg);
