@@ -20,7 +20,8 @@ from . import _ext
 from . import functional as Fn
 
 _DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned")
-DEFAULT_CACHE = os.path.join(_DIR, "mi355x.json")
+# HCB_TUNED_TABLE: another table file (A/B timing of two tunings on one box)
+DEFAULT_CACHE = os.environ.get("HCB_TUNED_TABLE") or os.path.join(_DIR, "mi355x.json")
 # bump whenever the kernel config set changes: entries of another version are re-tuned
 CACHE_VERSION = 5  # 5: keys carry the filter tap count
 

@@ -280,10 +280,13 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                # 3x3 / stride-1 kernels with the input patch resident in LDS (conv3x3_patch.hip)
                17: (128, 128), 18: (256, 128), 19: (256, 64), 20: (128, 64), 21: (128, 128),
                # LDS-DMA rings with two 64-deep k-steps per stage (one barrier per 128 of K)
-               22: (64, 128), 23: (128, 128), 24: (128, 128), 25: (64, 128), 26: (64, 64)}
+               22: (64, 128), 23: (128, 128), 24: (128, 128), 25: (64, 128), 26: (64, 64),
+               # two-slot rings sized for two / three workgroups per CU
+               27: (128, 128), 28: (128, 128), 29: (128, 64), 30: (64, 128)}
 PATCH_CFG0 = 17
 PATCH_CFGS = (17, 18, 19, 20, 21)
 TUNE_KU2 = False  # offer cfg 22-26 to the autotuner (see fwd_candidates)
+TUNE_OCC = False  # offer cfg 27-30 to the autotuner (see fwd_candidates)
 # weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
@@ -316,9 +319,14 @@ def fwd_candidates(N: int, patch: bool = False):
     # back-to-back timing they win per layer (stage-3 3x3 23.2 vs 24.3 us) yet the step runs 1.2%
     # slower with them, and equal under per-launch isolated timing (profiles/r3x_ku2_cache_ab.txt)
     ku2 = [22, 23, 24, 25, 26] if TUNE_KU2 else []
+    # cfg 27-30 (two-slot rings for two / three workgroups per CU) likewise: the per-layer tuner
+    # picks them for 25 of ResNet-50's 45 bf16 problems, and the step then runs 0.7% SLOWER
+    # (9436 vs 9507 img/s, interleaved A/B on one box: profiles/r4x_bf16_occ_ab.txt) -- unlike
+    # the fp32 plane GEMMs, whose occupancy tiles win in the step too
+    occ = [27, 28, 29, 30] if TUNE_OCC else []
     if N <= 64:
-        return [1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([19, 20] if patch else [])
-    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2
+        return [1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([29] if occ else []) + ([19, 20] if patch else [])
+    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2 + occ
     c = c + [15] if N > 128 else c
     return c + ([17, 18, 19, 20, 21] if patch else [])
 

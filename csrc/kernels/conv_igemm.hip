@@ -231,8 +231,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 // ============================================================== LDS-DMA multi-stage main loop
 // KU: 64-deep k-steps per ring stage (one wait + barrier per stage: KU = 2 halves the barriers
 // and doubles the MFMA run between them; a block's last stage may carry an all-zero k-step)
-template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB, int KU = 1>
-__global__ __launch_bounds__(WM * WN * 64) void conv_igemm_glds_kernel(ConvParams p) {
+// OCC: workgroups per CU the config is built for (its LDS fits OCC rings; __launch_bounds__ caps the
+// registers at 512 / (OCC x waves per SIMD)), so one workgroup's barrier / DMA waits overlap another's MFMAs
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB, int KU = 1, int OCC = 1>
+__global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_glds_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, RP = NT / 8;  // threads; tile rows per load pass
@@ -401,7 +403,7 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>), dim3(tiles), dim3(256), lds, st, p);
 }
 
-template <int WM, int WN, int TM, int TN, int NST, bool BNB, int KU = 1>
+template <int WM, int WN, int TM, int TN, int NST, bool BNB, int KU = 1, int OCC = 1>
 static void launch_glds(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
@@ -419,23 +421,23 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU>), dim3(tiles), dim3(NT),
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC>), dim3(tiles), dim3(NT),
                        lds, st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC>), dim3(tiles), dim3(NT), lds,
                        st, p);
 }
 
@@ -446,16 +448,18 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
 // 4x2 of 32x64, 256x128 (4x2 of 64x64), 128x256 (2x4 of 64x64), 64x128 (2x4 of 32x32);
 // 17..21 the 3x3 patch kernels (conv3x3_patch.hip): 128x128, 256x128, 256x64, 128x64, 128x128;
 // 22..26 LDS-DMA rings with two k-steps per stage (KU = 2): 64x128 (1x4 waves of 64x32),
-// 128x128 (4x2 of 32x64), 128x128 (2x4 of 64x32), 64x128 (2x4 of 32x32), 64x64 (2x2 of 32x32)
-constexpr int N_CONV_CFG = 27;
+// 128x128 (4x2 of 32x64), 128x128 (2x4 of 64x32), 64x128 (2x4 of 32x32), 64x64 (2x2 of 32x32);
+// 27..30 two-slot rings sized for two / three workgroups per CU: 128x128 (2x2 of 64x64, OCC 2),
+// 128x128 (2x4 of 64x32, OCC 2), 128x64 (2x2 of 64x32, OCC 3), 64x128 (2x2 of 32x64, OCC 3)
+constexpr int N_CONV_CFG = 31;
 int conv_tile_m(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128,
-                                    256, 128, 64,  128, 256, 256, 128, 128, 64,  128, 128, 64, 64};
+  static const int t[N_CONV_CFG] = {128, 128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 256, 128,
+                                    64,  128, 256, 256, 128, 128, 64,  128, 128, 64,  64,  128, 128, 128, 64};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
-  static const int t[N_CONV_CFG] = {128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 128,
-                                    128, 256, 128, 128, 128, 64,  64,  128, 128, 128, 128, 128, 64};
+  static const int t[N_CONV_CFG] = {128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 128, 128, 256,
+                                    128, 128, 128, 64,  64,  128, 128, 128, 128, 128, 64,  128, 128, 64,  128};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 
@@ -484,6 +488,10 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
     case 24: launch_glds<2, 4, 64, 32, 2, BNB, 2>(p, st); break;
     case 25: launch_glds<2, 4, 32, 32, 2, BNB, 2>(p, st); break;
     case 26: launch_glds<2, 2, 32, 32, 3, BNB, 2>(p, st); break;
+    case 27: launch_glds<2, 2, 64, 64, 2, BNB, 1, 2>(p, st); break;
+    case 28: launch_glds<2, 4, 64, 32, 2, BNB, 1, 2>(p, st); break;
+    case 29: launch_glds<2, 2, 64, 32, 2, BNB, 1, 3>(p, st); break;
+    case 30: launch_glds<2, 2, 32, 64, 2, BNB, 1, 3>(p, st); break;
     default: launch_reg<2, 2, 64, 64, BNB>(p, st); break;
   }
 }

@@ -49,7 +49,7 @@ for step in "$@"; do
       for r in 1 2; do for v in base var; do
         if [ $v = base ]; then e=""; else e="$args"; fi
         env $e timeout -k 10 400 python bench.py --steps 40 --warmup 10 > ${O}_ab.json 2> ${O}_ab.err || fail benchab ${O}_ab.err
-        echo "$v [$e] $(python -c "import json;d=json.load(open('${O}_ab.json'));print(d['value'], d['ms_per_step'])")"
+        echo "$v [$e] $(python -c "import json;d=json.load(open('${O}_ab.json'));print(d['value'], d['ms_per_step'], 'bf16', d.get('bf16_value'), d.get('bf16_ms_per_step'))")"
       done; done ;;
     prof)
       pargs=${args:---steps 10 --warmup 3}
