@@ -348,7 +348,7 @@ class ConvBN(Layer):
                 Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
                 gres = dz
-        self._wgrad(dz, x)
+        run_wgrad(self, dz, x)
         if self.need_dx:
             H, W, Cin = self.in_shape
             if dx is None:
@@ -363,6 +363,34 @@ class ConvBN(Layer):
     def clear(self):
         self._saved = None
         self._pre_reduced = False
+
+
+# Weight-gradient GEMMs on a side stream (set by the Trainer around a step, HCB_WGRAD_STREAM=1):
+# layer i's dW GEMM forks off the main stream right after its dz exists and runs beside the data-
+# gradient chain, filling the CUs the dgrad grid leaves idle (e.g. 196 tiles on 256 CUs); the
+# Trainer joins before a segment's gradients are reduced / the optimizer runs. The operands are
+# kept referenced until the join, so the caching allocator cannot hand their memory to a later
+# main-stream tensor while the side stream still reads it.
+WGRAD_SIDE = {"stream": None, "keep": []}
+
+
+def run_wgrad(layer, dz, x):
+    s = WGRAD_SIDE["stream"]
+    if s is None or not Fn.native(dz):
+        layer._wgrad(dz, x)
+        return
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        layer._wgrad(dz, x)
+    WGRAD_SIDE["keep"].append((dz, x))
+
+
+def wgrad_join():
+    """The main stream waits for every weight-gradient GEMM issued on the side stream."""
+    s = WGRAD_SIDE["stream"]
+    if s is not None and WGRAD_SIDE["keep"]:
+        torch.cuda.current_stream().wait_stream(s)
+        WGRAD_SIDE["keep"].clear()
 
 
 # GPU ResNet stem as a space-to-depth 4x4/1 GEMM (False: the direct padded 7x7/2 form)

@@ -35,6 +35,7 @@ from typing import Callable, Optional
 
 import torch
 
+from .nn import layers as L
 from .nn.layers import Logits
 from .ops import functional as Fn
 from .ops import _ext
@@ -123,6 +124,9 @@ class Trainer:
             self.dlogits32 = torch.zeros((batch_size, ld), dtype=torch.float32, device=self.dev)
             fc.dl32 = self.dlogits32
             fc.dl32_src = self.dlogits
+        # weight-gradient GEMMs on a side stream (nn/layers.py run_wgrad), HCB_WGRAD_STREAM=1
+        self._wg_stream = (torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda"
+                           and os.environ.get("HCB_WGRAD_STREAM", "0") == "1" else None)
         self.l2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.steps_done = 0
@@ -161,6 +165,7 @@ class Trainer:
             self.model.clear()
             return
         self.model.backward(self.dlogits)
+        L.wgrad_join()
 
     def _ranges(self, i, layers):
         if i not in self._seg_ranges:
@@ -202,6 +207,7 @@ class Trainer:
                     layers, _ = next(gen)
                 except StopIteration:
                     break
+                L.wgrad_join()  # the segment's weight gradients are complete before they are reduced
             if not self._skip_comm:
                 if self.comm_check:
                     self._check_snapshot(self._ranges(i, layers))
@@ -328,11 +334,13 @@ class Trainer:
                 self._forward(images, labels)
                 gen = self.model.backward_segments(self.dlogits)
                 layers, last = next(gen)
+                L.wgrad_join()
             segs.append((g, self._ranges(0, layers)))
             while not last:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
                     layers, last = next(gen)
+                    L.wgrad_join()
                 segs.append((g, self._ranges(len(segs), layers)))
             gen.close()
             g2 = torch.cuda.CUDAGraph()
@@ -364,6 +372,14 @@ class Trainer:
             return self._step(images, labels)
 
     def _step(self, images, labels):
+        L.WGRAD_SIDE["stream"] = self._wg_stream
+        try:
+            return self._step_body(images, labels)
+        finally:
+            L.WGRAD_SIDE["stream"] = None
+            L.WGRAD_SIDE["keep"].clear()
+
+    def _step_body(self, images, labels):
         self.hyper[0:1].fill_(float(self.lr_fn(self.steps_done)))  # host write, outside the graph
         if not self.use_graph:
             self._eager_step(images, labels)
