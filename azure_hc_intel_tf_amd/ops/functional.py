@@ -287,10 +287,13 @@ PATCH_CFG0 = 17
 PATCH_CFGS = (17, 18, 19, 20, 21)
 TUNE_KU2 = False  # offer cfg 22-26 to the autotuner (see fwd_candidates)
 TUNE_OCC = False  # offer cfg 27-30 to the autotuner (see fwd_candidates)
-# weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring
+# weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring, 100-107 slot rings
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
-                12: (64, 128), 13: (128, 64), 14: (64, 128)}
+                12: (64, 128), 13: (128, 64), 14: (64, 128),
+                # 100-107: the fp32 path's slot-ring kernel on one 16-bit plane (conv_wgrad_s1.hip)
+                100: (128, 128), 101: (128, 128), 102: (128, 128), 103: (256, 128), 104: (128, 64),
+                105: (64, 64), 106: (64, 128), 107: (128, 128)}
 N_CU = 256
 _tuned: dict = {}
 
@@ -344,6 +347,8 @@ def wgrad_candidates(Nout: int, K: int, M: int):
     ksteps = math.ceil(M / 64)
     out = []
     for c, (bm, bn) in _WGRAD_TILES.items():
+        if c >= 100 and ((Nout <= 64 and bm > 64) or (K <= 64 and bn > 64) or (Nout < 256 and bm > 128)):
+            continue
         tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
         for s in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512):
             if s > 1 and ksteps // s < 2:

@@ -329,6 +329,11 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArra
   p.dw = dw.data_ptr<float>();
   p.dy_bytes = (uint32_t)yb;
   p.x_bytes = (uint32_t)xb;
+  if (cfg >= hcb::WGRAD_S1_BASE) {  // the slot-ring weight-grad kernel on one 16-bit plane (conv_wgrad_s1.hip)
+    TORCH_CHECK(!f32 && cfg < hcb::WGRAD_S1_BASE + hcb::N_WS1_CFG, "hcb.conv_wgrad: bad s1 cfg");
+    hcb::launch_wgrad_s1(p, (int)cfg - hcb::WGRAD_S1_BASE, eff_splits, cur_stream());
+    return;
+  }
   hcb::launch_conv_wgrad(p, (int)cfg, eff_splits, cur_stream());
 }
 

@@ -23,10 +23,10 @@ __device__ __forceinline__ int p3_swz(int row) {
 }
 
 // the fragments of one slot (KS = KW / 32 halves of 32, three planes of each operand) in registers
-template <int TM, int TN, int KS>
+template <int TM, int TN, int KS, int NPL = 3>
 struct P3Frags {
   static constexpr int MI = TM / 16, NI = TN / 16;
-  u32x4 a[KS][3][MI], b[KS][3][NI];
+  u32x4 a[KS][NPL][MI], b[KS][NPL][NI];
 };
 
 // every fragment read of the slot (LDS -> registers), issued back to back
@@ -54,22 +54,28 @@ __device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<
   }
 }
 
-// the KS x MI x NI x 6 MFMAs of the slot on register fragments
-template <int TM, int TN, int KS>
-__device__ __forceinline__ void p3_mma(const P3Frags<TM, TN, KS>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
+// the KS x MI x NI x 6 MFMAs of the slot on register fragments (NPL = 1: one 16-bit product of
+// the build's activation type)
+template <int TM, int TN, int KS, int NPL = 3>
+__device__ __forceinline__ void p3_mma(const P3Frags<TM, TN, KS, NPL>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
   constexpr int MI = TM / 16, NI = TN / 16;
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {  // small terms first
-        acc[i][j] = mfma_bf16(f.a[ks][2][i], f.b[ks][0][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][2][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(f.a[ks][1][i], f.b[ks][1][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(f.a[ks][1][i], f.b[ks][0][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][1][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][0][j], acc[i][j]);
+      for (int j = 0; j < NI; ++j) {
+        if constexpr (NPL == 1) {
+          acc[i][j] = mfma16(__builtin_bit_cast(act16x8, f.a[ks][0][i]), __builtin_bit_cast(act16x8, f.b[ks][0][j]),
+                             acc[i][j]);
+        } else {  // small terms first
+          acc[i][j] = mfma_bf16(f.a[ks][2][i], f.b[ks][0][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][2][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(f.a[ks][1][i], f.b[ks][1][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(f.a[ks][1][i], f.b[ks][0][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][1][j], acc[i][j]);
+          acc[i][j] = mfma_bf16(f.a[ks][0][i], f.b[ks][0][j], acc[i][j]);
+        }
       }
 }
 

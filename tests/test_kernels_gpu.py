@@ -240,10 +240,11 @@ def test_conv_wgrad(case):
     assert rel_err(dw, ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(15)))
+@pytest.mark.parametrize("cfg", list(range(15)) + list(range(100, 108)))
 def test_conv_wgrad_all_configs(cfg):
     """Every weight-grad tile config (register-staged 0-2 and 13-14, LDS-DMA ring 3-9,
-    intra-workgroup k-split 10-12) with split-K on
+    intra-workgroup k-split 10-12; 100-107: the plane kernel's slot rings on one 16-bit plane,
+    conv_wgrad_s1.hip) with split-K on
     1x1 / 3x3 / strided / odd-channel geometries (partial tiles in Nout, K and pixels)."""
     torch.manual_seed(6)
     for cin, cout, k, s, pads, H, splits in [(64, 256, 1, 1, (0, 0, 0, 0), 14, 3),
