@@ -282,11 +282,17 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                # LDS-DMA rings with two 64-deep k-steps per stage (one barrier per 128 of K)
                22: (64, 128), 23: (128, 128), 24: (128, 128), 25: (64, 128), 26: (64, 64),
                # two-slot rings sized for two / three workgroups per CU
-               27: (128, 128), 28: (128, 128), 29: (128, 64), 30: (64, 128)}
+               27: (128, 128), 28: (128, 128), 29: (128, 64), 30: (64, 128),
+               # register-pipelined LDS-DMA loop on cfg 4, 5, 7, 12, 13, 14, 16's tiles
+               31: (128, 128), 32: (128, 64), 33: (64, 128), 34: (128, 128), 35: (128, 128), 36: (256, 128),
+               37: (64, 128)}
 PATCH_CFG0 = 17
 PATCH_CFGS = (17, 18, 19, 20, 21)
 TUNE_KU2 = False  # offer cfg 22-26 to the autotuner (see fwd_candidates)
 TUNE_OCC = False  # offer cfg 27-30 to the autotuner (see fwd_candidates)
+# offer cfg 31-37 (register-pipelined LDS-DMA loop) to the autotuner: a full bf16 retune with them
+# picked none of them for ResNet-50's 45 problems (profiles/r4ab_bf16_pipe_retune.txt)
+TUNE_PIPE = False
 # weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring, 100-107 slot rings
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
@@ -327,9 +333,11 @@ def fwd_candidates(N: int, patch: bool = False):
     # (9436 vs 9507 img/s, interleaved A/B on one box: profiles/r4x_bf16_occ_ab.txt) -- unlike
     # the fp32 plane GEMMs, whose occupancy tiles win in the step too
     occ = [27, 28, 29, 30] if TUNE_OCC else []
+    pipe = [31, 32, 33, 34, 35, 36, 37] if TUNE_PIPE else []
     if N <= 64:
-        return [1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([29] if occ else []) + ([19, 20] if patch else [])
-    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2 + occ
+        return ([1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([29] if occ else []) + ([32] if pipe else [])
+                + ([19, 20] if patch else []))
+    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2 + occ + pipe
     c = c + [15] if N > 128 else c
     return c + ([17, 18, 19, 20, 21] if patch else [])
 

@@ -112,6 +112,41 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
   }
 }
 
+// One 64-deep k-step's fragments in registers (both 32-deep halves), and its MFMAs: the
+// register-pipelined LDS-DMA loop (PIPE) reads step k+1's fragments while step k's MFMAs run.
+template <int TM, int TN>
+struct GFrags {
+  act16x8 a[2][TM / 16], b[2][TN / 16];
+};
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void gfrag_read(const u32x4* Ab, const u32x4* Bb, GFrags<TM, TN>& f, int wm, int wn,
+                                           int lane) {
+  const int frow = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int ch = ks * 4 + fq;
+#pragma unroll
+    for (int i = 0; i < TM / 16; ++i) {
+      const int row = wm * TM + i * 16 + frow;
+      f.a[ks][i] = __builtin_bit_cast(act16x8, Ab[row * 8 + (ch ^ ((row >> 1) & 7))]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN / 16; ++j) {
+      const int row = wn * TN + j * 16 + frow;
+      f.b[ks][j] = __builtin_bit_cast(act16x8, Bb[row * 8 + (ch ^ ((row >> 1) & 7))]);
+    }
+  }
+}
+template <int TM, int TN>
+__device__ __forceinline__ void gfrag_mma(const GFrags<TM, TN>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < TM / 16; ++i)
+#pragma unroll
+      for (int j = 0; j < TN / 16; ++j) acc[i][j] = mfma16(f.a[ks][i], f.b[ks][j], acc[i][j]);
+}
+
 // ============================================================== register-staged main loop
 // F32: fp32 x split into bf16 hi / mid / lo images while staged, the weights as three bf16 packs
 // (ConvParams::w, w_lo, w_lo2), bf16x6 MFMAs (the --compute_dtype fp32 path); fp32 epilogue
@@ -233,7 +268,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 // and doubles the MFMA run between them; a block's last stage may carry an all-zero k-step)
 // OCC: workgroups per CU the config is built for (its LDS fits OCC rings; __launch_bounds__ caps the
 // registers at 512 / (OCC x waves per SIMD)), so one workgroup's barrier / DMA waits overlap another's MFMAs
-template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB, int KU = 1, int OCC = 1>
+// PIPE (KU = 1): register double-buffered fragments -- after the barrier of step k the wave issues
+// step k+1's fragment reads, then step k's MFMAs; one barrier per step, which both publishes step
+// k+1's DMA and retires every wave's reads of step k, whose stage is refilled with step k+NST.
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB, int KU = 1, int OCC = 1,
+          bool PIPE = false>
 __global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_glds_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
@@ -245,6 +284,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_gl
   static_assert((WM * WN == 4 || WM * WN == 8) && NST >= 2 && NST <= 6 && (KU == 1 || KU == 2), "config");
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 2) <= 63, "vmcnt range");
+  static_assert(!PIPE || (KU == 1 && LOADS * (NST - 1) <= 63), "PIPE: one k-step per stage");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -307,6 +347,50 @@ __global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_gl
   if constexpr (BNB && PARAM_LDS) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
   const bool early = BNB && S == 1 && nk_steps <= EARLY_EPI_KSTEPS;
   if (early) pre.load(p, 0, m0, n0, tid);
+  if constexpr (PIPE) {
+    // NST stages in flight from the start; at step k at most the stages after k+1 may be pending
+    auto wait_ahead = [&](int ahead) {
+      if (ahead >= 4)
+        wait_vmcnt<(NST >= 5 ? 4 : 0) * LOADS>();
+      else if (ahead == 3)
+        wait_vmcnt<(NST >= 4 ? 3 : 0) * LOADS>();
+      else if (ahead == 2)
+        wait_vmcnt<(NST >= 3 ? 2 : 0) * LOADS>();
+      else if (ahead == 1)
+        wait_vmcnt<LOADS>();
+      else
+        wait_vmcnt<0>();
+    };
+    auto read = [&](int k, GFrags<TM, TN>& f) {
+      const char* sb = smem + (k % NST) * STAGE;
+      gfrag_read<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + BM * 128), f,
+                                 wm, wn, lane);
+    };
+#pragma unroll
+    for (int s = 0; s < NST; ++s)
+      if (s < nk) issue(s, s);
+    GFrags<TM, TN> fr[2];
+    if (nk > 0) {
+      wait_ahead(min(NST - 1, nk - 1));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read(0, fr[0]);
+    }
+    auto body = [&](int k, GFrags<TM, TN>& cur, GFrags<TM, TN>& nxt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of step k are done
+      if (k + 1 < nk) wait_ahead(min(NST - 2, nk - 2 - k));  // step k+1 landed for this thread
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (k + NST < nk) issue(k % NST, k + NST);
+      if (k + 1 < nk) read(k + 1, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      gfrag_mma<TM, TN>(cur, acc);
+    };
+    for (int k = 0; k < nk; k += 2) {
+      body(k, fr[0], fr[1]);
+      if (k + 1 < nk) body(k + 1, fr[1], fr[0]);
+    }
+  } else {
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
     if (s < nk) issue(s, s);
@@ -333,6 +417,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_gl
       mfma_tile_step<WM, WN, TM, TN, true>(reinterpret_cast<const u32x4*>(sb),
                                                      reinterpret_cast<const u32x4*>(sb + BM * 128), acc, wm, wn, lane);
     }
+  }
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
   if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
@@ -403,7 +488,7 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>), dim3(tiles), dim3(256), lds, st, p);
 }
 
-template <int WM, int WN, int TM, int TN, int NST, bool BNB, int KU = 1, int OCC = 1>
+template <int WM, int WN, int TM, int TN, int NST, bool BNB, int KU = 1, int OCC = 1, bool PIPE = false>
 static void launch_glds(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
@@ -421,23 +506,23 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC, PIPE>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC, PIPE>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC, PIPE>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC, PIPE>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC>), dim3(tiles), dim3(NT),
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT),
                        lds, st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT), lds,
                        st, p);
 }
 
@@ -450,16 +535,19 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
 // 22..26 LDS-DMA rings with two k-steps per stage (KU = 2): 64x128 (1x4 waves of 64x32),
 // 128x128 (4x2 of 32x64), 128x128 (2x4 of 64x32), 64x128 (2x4 of 32x32), 64x64 (2x2 of 32x32);
 // 27..30 two-slot rings sized for two / three workgroups per CU: 128x128 (2x2 of 64x64, OCC 2),
-// 128x128 (2x4 of 64x32, OCC 2), 128x64 (2x2 of 64x32, OCC 3), 64x128 (2x2 of 32x64, OCC 3)
-constexpr int N_CONV_CFG = 31;
+// 128x128 (2x4 of 64x32, OCC 2), 128x64 (2x2 of 64x32, OCC 3), 64x128 (2x2 of 32x64, OCC 3);
+// 31..37 the register-pipelined loop (PIPE) on cfg 4, 5, 7, 12, 13, 14, 16's tiles and rings
+constexpr int N_CONV_CFG = 38;
 int conv_tile_m(int cfg) {
   static const int t[N_CONV_CFG] = {128, 128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 256, 128,
-                                    64,  128, 256, 256, 128, 128, 64,  128, 128, 64,  64,  128, 128, 128, 64};
+                                    64,  128, 256, 256, 128, 128, 64,  128, 128, 64,  64,  128, 128, 128, 64,
+                                    128, 128, 64,  128, 128, 256, 64};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
   static const int t[N_CONV_CFG] = {128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 128, 128, 256,
-                                    128, 128, 128, 64,  64,  128, 128, 128, 128, 128, 64,  128, 128, 64,  128};
+                                    128, 128, 128, 64,  64,  128, 128, 128, 128, 128, 64,  128, 128, 64,  128,
+                                    128, 64,  128, 128, 128, 128, 128};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 
@@ -492,6 +580,13 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
     case 28: launch_glds<2, 4, 64, 32, 2, BNB, 1, 2>(p, st); break;
     case 29: launch_glds<2, 2, 64, 32, 2, BNB, 1, 3>(p, st); break;
     case 30: launch_glds<2, 2, 32, 64, 2, BNB, 1, 3>(p, st); break;
+    case 31: launch_glds<2, 2, 64, 64, 3, BNB, 1, 1, true>(p, st); break;
+    case 32: launch_glds<4, 1, 32, 64, 3, BNB, 1, 1, true>(p, st); break;
+    case 33: launch_glds<1, 4, 64, 32, 3, BNB, 1, 1, true>(p, st); break;
+    case 34: launch_glds<2, 4, 64, 32, 3, BNB, 1, 1, true>(p, st); break;
+    case 35: launch_glds<4, 2, 32, 64, 3, BNB, 1, 1, true>(p, st); break;
+    case 36: launch_glds<4, 2, 64, 64, 3, BNB, 1, 1, !BNB>(p, st); break;  // BNB: spills with PIPE
+    case 37: launch_glds<2, 4, 32, 32, 4, BNB, 1, 1, true>(p, st); break;
     default: launch_reg<2, 2, 64, 64, BNB>(p, st); break;
   }
 }
