@@ -101,7 +101,11 @@ def test_segmented_overlap_step_matches_single_graph(model_name):
         runs.append(losses)
     a, b = torch.tensor(runs[0]), torch.tensor(runs[1])
     assert torch.isfinite(b).all()
-    assert torch.allclose(a[:4], b[:4], rtol=3e-2, atol=3e-2), (runs[0], runs[1])
+    # run-to-run spread of this non-deterministic step (tools/pc_noise_probe.py, 3 runs each, single
+    # and dp graphs): <= 0.3% at step 0 growing to ~4% at step 3 (4.62-4.80) as the tiny batch is
+    # memorised; 3% at step 3 failed a correct pair (4.754 vs 4.569)
+    assert torch.allclose(a[:3], b[:3], rtol=3e-2, atol=3e-2), (runs[0], runs[1])
+    assert torch.allclose(a[3], b[3], rtol=8e-2), (runs[0], runs[1])
     assert b[-1] < 0.9 * b[0] and a[-1] < 0.9 * a[0], (runs[0], runs[1])
 
 
