@@ -708,8 +708,7 @@ class Logits(Layer):
             geom = [B, 1, 1, C, C, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, self.cin, C, self.pack.Kpad_t, self.cin,
                     0, 1, 1, 1, 1, 0, Fn._f32o(dx)]
             cfgd = Fn.conv_plan(B, self.cin, C)[0]
-            w_lo = Fn.lo_pack(self.pack.tr) if dlogits.dtype == torch.float32 else None
-            hcb.conv_igemm(dlogits, self.pack.tr, dx, None, None, None, geom, cfgd, None, w_lo)
+            hcb.conv_igemm(dlogits, self.pack.tr, dx, None, None, None, geom, cfgd, None, None)
         else:
             g = dlogits[:, :self.ncls]
             self.w.grad.view(self.ncls, self.cin).add_((g.t() @ x).float())

@@ -592,12 +592,7 @@ def conv_forward(x, spec: ConvSpec, wpack, w_master, out, stats=None, bias=None,
                 1 if residual is not None else 0, 1 if out_f32 else 0, 1 if relu else 0, int(stats_R), splits]
         if residual is not None:  # beta-accumulate epilogue: out = conv(x) + residual (same layout)
             assert ld(residual) == ld(out) and residual.shape == out.shape
-        w_lo = None
-        if x.dtype == torch.float32:  # bf16x6: register-staged tiles, no split-K
-            w_lo = lo_pack(wpack)
-            assert w_lo is not None and out_f32, "fp32 conv needs the residual weight pack and an fp32 output"
-            geom[-1] = 1
-        _ext.ops().conv_igemm(x, wpack, out, residual, bias, stats, geom, cfg, stats_shift, w_lo)
+        _ext.ops().conv_igemm(x, wpack, out, residual, bias, stats, geom, cfg, stats_shift, None)
         return out
     xt = x.permute(0, 3, 1, 2)
     if spec.pt or spec.pb or spec.pl or spec.pr:
@@ -834,14 +829,13 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
         if cfg is None and bnb is not None:
             cfg = _tuned.get(dgb_key(M, spec.cin_pad, K, taps))
         cfg, splits = _plan(cfg, M, spec.cin_pad, K, dz.device, taps)
-        w_lo = None
         geom = geom + [0, 0, splits]
         if bnb is not None:
             _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
                                       bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
                                       bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
         else:
-            _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg, None, w_lo)
+            _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg, None, None)
         return dx
     Hp = H + spec.pt + spec.pb
     Wp = W + spec.pl + spec.pr

@@ -206,21 +206,8 @@ void conv_igemm(const Tensor& x, const Tensor& w, const Tensor& y, const c10::op
   TORCH_CHECK(!stats_shift.has_value() || p.stats != nullptr, "hcb.conv_igemm: stats_shift without stats");
   p.stats_shift = opt_f32(stats_shift, p.Nout, "stats_shift");
   p.w_lo = p.w_lo2 = nullptr;
-  if (x.scalar_type() == at::kFloat) {  // fp32 path: hi / mid / lo weight packs, register-staged, no split-K
-    // w_lo: [2][n] -- the mid pack and the lo pack, each row contiguous (rows need not be adjacent)
-    TORCH_CHECK(w_lo.has_value(), "hcb.conv_igemm: fp32 x needs the residual weight packs w_lo");
-    TORCH_CHECK(w_lo->dim() == 2 && w_lo->size(0) == 2 && w_lo->stride(1) == 1 &&
-                    w_lo->scalar_type() == w.scalar_type() && w_lo->size(1) >= (int64_t)p.Nout * p.Kpad,
-                "hcb.conv_igemm: w_lo must be [2][>= Nout*Kpad] of the pack's type");
-    const Tensor m = w_lo->select(0, 0), l = w_lo->select(0, 1);
-    check_align16(m.data_ptr(), "w_lo[0]");
-    check_align16(l.data_ptr(), "w_lo[1]");
-    TORCH_CHECK(p.splits == 1, "hcb.conv_igemm: no split-K on the fp32 path");
-    p.w_lo = m.data_ptr();
-    p.w_lo2 = l.data_ptr();
-  } else {
-    TORCH_CHECK(!w_lo.has_value(), "hcb.conv_igemm: w_lo only with fp32 x");
-  }
+  TORCH_CHECK(x.scalar_type() != at::kFloat && !w_lo.has_value(),
+              "hcb.conv_igemm: 16-bit operands only (fp32 runs on the plane GEMMs: hcb.conv_p3)");
   hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
 }
 
@@ -293,11 +280,11 @@ int64_t conv_tiles_m(int64_t M, int64_t cfg) {
 void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArrayRef g, int64_t cfg,
                 int64_t splits) {
   TORCH_CHECK(g.size() == 17, "hcb.conv_wgrad: geom must have 17 entries");
-  const bool f32 = same_act(dy, x, "x");  // fp32: bf16x6 path
+  const bool f32 = same_act(dy, x, "x");
+  TORCH_CHECK(!f32, "hcb.conv_wgrad: 16-bit operands only (fp32 runs on the plane GEMMs: hcb.conv_wgrad_p3)");
   check_f32(dw, "dw");
   hcb::WgradParams p{};
-  p.f32in = f32 ? 1 : 0;
-  const int64_t e = f32 ? 4 : 2;
+  const int64_t e = 2;
   p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];
   p.P = g[5]; p.Q = g[6]; p.R = g[7]; p.S = g[8];
   p.stride_h = g[9]; p.stride_w = g[10]; p.pad_h = g[11]; p.pad_w = g[12];

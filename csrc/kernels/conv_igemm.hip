@@ -148,23 +148,17 @@ __device__ __forceinline__ void gfrag_mma(const GFrags<TM, TN>& f, f32x4 (&acc)[
 }
 
 // ============================================================== register-staged main loop
-// F32: fp32 x split into bf16 hi / mid / lo images while staged, the weights as three bf16 packs
-// (ConvParams::w, w_lo, w_lo2), bf16x6 MFMAs (the --compute_dtype fp32 path); fp32 epilogue
-template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB, bool F32 = false>
+// (16-bit operands; fp32 runs on the plane GEMMs, conv_p3.hip)
+template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AV = BM / 32, BV = BN / 32;  // 16-byte vectors per thread per k-step
-  constexpr int ESZ = F32 ? 4 : 2;
   static_assert(WM * WN == 4, "4 waves");
-  static_assert(!(F32 && BNB), "no fused BN-backward epilogue on the fp32 path");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int NB = p.Kpad > 64 ? 2 : 1;  // LDS buffers (one for a single k-step)
   u32x4* As = reinterpret_cast<u32x4*>(smem);  // [NB][BM*8]
   u32x4* Bs = As + NB * BM * 8;                 // [NB][BN*8]
-  // fp32 path: the images are [3][NB][BM*8] (A) and [3][NB][BN*8] (B), hi first
-  u32x4* Bs3 = As + 3 * NB * BM * 8;
-  if constexpr (F32) Bs = Bs3;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -176,9 +170,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
-  const __amdgpu_buffer_rsrc_t wlr = make_rsrc(F32 ? p.w_lo : p.w, p.w_bytes);
-  const __amdgpu_buffer_rsrc_t wlr2 = make_rsrc(F32 ? p.w_lo2 : p.w, p.w_bytes);
-  ALoader<AV, CBIG, LHSDIL, 32, ESZ> al;
+  ALoader<AV, CBIG, LHSDIL, 32, 2> al;
   al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
 #pragma unroll
@@ -187,9 +179,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
   }
 
-  // F32: ra / ra2 hold the two 16-byte halves of each 8-value fp32 vector, rb2 / rb3 the mid
-  // and lo weights
-  u32x4 ra[AV], rb[BV], ra2[F32 ? AV : 1], rb2[F32 ? BV : 1], rb3[F32 ? BV : 1];
+  u32x4 ra[AV], rb[BV];
   f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -200,42 +190,20 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
     uint32_t off[AV];
     al.offsets(p, kt, chunk, off);
 #pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      ra[v] = buf_load16(xr, off[v]);
-      if constexpr (F32) ra2[v] = buf_load16(xr, off[v] + 16u);  // HCB_OOB + 16 stays out of range
-    }
+    for (int v = 0; v < AV; ++v) ra[v] = buf_load16(xr, off[v]);
 #pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u;
-      rb[v] = buf_load16(wr, o);
-      if constexpr (F32) {
-        rb2[v] = buf_load16(wlr, o);
-        rb3[v] = buf_load16(wlr2, o);
-      }
-    }
+    for (int v = 0; v < BV; ++v) rb[v] = buf_load16(wr, b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
-      const int row = (tid >> 3) + 32 * v, idx = buf * BM * 8 + row * 8 + (chunk ^ ((row >> 1) & 7));
-      if constexpr (F32) {
-        u32x4 hi, mid, lo;
-        split3_8(ra[v], ra2[v], hi, mid, lo);
-        As[idx] = hi;
-        As[NB * BM * 8 + idx] = mid;
-        As[2 * NB * BM * 8 + idx] = lo;
-      } else {
-        As[idx] = ra[v];
-      }
+      const int row = (tid >> 3) + 32 * v;
+      As[buf * BM * 8 + row * 8 + (chunk ^ ((row >> 1) & 7))] = ra[v];
     }
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
-      const int row = (tid >> 3) + 32 * v, idx = buf * BN * 8 + row * 8 + (chunk ^ ((row >> 1) & 7));
-      Bs[idx] = rb[v];
-      if constexpr (F32) {
-        Bs[NB * BN * 8 + idx] = rb2[v];
-        Bs[2 * NB * BN * 8 + idx] = rb3[v];
-      }
+      const int row = (tid >> 3) + 32 * v;
+      Bs[buf * BN * 8 + row * 8 + (chunk ^ ((row >> 1) & 7))] = rb[v];
     }
   };
 
@@ -252,11 +220,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    if constexpr (F32)
-      mfma_tile_step6<WM, WN, TM, TN>(As + cur * BM * 8, Bs + cur * BN * 8, NB * BM * 8, NB * BN * 8, acc, wm,
-                                      wn, lane);
-    else
-      mfma_tile_step<WM, WN, TM, TN, false>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
+    mfma_tile_step<WM, WN, TM, TN, false>(As + cur * BM * 8, Bs + cur * BN * 8, acc, wm, wn, lane);
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
@@ -437,11 +401,8 @@ template <int WM, int WN, int TM, int TN, bool BNB>
 static void launch_reg(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
-  const bool f32 = p.w_lo != nullptr;
-  // a single k-step (1x1 over <= 64 channels) uses one buffer pair; the fp32 path stages three
-  // images (hi / mid / lo) of both operands -- no 128x128 tile (192 KB)
-  constexpr bool F32OK = !BNB && 2 * (BM + BN) * 128 * 3 <= 160 * 1024;
-  size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16 * (f32 ? 3 : 1);
+  // a single k-step (1x1 over <= 64 channels) uses one buffer pair
+  size_t lds_main = (size_t)(p.Kpad > 64 ? 2 : 1) * (BM + BN) * 8 * 16;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   if (BNB) lds = reg_param_off(BM, BN, WM) + bnb_param_lds(BN);
@@ -453,30 +414,7 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, true, BNB>);
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, false, BNB>);
     set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>);
-    if constexpr (F32OK) {
-      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, false, false, true>);
-      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, true, true, false, true>);
-      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, false, false, true>);
-      set_lds_once(conv_igemm_kernel<WM, WN, TM, TN, false, true, false, true>);
-    }
     once = true;
-  }
-  if constexpr (F32OK) {
-    if (f32) {
-      if (cbig && !lhs)
-        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, false, false, true>), dim3(tiles), dim3(256), lds,
-                           st, p);
-      else if (cbig && lhs)
-        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, true, false, true>), dim3(tiles), dim3(256), lds,
-                           st, p);
-      else if (!cbig && !lhs)
-        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, false, false, true>), dim3(tiles), dim3(256), lds,
-                           st, p);
-      else
-        hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true, false, true>), dim3(tiles), dim3(256), lds,
-                           st, p);
-      return;
-    }
   }
   if (cbig && !lhs)
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, true, false, BNB>), dim3(tiles), dim3(256), lds, st, p);
@@ -592,12 +530,6 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
 }
 
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
-  if (p.w_lo != nullptr) {  // fp32 path: a register-staged config of <= 128x64 / 64x128, no split-K
-    const int bm = conv_tile_m(cfg), bn = conv_tile_n(cfg);
-    const int rc = bm == 64 ? (bn == 64 ? 2 : 3) : 1;
-    launch_cfg<false>(p, rc, st);
-    return;
-  }
   if (cfg >= CONV_PATCH_CFG0 && cfg < CONV_PATCH_CFG0 + 5) {
     if (launch_conv3x3_patch(p, cfg, st)) return;
     // not a 3x3 / stride-1 problem (or its patch does not fit LDS): an LDS-DMA kernel of the

@@ -101,7 +101,7 @@ struct WgSeg {
   }
 };
 
-// dY operand: rows m, columns = output channels [i0, i0 + COLS). ESZ 4 (fp32 path): a vector of 8
+// dY operand: rows m, columns = output channels [i0, i0 + COLS). ESZ 4 (fp32 operands): a vector of 8
 // values is two 16-byte loads, the second into d2
 template <int ROWS, int COLS, int NT, int ESZ = 2>
 struct WgALoad {
@@ -268,23 +268,18 @@ struct WgBLoadShared {
 };
 
 // RIS: the X loader shares rows across lanes (every column of a tile in one filter tap), else
-// per-lane rows. F32: fp32 dY / X (--compute_dtype fp32), split into bf16 hi / mid / lo while
-// staged to LDS, bf16x6 MFMAs (the six products down to 2^-16 relative, fp32 accumulation).
-template <int WM, int WN, int TM, int TN, bool RIS, bool F32 = false>
+// per-lane rows. (16-bit operands; fp32 runs on the plane GEMMs, conv_p3_wgrad.h.)
+template <int WM, int WN, int TM, int TN, bool RIS>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AVR = BM / 8, BVR = BN / 8;        // 16-byte vectors per LDS row
   constexpr int AV = BK * AVR / 256, BV = BK * BVR / 256;  // vectors per thread
-  constexpr int ESZ = F32 ? 4 : 2;
+  constexpr int ESZ = 2;
   static_assert(WM * WN == 4, "4 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* As = smem;                       // [2][BK][BM] bf16, 2*BM bytes per row
   char* Bs = smem + 2 * BK * BM * 2;     // [2][BK][BN]
-  char* Asl = Bs + 2 * BK * BN * 2;      // fp32 path: the lo and mid images
-  char* Bsl = Asl + 2 * BK * BM * 2;
-  char* Asm = Bsl + 2 * BK * BN * 2;
-  char* Bsm = Asm + 2 * BK * BM * 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -361,54 +356,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
           acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
   };
-  // fp32 path: hi / lo fragments of both operands (same transposed reads on the two images)
-  auto frag = [&](auto rd, const char* base, int krow, int col) -> u32x4 {
-    short4v lo = rd(base, krow, col);
-    short4v hi = rd(base, krow + 4, col);
-    short8 t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(u32x4, t);
-  };
-  auto mfma_kstep6 = [&](int off_a, int off_b) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      u32x4 ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        ah[i] = frag(tr_read_a, As + off_a, ks * 32 + 8 * g, wm * TM + i * 16);
-        am[i] = frag(tr_read_a, Asm + off_a, ks * 32 + 8 * g, wm * TM + i * 16);
-        al[i] = frag(tr_read_a, Asl + off_a, ks * 32 + 8 * g, wm * TM + i * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        bh[j] = frag(tr_read_b, Bs + off_b, ks * 32 + 8 * g, wn * TN + j * 16);
-        bm[j] = frag(tr_read_b, Bsm + off_b, ks * 32 + 8 * g, wn * TN + j * 16);
-        bl[j] = frag(tr_read_b, Bsl + off_b, ks * 32 + 8 * g, wn * TN + j * 16);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {  // small terms first
-          acc[i][j] = mfma_bf16(al[i], bh[j], acc[i][j]);
-          acc[i][j] = mfma_bf16(ah[i], bl[j], acc[i][j]);
-          acc[i][j] = mfma_bf16(am[i], bm[j], acc[i][j]);
-          acc[i][j] = mfma_bf16(am[i], bh[j], acc[i][j]);
-          acc[i][j] = mfma_bf16(ah[i], bm[j], acc[i][j]);
-          acc[i][j] = mfma_bf16(ah[i], bh[j], acc[i][j]);
-        }
-    }
-  };
-
   // Two register sets: the loads of k-step k+2 are issued while k-step k is multiplied and
   // k+1 is stored to LDS, so a load has two k-steps (not one) of MFMA time to land -- the
   // 64x64 tile's 8 MFMAs per wave and k-step are far shorter than an L2 round trip.
-  u32x4 sa[2][AV], sb[2][BV], sa2[2][F32 ? AV : 1], sb2[2][F32 ? BV : 1];
+  u32x4 sa[2][AV], sb[2][BV];
   // rows past this split's range come back as zeros without memory traffic, so the loads
   // and stores of the pipeline tail need no conditions (straight-line k-loop)
   const int mend = min(kt_end * BK, p.M);
   auto ld = [&](auto set_c) {
     constexpr int S = decltype(set_c)::value;
-    ald.load(dyr, mend, sa[S], F32 ? sa2[S] : nullptr);
-    bld.load(p, xr, mend, sb[S], F32 ? sb2[S] : nullptr);
+    ald.load(dyr, mend, sa[S], nullptr);
+    bld.load(p, xr, mend, sb[S], nullptr);
     ald.advance(a_step);
     bld.advance(adv, p.stride_h);
   };
@@ -417,28 +375,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       const int o = buf * BK * BM * 2 + GA::lds_off(tid, v / GA::SEGV, v % GA::SEGV);
-      if constexpr (F32) {
-        u32x4 hi, mid, lo;
-        split3_8(sa[S][v], sa2[S][v], hi, mid, lo);
-        *reinterpret_cast<u32x4*>(As + o) = hi;
-        *reinterpret_cast<u32x4*>(Asm + o) = mid;
-        *reinterpret_cast<u32x4*>(Asl + o) = lo;
-      } else {
-        *reinterpret_cast<u32x4*>(As + o) = sa[S][v];
-      }
+      *reinterpret_cast<u32x4*>(As + o) = sa[S][v];
     }
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const int o = buf * BK * BN * 2 + GB::lds_off(tid, v / GB::SEGV, v % GB::SEGV);
-      if constexpr (F32) {
-        u32x4 hi, mid, lo;
-        split3_8(sb[S][v], sb2[S][v], hi, mid, lo);
-        *reinterpret_cast<u32x4*>(Bs + o) = hi;
-        *reinterpret_cast<u32x4*>(Bsm + o) = mid;
-        *reinterpret_cast<u32x4*>(Bsl + o) = lo;
-      } else {
-        *reinterpret_cast<u32x4*>(Bs + o) = sb[S][v];
-      }
+      *reinterpret_cast<u32x4*>(Bs + o) = sb[S][v];
     }
   };
   using I0 = std::integral_constant<int, 0>;
@@ -451,10 +393,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   auto kstep = [&](auto cur_c, int k) {
     constexpr int cur = decltype(cur_c)::value;
     ld(cur_c);  // k-step k + 2 into set `cur` (stored to LDS one k-step ago)
-    if constexpr (F32)
-      mfma_kstep6(cur * BK * BM * 2, cur * BK * BN * 2);
-    else
-      mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
+    mfma_kstep(As + cur * BK * BM * 2, Bs + cur * BK * BN * 2);
     st(std::integral_constant<int, cur ^ 1>{}, cur ^ 1);  // k-step k + 1
     __syncthreads();
   };
@@ -905,9 +844,7 @@ template <int WM, int WN, int TM, int TN>
 static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
-  // fp32: three staged images per operand (no 128x128 tile: 192 KB)
-  constexpr bool F32OK = 2 * 64 * (BM + BN) * 2 * 3 <= 160 * 1024;
-  size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2 * (p.f32in ? 3 : 1);
+  size_t lds_main = (size_t)2 * 64 * (BM + BN) * 2;
   size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   dim3 grid(tiles * splits);
@@ -917,29 +854,12 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if constexpr (F32OK) {
-      (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, false, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)conv_wgrad_kernel<WM, WN, TM, TN, true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    }
     once = true;
   }
-  const bool shared = wgrad_one_tap(p, BN);
-  if constexpr (F32OK) {
-    if (p.f32in) {
-      if (shared)
-        hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true, true>), grid, dim3(256), lds, st, p);
-      else
-        hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false, true>), grid, dim3(256), lds, st, p);
-      return;
-    }
-  }
-  if (shared) {
+  if (wgrad_one_tap(p, BN))
     hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, true>), grid, dim3(256), lds, st, p);
-  } else {
+  else
     hipLaunchKernelGGL((conv_wgrad_kernel<WM, WN, TM, TN, false>), grid, dim3(256), lds, st, p);
-  }
 }
 
 // cfg 0..2: register-staged {128x128, 64x128, 64x64}; 3..9: LDS-DMA ring {128x128 (4 waves of
@@ -961,13 +881,6 @@ int wgrad_tile_n(int cfg) {
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st) {
   // the register-staged loaders keep a thread's 16-byte vector inside one filter tap (every
   // weight pack already requires C % 8 == 0; bindings.cpp checks it)
-  if (p.f32in) {  // fp32 path: the register-staged kernel of the nearest tile (split-K kept)
-    const int bm = wgrad_tile_m(cfg), bn = wgrad_tile_n(cfg);
-    if (bm >= 128) wlaunch<2, 2, 64, 32>(p, splits, st);
-    else if (bn >= 128) wlaunch<1, 4, 64, 32>(p, splits, st);
-    else wlaunch<2, 2, 32, 32>(p, splits, st);
-    return;
-  }
   switch (cfg) {
     case 0: wlaunch<2, 2, 64, 64>(p, splits, st); break;  // 128 x 128
     case 1: wlaunch<1, 4, 64, 32>(p, splits, st); break;  // 64 x 128

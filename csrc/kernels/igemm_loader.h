@@ -125,40 +125,4 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// bf16x6 step of the fp32 path: the A / B tiles staged as three bf16 images each (hi, mid, lo
-// at IMG u32x4 apart); the six products down to 2^-16 relative, small terms first
-template <int WM, int WN, int TM, int TN>
-__device__ __forceinline__ void mfma_tile_step6(const u32x4* A, const u32x4* B, int aimg, int bimg,
-                                                f32x4 (&acc)[TM / 16][TN / 16], int wm, int wn, int lane) {
-  constexpr int MI = TM / 16, NI = TN / 16;
-  const int frow = lane & 15, fq = lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    u32x4 a[3][MI], b[3][NI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int row = wm * TM + i * 16 + frow, ch = ks * 4 + fq, o = row * 8 + (ch ^ ((row >> 1) & 7));
-#pragma unroll
-      for (int t = 0; t < 3; ++t) a[t][i] = A[t * aimg + o];
-    }
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int row = wn * TN + j * 16 + frow, ch = ks * 4 + fq, o = row * 8 + (ch ^ ((row >> 1) & 7));
-#pragma unroll
-      for (int t = 0; t < 3; ++t) b[t][j] = B[t * bimg + o];
-    }
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        acc[i][j] = mfma_bf16(a[2][i], b[0][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[0][i], b[2][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[1][i], b[1][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[1][i], b[0][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[0][i], b[1][j], acc[i][j]);
-        acc[i][j] = mfma_bf16(a[0][i], b[0][j], acc[i][j]);
-      }
-  }
-}
-
 }  // namespace hcb

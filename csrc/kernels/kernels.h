@@ -73,12 +73,7 @@ struct ConvParams {
   // stream-K (plane GEMMs): sk_grid > 0 workgroups each take an even share of all (tile, k-slot)
   // iterations; a tile's shares meet in ws slabs [tile][sk_smax][tile elems] (splits == 1)
   int sk_grid, sk_smax;
-  // fp32 activations (the reference's precision, --compute_dtype fp32): x is fp32 NHWC and the
-  // weights come as three bf16 packs, w (high part), w_lo (bf16 of the residual) and w_lo2 (bf16
-  // of what is left); the register-staged loop splits every loaded fp32 value into bf16
-  // hi + mid + lo the same way while staging it to LDS and issues the six MFMA products down to
-  // 2^-16 relative (bf16x6: ~2^-24 per product, fp32 accumulation); output fp32 (out_f32).
-  // Register-staged tile configs of <= 128x64 only, no split-K.
+  // plane GEMMs (conv_p3.hip, the fp32 path): the mid and lo bf16 weight packs beside w (hi)
   const void* w_lo;
   const void* w_lo2;
   // 3x3 / stride-1 patch kernels (conv3x3_patch.hip; set by their launcher): LDS rows reserved
@@ -104,8 +99,8 @@ int conv_tile_n(int cfg);
 
 // weight-gradient implicit GEMM: dW[Nout][K] += sum_m dY[m][Nout] * im2col(X)[m][K]
 struct WgradParams {
-  const void* dy;  // [M][ldy] bf16 (fp32 when f32in)
-  const void* x;   // NHWC bf16 (fp32 when f32in), pixel stride ldx
+  const void* dy;  // [M][ldy] 16-bit (the hi plane on the plane path)
+  const void* x;   // NHWC 16-bit (the hi plane on the plane path), pixel stride ldx
   float* dw;       // [Nout][K] fp32 (atomically accumulated)
   int N, H, W, C, ldx;
   int P, Q, R, S;
@@ -114,7 +109,6 @@ struct WgradParams {
   int ksteps_per_split;
   FastDiv fd_pq, fd_q, fd_c, fd_s;
   uint32_t dy_bytes, x_bytes;
-  int f32in;  // fp32 operands, split into bf16 hi + mid + lo while staged (register-staged cfgs only)
   // bf16-plane operands (conv_p3.hip): dy / x as three bf16 planes dy_plane / x_plane bytes apart
   uint32_t dy_plane, x_plane;
 };
