@@ -71,8 +71,9 @@ TUNE_ISOLATE = False
 
 
 def _time(fn, reps=None) -> float:
-    # HCB_TUNE_REPS: timed launches per candidate (default 5; more = less noise, slower tuning)
-    reps = reps or int(os.environ.get("HCB_TUNE_REPS", "5"))
+    # HCB_TUNE_REPS: timed launches per candidate (default 20; a 20-launch fp32 retune ran the step
+    # 1.3% faster than the 5-launch one, interleaved A/B: profiles/r4rt_fp32_retune_reps.txt)
+    reps = reps or int(os.environ.get("HCB_TUNE_REPS", "20"))
     fn()
     if TUNE_ISOLATE:
         # step-like timing: each launch timed on its own, after a 64 MB write that evicts the
