@@ -67,7 +67,7 @@ _SCRATCH = {}
 # per-launch isolated timing (module switch): each candidate launch timed on its own after a 64 MB
 # eviction write, median of the launches. Measured against the default back-to-back timing:
 # +0.3% step (within run-to-run noise), equal with the KU=2 configs offered (profiles/r3x_ku2_cache_ab.txt)
-TUNE_ISOLATE = False
+TUNE_ISOLATE = os.environ.get("HCB_TUNE_ISOLATE", "0") == "1"
 
 
 def _time(fn, reps=None) -> float:
