@@ -55,14 +55,15 @@ if red is not None:
 """
 
 
-def _run(mode, serialize):
+def _run(mode, serialize, extra_env=None):
     env = dict(os.environ)
+    env.update(extra_env or {})
     if serialize:
         env.update(AMD_SERIALIZE_KERNEL="3", AMD_SERIALIZE_COPY="3", HIP_LAUNCH_BLOCKING="1")
     if mode == "dp":
         env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29650 + int(serialize)), RANK="0", WORLD_SIZE="1",
                    LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
-    out = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, mode], env=env, capture_output=True, text=True,
+    out = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, mode.split("+")[0]], env=env, capture_output=True, text=True,
                          timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
     return json.loads(out.stdout.strip().splitlines()[-1])
@@ -75,3 +76,18 @@ def test_serialised_run_equals_async_run(mode):
     assert a["graph"] and a["overlap"] == (mode == "dp")
     assert a["losses"] == s["losses"], (a["losses"], s["losses"])
     assert a["master"] == s["master"], "weights differ between the asynchronous and the serialised run"
+
+
+@pytest.mark.parametrize("mode", ["single", "dp"])
+def test_wgrad_side_stream_equals_serialised_and_main_stream(mode):
+    """HCB_WGRAD_STREAM=1 (weight-gradient GEMMs forked onto a side stream beside the data-gradient
+    chain, joined per backward segment): bitwise equal to its kernel-serialised run AND to the
+    main-stream run -- the fork / join and the operand lifetimes (nn/layers.py run_wgrad) leave
+    no race."""
+    side = {"HCB_WGRAD_STREAM": "1"}
+    a = _run(mode, serialize=False, extra_env=side)
+    s = _run(mode, serialize=True, extra_env=side)
+    m = _run(mode, serialize=False)
+    assert a["graph"]
+    assert a["losses"] == s["losses"] == m["losses"], (a["losses"], s["losses"], m["losses"])
+    assert a["master"] == s["master"] == m["master"]
