@@ -144,8 +144,11 @@ class ResNet(CNNModel):
             if cut:
                 yield seg, False
                 seg = []
-        dx = self.pool.backward(dx)
-        self.stem.backward(dx)
+        if L.FUSE_STEM_POOL_BWD and getattr(self.stem, "_pool_fused", None) is self.pool and Fn.native(dx):
+            self.stem.backward_from_maxpool(dx, self.pool)  # no max-pool backward kernel
+        else:
+            dx = self.pool.backward(dx)
+            self.stem.backward(dx)
         self._last = None
         yield seg + [self.pool, self.stem], True
 

@@ -119,6 +119,8 @@ class Layer:
 class ConvBN(Layer):
     """conv(k x k, stride, padding) -> BatchNorm(train) -> [residual add] -> [ReLU]."""
 
+    _pool_fused = None  # the Pool whose forward ran fused into this layer's BN (forward_maxpool)
+
     def __init__(self, ps: ParamStore, name: str, in_shape, cout: int, kh: int, kw: int, sh: int = 1,
                  sw: int = 1, mode="SAME", relu: bool = True, bn: bool = True, need_dx: bool = True,
                  eps: float = 1e-5, decay: float = 0.9, logical_cin: Optional[int] = None,
@@ -272,7 +274,30 @@ class ConvBN(Layer):
                                        amax, *pool.k, *pool.s, pool.pads, shift=self._shift())
         self._saved = (x, z, None, saved, False)
         pool._saved = (z, y, amax)  # the argmax backward reads only shapes from x / y
+        self._pool_fused = pool
         return y
+
+    def backward_from_maxpool(self, dyp, pool: "Pool"):
+        """Backward of forward_maxpool without the full-size BN output gradient: the BN backward
+        reduce and apply gather it from the pool's gradient ``dyp`` through the saved argmax
+        (bn.hip pool_gather), so the max-pool backward kernel and its conv-sized output (written
+        once, read twice) are gone. Then the weight gradient; the stem needs no dx."""
+        assert self._pool_fused is pool and not self.need_dx
+        x, z, _, saved, _ = self._saved
+        _, _, amax = pool._saved
+        N = dyp.shape[0]
+        H, W, C = self.out_shape
+        P, Q, _ = pool.out_shape
+        pt, _, pl, _ = pool.pads
+        dz = empty_op((N, H, W, C), dyp.device)
+        _, acc_b, R = self._acc
+        Fn.bn_backward_acc(dyp, None, z, saved, self.gamma.data, self.beta.data, 2, self.gamma.grad, self.beta.grad,
+                           dz, acc_b, R, None, shift_out=self._shift(),
+                           pool=(amax, [H, W, P, Q, pool.k[0], pool.s[0], pt, pl]))
+        run_wgrad(self, dz, x)
+        self._saved = None
+        self._pool_fused = None
+        pool._saved = None
 
     def _conv_fwd_stats(self, x, z):
         """GPU conv with the BN statistics in its epilogue; returns the tensor the weight
@@ -395,6 +420,10 @@ def wgrad_join():
 
 # GPU ResNet stem as a space-to-depth 4x4/1 GEMM (False: the direct padded 7x7/2 form)
 STEM_S2D = True
+
+
+# ResNet stem: the BN backward gathers dy from the max pool's gradient (ConvBN.backward_from_maxpool)
+FUSE_STEM_POOL_BWD = os.environ.get("HCB_FUSE_STEM_POOL_BWD", "1") == "1"
 
 
 class StemS2D(ConvBN):

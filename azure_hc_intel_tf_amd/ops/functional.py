@@ -978,12 +978,14 @@ def bn_relu_maxpool_acc(z, gamma, beta, running_mean, running_var, momentum, eps
 
 
 def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, acc, R: int,
-                    gres=None, pre_reduced: bool = False, shift_out=None):
+                    gres=None, pre_reduced: bool = False, shift_out=None, pool=None):
     """GPU BN(+ReLU) backward with the dgamma/dbeta reduction accumulated in ``acc`` replicas
     (zeroed per step) and consumed directly by the apply kernel. ``pre_reduced``: dy is already
     the gated g and ``acc`` already holds its sums (a BNBwdFuse data-grad epilogue produced it),
     so only the apply pass runs. ``shift_out``: receives this step's batch mean, the statistics
-    shift of the layer's next forward."""
+    shift of the layer's next forward. ``pool`` = (amax, [H, W, P, Q, k, s, pt, pl]): dy is the
+    gradient of the max pool that followed this BN+ReLU (the ResNet stem) and both passes gather
+    the full-size dy from it through the pool's argmax (it is never materialised)."""
     N, H, W, C = z.shape
     M = N * H * W
     hcb = _ext.ops()
@@ -993,10 +995,11 @@ def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamm
                              beta, acc, R, dgamma, dbeta, 0, shift_out)
         return dz
     ym = _pl(y) if relu_mode == 1 else None
+    pa, pg = pool if pool is not None else (None, None)
     hcb.bn_bwd_reduce_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), M, C, saved.mean, saved.invstd,
-                          gamma, beta, relu_mode, acc, R, gres, ld(gres) if gres is not None else 0)
+                          gamma, beta, relu_mode, acc, R, gres, ld(gres) if gres is not None else 0, pa, pg)
     hcb.bn_bwd_apply_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), _pl(dz), ld(dz), M, C, saved.mean,
-                         saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode, shift_out)
+                         saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode, shift_out, pa, pg)
     return dz
 
 

@@ -713,16 +713,45 @@ void bn_apply_acc(const Tensor& x, int64_t ldx, const Tensor& y, int64_t ldy, co
                            res_acc.has_value() ? &rb : nullptr, cur_stream(), f32, yps, rps);
 }
 
+// pooled-gradient source (pool_amax / pool_geom = [H, W, P, Q, k, s, pt, pl]): dy is the max-pool
+// gradient [N][P][Q] (row stride lddy) and amax its window-local argmax [N][P][Q][C]; returns the
+// number of dy rows to range-check
+int64_t pool_src(hcb::PoolSrc& ps, const Tensor& dy, int64_t lddy, int64_t M, int64_t C,
+                 const c10::optional<Tensor>& amax, at::OptionalIntArrayRef geom) {
+  TORCH_CHECK(amax.has_value() == geom.has_value(), "hcb.bn_bwd: pool_amax and pool_geom go together");
+  if (!amax.has_value()) return M;
+  TORCH_CHECK(geom->size() == 8, "hcb.bn_bwd: pool_geom = [H, W, P, Q, k, s, pt, pl]");
+  const auto g = *geom;
+  ps.H = (int)g[0]; ps.W = (int)g[1]; ps.P = (int)g[2]; ps.Q = (int)g[3];
+  ps.k = (int)g[4]; ps.s = (int)g[5]; ps.pt = (int)g[6]; ps.pl = (int)g[7];
+  ps.C = (int)C;
+  ps.ldp = (int)lddy;
+  TORCH_CHECK(ps.H > 0 && ps.W > 0 && M % ((int64_t)ps.H * ps.W) == 0, "hcb.bn_bwd: M vs H x W");
+  TORCH_CHECK(ps.s >= 1 && ps.k >= 1 && ps.k <= 2 * ps.s && ps.pt >= 0 && ps.pl >= 0 && ps.pt < ps.k && ps.pl < ps.k,
+              "hcb.bn_bwd: pool windows must overlap at most 2 x 2 per pixel");
+  const int64_t N = M / ((int64_t)ps.H * ps.W), rows = N * ps.P * ps.Q;
+  TORCH_CHECK(amax->scalar_type() == at::kByte && amax->is_cuda() && amax->is_contiguous() &&
+                  amax->numel() >= rows * C, "hcb.bn_bwd: pool_amax must be uint8 [N][P][Q][C]");
+  TORCH_CHECK(lddy % 8 == 0, "hcb.bn_bwd: pooled dy row stride");
+  ps.dyp = dy.data_ptr();
+  ps.amax = amax->data_ptr<uint8_t>();
+  return rows;
+}
+
 void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
                        const Tensor& x, int64_t ldx, int64_t M, int64_t C, const Tensor& mean, const Tensor& invstd,
                        const Tensor& gamma, const Tensor& beta, int64_t relu, const Tensor& acc, int64_t R,
-                       const c10::optional<Tensor>& gout, int64_t ldg) {
+                       const c10::optional<Tensor>& gout, int64_t ldg, const c10::optional<Tensor>& pool_amax,
+                       at::OptionalIntArrayRef pool_geom) {
   const bool f32 = check_act_or_f32(dy, "dy");
   same_act(dy, x, "x");
   const int64_t e = f32 ? 4 : 2;
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_reduce_acc: C/R");
-  check_range(dy, ((M - 1) * lddy + C) * e, "dy");
+  hcb::PoolSrc ps{};
+  const int64_t dyrows = pool_src(ps, dy, lddy, M, C, pool_amax, pool_geom);
+  TORCH_CHECK(!pool_amax.has_value() || (!gout.has_value() && relu != 1), "hcb.bn_bwd_reduce_acc: pooled dy: no gout / y");
+  check_range(dy, ((dyrows - 1) * lddy + C) * e, "dy");
   check_range(x, ((M - 1) * ldx + C) * e, "x");
   const void* yp = nullptr;
   bool yh = false;  // fp32 path: y given as its bf16 planes, the mask read from the hi plane
@@ -747,14 +776,15 @@ void bn_bwd_reduce_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tenso
   hcb::launch_bn_bwd_reduce_acc(dy.data_ptr(), (int)lddy, yp, (int)ldyv, x.data_ptr(), (int)ldx, (int)M, (int)C,
                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
                                 beta.data_ptr<float>(), (int)relu, acc.data_ptr<float>(), (int)R, gp, (int)ldg,
-                                cur_stream(), f32, yh);
+                                cur_stream(), f32, yh, pool_amax.has_value() ? &ps : nullptr);
 }
 
 void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor>& y, int64_t ldyv,
                       const Tensor& x, int64_t ldx, const Tensor& dx, int64_t lddx, int64_t M, int64_t C,
                       const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
                       const Tensor& acc, int64_t R, const Tensor& dgamma, const Tensor& dbeta, int64_t relu,
-                      const c10::optional<Tensor>& shift_out) {
+                      const c10::optional<Tensor>& shift_out, const c10::optional<Tensor>& pool_amax,
+                      at::OptionalIntArrayRef pool_geom) {
   const bool f32 = check_act_or_f32(dy, "dy");
   same_act(dy, x, "x");
   // fp32 dy with a bf16 dx: dx is written as [3, ...] bf16 planes (the data / weight-gradient
@@ -765,7 +795,10 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
   const int64_t e = f32 ? 4 : 2;
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_apply_acc: C/R");
-  check_range(dy, ((M - 1) * lddy + C) * e, "dy");
+  hcb::PoolSrc ps{};
+  const int64_t dyrows = pool_src(ps, dy, lddy, M, C, pool_amax, pool_geom);
+  TORCH_CHECK(!pool_amax.has_value() || (relu != 1 && dp3 == f32), "hcb.bn_bwd_apply_acc: pooled dy: no y; fp32 writes planes");
+  check_range(dy, ((dyrows - 1) * lddy + C) * e, "dy");
   check_range(x, ((M - 1) * ldx + C) * e, "x");
   check_range(dx, dp3 ? (2 * dxps + (M - 1) * lddx + C) * 2 : ((M - 1) * lddx + C) * e, "dx");
   const void* yp = nullptr;
@@ -786,7 +819,8 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
                                (int)lddx, (int)M, (int)C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                gamma.data_ptr<float>(), beta.data_ptr<float>(), acc.data_ptr<float>(), (int)R,
                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu,
-                               const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream(), f32, yh, dxps);
+                               const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream(), f32, yh, dxps,
+                               pool_amax.has_value() ? &ps : nullptr);
 }
 
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
@@ -1141,8 +1175,8 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("scale_f32(Tensor(a!) x, float s) -> ()");
   m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
   m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor? shift=None, Tensor? res_acc=None, Tensor? res_gamma=None, Tensor? res_beta=None, Tensor(g!)? res_saved_mean=None, Tensor(h!)? res_saved_invstd=None, Tensor(i!)? res_running_mean=None, Tensor(j!)? res_running_var=None, Tensor? res_shift=None) -> ()");
-  m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg) -> ()");
-  m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu, Tensor(d!)? shift_out=None) -> ()");
+  m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg, Tensor? pool_amax=None, int[]? pool_geom=None) -> ()");
+  m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu, Tensor(d!)? shift_out=None, Tensor? pool_amax=None, int[]? pool_geom=None) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
   m.def("preprocess_images(Tensor src, Tensor desc, Tensor desc_host, Tensor(a!) out, float[] scale, float[] bias) -> ()");
   m.def("bn_relu_maxpool_acc(Tensor z, Tensor(a!) y, Tensor(b!) amax, int[] geom, Tensor acc, int R, float eps, "

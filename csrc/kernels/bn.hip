@@ -237,14 +237,55 @@ __device__ __forceinline__ void bwd_math(const u32x4& dv, const u32x4& xvv, cons
 // element-type generic forms (T = the build's 16-bit type or fp32) used by the finalize-free kernels
 // TY: element type of the ReLU-mask source y -- T, or (fp32 path) uint16_t: the bf16 hi plane of the
 // plane-stored activation (hi > 0 exactly when y > 0 for every normal y)
-template <typename T, typename TY = T>
+// BN backward fed straight from a max-pool's gradient (the ResNet stem: BN -> ReLU -> 3x3/2 max
+// pool): dy of pixel (n, h, w) is gathered from the pooled gradient dyp of the <= 2x2 windows that
+// contain it and whose argmax (amax, window-local index per channel) is this pixel -- the
+// full-size dy is never written (it was written by maxpool_bwd_amax_kernel and read twice).
+template <typename T>
+__device__ __forceinline__ void pool_gather(const PoolSrc& ps, int m, int M, int cv, Act8<T>& d) {
+  float g[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = 0.f;
+  if (m < M) {
+    const int w = m % ps.W, t = m / ps.W;
+    const int h = t % ps.H, n = t / ps.H;
+    const int p_hi = (h + ps.pt) / ps.s, q_hi = (w + ps.pl) / ps.s;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = p_hi - i;
+      if (p < 0 || p >= ps.P || h - (p * ps.s - ps.pt) >= ps.k) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q = q_hi - j;
+        if (q < 0 || q >= ps.Q || w - (q * ps.s - ps.pl) >= ps.k) continue;
+        const size_t o = (size_t)(n * ps.P + p) * ps.Q + q;
+        const int mine = (h - (p * ps.s - ps.pt)) * ps.k + (w - (q * ps.s - ps.pl));
+        const u32x2 a = *reinterpret_cast<const u32x2*>(ps.amax + o * ps.C + cv * 8);
+        Act8<T> dv;
+        dv.load(reinterpret_cast<const T*>(ps.dyp) + o * ps.ldp + cv * 8);
+        float f[8];
+        dv.to_f(f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((a[e >> 2] >> (8 * (e & 3))) & 0xff) == mine) g[e] += f[e];
+      }
+    }
+  }
+  d.set_f(g);
+}
+
+template <typename T, typename TY = T, bool POOL = false>
 struct BwdSrcT {
   __amdgpu_buffer_rsrc_t dyr, xr, yr;
   int lddy, ldx, ldyv, cv;
+  PoolSrc pool;
   __device__ __forceinline__ void load(int m, int M, int relu, Act8<T>& d, Act8<T>& x, Act8<TY>& y) const {
     const bool ok = m < M;
     constexpr uint32_t E = Act8<T>::ESZ;
-    d.load(dyr, ok ? (uint32_t)((size_t)m * lddy + cv * 8) * E : HCB_OOB);
+    if constexpr (POOL)
+      pool_gather<T>(pool, m, M, cv, d);
+    else
+      d.load(dyr, ok ? (uint32_t)((size_t)m * lddy + cv * 8) * E : HCB_OOB);
     x.load(xr, ok ? (uint32_t)((size_t)m * ldx + cv * 8) * E : HCB_OOB);
     if (relu == 1) y.load(yr, ok ? (uint32_t)((size_t)m * ldyv + cv * 8) * Act8<TY>::ESZ : HCB_OOB);
   }
@@ -722,11 +763,11 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
   }
 }
 
-template <typename T = uint16_t, typename TY = T>
+template <typename T = uint16_t, typename TY = T, bool POOL = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
     const T* __restrict__ dy, int lddy, const TY* __restrict__ y, int ldyv,
     const T* __restrict__ x, int ldx, int M, int C, int CVB, const float* mean, const float* invstd,
-    const float* gamma, const float* beta, int relu, float* acc, int R, T* gout, int ldg) {
+    const float* gamma, const float* beta, int relu, float* acc, int R, T* gout, int ldg, PoolSrc pool) {
   constexpr uint32_t E = Act8<T>::ESZ;
   extern __shared__ __attribute__((aligned(16))) float lds_f[];  // [2][rows][CB]
   const GroupMap gm = groupmap(CVB);
@@ -743,9 +784,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
       sh[e] = beta[c] - mu[e] * sc[e];
     }
     constexpr uint32_t EY = Act8<TY>::ESZ;
-    BwdSrcT<T, TY> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
-                       y != nullptr ? make_rsrc(y, rsrc_bytes(M, ldyv, EY)) : make_rsrc(x, rsrc_bytes(M, ldx, E)), lddy,
-                       ldx, ldyv, gm.cv};
+    BwdSrcT<T, TY, POOL> src{make_rsrc(POOL ? x : dy, rsrc_bytes(M, POOL ? ldx : lddy, E)),
+                             make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                             y != nullptr ? make_rsrc(y, rsrc_bytes(M, ldyv, EY)) : make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                             lddy, ldx, ldyv, gm.cv, pool};
     const int stride = gridDim.x * gm.rows;
     for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
       Act8<T> dv[BN_U], xv[BN_U];
@@ -790,20 +832,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
 
 // P3 (fp32 path): dx is written as bf16 hi / mid / lo planes (plane stride dxps elements), the
 // operand format of the data- and weight-gradient GEMMs that consume it
-template <typename T = uint16_t, typename TY = T, bool P3 = false>
+template <typename T = uint16_t, typename TY = T, bool P3 = false, bool POOL = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     const T* __restrict__ dy, int lddy, const TY* __restrict__ y, int ldyv,
     const T* __restrict__ x, int ldx, void* __restrict__ dxv, int lddx, int M, int C, int CVB,
     const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
-    int R, float* dgamma, float* dbeta, int relu, float* shift_out, int64_t dxps) {
+    int R, float* dgamma, float* dbeta, int relu, float* shift_out, int64_t dxps, PoolSrc pool) {
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]: dbeta, dgamma
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
   constexpr uint32_t E = Act8<T>::ESZ, EY = Act8<TY>::ESZ;
   T* __restrict__ dx = reinterpret_cast<T*>(dxv);
-  BwdSrcT<T, TY> src{make_rsrc(dy, rsrc_bytes(M, lddy, E)), make_rsrc(x, rsrc_bytes(M, ldx, E)),
-                     y != nullptr ? make_rsrc(y, rsrc_bytes(M, ldyv, EY)) : make_rsrc(x, rsrc_bytes(M, ldx, E)), lddy,
-                     ldx, ldyv, gm.cv};
+  BwdSrcT<T, TY, POOL> src{make_rsrc(POOL ? x : dy, rsrc_bytes(M, POOL ? ldx : lddy, E)),
+                           make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                           y != nullptr ? make_rsrc(y, rsrc_bytes(M, ldyv, EY)) : make_rsrc(x, rsrc_bytes(M, ldx, E)),
+                           lddy, ldx, ldyv, gm.cv, pool};
   const int stride = gridDim.x * gm.rows;
   const int mfirst = blockIdx.x * gm.rows + gm.r0;
   Act8<T> dv[BN_U], xv[BN_U];
@@ -1058,51 +1101,70 @@ void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void*
 
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
-                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32, bool yh) {
+                              int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32, bool yh,
+                              const PoolSrc* pool) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   // every block adds into replica blockIdx.x % R; deterministic mode: at most R row blocks, so
   // each replica slot gets one add (the kernel strides over the rows with any grid)
   if (deterministic() && (int)grid.x > R) grid.x = R;
   size_t lds = (size_t)2 * (256 / cvb) * cvb * 8 * 4;
-  if (f32 && yh)
+  const PoolSrc ps = pool != nullptr ? *pool : PoolSrc{};
+  if (pool != nullptr && f32)
+    hipLaunchKernelGGL((bn_bwd_reduce_acc_kernel<float, float, true>), grid, dim3(256), lds, st, (const float*)dy,
+                       lddy, (const float*)y, ldyv, (const float*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu,
+                       acc, R, (float*)gout, ldg, ps);
+  else if (pool != nullptr)
+    hipLaunchKernelGGL((bn_bwd_reduce_acc_kernel<uint16_t, uint16_t, true>), grid, dim3(256), lds, st,
+                       (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, cvb, mean,
+                       invstd, gamma, beta, relu, acc, R, (uint16_t*)gout, ldg, ps);
+  else if (f32 && yh)
     hipLaunchKernelGGL((bn_bwd_reduce_acc_kernel<float, uint16_t>), grid, dim3(256), lds, st, (const float*)dy, lddy,
                        (const uint16_t*)y, ldyv, (const float*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu, acc,
-                       R, (float*)gout, ldg);
+                       R, (float*)gout, ldg, ps);
   else if (f32)
     hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel<float>, grid, dim3(256), lds, st, (const float*)dy, lddy,
                        (const float*)y, ldyv, (const float*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu, acc, R,
-                       (float*)gout, ldg);
+                       (float*)gout, ldg, ps);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_acc_kernel<uint16_t>, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
                        (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, M, C, cvb, mean, invstd, gamma, beta, relu,
-                       acc, R, (uint16_t*)gout, ldg);
+                       acc, R, (uint16_t*)gout, ldg, ps);
 }
 
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
-                             float* shift_out, hipStream_t st, bool f32, bool yh, int64_t dxps) {
+                             float* shift_out, hipStream_t st, bool f32, bool yh, int64_t dxps, const PoolSrc* pool) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   const size_t lds = (size_t)2 * cvb * 8 * 4;
-  if (f32 && dxps > 0) {
+  const PoolSrc ps = pool != nullptr ? *pool : PoolSrc{};
+  if (pool != nullptr && f32 && dxps > 0) {
+    hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, float, true, true>), grid, dim3(256), lds, st,
+                       (const float*)dy, lddy, (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean,
+                       invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps);
+  } else if (pool != nullptr && !f32) {
+    hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<uint16_t, uint16_t, false, true>), grid, dim3(256), lds, st,
+                       (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, dx, lddx, M, C,
+                       cvb, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps);
+  } else if (f32 && dxps > 0) {
     if (yh)
       hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, uint16_t, true>), grid, dim3(256), lds, st, (const float*)dy,
                          lddy, (const uint16_t*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd,
-                         gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps);
+                         gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps);
     else
       hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, float, true>), grid, dim3(256), lds, st, (const float*)dy,
                          lddy, (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma,
-                         beta, acc, R, dgamma, dbeta, relu, shift_out, dxps);
+                         beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps);
   } else if (f32) {
     hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<float>, grid, dim3(256), lds, st, (const float*)dy, lddy,
                        (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma, beta, acc,
-                       R, dgamma, dbeta, relu, shift_out, (int64_t)0);
+                       R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps);
   } else {
     hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<uint16_t>, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
                        (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma,
-                       beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0);
+                       beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps);
   }
 }
 

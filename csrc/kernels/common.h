@@ -157,6 +157,7 @@ struct Act8<uint16_t> {
   __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t off) { v = buf_load16(r, off); }
   __device__ __forceinline__ void load(const uint16_t* p) { v = *reinterpret_cast<const u32x4*>(p); }
   __device__ __forceinline__ void to_f(float* f) const { unpack8(v, f); }
+  __device__ __forceinline__ void set_f(const float* f) { v = pack8(f); }
   __device__ __forceinline__ static void store(uint16_t* p, const float* f) {
     *reinterpret_cast<u32x4*>(p) = pack8(f);
   }
@@ -178,6 +179,13 @@ struct Act8<float> {
     for (int i = 0; i < 4; ++i) {
       f[i] = __uint_as_float(a[i]);
       f[4 + i] = __uint_as_float(b[i]);
+    }
+  }
+  __device__ __forceinline__ void set_f(const float* f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = __float_as_uint(f[i]);
+      b[i] = __float_as_uint(f[4 + i]);
     }
   }
   __device__ __forceinline__ static void store(float* p, const float* f) {

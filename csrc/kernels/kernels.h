@@ -198,14 +198,22 @@ void launch_bn_relu_maxpool_acc(const void* z, int N, int H, int W, int C, void*
                                 float momentum, const float* gamma, const float* beta, float* saved_mean,
                                 float* saved_invstd, float* run_mean, float* run_var, const float* shift, hipStream_t st,
                                 bool f32 = false, int64_t yps = 0);
+// pooled-gradient source of the BN backward kernels (bn.hip pool_gather): dy of pixel m of an
+// [N][H][W][C] map gathered from the max-pool gradient dyp [N][P][Q] (row stride ldp) through the
+// window-local argmax amax [N][P][Q][C] of a k x k / s pool with top / left padding pt / pl
+struct PoolSrc {
+  const void* dyp;
+  const uint8_t* amax;
+  int ldp, H, W, P, Q, k, s, pt, pl, C;
+};
 void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, int M,
                               int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
                               int relu, float* acc, int R, void* gout, int ldg, hipStream_t st, bool f32 = false,
-                              bool yh = false);
+                              bool yh = false, const PoolSrc* pool = nullptr);
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu, float* shift_out, hipStream_t st,
-                             bool f32 = false, bool yh = false, int64_t dxps = 0);
+                             bool f32 = false, bool yh = false, int64_t dxps = 0, const PoolSrc* pool = nullptr);
 // fp32 path, plane-stored tensors: (yps / rps / dxps > 0) outputs / residuals as bf16 hi / mid / lo
 // planes with that plane stride in elements; yh: the ReLU-mask source y is the bf16 hi plane
 
