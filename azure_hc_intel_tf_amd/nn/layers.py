@@ -422,8 +422,11 @@ def wgrad_join():
 STEM_S2D = True
 
 
-# ResNet stem: the BN backward gathers dy from the max pool's gradient (ConvBN.backward_from_maxpool)
-FUSE_STEM_POOL_BWD = os.environ.get("HCB_FUSE_STEM_POOL_BWD", "1") == "1"
+# ResNet stem: the BN backward gathers dy from the max pool's gradient (ConvBN.backward_from_maxpool).
+# Bitwise equal (tests/test_stem_pool_bwd_gpu.py) but not faster: the per-pixel window gather (<= 4
+# argmax / gradient loads + index math per 8 channels) costs what the removed 205 MB round trip
+# saved -- fp32 4009 vs 4008 img/s, bf16 0.7% slower (profiles/r4sp_stem_pool_bwd_ab.txt). Off.
+FUSE_STEM_POOL_BWD = os.environ.get("HCB_FUSE_STEM_POOL_BWD", "0") == "1"
 
 
 class StemS2D(ConvBN):

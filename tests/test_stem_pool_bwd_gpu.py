@@ -23,7 +23,7 @@ def _grads(dtype, fused):
         torch.cuda.synchronize()
         return m.ps.grad.clone(), {p.name: p.grad.clone() for p in m.ps.params if p.name.startswith("conv0")}
     finally:
-        L.FUSE_STEM_POOL_BWD = True
+        L.FUSE_STEM_POOL_BWD = False
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
