@@ -10,4 +10,13 @@ the fc-bias gradient's column sum, whose zeroing was a ``hipMemsetAsync`` node i
 third replay). Its zeroing is now part of the kernel (csrc/kernels/misc.hip launch_colsum2) and
 the step graph contains no memset node: with capture on, single-graph and data-parallel replays
 are bitwise equal to capture off (profiles/r4_packet_capture_root_cause.txt).
+
+Multi-rank processes (WORLD_SIZE > 1) still default to packet capture OFF unless the user set the
+variable: the step graph of a real multi-rank job carries RCCL's kernels, a combination only ever
+validated with capture off (the bisection above used a 1-rank communicator); capture on/off makes
+no measurable throughput difference on one GPU.
 """
+import os as _os
+
+if int(_os.environ.get("WORLD_SIZE", "1") or 1) > 1:
+    _os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
