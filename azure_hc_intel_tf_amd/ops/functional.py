@@ -286,6 +286,8 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                # register-pipelined LDS-DMA loop on cfg 4, 5, 7, 12, 13, 14, 16's tiles
                31: (128, 128), 32: (128, 64), 33: (64, 128), 34: (128, 128), 35: (128, 128), 36: (256, 128),
                37: (64, 128)}
+# 100 + i: the plane-GEMM kernel (conv_p3_fwd.h cfg i) on one 16-bit plane (conv_s1.hip); filled in
+# below from _P3_TILES
 PATCH_CFG0 = 17
 PATCH_CFGS = (17, 18, 19, 20, 21)
 TUNE_KU2 = False  # offer cfg 22-26 to the autotuner (see fwd_candidates)
@@ -334,10 +336,11 @@ def fwd_candidates(N: int, patch: bool = False):
     # the fp32 plane GEMMs, whose occupancy tiles win in the step too
     occ = [27, 28, 29, 30] if TUNE_OCC else []
     pipe = [31, 32, 33, 34, 35, 36, 37] if TUNE_PIPE else []
+    s1 = [CONV_S1_BASE + c for c, (bm, bn) in _P3_TILES.items() if bn <= max(64, N)] if TUNE_S1 else []
     if N <= 64:
         return ([1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([29] if occ else []) + ([32] if pipe else [])
-                + ([19, 20] if patch else []))
-    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2 + occ + pipe
+                + ([19, 20] if patch else []) + s1)
+    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2 + occ + pipe + s1
     c = c + [15] if N > 128 else c
     return c + ([17, 18, 19, 20, 21] if patch else [])
 
@@ -459,6 +462,11 @@ def set_tuned(table: dict) -> None:
 _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
              7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
              13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64)}
+_CONV_TILES.update({100 + c: t for c, t in _P3_TILES.items()})
+CONV_S1_BASE = 100
+# offer the one-plane slot-ring kernel (cfg 100-117) to the bf16 / fp16 autotuner: a retune picks it for 19
+# of ResNet-50's 45 problems and the step is unchanged (profiles/r4s1_bf16_slot_ring_fwd.txt)
+TUNE_S1 = False
 # workgroups per CU each plane-GEMM cfg is built for (its stream-K grid: N_CU x occupancy)
 _P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3}
 # wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles),

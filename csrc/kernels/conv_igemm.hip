@@ -477,12 +477,14 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
 // 31..37 the register-pipelined loop (PIPE) on cfg 4, 5, 7, 12, 13, 14, 16's tiles and rings
 constexpr int N_CONV_CFG = 38;
 int conv_tile_m(int cfg) {
+  if (cfg >= CONV_S1_BASE) return p3_tile_m(cfg - CONV_S1_BASE);
   static const int t[N_CONV_CFG] = {128, 128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 256, 128,
                                     64,  128, 256, 256, 128, 128, 64,  128, 128, 64,  64,  128, 128, 128, 64,
                                     128, 128, 64,  128, 128, 256, 64};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
+  if (cfg >= CONV_S1_BASE) return p3_tile_n(cfg - CONV_S1_BASE);
   static const int t[N_CONV_CFG] = {128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 128, 128, 256,
                                     128, 128, 128, 64,  64,  128, 128, 128, 128, 128, 64,  128, 128, 64,  128,
                                     128, 64,  128, 128, 128, 128, 128};
@@ -530,6 +532,10 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
 }
 
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
+  if (cfg >= CONV_S1_BASE) {
+    launch_conv_s1(p, cfg - CONV_S1_BASE, st);
+    return;
+  }
   if (cfg >= CONV_PATCH_CFG0 && cfg < CONV_PATCH_CFG0 + 5) {
     if (launch_conv3x3_patch(p, cfg, st)) return;
     // not a 3x3 / stride-1 problem (or its patch does not fit LDS): an LDS-DMA kernel of the

@@ -30,9 +30,9 @@ struct P3Frags {
 };
 
 // every fragment read of the slot (LDS -> registers), issued back to back
-template <int WM, int WN, int TM, int TN, int KW>
-__device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<TM, TN, KW / 32>& f, int wm, int wn,
-                                        int lane) {
+template <int WM, int WN, int TM, int TN, int KW, int NPL = 3>
+__device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<TM, TN, KW / 32, NPL>& f, int wm,
+                                        int wn, int lane) {
   constexpr int MI = TM / 16, NI = TN / 16, BM = WM * TM, BN = WN * TN, CPR = KW / 8;
   constexpr int AIMG = BM * CPR, BIMG = BN * CPR;  // one plane image, in u32x4
   const int frow = lane & 15, fq = lane >> 4;
@@ -43,13 +43,13 @@ __device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<
     for (int i = 0; i < MI; ++i) {
       const int row = wm * TM + i * 16 + frow, o = row * CPR + (ch ^ p3_swz<KW>(row));
 #pragma unroll
-      for (int t = 0; t < 3; ++t) f.a[ks][t][i] = A[t * AIMG + o];
+      for (int t = 0; t < NPL; ++t) f.a[ks][t][i] = A[t * AIMG + o];
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int row = wn * TN + j * 16 + frow, o = row * CPR + (ch ^ p3_swz<KW>(row));
 #pragma unroll
-      for (int t = 0; t < 3; ++t) f.b[ks][t][j] = B[t * BIMG + o];
+      for (int t = 0; t < NPL; ++t) f.b[ks][t][j] = B[t * BIMG + o];
     }
   }
 }
@@ -79,14 +79,14 @@ __device__ __forceinline__ void p3_mma(const P3Frags<TM, TN, KS, NPL>& f, f32x4 
       }
 }
 
-template <int BM, int BN, int KW>
+template <int BM, int BN, int KW, int NPL = 3>
 constexpr size_t p3_stage_bytes() {
-  return (size_t)3 * (BM + BN) * KW * 2;
+  return (size_t)NPL * (BM + BN) * KW * 2;
 }
 // LDS offset of the fused BN-backward parameters: above the ring and the epilogue staging
-template <int BM, int BN, int WM, int KW, int NST>
+template <int BM, int BN, int WM, int KW, int NST, int NPL = 3>
 constexpr size_t p3_param_off() {
-  const size_t a = NST * p3_stage_bytes<BM, BN, KW>(), b = igemm_epilogue_lds(BM, BN, WM);
+  const size_t a = NST * p3_stage_bytes<BM, BN, KW, NPL>(), b = igemm_epilogue_lds(BM, BN, WM);
   return a > b ? a : b;
 }
 // data-grad GEMMs with at most this many 64-deep k-steps fetch their fused BN-backward epilogue
@@ -107,20 +107,22 @@ template <int OCC, int NW>
 constexpr int p3_regs_per_wave() {
   return 512 / (OCC * NW / 4 > 0 ? OCC * NW / 4 : 1);
 }
+// NPL: operand planes -- 3 (fp32 as bf16 hi / mid / lo, six products, fp32 epilogue) or 1 (a plain
+// 16-bit operand of the build's type, one product, the 16-bit kernels' epilogue: conv_s1.hip)
 template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool LHSDIL, bool BNB, int OCC = 1,
-          bool SK = false>
+          bool SK = false, int NPL = 3>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, CPR = KW / 8, RB = KW * 2;  // threads; chunks and bytes per LDS row
   constexpr int RP = NT / CPR;                                    // tile rows per load pass
   constexpr int AV = BM / RP, BV = BN / RP;
-  constexpr int LOADS = 3 * (AV + BV);  // LDS-DMA instructions per thread per slot
+  constexpr int LOADS = NPL * (AV + BV);  // LDS-DMA instructions per thread per slot
   constexpr int AIMG = BM * RB, BIMG = BN * RB;
-  constexpr int STAGE = (int)p3_stage_bytes<BM, BN, KW>();
+  constexpr int STAGE = (int)p3_stage_bytes<BM, BN, KW, NPL>();
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 1) <= 63 && NST >= 2 && NST <= 4, "vmcnt range");
-  static_assert(p3_param_off<BM, BN, WM, KW, NST>() + bnb_param_lds(BN) <= 160 * 1024,
+  static_assert(p3_param_off<BM, BN, WM, KW, NST, NPL>() + bnb_param_lds(BN) <= 160 * 1024,
                 "ring + BN parameters must fit LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -203,22 +205,26 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       glds16(xr0, sa + RP * v * RB, off[v]);
-      glds16(xr1, sa + AIMG + RP * v * RB, off[v]);
-      glds16(xr2, sa + 2 * AIMG + RP * v * RB, off[v]);
+      if constexpr (NPL > 1) {
+        glds16(xr1, sa + AIMG + RP * v * RB, off[v]);
+        glds16(xr2, sa + 2 * AIMG + RP * v * RB, off[v]);
+      }
     }
-    char* sb = smem + stage * STAGE + 3 * AIMG + wid * WROWS * RB;
+    char* sb = smem + stage * STAGE + NPL * AIMG + wid * WROWS * RB;
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * (uint32_t)RB;
       glds16(wr0, sb + RP * v * RB, o);
-      glds16(wr1, sb + BIMG + RP * v * RB, o);
-      glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
+      if constexpr (NPL > 1) {
+        glds16(wr1, sb + BIMG + RP * v * RB, o);
+        glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
+      }
     }
   };
   if (kb > 0) al.seek(p, kb);
-  EpiPrefetch<WM, WN, TM, TN, BNB, true> pre;
+  EpiPrefetch<WM, WN, TM, TN, BNB, NPL == 3> pre;
   pre.load_shift(p, n0, wn, lane);
-  constexpr size_t PARAM_OFF = p3_param_off<BM, BN, WM, KW, NST>();
+  constexpr size_t PARAM_OFF = p3_param_off<BM, BN, WM, KW, NST, NPL>();
   if constexpr (BNB) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
   const bool early = BNB && parts == 1 && nk * KW <= EARLY_EPI_KSTEPS_P3 * 64;
   if (early) pre.load(p, 0, m0, n0, tid);
@@ -236,27 +242,27 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
     else
       wait_vmcnt<0>();
   };
-  auto read = [&](int k, P3Frags<TM, TN, KW / 32>& f) {
+  auto read = [&](int k, P3Frags<TM, TN, KW / 32, NPL>& f) {
     const char* sb = smem + (k % NST) * STAGE;
-    p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + 3 * AIMG), f,
+    p3_read<WM, WN, TM, TN, KW, NPL>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + NPL * AIMG), f,
                                 wm, wn, lane);
   };
   // two register fragment sets when they fit (PIPE): slot k+1's fragment reads are in flight
   // while slot k's MFMAs run, and ONE barrier per slot both publishes slot k+1's DMA and retires
   // every wave's reads of slot k (which is refilled right after it); otherwise one set, read,
   // then a second barrier before the refill
-  constexpr int FREGS = (MI + NI) * 3 * 4 * (KW / 32), AREGS = MI * NI * 4;
+  constexpr int FREGS = (MI + NI) * NPL * 4 * (KW / 32), AREGS = MI * NI * 4;
   constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 56 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 56 : 400;
   constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET && !(BNB && RBUDGET < 400);
   if constexpr (PIPE) {
-    P3Frags<TM, TN, KW / 32> fr[2];
+    P3Frags<TM, TN, KW / 32, NPL> fr[2];
     if (nk > 0) {
       wait_ahead(min(NST - 1, nk - 1));
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       read(0, fr[0]);
     }
-    auto body = [&](int k, P3Frags<TM, TN, KW / 32>& cur, P3Frags<TM, TN, KW / 32>& nxt) {
+    auto body = [&](int k, P3Frags<TM, TN, KW / 32, NPL>& cur, P3Frags<TM, TN, KW / 32, NPL>& nxt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot k are done
       if (k + 1 < nk) wait_ahead(min(NST - 2, nk - 2 - k));  // slot k+1 landed for this thread
       __builtin_amdgcn_s_barrier();
@@ -264,14 +270,14 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
       if (k + NST < nk) issue(k % NST, k + NST);
       if (k + 1 < nk) read(k + 1, nxt);
       __builtin_amdgcn_sched_barrier(0);
-      p3_mma<TM, TN, KW / 32>(cur, acc);
+      p3_mma<TM, TN, KW / 32, NPL>(cur, acc);
     };
     for (int k = 0; k < nk; k += 2) {
       body(k, fr[0], fr[1]);
       if (k + 1 < nk) body(k + 1, fr[1], fr[0]);
     }
   } else {
-    P3Frags<TM, TN, KW / 32> fr;
+    P3Frags<TM, TN, KW / 32, NPL> fr;
     for (int kt = 0; kt < nk; ++kt) {
       // slot kt has landed for this thread once at most the later slots' loads are outstanding;
       // the barrier publishes every thread's DMA
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
         asm volatile("" ::: "memory");
         issue(kt % NST, kt + NST);
       }
-      p3_mma<TM, TN, KW / 32>(fr, acc);
+      p3_mma<TM, TN, KW / 32, NPL>(fr, acc);
     }
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
@@ -294,7 +300,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
     if constexpr (SK) continue;
     else return;
   }
-  igemm_epilogue<WM, WN, TM, TN, BNB, true>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early,
+  igemm_epilogue<WM, WN, TM, TN, BNB, NPL == 3>(p, acc, smem, tm, m0, n0, wm, wn, lane, tid, pre, early,
                                             BNB ? smem + PARAM_OFF : nullptr);
   if constexpr (!SK) return;  // one tile share: the loop never repeats
   }
@@ -305,36 +311,36 @@ static void p3_set_lds_once(K kern) {
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-template <int WM, int WN, int TM, int TN, int KW, int NST, bool BNB, int OCC = 1, bool SK = false>
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool BNB, int OCC = 1, bool SK = false, int NPL = 3>
 static void launch_p3(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   const int tiles = SK ? p.sk_grid : ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
   const int slots = SK ? NST : (p.Kpad / KW + p.splits - 1) / p.splits;
-  const size_t lds_main = (size_t)(slots < NST ? slots : NST) * p3_stage_bytes<BM, BN, KW>();
+  const size_t lds_main = (size_t)(slots < NST ? slots : NST) * p3_stage_bytes<BM, BN, KW, NPL>();
   const size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-  if (BNB) lds = p3_param_off<BM, BN, WM, KW, NST>() + bnb_param_lds(BN);
+  if (BNB) lds = p3_param_off<BM, BN, WM, KW, NST, NPL>() + bnb_param_lds(BN);
   const bool cbig = (p.C % 64) == 0;
   const bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB, OCC, SK>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB, OCC, SK>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB, OCC, SK>);
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB, OCC, SK>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB, OCC, SK, NPL>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB, OCC, SK, NPL>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB, OCC, SK, NPL>);
+    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB, OCC, SK, NPL>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB, OCC, SK>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, BNB, OCC, SK, NPL>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB, OCC, SK>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, true, BNB, OCC, SK, NPL>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB, OCC, SK>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, false, BNB, OCC, SK, NPL>), dim3(tiles), dim3(NT), lds,
                        st, p);
   else
-    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB, OCC, SK>), dim3(tiles), dim3(NT), lds,
+    hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB, OCC, SK, NPL>), dim3(tiles), dim3(NT), lds,
                        st, p);
 }
 
@@ -349,27 +355,27 @@ static void launch_p3(const ConvParams& p, hipStream_t st) {
 //   32-deep, two per CU:     14 128x64 (2x2 of 64x32, 2 slots), 15 64x128 (2x2 of 32x64, 2 slots),
 //                            16 64x64 (2x2 of 32x32, 3 slots)
 //   32-deep, three per CU:   17 64x64 (2x2 of 32x32, 2 slots)
-template <bool BNB, bool SK>
+template <bool BNB, bool SK, int NPL = 3>
 static void launch_p3_cfg(const ConvParams& p, int cfg, hipStream_t st) {
   switch (cfg) {
-    case 1: launch_p3<2, 2, 32, 64, 64, 2, BNB, 1, SK>(p, st); break;
-    case 2: launch_p3<4, 2, 32, 32, 64, 2, BNB, 1, SK>(p, st); break;
-    case 3: launch_p3<2, 4, 32, 32, 64, 2, BNB, 1, SK>(p, st); break;
-    case 4: launch_p3<2, 2, 32, 32, 64, 2, BNB, 1, SK>(p, st); break;
-    case 5: launch_p3<4, 1, 32, 64, 64, 2, BNB, 1, SK>(p, st); break;
-    case 6: launch_p3<1, 4, 64, 32, 64, 2, BNB, 1, SK>(p, st); break;
-    case 7: launch_p3<2, 4, 64, 32, 32, 3, BNB, 1, SK>(p, st); break;
-    case 8: launch_p3<4, 2, 32, 64, 32, 3, BNB, 1, SK>(p, st); break;
-    case 9: launch_p3<2, 2, 64, 64, 32, 3, BNB, 1, SK>(p, st); break;
-    case 10: launch_p3<4, 2, 64, 64, 32, 2, BNB, 1, SK>(p, st); break;
-    case 11: launch_p3<2, 4, 64, 64, 32, 2, BNB, 1, SK>(p, st); break;
-    case 12: launch_p3<2, 2, 32, 64, 32, 4, BNB, 1, SK>(p, st); break;
-    case 13: launch_p3<2, 2, 64, 32, 32, 4, BNB, 1, SK>(p, st); break;
-    case 14: launch_p3<2, 2, 64, 32, 32, 2, BNB, 2, SK>(p, st); break;
-    case 15: launch_p3<2, 2, 32, 64, 32, 2, BNB, 2, SK>(p, st); break;
-    case 16: launch_p3<2, 2, 32, 32, 32, 3, BNB, 2, SK>(p, st); break;
-    case 17: launch_p3<2, 2, 32, 32, 32, 2, BNB, 3, SK>(p, st); break;
-    default: launch_p3<2, 2, 64, 32, 64, 2, BNB, 1, SK>(p, st); break;
+    case 1: launch_p3<2, 2, 32, 64, 64, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 2: launch_p3<4, 2, 32, 32, 64, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 3: launch_p3<2, 4, 32, 32, 64, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 4: launch_p3<2, 2, 32, 32, 64, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 5: launch_p3<4, 1, 32, 64, 64, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 6: launch_p3<1, 4, 64, 32, 64, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 7: launch_p3<2, 4, 64, 32, 32, 3, BNB, 1, SK, NPL>(p, st); break;
+    case 8: launch_p3<4, 2, 32, 64, 32, 3, BNB, 1, SK, NPL>(p, st); break;
+    case 9: launch_p3<2, 2, 64, 64, 32, 3, BNB, 1, SK, NPL>(p, st); break;
+    case 10: launch_p3<4, 2, 64, 64, 32, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 11: launch_p3<2, 4, 64, 64, 32, 2, BNB, 1, SK, NPL>(p, st); break;
+    case 12: launch_p3<2, 2, 32, 64, 32, 4, BNB, 1, SK, NPL>(p, st); break;
+    case 13: launch_p3<2, 2, 64, 32, 32, 4, BNB, 1, SK, NPL>(p, st); break;
+    case 14: launch_p3<2, 2, 64, 32, 32, 2, BNB, 2, SK, NPL>(p, st); break;
+    case 15: launch_p3<2, 2, 32, 64, 32, 2, BNB, 2, SK, NPL>(p, st); break;
+    case 16: launch_p3<2, 2, 32, 32, 32, 3, BNB, 2, SK, NPL>(p, st); break;
+    case 17: launch_p3<2, 2, 32, 32, 32, 2, BNB, 3, SK, NPL>(p, st); break;
+    default: launch_p3<2, 2, 64, 32, 64, 2, BNB, 1, SK, NPL>(p, st); break;
   }
 }
 

@@ -123,6 +123,9 @@ int p3_tile_m(int cfg);
 int p3_tile_n(int cfg);
 int p3_slot_k(int cfg);
 void launch_conv_p3_sk(const ConvParams& p, int cfg, hipStream_t st);
+// the plane-GEMM kernel on one 16-bit plane (conv_s1.hip): cfg CONV_S1_BASE + i of the 16-bit ops
+constexpr int CONV_S1_BASE = 100;
+void launch_conv_s1(const ConvParams& p, int cfg, hipStream_t st);
 void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st);
 int wgrad_p3_tile_m(int cfg);
 int wgrad_p3_tile_n(int cfg);

@@ -102,7 +102,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
             assert rel_err(dx, dref) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("cfg", list(range(38)))
+@pytest.mark.parametrize("cfg", list(range(38)) + list(range(100, 118)))
 def test_conv_fwd_all_tile_configs(cfg):
     torch.manual_seed(1)
     spec, p, pk = make_conv(128, 192, 3, 3, 1, 1, (1, 1, 1, 1))
@@ -179,7 +179,7 @@ def test_conv_dgrad(case, accumulate):
                          ids=["1x1", "3x3", "1x1s2", "cin80"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [2, 4, 12, 23, 26, 27, 28, 29, 30, 31, 34, 36, 37])
+@pytest.mark.parametrize("cfg", [2, 4, 12, 23, 26, 27, 28, 29, 30, 31, 34, 36, 37, 100, 107, 109, 114, 117])
 def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
     """data-grad GEMM with the consuming BN layer's ReLU gating and backward sums fused into
     its epilogue (ConvParams::bnb_*), vs the CPU gating + fp32 reductions."""
