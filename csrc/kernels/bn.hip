@@ -626,6 +626,79 @@ __device__ __forceinline__ void reduce_group_replicas(const float* acc, int R, i
   __syncthreads();
 }
 
+// Per-block channel coefficients, derived ONCE per channel of the block's group and left in LDS:
+// thread i < CB reduces channel c0 + i's R replicas (sum, sum of squares) and loads its affine
+// parameters, all in one round trip; the row threads then read 8 channels' worth with 16-byte
+// LDS reads. (The per-lane form -- 16-32 scalar parameter loads per thread plus a second round
+// trip for the statistic shift after the barrier -- was the fixed cost of the small launches:
+// in-graph, a 3 MB stage-4 apply took 4.0 us against 2.5 us for a copy, tools/bn_bw_probe.py.)
+// coef: [0][CB] scale, [1][CB] shift of y = scale * z + shift.
+// channel c's two replica sums (R replicas of [2][C]). R8 (the STAT_R = 8 training case): straight-
+// line loads, so the whole coefficient body is one block whose loads issue in one round trip (a
+// runtime replica loop let the compiler hoist the parameter math above it: two round trips)
+template <bool R8>
+__device__ __forceinline__ void sum_replicas2(const float* __restrict__ acc, int R, int C, int c, float& s, float& q) {
+  s = 0.f;
+  q = 0.f;
+  if constexpr (R8) {
+    float a[8], b[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      a[r] = acc[(size_t)r * 2 * C + c];
+      b[r] = acc[(size_t)r * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      s += a[r];
+      q += b[r];
+    }
+  } else {
+    for (int r = 0; r < R; ++r) {
+      s += acc[(size_t)r * 2 * C + c];
+      q += acc[(size_t)r * 2 * C + C + c];
+    }
+  }
+}
+template <bool R8>
+__device__ __forceinline__ void bn_coef_fwd(const float* __restrict__ acc, int R, int C, int c0, int CB, int M,
+                                            float eps, float momentum, const float* __restrict__ gamma,
+                                            const float* __restrict__ beta, const float* __restrict__ K, bool publish,
+                                            float* smean, float* sinv, float* rmean, float* rvar, float* coef,
+                                            int i0, int step) {
+  const float inv_n = 1.f / (float)M;
+  for (int i = i0; i < CB; i += step) {
+    const int c = c0 + i;
+    float s, q;
+    sum_replicas2<R8>(acc, R, C, c, s, q);
+    const float g = gamma[c], bt = beta[c], k = K != nullptr ? K[c] : 0.f;
+    const float d = s * inv_n;  // E[v - K]
+    const float mu = d + k;
+    const float var = fmaxf(q * inv_n - d * d, 0.f);
+    const float is = rsqrtf(var + eps);
+    const float sc = g * is;
+    coef[i] = sc;
+    coef[CB + i] = bt - mu * sc;
+    if (publish) {
+      smean[c] = mu;
+      sinv[c] = is;
+      if (rmean != nullptr) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        rmean[c] = momentum * rmean[c] + (1.f - momentum) * mu;
+        rvar[c] = momentum * rvar[c] + (1.f - momentum) * unb;
+      }
+    }
+  }
+}
+// 8 consecutive floats of an LDS table (16-byte aligned) into registers
+__device__ __forceinline__ void lds_read8(const float* p, float* o) {
+  const f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    o[e] = a[e];
+    o[4 + e] = b[e];
+  }
+}
+
 // RBN: the residual operand is a projection shortcut's raw conv output normalised here (ResBN);
 // its own instantiation, so the common kernel keeps its register budget
 // P3 (fp32 path): y is written as bf16 hi / mid / lo planes (plane stride yps elements) -- the
@@ -640,8 +713,7 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
   constexpr bool RP3 = P3 && !RBN;  // residual planes
   T* __restrict__ y = reinterpret_cast<T*>(yv);
   const T* __restrict__ res = reinterpret_cast<const T*>(resv);
-  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB] (+ [2][CB] of the residual BN)
-  constexpr bool rbn = RBN;
+  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB] coefficients (+ the residual BN's)
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
   const int cl = (threadIdx.x % CVB) * 8;
@@ -672,60 +744,32 @@ __global__ __launch_bounds__(256) void bn_apply_acc_kernel(
       }
     }
   };
-  // First rows and the affine parameters are in flight while the statistics are reduced.
-  float gam[8], bet[8], gam2[RBN ? 8 : 1], bet2[RBN ? 8 : 1];
-  if (active) {
-    load_rows(m0);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      gam[e] = gamma[gm.c0 + cl + e];
-      bet[e] = beta[gm.c0 + cl + e];
-      if constexpr (RBN) {
-        gam2[e] = rb.gamma[gm.c0 + cl + e];
-        bet2[e] = rb.beta[gm.c0 + cl + e];
-      }
-    }
-  }
-  if constexpr (RBN) {  // both reductions, one barrier each
-    reduce_group_replicas(rb.acc, R, C, gm.c0, gm.CB, sums + 2 * gm.CB);
-  }
-  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
-  const float inv_n = 1.f / (float)M;
-  // mean / invstd of channel group sums s[0..CB) / s[CB..2CB) (shifted by K), block 0 publishes
-  auto finalize = [&](const float* s, const float* K, float* smean, float* sinv, float* rmean, float* rvar) {
-    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
-      const int c = gm.c0 + i;
-      const float d = s[i] * inv_n;  // E[v - K]
-      float mu = d + (K != nullptr ? K[c] : 0.f);
-      float var = fmaxf(s[gm.CB + i] * inv_n - d * d, 0.f);
-      smean[c] = mu;
-      sinv[c] = rsqrtf(var + eps);
-      if (rmean != nullptr) {
-        float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-        rmean[c] = momentum * rmean[c] + (1.f - momentum) * mu;
-        rvar[c] = momentum * rvar[c] + (1.f - momentum) * unb;
-      }
-    }
+  // First rows are in flight while the block derives its channel coefficients (bn_coef_fwd).
+  if (active) load_rows(m0);
+  const bool pub = blockIdx.x == 0;
+  const int t = threadIdx.x;
+  auto coef = [&](auto r8) {
+    constexpr bool R8 = decltype(r8)::value;
+    if (!RBN || t < 128)  // RBN: the two BNs' channels on the two halves of the block, concurrently
+      bn_coef_fwd<R8>(acc, R, C, gm.c0, gm.CB, M, eps, momentum, gamma, beta, shift, pub, saved_mean, saved_invstd,
+                      run_mean, run_var, sums, t, RBN ? 128 : 256);
+    else
+      bn_coef_fwd<R8>(rb.acc, R, C, gm.c0, gm.CB, M, eps, momentum, rb.gamma, rb.beta, rb.shift, pub, rb.saved_mean,
+                      rb.saved_invstd, rb.run_mean, rb.run_var, sums + 2 * gm.CB, t - 128, 128);
   };
-  if (blockIdx.x == 0) {
-    finalize(sums, shift, saved_mean, saved_invstd, run_mean, run_var);
-    if constexpr (RBN) finalize(sums + 2 * gm.CB, rb.shift, rb.saved_mean, rb.saved_invstd, rb.run_mean, rb.run_var);
-  }
+  if (R == 8)
+    coef(std::true_type{});
+  else
+    coef(std::false_type{});
+  __syncthreads();
   if (!active) return;
   float sc[8], sh[8], sc2[RBN ? 8 : 1], sh2[RBN ? 8 : 1];
-  auto affine = [&](const float* s, const float* K, const float* g, const float* b, float* a, float* o) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = s[cl + e] * inv_n;
-      float mu = d + (K != nullptr ? K[gm.c0 + cl + e] : 0.f);
-      float var = fmaxf(s[gm.CB + cl + e] * inv_n - d * d, 0.f);
-      float v = g[e] * rsqrtf(var + eps);
-      a[e] = v;
-      o[e] = b[e] - mu * v;
-    }
-  };
-  affine(sums, shift, gam, bet, sc, sh);
-  if constexpr (RBN) affine(sums + 2 * gm.CB, rb.shift, gam2, bet2, sc2, sh2);
+  lds_read8(sums + cl, sc);
+  lds_read8(sums + gm.CB + cl, sh);
+  if constexpr (RBN) {
+    lds_read8(sums + 2 * gm.CB + cl, sc2);
+    lds_read8(sums + 3 * gm.CB + cl, sh2);
+  }
   for (; m0 < M; m0 += BN_U * stride) {
     if (m0 != blockIdx.x * gm.rows + gm.r0) load_rows(m0);
 #pragma unroll
@@ -830,6 +874,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
   }
 }
 
+// backward coefficients of the block's channel group: [6][CB] mean invstd scale shift k1 k2 (k1, k2:
+// the dbeta / dgamma sums over M); block 0 publishes dgamma / dbeta and the next step's shift
+template <bool R8>
+__device__ __forceinline__ void bn_coef_bwd(const float* __restrict__ acc, int R, int C, int c0, int CB, int M,
+                                            const float* mean, const float* invstd, const float* gamma,
+                                            const float* beta, float* dgamma, float* dbeta, float* shift_out,
+                                            float* coef) {
+  const float invM = 1.f / (float)M;
+  for (int i = threadIdx.x; i < CB; i += blockDim.x) {
+    const int c = c0 + i;
+    float sb, sg;
+    sum_replicas2<R8>(acc, R, C, c, sb, sg);
+    const float mu = mean[c], is = invstd[c];
+    const float sc = gamma[c] * is;
+    coef[i] = mu;
+    coef[CB + i] = is;
+    coef[2 * CB + i] = sc;
+    coef[3 * CB + i] = beta[c] - mu * sc;
+    coef[4 * CB + i] = sb * invM;
+    coef[5 * CB + i] = sg * invM;
+    if (blockIdx.x == 0) {
+      dbeta[c] = sb;
+      dgamma[c] = sg;
+      // this step's batch mean becomes the next step's statistic shift (the forward readers of
+      // the shift have all run: no block of this launch reads it)
+      if (shift_out != nullptr) shift_out[c] = mu;
+    }
+  }
+}
+
 // P3 (fp32 path): dx is written as bf16 hi / mid / lo planes (plane stride dxps elements), the
 // operand format of the data- and weight-gradient GEMMs that consume it
 template <typename T = uint16_t, typename TY = T, bool P3 = false, bool POOL = false>
@@ -838,7 +912,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     const T* __restrict__ x, int ldx, void* __restrict__ dxv, int lddx, int M, int C, int CVB,
     const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
     int R, float* dgamma, float* dbeta, int relu, float* shift_out, int64_t dxps, PoolSrc pool) {
-  extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]: dbeta, dgamma
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [6][CB]: mean invstd scale shift k1 k2
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
   constexpr uint32_t E = Act8<T>::ESZ, EY = Act8<TY>::ESZ;
@@ -851,40 +925,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
   const int mfirst = blockIdx.x * gm.rows + gm.r0;
   Act8<T> dv[BN_U], xv[BN_U];
   Act8<TY> yv[BN_U];
-  float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
-  // First rows and the per-channel parameters are in flight while dgamma/dbeta are reduced.
+  // First rows are in flight while the block derives its channel coefficients: thread i < CB
+  // reduces channel c0 + i's dbeta / dgamma replicas and folds its parameters into LDS
   if (active) {
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) src.load(mfirst + u * stride, M, relu, dv[u], xv[u], yv[u]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      int c = gm.cv * 8 + e;
-      mu[e] = mean[c];
-      is[e] = invstd[c];
-      sc[e] = gamma[c];
-      sh[e] = beta[c];
-    }
   }
-  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
-  if (blockIdx.x == 0) {
-    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
-      dbeta[gm.c0 + i] = sums[i];
-      dgamma[gm.c0 + i] = sums[gm.CB + i];
-      // this step's batch mean becomes the next step's statistic shift (the forward readers of
-      // the shift have all run: no block of this launch reads it)
-      if (shift_out != nullptr) shift_out[gm.c0 + i] = mean[gm.c0 + i];
-    }
-  }
+  if (R == 8)
+    bn_coef_bwd<true>(acc, R, C, gm.c0, gm.CB, M, mean, invstd, gamma, beta, dgamma, dbeta, shift_out, coef);
+  else
+    bn_coef_bwd<false>(acc, R, C, gm.c0, gm.CB, M, mean, invstd, gamma, beta, dgamma, dbeta, shift_out, coef);
+  __syncthreads();
   if (!active) return;
-  const float invM = 1.f / (float)M;
   const int cl = (threadIdx.x % CVB) * 8;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = sc[e] * is[e];
-    sh[e] = sh[e] - mu[e] * sc[e];
-    k1[e] = sums[cl + e] * invM;
-    k2[e] = sums[gm.CB + cl + e] * invM;
-  }
+  float mu[8], is[8], sc[8], sh[8], k1[8], k2[8];
+  lds_read8(coef + cl, mu);
+  lds_read8(coef + gm.CB + cl, is);
+  lds_read8(coef + 2 * gm.CB + cl, sc);
+  lds_read8(coef + 3 * gm.CB + cl, sh);
+  lds_read8(coef + 4 * gm.CB + cl, k1);
+  lds_read8(coef + 5 * gm.CB + cl, k2);
   for (int m0 = mfirst; m0 < M; m0 += BN_U * stride) {
     if (m0 != mfirst) {
 #pragma unroll
@@ -1033,12 +1093,19 @@ static dim3 bn_grid_groups(int M, int C, int* cvb_out) {
   const int groups = CV / cvb;
   const int rows = 256 / cvb;
   int need = (M + rows - 1) / rows;
-  int target = 2048 / groups;
+  static const int blocks = [] {
+    const char* e = getenv("HCB_BN_BLOCKS");
+    return e != nullptr && atoi(e) > 0 ? atoi(e) : 2048;
+  }();
+  int target = blocks / groups;
   if (target < 1) target = 1;
   // Small tensors: give every thread up to BN_U rows (all loads in flight at once) rather than
   // one row per thread -- fewer workgroups to dispatch and one memory round trip, while the
   // grid still covers every CU.
-  constexpr int rpt = BN_U;
+  static const int rpt = [] {
+    const char* e = getenv("HCB_BN_RPT");
+    return e != nullptr && atoi(e) > 0 ? atoi(e) : BN_U;
+  }();
   int floor_s = (256 + groups - 1) / groups;
   int want = (need + rpt - 1) / rpt;
   if (want < floor_s) want = floor_s < need ? floor_s : need;
@@ -1138,7 +1205,7 @@ void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, 
                              float* shift_out, hipStream_t st, bool f32, bool yh, int64_t dxps, const PoolSrc* pool) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
-  const size_t lds = (size_t)2 * cvb * 8 * 4;
+  const size_t lds = (size_t)6 * cvb * 8 * 4;
   const PoolSrc ps = pool != nullptr ? *pool : PoolSrc{};
   if (pool != nullptr && f32 && dxps > 0) {
     hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, float, true, true>), grid, dim3(256), lds, st,
