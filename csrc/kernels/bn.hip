@@ -19,6 +19,8 @@
 namespace hcb {
 
 constexpr int BN_U = 4;  // rows in flight per thread in the streaming kernels
+constexpr int BN_UB = 2;  // the backward apply: 2 rows (x 3 tensors) in flight -- 119 VGPRs, occupancy 4,
+                          // against 151 / 3 at 4 rows (+18% on the mid-size tensors, profiles/r4bn_rows_ab.txt)
 
 // buffer-resource byte range covering rows [0, M) of a [M][ld] bf16 tensor (clamped to 2 GiB)
 __device__ __forceinline__ uint32_t rsrc_bytes(int M, int ld, int esz = 2) {
@@ -923,13 +925,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
                            lddy, ldx, ldyv, gm.cv, pool};
   const int stride = gridDim.x * gm.rows;
   const int mfirst = blockIdx.x * gm.rows + gm.r0;
-  Act8<T> dv[BN_U], xv[BN_U];
-  Act8<TY> yv[BN_U];
+  Act8<T> dv[BN_UB], xv[BN_UB];
+  Act8<TY> yv[BN_UB];
   // First rows are in flight while the block derives its channel coefficients: thread i < CB
   // reduces channel c0 + i's dbeta / dgamma replicas and folds its parameters into LDS
   if (active) {
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) src.load(mfirst + u * stride, M, relu, dv[u], xv[u], yv[u]);
+    for (int u = 0; u < BN_UB; ++u) src.load(mfirst + u * stride, M, relu, dv[u], xv[u], yv[u]);
   }
   if (R == 8)
     bn_coef_bwd<true>(acc, R, C, gm.c0, gm.CB, M, mean, invstd, gamma, beta, dgamma, dbeta, shift_out, coef);
@@ -945,13 +947,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
   lds_read8(coef + 3 * gm.CB + cl, sh);
   lds_read8(coef + 4 * gm.CB + cl, k1);
   lds_read8(coef + 5 * gm.CB + cl, k2);
-  for (int m0 = mfirst; m0 < M; m0 += BN_U * stride) {
+  for (int m0 = mfirst; m0 < M; m0 += BN_UB * stride) {
     if (m0 != mfirst) {
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+      for (int u = 0; u < BN_UB; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < BN_UB; ++u) {
       const int m = m0 + u * stride;
       float g[8], xh[8], o[8];
       bwd_math_t<T, TY>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
