@@ -19,7 +19,7 @@
 namespace hcb {
 
 constexpr int BN_U = 4;  // rows in flight per thread in the streaming kernels
-constexpr int BN_UB = 2;  // the backward apply: 2 rows (x 3 tensors) in flight -- 119 VGPRs, occupancy 4,
+constexpr int BN_UB = 2;  // the backward reduce / apply: 2 rows (x 3 tensors) in flight -- 119 VGPRs, occupancy 4,
                           // against 151 / 3 at 4 rows (+18% on the mid-size tensors, profiles/r4bn_rows_ab.txt)
 
 // buffer-resource byte range covering rows [0, M) of a [M][ld] bf16 tensor (clamped to 2 GiB)
@@ -815,33 +815,41 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_acc_kernel(
     const T* __restrict__ x, int ldx, int M, int C, int CVB, const float* mean, const float* invstd,
     const float* gamma, const float* beta, int relu, float* acc, int R, T* gout, int ldg, PoolSrc pool) {
   constexpr uint32_t E = Act8<T>::ESZ;
-  extern __shared__ __attribute__((aligned(16))) float lds_f[];  // [2][rows][CB]
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];  // [2][rows][CB] partials, [4][CB] coefficients
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
   float s1[8] = {0}, s2[8] = {0};
+  float* coef = lds_f + 2 * gm.rows * gm.CB;  // mean invstd scale shift, one thread per channel
+  for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
+    const int c = gm.c0 + i;
+    const float mu = mean[c], is = invstd[c];
+    const float sc = gamma[c] * is;
+    coef[i] = mu;
+    coef[gm.CB + i] = is;
+    coef[2 * gm.CB + i] = sc;
+    coef[3 * gm.CB + i] = beta[c] - mu * sc;
+  }
+  __syncthreads();
   if (active) {
+    const int cl = (threadIdx.x % CVB) * 8;
     float mu[8], is[8], sc[8], sh[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      int c = gm.cv * 8 + e;
-      mu[e] = mean[c];
-      is[e] = invstd[c];
-      sc[e] = gamma[c] * is[e];
-      sh[e] = beta[c] - mu[e] * sc[e];
-    }
+    lds_read8(coef + cl, mu);
+    lds_read8(coef + gm.CB + cl, is);
+    lds_read8(coef + 2 * gm.CB + cl, sc);
+    lds_read8(coef + 3 * gm.CB + cl, sh);
     constexpr uint32_t EY = Act8<TY>::ESZ;
     BwdSrcT<T, TY, POOL> src{make_rsrc(POOL ? x : dy, rsrc_bytes(M, POOL ? ldx : lddy, E)),
                              make_rsrc(x, rsrc_bytes(M, ldx, E)),
                              y != nullptr ? make_rsrc(y, rsrc_bytes(M, ldyv, EY)) : make_rsrc(x, rsrc_bytes(M, ldx, E)),
                              lddy, ldx, ldyv, gm.cv, pool};
     const int stride = gridDim.x * gm.rows;
-    for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
-      Act8<T> dv[BN_U], xv[BN_U];
-      Act8<TY> yv[BN_U];
+    for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_UB * stride) {
+      Act8<T> dv[BN_UB], xv[BN_UB];
+      Act8<TY> yv[BN_UB];
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+      for (int u = 0; u < BN_UB; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
+      for (int u = 0; u < BN_UB; ++u) {
         const int m = m0 + u * stride;
         float g[8], xh[8];
         bwd_math_t<T, TY>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
@@ -1177,7 +1185,7 @@ void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv,
   // every block adds into replica blockIdx.x % R; deterministic mode: at most R row blocks, so
   // each replica slot gets one add (the kernel strides over the rows with any grid)
   if (deterministic() && (int)grid.x > R) grid.x = R;
-  size_t lds = (size_t)2 * (256 / cvb) * cvb * 8 * 4;
+  size_t lds = ((size_t)2 * (256 / cvb) + 4) * cvb * 8 * 4;
   const PoolSrc ps = pool != nullptr ? *pool : PoolSrc{};
   if (pool != nullptr && f32)
     hipLaunchKernelGGL((bn_bwd_reduce_acc_kernel<float, float, true>), grid, dim3(256), lds, st, (const float*)dy,
