@@ -359,6 +359,71 @@ __global__ __launch_bounds__(256) void maxpool_bwd_amax_kernel(
   Act8<T>::store(dp, g);
 }
 
+// The ResNet stem pool (3x3, stride 2, top / left pad 0 or 1 -- TF 'SAME' pads 0 before, 1 after --
+// even H / W): one thread per 2x2 input block (rows 2a, 2a+1; cols 2b, 2b+1) x 8 channels. The
+// block meets exactly the windows p in {a-1+ph, a+ph}, q in {b-1+pw, b+pw}, so 4 window loads
+// (dy + argmax) serve 4 pixels -- the per-pixel kernel above loads 4 windows for EVERY pixel,
+// ~4x the L2 -> CU traffic for the same result.
+template <typename T = uint16_t>
+__global__ __launch_bounds__(256) void maxpool_bwd_amax_s2_kernel(
+    const T* __restrict__ dy, T* __restrict__ dx, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
+    int ph, int pw, int accum, const uint8_t* __restrict__ amax, int cv_shift) {
+  const int CV = C >> 3, W2 = W >> 1, H2 = H >> 1;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= W2 * CV) return;
+  const int b = cv_shift >= 0 ? idx >> cv_shift : idx / CV;
+  const int cv = idx - b * CV;
+  const int t = blockIdx.y;  // n * H2 + a (uniform)
+  const int n = t / H2, a = t - n * H2;
+  Act8<T> d[2][2];
+  u32x2 am[2][2];
+  bool ok[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = a - 1 + ph + i, q = b - 1 + pw + j;
+      ok[i][j] = p >= 0 && p < P && q >= 0 && q < Q;
+      const uint32_t o = (uint32_t)(n * P + (ok[i][j] ? p : 0)) * (uint32_t)Q + (uint32_t)(ok[i][j] ? q : 0);
+      d[i][j].load(dy + o * (uint32_t)ldy + cv * 8);
+      am[i][j] = *reinterpret_cast<const u32x2*>(amax + o * (uint32_t)C + cv * 8);
+    }
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int h = 2 * a + dh, w = 2 * b + dw;
+      float g[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = 0.f;
+      // higher window first, the per-pixel kernels' summation order (bitwise-equal results)
+#pragma unroll
+      for (int i = 1; i >= 0; --i)
+#pragma unroll
+        for (int j = 1; j >= 0; --j) {
+          // position in window (p, q), which starts at row 2p - ph, column 2q - pw
+          const int rh = h - (2 * (a - 1 + ph + i) - ph), rw = w - (2 * (b - 1 + pw + j) - pw);
+          if (!ok[i][j] || rh < 0 || rh > 2 || rw < 0 || rw > 2) continue;
+          const int mine = rh * 3 + rw;
+          float f[8];
+          d[i][j].to_f(f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if ((int)((am[i][j][e >> 2] >> (8 * (e & 3))) & 0xff) == mine) g[e] += f[e];
+        }
+      T* dp = dx + ((uint32_t)(n * H + h) * (uint32_t)W + (uint32_t)w) * (uint32_t)ldx + cv * 8;
+      if (accum) {
+        float o[8];
+        Act8<T> ov;
+        ov.load(dp);
+        ov.to_f(o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] += o[e];
+      }
+      Act8<T>::store(dp, g);
+    }
+}
+
 // global average pool [N][HW][C] -> [N][C]
 template <typename T = uint16_t>
 __global__ __launch_bounds__(256) void gap_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int HW,
@@ -441,6 +506,16 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
   const int cvn = C / 8;
   const int cv_shift = (cvn & (cvn - 1)) == 0 ? __builtin_ctz((unsigned)cvn) : -1;
   const dim3 agrid((unsigned)((W * cvn + 255) / 256), (unsigned)(N * H));
+  if (amax_ok && kh == 3 && sh == 2 && ph >= 0 && ph <= 1 && pw >= 0 && pw <= 1 && H % 2 == 0 && W % 2 == 0) {
+    const dim3 g2((unsigned)((W / 2 * cvn + 255) / 256), (unsigned)(N * H / 2));
+    if (f32)
+      hipLaunchKernelGGL((maxpool_bwd_amax_s2_kernel<float>), g2, dim3(256), 0, st, (const float*)dy, (float*)dx, N, H,
+                         W, C, ldx, P, Q, ldy, ph, pw, accum, (const uint8_t*)idx, cv_shift);
+    else
+      hipLaunchKernelGGL((maxpool_bwd_amax_s2_kernel<uint16_t>), g2, dim3(256), 0, st, (const uint16_t*)dy,
+                         (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, ph, pw, accum, (const uint8_t*)idx, cv_shift);
+    return;
+  }
   if (f32) {  // fp32 path: the argmax gather only (the stem pool of the ResNets)
     if (!amax_ok || (kh + sh - 1) / sh > 3) return;  // rejected on the host (bindings.cpp)
     if ((kh + sh - 1) / sh <= 2)

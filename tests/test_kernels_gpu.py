@@ -338,13 +338,16 @@ def test_bn_fwd_bwd(C, relu, residual):
 
 
 @pytest.mark.parametrize("kind", ["max3s2same", "avg3s1same", "max3s2valid", "avg8valid", "max3s1same",
-                                  "avg3s1valid"])
+                                  "avg3s1valid", "max3s2same_even", "max3s2valid_even"])
 def test_pool_fwd_bwd(kind):
     from azure_hc_intel_tf_amd.nn.layers import Pool
 
     torch.manual_seed(7)
     N, H, C = 2, 17, 64
-    if kind == "max3s2same":
+    if kind.endswith("_even"):  # even H: the 2x2-block argmax gather (maxpool_bwd_amax_s2_kernel)
+        H = 16
+        layer = Pool("p", (H, H, C), 3, 3, 2, 2, "SAME" if "same" in kind else "VALID", is_max=True)
+    elif kind == "max3s2same":
         layer = Pool("p", (H, H, C), 3, 3, 2, 2, "SAME", is_max=True)
     elif kind == "avg3s1same":
         layer = Pool("p", (H, H, C), 3, 3, 1, 1, "SAME", is_max=False)
