@@ -92,6 +92,9 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
     b_ok[v] = col < p.K;
   }
 
+  // HCB_P3_ILV: every slot issue is made, also past the last k-step (rows >= mend read as zeros
+  // into a slot nobody reads again), so the vmcnt arithmetic is uniform and the issue can be
+  // interleaved with the MFMAs of the same basic block (conv_p3_fwd.h p3_ilv)
   auto issue = [&](int stage, int kl) {
     const int mb = mbeg + kl * BK;
     char* sA = smem + stage * STAGE;
@@ -99,7 +102,8 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
 #pragma unroll
     for (int v = 0; v < AI; ++v) {
       const int m = mb + a_row[v];
-      const uint32_t off = (a_col[v] < p.Nout && m < mend) ? (uint32_t)(m * p.ldy + a_col[v]) * 2u : HCB_OOB;
+      const bool ok = (a_col[v] < p.Nout) & (m < mend);
+      const uint32_t off = ((uint32_t)(m * p.ldy + a_col[v]) * 2u) | ((uint32_t)!ok << 31);
       char* d = sA + (wid * AI + v) * ARPI * BM * 2;
       glds16(dyr0, d, off);
       if constexpr (NPL > 1) {
@@ -110,16 +114,16 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
 #pragma unroll
     for (int v = 0; v < BI; ++v) {
       const int m = mb + b_row[v];
-      uint32_t off = HCB_OOB;
-      if (b_ok[v] && m < mend) {
-        const int n = (int)fdiv((uint32_t)m, p.fd_pq);
-        const int rem = m - n * p.P * p.Q;
-        const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
-        const int qq = rem - pp * p.Q;
-        const int h = pp * p.stride_h + b_dh[v], w = qq * p.stride_w + b_dw[v];
-        if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W)
-          off = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c[v]) * 2u;
-      }
+      // branch-free (a divergent branch here would split the slot's basic block and keep the
+      // issue out of the MFMA interleave): every lane computes its offset, a select rejects it
+      const int n = (int)fdiv((uint32_t)m, p.fd_pq);
+      const int rem = m - n * p.P * p.Q;
+      const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
+      const int qq = rem - pp * p.Q;
+      const int h = pp * p.stride_h + b_dh[v], w = qq * p.stride_w + b_dw[v];
+      const bool ok = b_ok[v] & (m < mend) & ((unsigned)h < (unsigned)p.H) & ((unsigned)w < (unsigned)p.W);
+      const uint32_t raw = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c[v]) * 2u;
+      const uint32_t off = raw | ((uint32_t)!ok << 31);  // >= HCB_OOB: out of range
       char* d = sB + (wid * BI + v) * BRPI * BN * 2;
       glds16(xr0, d, off);
       if constexpr (NPL > 1) {
@@ -177,11 +181,33 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   const int nk = (mend - mbeg + BK - 1) / BK;
 #pragma unroll
   for (int s = 0; s < NST; ++s)
-    if (s < nk) issue(s, s);
+    if (HCB_P3_ILV || s < nk) issue(s, s);
   constexpr int FREGS = (MI + NI) * NPL * 4 * KS, AREGS = MI * NI * 4;
   constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 88 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 88 : 400;
   constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET;
-  if constexpr (PIPE) {
+  constexpr int NMF = KS * MI * NI * (NPL == 3 ? 6 : 1), NRD = 2 * KS * (MI + NI) * NPL;
+  if constexpr (PIPE && HCB_P3_ILV) {
+    Fr fr[2];
+    wait_ahead(NST - 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(0, fr[0]);
+    auto body = [&](int k, Fr& cur, Fr& nxt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot k are done
+      wait_ahead(NST - 2);                                 // slot k+1 landed for this thread
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue(k % NST, k + NST);
+      read(k + 1, nxt);
+      p3_mma<TM, TN, KS, NPL>(cur, acc);
+      p3_ilv<NMF, LOADS, NRD>();
+    };
+    for (int k = 0; k < nk; k += 2) {
+      body(k, fr[0], fr[1]);
+      if (k + 1 < nk) body(k + 1, fr[1], fr[0]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy pieces have landed before LDS reuse
+  } else if constexpr (PIPE) {
     Fr fr[2];
     if (nk > 0) {
       wait_ahead(min(NST - 1, nk - 1));
@@ -206,18 +232,21 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   } else {
     Fr fr;
     for (int k = 0; k < nk; ++k) {
-      wait_ahead(min(NST - 1, nk - 1 - k));
+      if constexpr (HCB_P3_ILV) wait_ahead(NST - 1);
+      else wait_ahead(min(NST - 1, nk - 1 - k));
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       read(k, fr);
-      if (k + NST < nk) {
+      if (HCB_P3_ILV || k + NST < nk) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
         __builtin_amdgcn_s_barrier();                        // ... and every other wave's
         asm volatile("" ::: "memory");
         issue(k % NST, k + NST);
       }
       p3_mma<TM, TN, KS, NPL>(fr, acc);
+      if constexpr (HCB_P3_ILV) p3_ilv<NMF, LOADS, 0>();
     }
+    if constexpr (HCB_P3_ILV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();  // every wave is done with the ring before the epilogue reuses LDS
 

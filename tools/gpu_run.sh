@@ -11,6 +11,8 @@
 #   tests[:files]    pytest -m gpu (whole suite, or the comma-separated files)
 #   bench[:args]     python bench.py (args comma-separated, e.g. bench:--batch_size=256)
 #   benchab:ENV      bench.py with and without ENV (e.g. benchab:HCB_X=0), interleaved 2 rounds
+#   convab:DIR       tools/conv_bench.py per-layer timings (CB_ARGS, default --fp32) with the in-tree
+#                    library and with the variant build DIR/_hcb_kernels.so (tools/build_variant.py)
 #   prof[:args]      rocprofv3 --kernel-trace --stats of bench.py, summarised by tools/kstats.py
 #   pmc:COUNTERS     one rocprofv3 --pmc pass (counters comma-separated) over bench.py --steps 3
 #   dpsweep[:dtype]  forced 1-rank DP path (native RCCL engine): backward_segments stage|block x
@@ -51,6 +53,13 @@ for step in "$@"; do
         env $e timeout -k 10 400 python bench.py --steps 40 --warmup 10 > ${O}_ab.json 2> ${O}_ab.err || fail benchab ${O}_ab.err
         echo "$v [$e] $(python -c "import json;d=json.load(open('${O}_ab.json'));print(d['value'], d['ms_per_step'], 'bf16', d.get('bf16_value'), d.get('bf16_ms_per_step'))")"
       done; done ;;
+    convab)
+      for v in base var; do
+        if [ $v = base ]; then e=""; else e="HCB_KERNELS_SO=$args/_hcb_kernels.so"; fi
+        env $e timeout -k 10 300 python tools/conv_bench.py ${CB_ARGS:---fp32} > ${O}_conv_$v.txt 2>&1 \
+          || fail convab ${O}_conv_$v.txt
+        echo "$v [$e] $(tail -1 ${O}_conv_$v.txt)"
+      done ;;
     prof)
       pargs=${args:---steps 10 --warmup 3}
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_prof -o run \
