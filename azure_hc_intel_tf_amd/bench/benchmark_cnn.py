@@ -21,7 +21,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .flags import Params, noop_flags_set, parse_flags
+from .flags import Params, compute_dtype_of, noop_flags_set, parse_flags
 
 MODEL_DEFAULT_BATCH = {"inception3": 32, "trivial": 32, "alexnet": 512, "googlenet": 32, "overfeat": 32,
                        "lenet": 32, "vgg11": 32, "vgg16": 32, "vgg19": 32}
@@ -99,9 +99,10 @@ class BenchmarkCNN:
 
         kw = {"device": self.device, "seed": p.tf_random_seed}
         if self.on_gpu:
-            # tf_cnn_benchmarks trains fp32 unless --use_fp16 (the reference runs fp32,
-            # run-tf-sing-ucx-openmpi.sh:62-81); on MI355X the default is the bf16 HIP-kernel path
-            self.compute_dtype = p.compute_dtype or (p.half_dtype if p.use_fp16 else "bf16")
+            # tf_cnn_benchmarks trains fp32 unless --use_fp16, and the reference runs it without
+            # (run-tf-sing-ucx-openmpi.sh:62-81): fp32 is the default here too, on the HIP plane
+            # GEMMs (bf16x6) for the models that have them; --compute_dtype bf16 / --use_fp16 opt out
+            self.compute_dtype = compute_dtype_of(p)
             kw["compute_dtype"] = self.compute_dtype
         else:
             self.compute_dtype = "fp32"
@@ -180,7 +181,7 @@ class BenchmarkCNN:
         log_fn(f"NUMA bind:   False")
         log_fn(f"Data format: {p.data_format} (logical; NHWC kernels)")
         log_fn(f"Precision:   {self.compute_dtype}" + (" (HIP kernels)" if self.model.native else
-                                                       " (PyTorch reference-precision path)" if self.on_gpu else ""))
+                                                       " (PyTorch/MIOpen path)" if self.on_gpu else " (CPU)"))
         log_fn(f"Optimizer:   {p.optimizer}")
         log_fn(f"Variables:   {p.variable_update}")
         log_fn(f"Workers:     {self.size} (one process per {'MI355X' if self.on_gpu else 'CPU worker'})")

@@ -67,11 +67,11 @@ FLAGS: List[Flag] = [
     Flag("num_decode_threads", None, int, "JPEG decode threads per worker (real data)"),
     # --- tf_cnn_benchmarks flags used by the BASELINE configs / common runs
     Flag("num_gpus", 1, int, "GPUs per process (horovod: 1)"),
-    Flag("use_fp16", False, parse_bool, "16-bit compute with loss scaling: IEEE fp16 (--half_dtype=fp16, the "
-         "PyTorch reference-precision path) or bf16 (--half_dtype=bf16, the HIP kernels)"),
+    Flag("use_fp16", False, parse_bool, "16-bit compute with loss scaling on the HIP kernels: IEEE fp16 "
+         "(--half_dtype=fp16, the -DHCB_F16 kernel build) or bf16 (--half_dtype=bf16)"),
     Flag("half_dtype", "fp16", str, "the 16-bit type --use_fp16 selects", choices=["fp16", "bf16"]),
-    Flag("compute_dtype", None, str, "activation / GEMM precision on the GPU: bf16 (HIP kernels, default) | "
-         "fp32 (the reference's precision) | fp16; overrides --use_fp16's choice",
+    Flag("compute_dtype", None, str, "activation / GEMM precision on the GPU: fp32 (default: the reference's "
+         "precision, tf_cnn_benchmarks without --use_fp16) | bf16 | fp16; overrides --use_fp16's choice",
          choices=["bf16", "fp32", "fp16"]),
     Flag("fp16_loss_scale", 128.0, float, "static loss scale for --use_fp16"),
     Flag("fp16_enable_auto_loss_scale", False, parse_bool, "dynamic loss scaling for --use_fp16"),
@@ -167,3 +167,26 @@ def parse_flags(argv: Optional[List[str]] = None, allow_unknown: bool = True) ->
 def noop_flags_set(p: Params) -> Dict[str, Any]:
     """TF-only flags explicitly given a non-default value (reported as no-ops on the GPU)."""
     return {f.name: p[f.name] for f in FLAGS if f.noop_on_gpu and p.get(f.name) != f.default}
+
+
+# Models whose fp32 step (--compute_dtype fp32, the default) runs on the hand-written HIP kernels
+# (bf16x6 plane GEMMs, fp32 BN / pool / loss): their classes set F32_NATIVE_OK. Kept here, torch-free,
+# for the launcher's config echo; tests/test_cli.py checks it against the model classes.
+FP32_NATIVE_MODELS = frozenset({"resnet50", "resnet50_v1.5", "resnet101", "resnet101_v1.5", "resnet152",
+                                "resnet152_v1.5"})
+
+
+def compute_dtype_of(p: Params) -> str:
+    """GPU compute precision of a run: --compute_dtype, else the 16-bit type of --use_fp16, else
+    fp32 -- tf_cnn_benchmarks' own default, and what the reference runs
+    (/root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16)."""
+    return p.compute_dtype or (p.half_dtype if p.use_fp16 else "fp32")
+
+
+def precision_label(p: Params) -> str:
+    """'fp32 (HIP kernels)' etc.: the precision and the code path a run of these flags takes."""
+    if p.device != "gpu":
+        return "fp32 (CPU)"
+    dt = compute_dtype_of(p)
+    native = dt != "fp32" or p.model in FP32_NATIVE_MODELS
+    return f"{dt} ({'HIP kernels' if native else 'PyTorch/MIOpen path'})"

@@ -183,6 +183,9 @@ def main(argv=None) -> int:
           f"INTRA_T: {plan.intra_t}  INTER_T: {plan.inter_t}  TOTAL_WORKERS: {plan.total_workers}")
     print(f"BATCH_SIZE: {plan.batch_size}  FABRIC: {plan.fabric} ({'RCCL P2P/xGMI' if plan.fabric == 'ib' else 'RCCL sockets'})"
           f"  DEVICE: {plan.device}  FLAVOR: {a.flavor}")
+    from ..bench.flags import parse_flags, precision_label
+
+    print(f"Precision: {precision_label(parse_flags(targs))}")
     print("ENV: " + " ".join(f"{k}={v}" for k, v in sorted(fl["env"].items())) +
           (f"  (unset {' '.join(fl['unset'])})" if fl["unset"] else "") +
           f"  PINNING: {'per-GPU NUMA cores' if fl['pin'] else 'none'}")

@@ -111,118 +111,113 @@ def _bf(shape, dev):
     return torch.randn(shape, device=dev).to(_act())
 
 
-def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
-    """Tune fwd / dgrad / wgrad problems of one ConvBN layer (skips already-tuned keys)."""
-    hcb = _ext.ops()
+def _plans(cfgs_splits):
+    return [c if sp == 1 else [c, sp] for c, sp in cfgs_splits]
+
+
+def layer_problems(layer, batch: int, dev) -> List[Tuple]:
+    """The GEMM problems of one ConvBN layer on the 16-bit kernels: (key, candidate plans, run(plan))
+    for the forward, the data gradient (plain and with the fused BN-backward epilogue, or the
+    stride-phase GEMMs of a strided k x k data gradient) and the weight gradient. Scratch operands
+    of the real shapes are made once per layer, when the first run is called."""
     spec = layer.spec
     H, W, Cin = layer.in_shape
     P, Q, Cout = layer.out_shape
     N = batch
-    out = []
     M = N * P * Q
     geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
     taps = spec.kh * spec.kw
-    keys = [Fn.fwd_key(M, Cout, spec.K, taps), Fn.wgrad_key(Cout, spec.K, M, taps)]
     phases = Fn.dgrad_phases(spec, H, W) if layer.need_dx and Fn.uses_dgrad_phases(spec, H, W) else []
+    buf = {}
+
+    def ops():
+        if not buf:
+            buf["x"] = _bf((N, H, W, Cin), dev)
+            buf["dz"] = _bf((N, P, Q, Cout), dev)
+            buf["y"] = torch.empty((N, P, Q, Cout), dtype=_act(), device=dev)
+            buf["acc"] = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
+            buf["dx"] = torch.zeros((N, H, W, Cin), dtype=_act(), device=dev)
+            buf["dw"] = torch.zeros((Cout, spec.K), dtype=torch.float32, device=dev)
+            z, yv = _bf((N, H, W, Cin), dev), _bf((N, H, W, Cin), dev)
+            st = [torch.rand(Cin, device=dev) + 0.5 for _ in range(4)]
+            buf["bnb"] = Fn.BNBwdFuse(z, yv, Fn.BNSaved(st[0], st[1]), st[2], st[3], 1,
+                                      torch.zeros(8 * 2 * Cin, dtype=torch.float32, device=dev), 8)
+        return buf
+
+    out = []
+    fc = Fn.fwd_candidates(Cout, Fn.patch_eligible(spec))
+    out.append((Fn.fwd_key(M, Cout, spec.K, taps),
+                _plans((c, sp) for c in fc for sp in Fn.splitk_candidates(c, M, Cout, spec.K)),
+                lambda plan: Fn.conv_forward(ops()["x"], spec, layer.pack.pack, None, ops()["y"], stats=ops()["acc"],
+                                             cfg=plan, stats_R=8)))
     if layer.need_dx:
-        keys.append(Fn.fwd_key(geo[0], Cin, geo[1], taps))
-        keys.append(Fn.dgb_key(geo[0], Cin, geo[1], taps))
-    for ph in phases:  # the stride-phase GEMMs of a strided k x k data gradient
-        pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
-        keys += [Fn.fwd_key(pm, Cin, pk, pt), Fn.dgb_key(pm, Cin, pk, pt)]
-    if all(k in Fn._tuned for k in keys):
-        return out
-    x = _bf((N, H, W, Cin), dev)
-    dz = _bf((N, P, Q, Cout), dev)
-    # forward
-    k = Fn.fwd_key(M, Cout, spec.K, taps)
-    if k not in Fn._tuned:
-        y = torch.empty((N, P, Q, Cout), dtype=_act(), device=dev)
-        best = None
-        acc = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
-        for cfg in Fn.fwd_candidates(Cout, Fn.patch_eligible(spec)):
-            for sp in Fn.splitk_candidates(cfg, M, Cout, spec.K):
-                plan = cfg if sp == 1 else [cfg, sp]
-                t = _time(lambda: Fn.conv_forward(x, spec, layer.pack.pack, None, y, stats=acc, cfg=plan,
-                                                  stats_R=8))
-                if best is None or t < best[0]:
-                    best = (t, plan)
-        Fn._tuned[k] = best[1]
-        out.append((k, best))
-    # data gradient
-    if layer.need_dx:
-        dx = torch.zeros((N, H, W, Cin), dtype=_act(), device=dev)
         dpatch = Fn.patch_eligible(spec, dgrad=True) and not phases
-        k = Fn.fwd_key(geo[0], Cin, geo[1], taps)
-        if k not in Fn._tuned:
-            best = None
-            for cfg in Fn.fwd_candidates(Cin, dpatch):
-                for sp in Fn.splitk_candidates(cfg, geo[0], Cin, geo[1]):
-                    plan = cfg if sp == 1 else [cfg, sp]
-                    t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=plan))
-                    if best is None or t < best[0]:
-                        best = (t, plan)
-            Fn._tuned[k] = best[1]
-            out.append((k, best))
+        dc = _plans((c, sp) for c in Fn.fwd_candidates(Cin, dpatch)
+                    for sp in Fn.splitk_candidates(c, geo[0], Cin, geo[1]))
+        out.append((Fn.fwd_key(geo[0], Cin, geo[1], taps), dc,
+                    lambda plan: Fn.conv_dgrad(ops()["dz"], spec, layer.pack.tr, None, ops()["dx"], False, cfg=plan)))
         # the same GEMM with the fused BN-backward epilogue (ReLU mask from y, residual
         # beta-accumulate: the heaviest epilogue), used when a BN layer consumes this dx
-        k = Fn.dgb_key(geo[0], Cin, geo[1], taps)
-        if k not in Fn._tuned:
-            z = _bf((N, H, W, Cin), dev)
-            yv = _bf((N, H, W, Cin), dev)
-            stats = [torch.rand(Cin, device=dev) + 0.5 for _ in range(4)]
-            bacc = torch.zeros(8 * 2 * Cin, dtype=torch.float32, device=dev)
-            bnb = Fn.BNBwdFuse(z, yv, Fn.BNSaved(stats[0], stats[1]), stats[2], stats[3], 1, bacc, 8)
-            best = None
-            for cfg in Fn.fwd_candidates(Cin, dpatch):
-                for sp in Fn.splitk_candidates(cfg, geo[0], Cin, geo[1]):
-                    plan = cfg if sp == 1 else [cfg, sp]
-                    t = _time(lambda: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, True, cfg=plan, bnb=bnb))
-                    if best is None or t < best[0]:
-                        best = (t, plan)
-            Fn._tuned[k] = best[1]
-            out.append((k, best))
+        out.append((Fn.dgb_key(geo[0], Cin, geo[1], taps), dc,
+                    lambda plan: Fn.conv_dgrad(ops()["dz"], spec, layer.pack.tr, None, ops()["dx"], True, cfg=plan,
+                                               bnb=ops()["bnb"])))
         for ph in phases:
             pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
+            pc = _plans((c, sp) for c in Fn.fwd_candidates(Cin) for sp in Fn.splitk_candidates(c, pm, Cin, pk))
             for fused in (False, True):
-                k = (Fn.dgb_key if fused else Fn.fwd_key)(pm, Cin, pk, pt)
-                if k in Fn._tuned:
-                    continue
-                bnbp = None
-                if fused:
-                    z = _bf((N, H, W, Cin), dev)
-                    yv = _bf((N, H, W, Cin), dev)
-                    st = [torch.rand(Cin, device=dev) + 0.5 for _ in range(4)]
-                    bnbp = Fn.BNBwdFuse(z, yv, Fn.BNSaved(st[0], st[1]), st[2], st[3], 1,
-                                        torch.zeros(8 * 2 * Cin, dtype=torch.float32, device=dev), 8)
-                best = None
-                for cfg in Fn.fwd_candidates(Cin):
-                    for sp in Fn.splitk_candidates(cfg, pm, Cin, pk):
-                        plan = cfg if sp == 1 else [cfg, sp]
-                        t = _time(lambda: Fn.dgrad_phase(dz, spec, layer.pack.tr, dx, fused, ph, cfg=plan, bnb=bnbp))
-                        if best is None or t < best[0]:
-                            best = (t, plan)
-                Fn._tuned[k] = best[1]
-                out.append((k, best))
-    # weight gradient
-    k = Fn.wgrad_key(Cout, spec.K, M, taps)
-    if k not in Fn._tuned:
-        dw = torch.zeros((Cout, spec.K), dtype=torch.float32, device=dev)
-        best = None
-        for cfg, splits in Fn.wgrad_candidates(Cout, spec.K, M):
-            t = _time(lambda: Fn.conv_wgrad(dz, x, spec, dw, cfg=(cfg, splits)))
-            if best is None or t < best[0]:
-                best = (t, (cfg, splits))
-        Fn._tuned[k] = best[1]
-        out.append((k, best))
-    if verbose:
-        for kk, (t, c) in out:
-            print(f"  tuned {kk}: cfg={c} {t * 1000:.1f} us")
+                out.append(((Fn.dgb_key if fused else Fn.fwd_key)(pm, Cin, pk, pt), pc,
+                            lambda plan, ph=ph, fused=fused: Fn.dgrad_phase(
+                                ops()["dz"], spec, layer.pack.tr, ops()["dx"], fused, ph, cfg=plan,
+                                bnb=ops()["bnb"] if fused else None)))
+    out.append((Fn.wgrad_key(Cout, spec.K, M, taps), [(c, s) for c, s in Fn.wgrad_candidates(Cout, spec.K, M)],
+                lambda plan: Fn.conv_wgrad(ops()["dz"], ops()["x"], spec, ops()["dw"], cfg=tuple(plan))))
     return out
 
 
 def _planes(shape, dev):
     return Fn.Planes(torch.randn((3,) + tuple(shape), device=dev).to(torch.bfloat16))
+
+
+def layer_problems_p3(layer, batch: int, dev) -> List[Tuple]:
+    """fp32 path: the bf16-plane GEMMs (conv_p3.hip) of one ConvBN layer -- forward, data gradient
+    (or its stride phases, with the fused BN-backward epilogue), weight gradient -- as (key,
+    candidate plans, run(plan)) over their own tile / split-K sets."""
+    spec = layer.spec
+    H, W, Cin = layer.in_shape
+    P, Q, Cout = layer.out_shape
+    N = batch
+    M = N * P * Q
+    taps = spec.kh * spec.kw
+    geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
+    phases = Fn.dgrad_phases(spec, H, W) if layer.need_dx and Fn.uses_dgrad_phases(spec, H, W) else []
+    buf = {}
+
+    def ops():
+        if not buf:
+            buf["x"] = _planes((N, H, W, Cin), dev)
+            buf["dz"] = _planes((N, P, Q, Cout), dev)
+            buf["y"] = torch.empty((N, P, Q, Cout), dtype=torch.float32, device=dev)
+            buf["acc"] = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
+            buf["dx"] = torch.zeros((N, H, W, Cin), dtype=torch.float32, device=dev)
+            buf["dw"] = torch.zeros((Cout, spec.K), dtype=torch.float32, device=dev)
+        return buf
+
+    out = [(Fn.fwd3_key(M, Cout, spec.K, taps), [list(c) for c in Fn.p3_candidates(M, Cout, spec.K)],
+            lambda plan: Fn.conv_forward(ops()["x"], spec, layer.pack.pack, None, ops()["y"], stats=ops()["acc"],
+                                         cfg=plan, stats_R=8))]
+    if layer.need_dx:
+        if not phases:
+            out.append((Fn.fwd3_key(geo[0], Cin, geo[1], taps), [list(c) for c in Fn.p3_candidates(geo[0], Cin, geo[1])],
+                        lambda plan: Fn.conv_dgrad(ops()["dz"], spec, layer.pack.tr, None, ops()["dx"], False,
+                                                   cfg=plan)))
+        for ph in phases:
+            pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
+            out.append((Fn.fwd3_key(pm, Cin, pk, pt), [list(c) for c in Fn.p3_candidates(pm, Cin, pk)],
+                        lambda plan, ph=ph: Fn.dgrad_phase(ops()["dz"], spec, layer.pack.tr, ops()["dx"], True, ph,
+                                                           cfg=plan)))
+    out.append((Fn.wgrad3_key(Cout, spec.K, M, taps), [list(c) for c in Fn.wgrad_p3_candidates(Cout, spec.K, M)],
+                lambda plan: Fn.conv_wgrad(ops()["dz"], ops()["x"], spec, ops()["dw"], cfg=tuple(plan))))
+    return out
 
 
 def _best(cands, run):
@@ -234,60 +229,48 @@ def _best(cands, run):
     return best
 
 
-def tune_conv_layer_p3(layer, batch: int, dev, verbose=False) -> List[Tuple]:
-    """fp32 path: tune the bf16-plane GEMMs (conv_p3.hip) of one ConvBN layer -- forward, data
-    gradient (or its stride phases), weight gradient -- over their own tile / split-K sets."""
-    spec = layer.spec
-    H, W, Cin = layer.in_shape
-    P, Q, Cout = layer.out_shape
-    N = batch
-    M = N * P * Q
-    taps = spec.kh * spec.kw
-    geo = Fn.dgrad_problem(spec, N, H, W, P, Q)
-    phases = Fn.dgrad_phases(spec, H, W) if layer.need_dx and Fn.uses_dgrad_phases(spec, H, W) else []
-    keys = [Fn.fwd3_key(M, Cout, spec.K, taps), Fn.wgrad3_key(Cout, spec.K, M, taps)]
-    if layer.need_dx and not phases:
-        keys.append(Fn.fwd3_key(geo[0], Cin, geo[1], taps))
-    for ph in phases:
-        pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
-        keys.append(Fn.fwd3_key(pm, Cin, pk, pt))
+def model_problems(model, batch: int):
+    """Every distinct conv GEMM problem of a model: {key: [count, candidates, run]} in layer
+    order (count = how many layers of the step launch that problem)."""
+    from ..nn.layers import ConvBN
+
+    p3 = getattr(model, "compute_dtype", None) == "fp32" and model.native
+    probs = {}
+    for l in model.all_layers():
+        if isinstance(l, ConvBN) and l.bn:
+            view = l.tune_view() if hasattr(l, "tune_view") else l
+            for key, cands, run in (layer_problems_p3 if p3 else layer_problems)(view, batch, model.device):
+                if key in probs:
+                    probs[key][0] += 1
+                else:
+                    probs[key] = [1, cands, run]
+    return probs
+
+
+def tune_conv_layer(layer, batch: int, dev, verbose=False) -> List[Tuple]:
+    """Tune the untuned GEMM problems of one ConvBN layer (isolated launches of each candidate)."""
     out = []
-    if all(k in Fn._tuned for k in keys):
-        return out
-    x = _planes((N, H, W, Cin), dev)
-    dz = _planes((N, P, Q, Cout), dev)
-    k = keys[0]
-    if k not in Fn._tuned:
-        y = torch.empty((N, P, Q, Cout), dtype=torch.float32, device=dev)
-        acc = torch.zeros(8 * 2 * Cout, dtype=torch.float32, device=dev)
-        best = _best(Fn.p3_candidates(M, Cout, spec.K),
-                     lambda plan: Fn.conv_forward(x, spec, layer.pack.pack, None, y, stats=acc, cfg=plan, stats_R=8))
-        Fn._tuned[k] = list(best[1])
-        out.append((k, best))
-    if layer.need_dx:
-        dx = torch.zeros((N, H, W, Cin), dtype=torch.float32, device=dev)
-        if not phases:
-            k = Fn.fwd3_key(geo[0], Cin, geo[1], taps)
-            if k not in Fn._tuned:
-                best = _best(Fn.p3_candidates(geo[0], Cin, geo[1]),
-                             lambda plan: Fn.conv_dgrad(dz, spec, layer.pack.tr, None, dx, False, cfg=plan))
-                Fn._tuned[k] = list(best[1])
-                out.append((k, best))
-        for ph in phases:
-            pm, pk, pt = Fn.dgrad_phase_problem(spec, N, ph)
-            k = Fn.fwd3_key(pm, Cin, pk, pt)
-            if k in Fn._tuned:
-                continue
-            best = _best(Fn.p3_candidates(pm, Cin, pk),
-                         lambda plan: Fn.dgrad_phase(dz, spec, layer.pack.tr, dx, True, ph, cfg=plan))
-            Fn._tuned[k] = list(best[1])
-            out.append((k, best))
-    k = Fn.wgrad3_key(Cout, spec.K, M, taps)
-    if k not in Fn._tuned:
-        dw = torch.zeros((Cout, spec.K), dtype=torch.float32, device=dev)
-        best = _best(Fn.wgrad_p3_candidates(Cout, spec.K, M), lambda plan: Fn.conv_wgrad(dz, x, spec, dw, cfg=plan))
-        Fn._tuned[k] = list(best[1])
-        out.append((k, best))
+    for key, cands, run in layer_problems(layer, batch, dev):
+        if key in Fn._tuned:
+            continue
+        best = _best(cands, run)
+        Fn._tuned[key] = best[1]
+        out.append((key, best))
+    if verbose:
+        for kk, (t, c) in out:
+            print(f"  tuned {kk}: cfg={c} {t * 1000:.1f} us")
+    return out
+
+
+def tune_conv_layer_p3(layer, batch: int, dev, verbose=False) -> List[Tuple]:
+    """fp32 path: tune the untuned bf16-plane GEMM problems of one ConvBN layer."""
+    out = []
+    for key, cands, run in layer_problems_p3(layer, batch, dev):
+        if key in Fn._tuned:
+            continue
+        best = _best(cands, run)
+        Fn._tuned[key] = list(best[1])
+        out.append((key, best))
     if verbose:
         for kk, (t, c) in out:
             print(f"  tuned {kk}: cfg={c} {t * 1000:.1f} us")

@@ -474,6 +474,7 @@ _P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3}
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),
               6: (128, 128), 7: (128, 128), 8: (256, 128), 9: (128, 256), 10: (128, 128), 11: (128, 64),
               12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (64, 64)}
+_WP3_OCC = {12: 2, 13: 2, 14: 2, 15: 3}  # workgroups per CU the weight-grad tile is built for
 
 
 def fwd3_key(M: int, N: int, K: int, taps: int = 1):
@@ -541,7 +542,11 @@ def wgrad_p3_candidates(Nout: int, K: int, M: int):
                 or (K < 256 and bn > 128):
             continue
         tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
-        for s in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+        # powers of two, plus the split counts that fill whole rounds of the resident workgroups
+        # (36 128x128 tiles: 7 splits = 252 workgroups, where 8 = 288 runs a second, 1/8-full round)
+        slots = N_CU * _WP3_OCC.get(c, 1)
+        fill = {max(1, r * slots // tiles) for r in (1, 2, 3)}
+        for s in sorted({1, 2, 4, 8, 16, 32, 64, 128, 256} | fill):
             if s > 1 and ksteps // s < 2:
                 break
             if tiles * s > 4 * N_CU:

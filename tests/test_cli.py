@@ -97,6 +97,54 @@ def test_run_script_dry_run():
     assert bad.returncode != 0 and "usage" in bad.stderr
 
 
+def test_default_gpu_precision_is_fp32_on_hip_kernels():
+    """tf_cnn_benchmarks without --use_fp16 trains fp32 -- the reference's precision
+    (run-tf-sing-ucx-openmpi.sh:62-81) -- so the GPU default is fp32, on the HIP kernels for the
+    ResNets; --compute_dtype bf16 / --use_fp16 opt out."""
+    from azure_hc_intel_tf_amd.bench.flags import compute_dtype_of, precision_label
+
+    p = parse_flags(REFERENCE_FLAGS[:-2] + ["--device=gpu"])
+    assert compute_dtype_of(p) == "fp32"
+    assert precision_label(p) == "fp32 (HIP kernels)"
+    assert compute_dtype_of(parse_flags(["--use_fp16"])) == "fp16"
+    assert compute_dtype_of(parse_flags(["--use_fp16", "--half_dtype=bf16"])) == "bf16"
+    assert precision_label(parse_flags(["--compute_dtype=bf16"])) == "bf16 (HIP kernels)"
+
+
+def test_fp32_native_model_list_matches_model_classes():
+    from azure_hc_intel_tf_amd.bench.flags import FP32_NATIVE_MODELS
+    from azure_hc_intel_tf_amd.models import _MODELS, model_names
+    from azure_hc_intel_tf_amd.models import base
+
+    seen = {}
+    orig = base.CNNModel.__init__
+
+    def grab(self, *a, **kw):  # the class attribute, without building the model
+        seen["ok"] = type(self).F32_NATIVE_OK
+        raise StopIteration
+
+    base.CNNModel.__init__ = grab
+    try:
+        for name in model_names():
+            seen.clear()
+            try:
+                _MODELS[name](device="cpu")
+            except StopIteration:
+                pass
+            assert seen["ok"] == (name in FP32_NATIVE_MODELS), name
+    finally:
+        base.CNNModel.__init__ = orig
+
+
+def test_run_script_dry_run_logs_fp32_hip_precision():
+    env = dict(os.environ, DRY_RUN="1", GPUS_PER_NODE="8")
+    env.pop("DEVICE", None)
+    out = subprocess.run([os.path.join(ROOT, "benchmark-scripts", "run-tf-sing-ucx-openmpi.sh"), "1", "4", "64",
+                          "ib"], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "Precision: fp32 (HIP kernels)" in out.stdout
+
+
 def test_cpu_benchmark_end_to_end(tmp_path):
     js = tmp_path / "s.json"
     cmd = [sys.executable, os.path.join(ROOT, "tf_cnn_benchmarks.py"), "--device=cpu", "--model=resnet50",

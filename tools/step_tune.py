@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Step-level conv autotuner: accept a kernel configuration only if the REPLAYED TRAINING STEP gets
+faster (per-layer winners timed as isolated launches repeatedly lost or tied in
+the step, where L2 state and the neighbouring kernels differ).
+
+    python tools/step_tune.py [--dtype fp32|bf16] [--model resnet50] [--batch 64] [--top 24]
+                              [--cands 3] [--retune] [--out gpurun_out/step_tune.json]
+
+1. Every conv GEMM problem of the model (forward, data gradient, weight gradient) is enumerated
+   with its candidate plans (``autotune.model_problems``). With --retune the problems are first
+   re-tuned in isolation from scratch (the old per-layer method: the starting point).
+2. Every candidate of every problem is timed in isolation once; problems are ranked by
+   (isolated time of the current plan) x (launches per step).
+3. For the --top problems, the --cands best isolated candidates that differ from the current plan
+   are tried IN THE STEP: the step graph is re-captured with the candidate and timed by interleaved
+   A/B (current, candidate, current, candidate, ...; median of each) against the current plan. A
+   candidate is kept only if it beats the current plan by more than the noise band measured on
+   this box at start (spread of repeated measurements of one plan set), and is then re-confirmed.
+4. The table is saved (in-tree cache + --out copy) with the accepted changes; the log lists every
+   trial. The result is the starting table's step time vs the final one, same process.
+"""
+import argparse
+import json
+import os
+import shutil
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from azure_hc_intel_tf_amd.models import create_model
+from azure_hc_intel_tf_amd.ops import autotune
+from azure_hc_intel_tf_amd.ops import functional as Fn
+from azure_hc_intel_tf_amd.trainer import Trainer, resnet_lr_schedule, synthetic_batch
+
+
+def log(*a):
+    print(*a, flush=True)
+
+
+class StepTimer:
+    """Re-captures the trainer's step graph on demand and times replays with HIP events."""
+
+    def __init__(self, trainer, images, labels, reps):
+        self.tr, self.images, self.labels, self.reps = trainer, images, labels, reps
+        self.captures = 0
+
+    def recapture(self):
+        tr = self.tr
+        for g in (tr._g_all, tr._g_fb, tr._g_opt):
+            if g is not None:
+                g.reset()
+        tr._g_all = tr._g_fb = tr._g_opt = None
+        tr._segs = None
+        tr._static = None
+        self.tr.step(self.images, self.labels)  # captures (steps_done >= graph_warmup)
+        self.captures += 1
+
+    def time(self) -> float:
+        """ms per step over self.reps replays of the current graph (after 3 untimed)."""
+        for _ in range(3):
+            self.tr.step(self.images, self.labels)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(self.reps):
+            self.tr.step(self.images, self.labels)
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) / self.reps
+
+    def measure(self, table_patch=None) -> float:
+        saved = {}
+        if table_patch:
+            for k, v in table_patch.items():
+                saved[k] = Fn._tuned.get(k)
+                Fn._tuned[k] = v
+        try:
+            self.recapture()
+            return self.time()
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    Fn._tuned.pop(k, None)
+                else:
+                    Fn._tuned[k] = v
+
+
+def ab(timer, key, cur, cand, rounds):
+    """Interleaved A/B of one problem's plan: medians (ms/step) of the current and the candidate."""
+    a, b = [], []
+    for _ in range(rounds):
+        a.append(timer.measure({key: cur}))
+        b.append(timer.measure({key: cand}))
+    return statistics.median(a), statistics.median(b)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--top", type=int, default=24)
+    ap.add_argument("--cands", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--retune", action="store_true")
+    ap.add_argument("--budget_s", type=float, default=900.0)
+    ap.add_argument("--out", default="gpurun_out/step_tune.json")
+    a = ap.parse_args()
+    t_start = time.time()
+    dev = torch.device("cuda")
+    model = create_model(a.model, device=dev, compute_dtype=a.dtype)
+    autotune.load_cache()
+    model.ps.repack()
+    if hasattr(model, "activate"):
+        model.activate()
+    probs = autotune.model_problems(model, a.batch)
+    log(f"[step_tune] {a.model} bs{a.batch} {a.dtype}: {len(probs)} conv GEMM problems")
+    if a.retune:
+        for k in probs:
+            Fn._tuned.pop(k, None)
+        autotune.tune_model(model, a.batch, verbose=True, save=False)
+        log(f"[step_tune] isolated re-tune done ({time.time() - t_start:.0f} s)")
+    else:
+        autotune.tune_model(model, a.batch, save=False)  # fills any missing entry
+    start_table = {k: Fn._tuned[k] for k in probs}
+
+    # isolated timing of every candidate (ranking and candidate shortlist)
+    iso = {}
+    for k, (cnt, cands, run) in probs.items():
+        iso[k] = {json.dumps(c): autotune._time(lambda: run(c)) for c in cands}
+        cur = json.dumps(Fn._tuned[k] if not isinstance(Fn._tuned[k], tuple) else list(Fn._tuned[k]))
+        if cur not in iso[k]:
+            iso[k][cur] = autotune._time(lambda: run(json.loads(cur)))
+        log(f"  iso {k}: {len(cands)} candidates, current {cur} {iso[k][cur] * 1000:.1f} us, "
+            f"best {min(iso[k].values()) * 1000:.1f} us")
+    torch.cuda.synchronize()
+    log(f"[step_tune] isolated candidate timing done ({time.time() - t_start:.0f} s)")
+
+    def cur_s(k):
+        v = Fn._tuned[k]
+        return json.dumps(list(v) if isinstance(v, tuple) else v)
+
+    order = sorted(probs, key=lambda k: -iso[k][cur_s(k)] * probs[k][0])
+
+    images, labels = synthetic_batch(model, a.batch)
+    trainer = Trainer(model, a.batch, resnet_lr_schedule(a.batch), use_graph=True)
+    for _ in range(3):
+        trainer.step(images, labels)
+    timer = StepTimer(trainer, images, labels, a.reps)
+    base = [timer.measure() for _ in range(6)]
+    noise = (max(base) - min(base)) / 2
+    t0 = statistics.median(base)
+    log(f"[step_tune] start: {t0:.4f} ms/step (6 captures: {' '.join(f'{x:.4f}' for x in base)}; "
+        f"noise band {noise:.4f} ms)")
+
+    trials = []
+    for k in order[:a.top]:
+        if time.time() - t_start > a.budget_s:
+            log("[step_tune] time budget reached")
+            break
+        cur = cur_s(k)
+        shortlist = [c for c in sorted(iso[k], key=iso[k].get) if c != cur][:a.cands]
+        best_c, best_gain = None, 0.0
+        for c in shortlist:
+            ta, tb = ab(timer, k, json.loads(cur), json.loads(c), a.rounds)
+            gain = ta - tb
+            trials.append({"key": list(k), "count": probs[k][0], "cur": cur, "cand": c,
+                           "iso_cur_us": iso[k][cur] * 1000, "iso_cand_us": iso[k][c] * 1000,
+                           "step_cur_ms": ta, "step_cand_ms": tb})
+            log(f"  {k} x{probs[k][0]}: {cur} -> {c}: iso {iso[k][cur] * 1000:.1f} -> {iso[k][c] * 1000:.1f} us; "
+                f"step {ta:.4f} -> {tb:.4f} ms")
+            if gain > max(noise, 0.0005 * ta) and gain > best_gain:
+                best_c, best_gain = c, gain
+        if best_c is not None:
+            # re-confirm the winner before keeping it
+            ta, tb = ab(timer, k, json.loads(cur), json.loads(best_c), a.rounds + 1)
+            if ta - tb > max(noise, 0.0005 * ta):
+                Fn._tuned[k] = json.loads(best_c)
+                log(f"  ACCEPT {k}: {cur} -> {best_c} ({ta:.4f} -> {tb:.4f} ms)")
+                trials[-1]["accepted"] = True
+            else:
+                log(f"  reject {k}: {best_c} not confirmed ({ta:.4f} -> {tb:.4f} ms)")
+
+    # final: start table vs tuned table, interleaved
+    final_patch = {k: Fn._tuned[k] for k in probs}
+    s_t, f_t = [], []
+    for _ in range(4):
+        s_t.append(timer.measure(start_table))
+        f_t.append(timer.measure(final_patch))
+    changed = {str(k): [start_table[k], final_patch[k]] for k in probs if start_table[k] != final_patch[k]}
+    res = {"model": a.model, "batch": a.batch, "dtype": a.dtype, "problems": len(probs),
+           "start_ms": statistics.median(s_t), "final_ms": statistics.median(f_t), "noise_ms": noise,
+           "start_samples": s_t, "final_samples": f_t, "changed": changed, "trials": trials,
+           "captures": timer.captures, "seconds": time.time() - t_start}
+    log(f"[step_tune] start table {res['start_ms']:.4f} ms/step -> tuned {res['final_ms']:.4f} ms/step "
+        f"({len(changed)} problems changed, {timer.captures} captures, {res['seconds']:.0f} s)")
+    autotune.save_cache()
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1, default=str)
+    shutil.copy(autotune.DEFAULT_CACHE, os.path.join(os.path.dirname(os.path.abspath(a.out)), "mi355x.json"))
+
+
+if __name__ == "__main__":
+    main()
