@@ -11,12 +11,13 @@ third replay). Its zeroing is now part of the kernel (csrc/kernels/misc.hip laun
 the step graph contains no memset node: with capture on, single-graph and data-parallel replays
 are bitwise equal to capture off (profiles/r4_packet_capture_root_cause.txt).
 
-Multi-rank processes (WORLD_SIZE > 1) still default to packet capture OFF unless the user set the
-variable: the step graph of a real multi-rank job carries RCCL's kernels, a combination only ever
-validated with capture off (the bisection above used a 1-rank communicator); capture on/off makes
-no measurable throughput difference on one GPU.
+Packet capture nevertheless defaults to OFF in every process (``setdefault``: a user who exports
+the variable keeps their choice). The evidence that the memset node was THE cause is where the bad
+value appeared; no same-box A/B has yet shown the old memset path diverging and the fixed build not
+(the legacy path no longer reproduced on a later box), and the failure it guards against is silent
+inexact training. Capture on/off makes no measurable throughput difference on one GPU, so off costs
+nothing.
 """
 import os as _os
 
-if int(_os.environ.get("WORLD_SIZE", "1") or 1) > 1:
-    _os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")

@@ -176,8 +176,8 @@ def worker_env(base: Dict[str, str], rank: int, local_rank: int, world: int, npr
                 "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": str(node_rank), "NODE_RANK": str(node_rank),
                 "MASTER_ADDR": master_addr, "MASTER_PORT": str(master_port),
                 "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
-    if world > 1:  # see azure_hc_intel_tf_amd/__init__.py: multi-rank step graphs run with capture off
-        env.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+    # graph packet capture off unless the user chose (azure_hc_intel_tf_amd/__init__.py)
+    env.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
     env.update(fabric_env(fabric))
     env.update(rccl or {})
     if omp_threads:

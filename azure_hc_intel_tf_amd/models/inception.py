@@ -18,7 +18,7 @@ from typing import List
 
 import torch
 
-from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_act
+from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_op
 from .base import CNNModel
 
 BN_KW = dict(eps=1e-3, decay=0.999, scale=False)
@@ -95,7 +95,8 @@ class InceptionModule:
 
     def forward(self, x):
         N = x.shape[0]
-        out = empty_act((N,) + self.out_shape, x.device)
+        # the concat buffer: bf16, or on the fp32 path the Planes the next module's GEMMs read
+        out = empty_op((N,) + self.out_shape, x.device)
         term_slot = {id(t): (off, t.layer.out_shape[2]) for t, off in zip(self.terminals, self.offsets)}
         for n in self.nodes:
             inp = x if n.src is None else n.src.out
@@ -139,6 +140,10 @@ class InceptionModule:
 
 class InceptionV3(CNNModel):
     name = "inception3"
+    # --compute_dtype fp32 on the HIP kernels: bf16x6 plane GEMMs for every filter shape (1x1, 3x3,
+    # 5x5, 1x7 / 7x1, 1x3 / 3x1; SAME and VALID), max / average pools on planes, concat windows of
+    # a Planes buffer (each branch's BN writes its channel window)
+    F32_NATIVE_OK = True
     default_image_size = 299
     default_batch_size = 32
 

@@ -548,7 +548,12 @@ class Pool(Layer):
 
     def forward(self, x, out=None):
         N = x.shape[0]
-        y = out if out is not None else empty_act((N,) + self.out_shape, x.device)
+        if out is not None:
+            y = out
+        elif Fn.is_planes(x):  # fp32 path: the pooled tensor is the next GEMM's operand
+            y = Fn.Planes.empty((N,) + self.out_shape, x.device)
+        else:
+            y = empty_act((N,) + self.out_shape, x.device)
         amax = None
         if self.is_max and Fn.native(x):
             amax = torch.empty((N,) + self.out_shape, dtype=torch.uint8, device=x.device)

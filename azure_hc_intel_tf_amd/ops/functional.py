@@ -154,6 +154,13 @@ class Planes:
     def reshape(self, *shape) -> "Planes":
         return self.view(*shape)
 
+    def __getitem__(self, idx) -> "Planes":
+        """A view of the logical tensor (e.g. ``x[..., a:b]``: the channel window of a concat
+        buffer an Inception branch writes); the three planes keep their stride."""
+        if not isinstance(idx, tuple):
+            idx = (idx,)
+        return Planes(self.t[(slice(None),) + idx])
+
     def float(self) -> torch.Tensor:
         """The fp32 value (hi + (mid + lo), exact)."""
         return self.t[0].float() + (self.t[1].float() + self.t[2].float())
@@ -1065,6 +1072,10 @@ def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False, argmax=No
     """argmax (GPU, max pool): uint8 [N,P,Q,C] window position of the first maximum, which
     makes the backward a cheap gather."""
     pt, pb, pl, pr = pads
+    if is_planes(x):  # fp32 path: planes in, planes out (the consumer is a GEMM or a concat window)
+        assert is_planes(out), "a pool of Planes writes Planes"
+        _ext.ops().pool_fwd_p3(x.t, out.t, argmax, pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad))
+        return out
     if native(x):
         _ext.ops().pool_fwd(x, out, argmax, pool_geom(x, out, kh, kw, sh, sw, pt, pl, is_max, incl_pad))
         return out
@@ -1086,9 +1097,14 @@ def pool_forward(x, out, kh, kw, sh, sw, pads, is_max, incl_pad=False, argmax=No
 
 def pool_backward(dy, x, y, dx, kh, kw, sh, sw, pads, is_max, incl_pad=False, accumulate=False, argmax=None):
     pt, pb, pl, pr = pads
-    if is_planes(y):  # fp32 stem pool: the argmax gather reads dy and the argmax only
-        assert argmax is not None and is_max
+    if is_planes(x) or is_planes(y):
+        # fp32 path (the ResNet stem pool, Inception's pools): the argmax gather and the 3x3/1
+        # average gather read dy (and the argmax) only -- x / y stand in with fp32 tensors of
+        # their shapes (dx / dy)
+        assert (is_max and argmax is not None) or (not is_max and (kh, kw, sh, sw) == (3, 3, 1, 1))
         y = dy
+        if is_planes(x):
+            x = dx
     if native(x):
         # the kernel walks x / dx with one pixel stride and y / dy with another: align views
         if ld(y) != ld(dy):

@@ -29,16 +29,29 @@ class XgmiAllreduce:
         dev = torch.cuda.current_device() if device is None else int(device)
         cap = max(4, (int(capacity_bytes) // 4 + 3) // 4 * 4)
         self.capacity = cap
-        self.h = cc.xgmi_create(self.rank, self.world, cap, dev)
-        mine = cc.xgmi_handle(self.h)
+        self._cc = cc
+        self.h = None
+        # a local failure (create / export) must not skip the handle exchange: every rank joins the
+        # all-gather (an empty handle marks the failure), so all ranks issue the same collectives and
+        # then raise together instead of one rank moving on to the next collective while its peers
+        # still wait in this one
+        mine, err = b"", ""
+        try:
+            self.h = cc.xgmi_create(self.rank, self.world, cap, dev)
+            mine = bytes(cc.xgmi_handle(self.h).numpy().tobytes())
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
         if self.world > 1:
             got = [None] * self.world
-            dist.all_gather_object(got, bytes(mine.numpy().tobytes()), group=group)
-            handles = torch.stack([torch.frombuffer(bytearray(b), dtype=torch.uint8) for b in got])
+            dist.all_gather_object(got, mine, group=group)
         else:
-            handles = mine.view(1, -1)
+            got = [mine]
+        failed = [r for r, b in enumerate(got) if not b]
+        if failed:
+            self.close()
+            raise RuntimeError(f"xgmi region export failed on rank(s) {failed}" + (f" (here: {err})" if err else ""))
+        handles = torch.stack([torch.frombuffer(bytearray(b), dtype=torch.uint8) for b in got])
         cc.xgmi_open(self.h, handles)
-        self._cc = cc
 
     def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
         if t.numel() > self.capacity:

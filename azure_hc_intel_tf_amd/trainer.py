@@ -127,7 +127,10 @@ class Trainer:
         # weight-gradient GEMMs on a side stream (nn/layers.py run_wgrad), HCB_WGRAD_STREAM=1
         self._wg_stream = (torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda"
                            and os.environ.get("HCB_WGRAD_STREAM", "0") == "1" else None)
-        self.l2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        # sum of w^2 of the decayed tensors (the reported loss's weight-decay term): on the GPU the
+        # optimizer kernel's per-block partials (every slot written each step, no zeroing launch),
+        # summed in a fixed order by loss_total -- deterministic; on the CPU one accumulator
+        self.l2 = torch.zeros(4096 if self.dev.type == "cuda" else 1, dtype=torch.float32, device=self.dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.steps_done = 0
         self._g_fb = None
@@ -181,7 +184,8 @@ class Trainer:
         if self.forward_only:
             Fn.loss_total(self.row_loss, self.B, None, 0.0, self.loss)
             return
-        self.l2.zero_()
+        if self.l2.numel() == 1:
+            self.l2.zero_()
         if self.loss_scaling:
             self.hyper[4:5].zero_()
             Fn.nonfinite(self.ps.grad, self.hyper[4:5])

@@ -494,6 +494,26 @@ void pool_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx
                        g[9], g[10], g[11], g[12], g[13], g[14], g[15], ip, cur_stream());
 }
 
+// fp32 path: the pool on bf16 planes; x / y [3][N][H|P][W|Q][ld] (channel-slice views allowed)
+void pool_fwd_p3(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx, at::IntArrayRef g) {
+  TORCH_CHECK(g.size() == 16, "hcb.pool_fwd_p3: geom");
+  const int64_t xps = check_planes(x, "x"), yps = check_planes(y, "y");
+  TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_fwd_p3: C/ld % 8");
+  TORCH_CHECK(g[0] * g[5] * g[6] * (g[3] / 8) < (1ll << 31), "hcb.pool_fwd_p3: 32-bit index range");
+  check_range(x, (2 * xps + (g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * 2, "x");
+  check_range(y, (2 * yps + (g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * 2, "y");
+  void* ip = nullptr;
+  if (idx.has_value()) {
+    TORCH_CHECK(g[14] && idx->scalar_type() == at::kByte && idx->is_contiguous() &&
+                    idx->numel() >= g[0] * g[5] * g[6] * g[3],
+                "hcb.pool_fwd_p3: idx (max pool only) must be contiguous uint8 [N,P,Q,C]");
+    ip = idx->data_ptr();
+  }
+  hcb::launch_pool_fwd_p3((const uint16_t*)x.data_ptr(), xps, (uint16_t*)y.data_ptr(), yps, g[0], g[1], g[2], g[3],
+                          g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], g[15], ip,
+                          cur_stream());
+}
+
 void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx,
               const Tensor& dx, at::IntArrayRef g, bool accumulate) {
   TORCH_CHECK(g.size() == 16, "hcb.pool_bwd: geom");
@@ -506,11 +526,13 @@ void pool_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const c10::opt
   check_range(dx, ((g[0] * g[1] * g[2] - 1) * g[4] + g[3]) * e, "dx");
   check_range(y, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * e, "y");
   check_range(dy, ((g[0] * g[5] * g[6] - 1) * g[7] + g[3]) * e, "dy");
-  if (f32)  // the fp32 kernel set has the argmax-gather max-pool backward only
-    TORCH_CHECK(g[14] && idx.has_value() && g[8] == g[9] && g[10] == g[11] && (g[8] + g[10] - 1) / g[10] <= 3 &&
-                    g[0] * g[1] <= 65535 && g[0] * g[1] * g[2] * g[4] < (1ll << 31) &&
-                    g[0] * g[5] * g[6] * std::max(g[7], g[3]) < (1ll << 31),
-                "hcb.pool_bwd: fp32 supports the square max pool with its argmax only");
+  if (f32)  // the fp32 kernel set: the argmax-gather max-pool backward, the 3x3/1 average pool
+    TORCH_CHECK((g[14] && idx.has_value() && g[8] == g[9] && g[10] == g[11] && (g[8] + g[10] - 1) / g[10] <= 3 &&
+                 g[0] * g[1] <= 65535 && g[0] * g[1] * g[2] * g[4] < (1ll << 31) &&
+                 g[0] * g[5] * g[6] * std::max(g[7], g[3]) < (1ll << 31)) ||
+                    (!g[14] && g[8] == 3 && g[9] == 3 && g[10] == 1 && g[11] == 1 &&
+                     g[0] * g[5] * g[6] * g[7] * 4 < 0x7fffffffLL),
+                "hcb.pool_bwd: fp32 supports the square max pool with its argmax and the 3x3/1 average pool");
   TORCH_CHECK(g[3] % 8 == 0 && g[4] % 8 == 0 && g[7] % 8 == 0, "hcb.pool_bwd: C/ld % 8");
   TORCH_CHECK(g[0] * g[1] * g[2] * (g[3] / 8) < (1ll << 31), "hcb.pool_bwd: 32-bit index range");
   if (idx.has_value())
@@ -579,11 +601,11 @@ void loss_total(const Tensor& row_loss, int64_t B, const c10::optional<Tensor>& 
   const float* l2p = nullptr;
   if (l2.has_value()) {
     check_f32(*l2, "l2");
-    TORCH_CHECK(l2->numel() >= 1, "hcb.loss_total: l2");
+    TORCH_CHECK(l2->numel() >= 1 && l2->is_contiguous(), "hcb.loss_total: l2");
     l2p = l2->data_ptr<float>();
   }
-  hcb::launch_loss_total(row_loss.data_ptr<float>(), (int)B, l2p, (float)half_wd, loss.data_ptr<float>(),
-                         cur_stream());
+  hcb::launch_loss_total(row_loss.data_ptr<float>(), (int)B, l2p, l2p ? (int)l2->numel() : 0, (float)half_wd,
+                         loss.data_ptr<float>(), cur_stream());
 }
 
 void loss_scale_update(const Tensor& hyper, double world, bool dynamic) {
@@ -616,9 +638,16 @@ void sgd_momentum(const Tensor& w, const Tensor& mom, const Tensor& g, int64_t n
   check_align16(w.data_ptr(), "w");
   check_align16(mom.data_ptr(), "mom");
   check_align16(g.data_ptr(), "g");
+  int slots = 0;
+  if (l2.has_value()) {  // 1 slot: atomic sum (caller zeroes); more: per-block partials (loss_total sums)
+    check_f32(*l2, "l2");
+    slots = (int)l2->numel();
+    TORCH_CHECK(l2->is_contiguous() && (slots == 1 || slots >= hcb::sgd_grid(w.numel())),
+                "hcb.sgd_momentum: l2 must hold 1 or >= ", hcb::sgd_grid(w.numel()), " floats");
+  }
   hcb::launch_sgd_momentum(w.data_ptr<float>(), mom.data_ptr<float>(), g.data_ptr<float>(), w.numel(),
                            n_decay, hyper.data_ptr<float>(), l2.has_value() ? l2->data_ptr<float>() : nullptr,
-                           nesterov ? 1 : 0, (int)hyper.numel(), cur_stream());
+                           slots, nesterov ? 1 : 0, (int)hyper.numel(), cur_stream());
 }
 
 void weight_pack(const Tensor& master, const Tensor& pack, const Tensor& table, int64_t max_work, int64_t lo) {
@@ -1161,6 +1190,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("bn_bwd_apply(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor dgamma, Tensor dbeta, int relu) -> ()");
   m.def("pool_fwd(Tensor x, Tensor(a!) y, Tensor(b!)? idx, int[] geom) -> ()");
   m.def("pool_bwd(Tensor dy, Tensor x, Tensor y, Tensor? idx, Tensor(a!) dx, int[] geom, bool accumulate) -> ()");
+  m.def("pool_fwd_p3(Tensor x, Tensor(a!) y, Tensor(b!)? idx, int[] geom) -> ()");
   m.def("gap_fwd(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx, int N, int HW, int C) -> ()");
   m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale, Tensor? scale_dev=None, Tensor(c!)? dl32=None) -> ()");
@@ -1216,6 +1246,7 @@ HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("bn_bwd_apply", bn_bwd_apply);
   m.impl("pool_fwd", pool_fwd);
   m.impl("pool_bwd", pool_bwd);
+  m.impl("pool_fwd_p3", pool_fwd_p3);
   m.impl("gap_fwd", gap_fwd);
   m.impl("gap_bwd", gap_bwd);
   m.impl("softmax_xent", softmax_xent);

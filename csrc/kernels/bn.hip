@@ -608,33 +608,6 @@ __device__ __forceinline__ GroupMap groupmap(int CVB) {
   return g;
 }
 
-// block-cooperative: sums[i] = sum_r acc[r][0][c0+i], sums[CB+i] = sum_r acc[r][1][c0+i]
-// The replica loads are issued 8 at a time (one L2 round trip, not R dependent ones): in the
-// small late-stage layers this reduction is on the critical path of a one-wave kernel.
-__device__ __forceinline__ void reduce_group_replicas(const float* acc, int R, int C, int c0, int CB,
-                                                      float* sums) {
-  for (int i = threadIdx.x; i < 2 * CB; i += blockDim.x) {
-    const int off = i < CB ? c0 + i : C + c0 + (i - CB);
-    float s = 0.f;
-    for (int r0 = 0; r0 < R; r0 += 8) {
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = r0 + r < R ? acc[(size_t)(r0 + r) * 2 * C + off] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) s += v[r];
-    }
-    sums[i] = s;
-  }
-  __syncthreads();
-}
-
-// Per-block channel coefficients, derived ONCE per channel of the block's group and left in LDS:
-// thread i < CB reduces channel c0 + i's R replicas (sum, sum of squares) and loads its affine
-// parameters, all in one round trip; the row threads then read 8 channels' worth with 16-byte
-// LDS reads. (The per-lane form -- 16-32 scalar parameter loads per thread plus a second round
-// trip for the statistic shift after the barrier -- was the fixed cost of the small launches:
-// in-graph, a 3 MB stage-4 apply took 4.0 us against 2.5 us for a copy, tools/bn_bw_probe.py.)
-// coef: [0][CB] scale, [1][CB] shift of y = scale * z + shift.
 // channel c's two replica sums (R replicas of [2][C]). R8 (the STAT_R = 8 training case): straight-
 // line loads, so the whole coefficient body is one block whose loads issue in one round trip (a
 // runtime replica loop let the compiler hoist the parameter math above it: two round trips)
@@ -995,35 +968,19 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_acc_kernel(
   T* __restrict__ y = reinterpret_cast<T*>(yv);
   extern __shared__ __attribute__((aligned(16))) float sums[];  // [2][CB]
   const GroupMap gm = groupmap(CVB);
-  reduce_group_replicas(acc, R, C, gm.c0, gm.CB, sums);
-  const float inv_n = 1.f / (float)M;
-  if (blockIdx.x == 0) {
-    for (int i = threadIdx.x; i < gm.CB; i += blockDim.x) {
-      const int c = gm.c0 + i;
-      const float d = sums[i] * inv_n;
-      const float mu = d + (shift != nullptr ? shift[c] : 0.f);
-      const float var = fmaxf(sums[gm.CB + i] * inv_n - d * d, 0.f);
-      saved_mean[c] = mu;
-      saved_invstd[c] = rsqrtf(var + eps);
-      if (run_mean != nullptr) {
-        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-        run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * mu;
-        run_var[c] = momentum * run_var[c] + (1.f - momentum) * unb;
-      }
-    }
-  }
+  // channel coefficients once per block channel, one round trip, in LDS (bn_coef_fwd)
+  if (R == 8)
+    bn_coef_fwd<true>(acc, R, C, gm.c0, gm.CB, M, eps, momentum, gamma, beta, shift, blockIdx.x == 0, saved_mean,
+                      saved_invstd, run_mean, run_var, sums, threadIdx.x, 256);
+  else
+    bn_coef_fwd<false>(acc, R, C, gm.c0, gm.CB, M, eps, momentum, gamma, beta, shift, blockIdx.x == 0, saved_mean,
+                       saved_invstd, run_mean, run_var, sums, threadIdx.x, 256);
+  __syncthreads();
   if (gm.r0 >= gm.rows) return;
   float sc[8], sft[8];
   const int cl = (threadIdx.x % CVB) * 8;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float d = sums[cl + e] * inv_n;
-    const float mu = d + (shift != nullptr ? shift[gm.c0 + cl + e] : 0.f);
-    const float var = fmaxf(sums[gm.CB + cl + e] * inv_n - d * d, 0.f);
-    const float s = gamma[gm.c0 + cl + e] * rsqrtf(var + eps);
-    sc[e] = s;
-    sft[e] = beta[gm.c0 + cl + e] - mu * s;
-  }
+  lds_read8(sums + cl, sc);
+  lds_read8(sums + gm.CB + cl, sft);
   const unsigned PQ = (unsigned)P * Q, total = (unsigned)Nimg * PQ;
   for (unsigned op = blockIdx.x * gm.rows + gm.r0; op < total; op += gridDim.x * gm.rows) {
     const int n = (int)(op / PQ);

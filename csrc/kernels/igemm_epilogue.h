@@ -110,8 +110,8 @@ __device__ __forceinline__ void stage_bnb_params(const ConvParams& p, int n0, ch
 
 // In-launch split-K hand-off (cdna guide Guideline 16, counter form), shared by the LDS-DMA
 // kernels: every split parks its partial tile in a workspace slab, publishes it with one
-// agent-scope release + ticket; the last arriver acquires and sums the others into acc and
-// returns true (it then runs the epilogue), the others return false. Call after the main
+// agent-scope release + ticket; the last arriver acquires and sums ALL slabs in index order into
+// acc and returns true (it then runs the epilogue), the others return false. Call after the main
 // loop's final barrier (smem word 0 is used as the broadcast flag).
 // sstride: slabs reserved per tile (S for split-K; the maximum share count for stream-K).
 template <int MI, int NI, int NT>
@@ -142,8 +142,14 @@ __device__ __forceinline__ bool splitk_gather(const ConvParams& p, f32x4 (&acc)[
   const int last = *flag;
   __syncthreads();  // the flag word is epilogue staging space next
   if (!last) return false;
-  for (int s2 = 0; s2 < S; ++s2) {
-    if (s2 == split) continue;
+  // the sum in FIXED slab order 0..S-1 (the last arriver re-reads its own slab too): the fp32
+  // result does not depend on which split arrived last, so split-K / stream-K are run-to-run
+  // deterministic; one extra slab read per tile
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = slab[((size_t)0 * FR + i * NI + j) * NT + tid];
+  for (int s2 = 1; s2 < S; ++s2) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll

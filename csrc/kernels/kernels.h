@@ -228,6 +228,10 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
                      int C, int ldx, int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph,
                      int pw, int is_max, int count_include_pad, int accum, const void* idx,
                      hipStream_t st, bool f32 = false);
+// fp32 path: k x k max / average pool on bf16 planes (x / y plane strides xps / yps elements)
+void launch_pool_fwd_p3(const uint16_t* x, int64_t xps, uint16_t* y, int64_t yps, int N, int H, int W, int C, int ldx,
+                        int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
+                        int count_include_pad, void* idx, hipStream_t st);
 void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, bool f32 = false);
 void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st, bool f32 = false);
 
@@ -241,10 +245,13 @@ void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out,
 // hyper (device fp32): [lr, momentum, weight_decay, grad_scale(, found_inf, loss_scale,
 // good_steps, interval)] so a captured graph picks up a new learning rate every replay; with
 // hyper_n > 4 the update is skipped when found_inf != 0 (loss scaling)
+// l2_slots > 1: per-block w^2 partials into l2_out[0:l2_slots] (>= sgd_grid(n)), summed by loss_total
+int sgd_grid(int64_t n);
 void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
-                         const float* hyper, float* l2_out, int nesterov, int hyper_n, hipStream_t st);
+                         const float* hyper, float* l2_out, int l2_slots, int nesterov, int hyper_n, hipStream_t st);
 void launch_nonfinite(const float* g, int64_t n, float* flag, hipStream_t st);
-void launch_loss_total(const float* row_loss, int B, const float* l2, float half_wd, float* loss, hipStream_t st);
+void launch_loss_total(const float* row_loss, int B, const float* l2, int l2_n, float half_wd, float* loss,
+                       hipStream_t st);
 void launch_loss_scale_update(float* hyper, float world, int dynamic, hipStream_t st);
 struct WPackEntry {  // all int64 so the table is a plain int64 tensor [n][9]
   int64_t src_off;   // fp32 master offset (elements)

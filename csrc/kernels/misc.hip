@@ -117,11 +117,22 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w
                                                            const float* __restrict__ g, int64_t n,
                                                            int64_t n_decay,
                                                            const float* __restrict__ hyper,
-                                                           float* l2_out, int nesterov, int hyper_n) {
+                                                           float* l2_out, int l2_slots, int nesterov,
+                                                           int hyper_n) {
   __shared__ float red[4];
+  // l2_slots > 1: this block's sum of w^2 goes to its OWN slot l2_out[blockIdx.x] (plain store, no
+  // zeroing launch; block 0 clears the slots past the grid) and loss_total sums the slots in a fixed
+  // order -- the reported loss is run-to-run deterministic. l2_slots == 1: one atomic per block
+  // into l2_out[0] (zeroed by the caller).
   // loss scaling: hyper[4] = "non-finite gradient seen" -> skip the whole update (TF
   // LossScaleOptimizer semantics); the flag is wave-uniform so every block exits together
-  if (hyper_n > 4 && hyper[4] != 0.f) return;
+  if (hyper_n > 4 && hyper[4] != 0.f) {
+    if (l2_out != nullptr && l2_slots > 1) {
+      for (int i = threadIdx.x; i < l2_slots; i += blockDim.x)
+        if (i % (int)gridDim.x == (int)blockIdx.x) l2_out[i] = 0.f;
+    }
+    return;
+  }
   const float lr = hyper[0], mu = hyper[1], wd = hyper[2], gscale = hyper[3];
   float l2 = 0.f;
   const int64_t n4 = n >> 2;
@@ -161,7 +172,15 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w
     l2 = wave_sum(l2);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l2;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(l2_out, red[0] + red[1] + red[2] + red[3]);
+    if (threadIdx.x == 0) {
+      const float t = (red[0] + red[1]) + (red[2] + red[3]);
+      if (l2_slots > 1)
+        l2_out[blockIdx.x] = t;
+      else
+        atomicAdd(l2_out, t);
+    }
+    if (l2_slots > 1 && blockIdx.x == 0)
+      for (int i = (int)gridDim.x + threadIdx.x; i < l2_slots; i += blockDim.x) l2_out[i] = 0.f;
   }
 }
 
@@ -520,26 +539,36 @@ __global__ void loss_scale_update_kernel(float* hyper, float world, int dynamic)
   }
   hyper[3] = 1.f / (world * S);
 }
-// loss[0] = mean(row_loss[0:B]) + half_wd * l2[0] (l2 may be null): the step's reported loss in
-// one launch (one workgroup, fixed reduction order) instead of mean / mul / add / copy kernels.
+// loss[0] = mean(row_loss[0:B]) + half_wd * sum(l2[0:l2_n]) (l2 may be null; l2_n > 1: the
+// optimizer's per-block partials): the step's reported loss in one launch (one workgroup, fixed
+// reduction order) instead of mean / mul / add / copy kernels.
 __global__ __launch_bounds__(256) void loss_total_kernel(const float* __restrict__ row_loss, int B,
-                                                         const float* __restrict__ l2, float half_wd,
+                                                         const float* __restrict__ l2, int l2_n, float half_wd,
                                                          float* __restrict__ loss) {
-  __shared__ float part[4];
-  float s = 0.f;
+  __shared__ float part[8];
+  float s = 0.f, q = 0.f;
   for (int i = threadIdx.x; i < B; i += 256) s += row_loss[i];
+  if (l2)
+    for (int i = threadIdx.x; i < l2_n; i += 256) q += l2[i];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    q += __shfl_xor(q, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    part[threadIdx.x >> 6] = s;
+    part[4 + (threadIdx.x >> 6)] = q;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     float t = ((part[0] + part[1]) + (part[2] + part[3])) / (float)B;
-    if (l2) t += half_wd * l2[0];
+    if (l2) t += half_wd * ((part[4] + part[5]) + (part[6] + part[7]));
     loss[0] = t;
   }
 }
-void launch_loss_total(const float* row_loss, int B, const float* l2, float half_wd, float* loss, hipStream_t st) {
-  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(256), 0, st, row_loss, B, l2, half_wd, loss);
+void launch_loss_total(const float* row_loss, int B, const float* l2, int l2_n, float half_wd, float* loss,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(loss_total_kernel, dim3(1), dim3(256), 0, st, row_loss, B, l2, l2_n, half_wd, loss);
 }
 void launch_nonfinite(const float* g, int64_t n, float* flag, hipStream_t st) {
   hipLaunchKernelGGL(nonfinite_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, g, n, flag);
@@ -573,10 +602,11 @@ void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out,
   if (gx > 1) hipLaunchKernelGGL(zero_f32_kernel, dim3((N + 255) / 256), dim3(256), 0, st, out, N);
   hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, st, g, ld, M, N, is_f32, out, gx == 1 ? 1 : 0);
 }
+int sgd_grid(int64_t n) { return grid_for((n + 3) / 4); }
 void launch_sgd_momentum(float* w, float* mom, const float* g, int64_t n, int64_t n_decay,
-                         const float* hyper, float* l2_out, int nesterov, int hyper_n, hipStream_t st) {
-  hipLaunchKernelGGL(sgd_momentum_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, w, mom, g,
-                     n, n_decay, hyper, l2_out, nesterov, hyper_n);
+                         const float* hyper, float* l2_out, int l2_slots, int nesterov, int hyper_n, hipStream_t st) {
+  hipLaunchKernelGGL(sgd_momentum_kernel, dim3(sgd_grid(n)), dim3(256), 0, st, w, mom, g,
+                     n, n_decay, hyper, l2_out, l2_slots, nesterov, hyper_n);
 }
 void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st) {
   hipLaunchKernelGGL(l2norm_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, out);

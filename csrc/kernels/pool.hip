@@ -245,9 +245,11 @@ __global__ __launch_bounds__(256) void pool3s1_fwd_kernel(const uint16_t* __rest
 }
 
 // Average-pool 3x3/1 backward as a gather: the (up to) nine windows covering a pixel, each
-// scaled by 1 / (its valid-tap count), all loads in flight together.
-__global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const uint16_t* __restrict__ dy, uint32_t dy_bytes,
-                                                             uint16_t* __restrict__ dx, int N, int H, int W, int C,
+// scaled by 1 / (its valid-tap count), all loads in flight together. T: the 16-bit activation
+// type, or fp32 (the fp32 path's Inception pool branches: dy / dx are fp32 gradients).
+template <typename T = uint16_t>
+__global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const T* __restrict__ dy, uint32_t dy_bytes,
+                                                             T* __restrict__ dx, int N, int H, int W, int C,
                                                              int ldx, int P, int Q, int ldy, int ph, int pw,
                                                              int incl_pad, int accum) {
   const unsigned CV = (unsigned)C >> 3;
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const uint16_t* __r
     const unsigned t = pix / (unsigned)W;
     const int h = (int)(t % (unsigned)H);
     const int n = (int)(t / (unsigned)H);
-    u32x4 d[9];
+    Act8<T> d[9];
     float sc[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -268,7 +270,7 @@ __global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const uint16_t* __r
       for (int j = 0; j < 3; ++j) {
         const int p = h + ph - i, q = w + pw - j;  // windows p - ph <= h <= p - ph + 2
         const bool in = (unsigned)p < (unsigned)P && (unsigned)q < (unsigned)Q;
-        d[i * 3 + j] = buf_load16(dr, in ? (uint32_t)(((n * P + p) * Q + q) * ldy + cv * 8) * 2u : HCB_OOB);
+        d[i * 3 + j].load(dr, in ? (uint32_t)(((n * P + p) * Q + q) * ldy + cv * 8) * Act8<T>::ESZ : HCB_OOB);
         const int hs = p - ph, ws = q - pw;
         const int vr = ((unsigned)hs < (unsigned)H) + ((unsigned)(hs + 1) < (unsigned)H) + ((unsigned)(hs + 2) < (unsigned)H);
         const int vc = ((unsigned)ws < (unsigned)W) + ((unsigned)(ws + 1) < (unsigned)W) + ((unsigned)(ws + 2) < (unsigned)W);
@@ -280,18 +282,89 @@ __global__ __launch_bounds__(256) void avgpool3s1_bwd_kernel(const uint16_t* __r
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       float f[8];
-      unpack8(d[k], f);
+      d[k].to_f(f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[e] += f[e] * sc[k];
     }
-    uint16_t* dp = dx + ((size_t)(n * H + h) * W + w) * ldx + cv * 8;
+    T* dp = dx + ((size_t)(n * H + h) * W + w) * ldx + cv * 8;
     if (accum) {
       float o[8];
-      unpack8(*reinterpret_cast<const u32x4*>(dp), o);
+      Act8<T> ov;
+      ov.load(dp);
+      ov.to_f(o);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[e] += o[e];
     }
-    *reinterpret_cast<u32x4*>(dp) = pack8(g);
+    Act8<T>::store(dp, g);
+  }
+}
+
+// fp32 path (--compute_dtype fp32; Inception-v3's 3x3/2 max-pool reductions and 3x3/1 average /
+// max pool branches): k x k pool on bf16 PLANES -- x and y are [3][N][H|P][W|Q][ld] with plane
+// strides xps / yps (elements), each window value the exact fp32 hi + mid + lo. The maximum is
+// split back into planes (the split is canonical: the winning element's own planes, bit for bit);
+// the average is summed and divided in fp32, then split. One thread per output pixel x 8 channels,
+// the window's 3 plane loads per tap issued together.
+__global__ __launch_bounds__(256) void pool_fwd_p3_kernel(const uint16_t* __restrict__ x, int64_t xps,
+                                                          uint16_t* __restrict__ y, int64_t yps, int N, int H, int W,
+                                                          int C, int ldx, int P, int Q, int ldy, int kh, int kw,
+                                                          int sh, int sw, int ph, int pw, int is_max, int incl_pad,
+                                                          uint8_t* __restrict__ amax) {
+  const unsigned CV = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int cv = (int)(idx % CV);
+    const unsigned pix = idx / CV;
+    const int q = (int)(pix % (unsigned)Q);
+    const unsigned t = pix / (unsigned)Q;
+    const int p = (int)(t % (unsigned)P);
+    const int n = (int)(t / (unsigned)P);
+    const int h0 = p * sh - ph, w0 = q * sw - pw;
+    float acc[8];
+    int arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc[e] = is_max ? -INFINITY : 0.f;
+      arg[e] = 255;
+    }
+    int cnt = 0;
+    for (int r = 0; r < kh; ++r) {
+      const int h = h0 + r;
+      if (h < 0 || h >= H) continue;
+      for (int s2 = 0; s2 < kw; ++s2) {
+        const int w = w0 + s2;
+        if (w < 0 || w >= W) continue;
+        const uint16_t* src = x + ((size_t)(n * H + h) * W + w) * ldx + cv * 8;
+        float f[8];
+        merge_p3(*reinterpret_cast<const u32x4*>(src), *reinterpret_cast<const u32x4*>(src + xps),
+                 *reinterpret_cast<const u32x4*>(src + 2 * xps), f);
+        ++cnt;
+        if (is_max) {
+          const int pos = r * kw + s2;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (f[e] > acc[e]) {  // strict: the FIRST maximal element keeps the gradient
+              acc[e] = f[e];
+              arg[e] = pos;
+            }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += f[e];
+        }
+      }
+    }
+    if (!is_max) {
+      const float div = incl_pad ? (float)(kh * kw) : (float)(cnt > 0 ? cnt : 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] /= div;
+    }
+    store_p3(y + ((size_t)(n * P + p) * Q + q) * ldy + cv * 8, yps, acc);
+    if (is_max && amax != nullptr) {
+      u32x2 a;
+      a[0] = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) | ((uint32_t)arg[3] << 24);
+      a[1] = (uint32_t)arg[4] | ((uint32_t)arg[5] << 8) | ((uint32_t)arg[6] << 16) | ((uint32_t)arg[7] << 24);
+      *reinterpret_cast<u32x2*>(amax + ((size_t)(n * P + p) * Q + q) * C + cv * 8) = a;
+    }
   }
 }
 
@@ -516,7 +589,14 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
                          (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, ph, pw, accum, (const uint8_t*)idx, cv_shift);
     return;
   }
-  if (f32) {  // fp32 path: the argmax gather only (the stem pool of the ResNets)
+  if (f32) {  // fp32 path: the argmax-gather max pool, the 3x3/1 average pool
+    if (!is_max && kh == 3 && kw == 3 && sh == 1 && sw == 1) {
+      const long b32 = (long)N * P * Q * ldy * 4;
+      if (b32 >= 0x7fffffffL) return;  // rejected on the host
+      hipLaunchKernelGGL(avgpool3s1_bwd_kernel<float>, dim3(ew_grid(total)), dim3(256), 0, st, (const float*)dy,
+                         (uint32_t)b32, (float*)dx, N, H, W, C, ldx, P, Q, ldy, ph, pw, count_include_pad, accum);
+      return;
+    }
     if (!amax_ok || (kh + sh - 1) / sh > 3) return;  // rejected on the host (bindings.cpp)
     if ((kh + sh - 1) / sh <= 2)
       hipLaunchKernelGGL((maxpool_bwd_amax_kernel<2, float>), agrid, dim3(256), 0, st, (const float*)dy, (float*)dx, N,
@@ -538,7 +618,7 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
   }
   const long dybytes = (long)N * P * Q * ldy * 2;
   if (!is_max && kh == 3 && kw == 3 && sh == 1 && sw == 1 && dybytes < 0x7fffffffL) {
-    hipLaunchKernelGGL(avgpool3s1_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
+    hipLaunchKernelGGL(avgpool3s1_bwd_kernel<uint16_t>, dim3(ew_grid(total)), dim3(256), 0, st, (const uint16_t*)dy,
                        (uint32_t)dybytes, (uint16_t*)dx, N, H, W, C, ldx, P, Q, ldy, ph, pw, count_include_pad, accum);
     return;
   }
@@ -546,6 +626,14 @@ void launch_pool_bwd(const void* dy, const void* x, const void* y, void* dx, int
                      (const uint16_t*)x, (const uint16_t*)y, (uint16_t*)dx, N, H, W, C, ldx, P, Q,
                      ldy, kh, kw, sh, sw, ph, pw, is_max, count_include_pad, accum,
                      (const uint8_t*)idx);
+}
+
+void launch_pool_fwd_p3(const uint16_t* x, int64_t xps, uint16_t* y, int64_t yps, int N, int H, int W, int C, int ldx,
+                        int P, int Q, int ldy, int kh, int kw, int sh, int sw, int ph, int pw, int is_max,
+                        int count_include_pad, void* idx, hipStream_t st) {
+  const long total = (long)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(pool_fwd_p3_kernel, dim3(ew_grid(total)), dim3(256), 0, st, x, xps, y, yps, N, H, W, C, ldx, P,
+                     Q, ldy, kh, kw, sh, sw, ph, pw, is_max, count_include_pad, (uint8_t*)idx);
 }
 
 void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, bool f32) {

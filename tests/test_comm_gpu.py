@@ -64,49 +64,53 @@ def test_native_async_range_allreduce_overlap_one_rank():
 def test_segmented_overlap_step_matches_single_graph(model_name):
     """The multi-GPU training step (one graph per backward segment, each segment's gradient
     ranges handed to the C++ RCCL engine asynchronously, join, optimizer graph) on a forced
-    1-rank communicator must train like the single-graph step: the same losses up to the
-    GPU's run-to-run noise (fp32 atomics in the fused BN statistics reorder between runs,
-    ~0.3% on the first loss at this tiny batch), and the segments' gradient ranges must
-    cover the flat gradient buffer exactly once."""
+    1-rank communicator must train EXACTLY like the single-graph step: both run in deterministic
+    mode (no split-K, one accumulator replica per tile), where the 1-rank reduction is the
+    identity, so losses and master weights are compared bitwise -- a segment reduced before all
+    of its gradients were written would show up here (no tolerance that could absorb
+    a partial race). The segments' gradient ranges must cover the flat gradient buffer exactly once."""
     from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.ops import functional as Fn
     from azure_hc_intel_tf_amd.parallel.native import NativeReducer
     from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 
     size = 96 if model_name == "resnet50" else 139
-    runs = []
-    for seg in (False, True):
-        torch.manual_seed(0)
-        m = create_model(model_name, image_size=size, device="cuda")
-        img, lab = synthetic_batch(m, 8)
-        red = NativeReducer(force=True) if seg else None
-        t = Trainer(m, 8, constant_lr(0.002), reducer=red, world_size=1, use_graph=True, graph_warmup=2,
-                    force_overlap=seg)
-        # no host sync between steps (as in bench.py): losses are traced device-side
-        tr = torch.zeros(8, device="cuda")
-        for i in range(8):
-            tr[i:i + 1].copy_(t.step(img, lab))
-        losses = tr.tolist()
-        if seg:
-            # collectives captured in the step graph: one graph, >= 2 segments reduced in it
-            assert t._g_all is not None and t._segs is None and len(t._seg_ranges) >= 2
-            cover = torch.zeros(m.ps.grad.numel(), dtype=torch.int32)
-            for rng in t._seg_ranges.values():
-                for off, n in rng:
-                    cover[off:off + n] += 1
-            # every gradient exactly once (the buffer carries alignment padding between tensors)
-            assert int(cover.max()) == 1 and int(cover.sum()) >= m.num_params() - 64
-            red.close()
-        else:
-            assert t._g_all is not None
-        runs.append(losses)
+    runs, masters = [], []
+    Fn.set_deterministic(True)
+    try:
+        for seg in (False, True):
+            torch.manual_seed(0)
+            m = create_model(model_name, image_size=size, device="cuda")
+            img, lab = synthetic_batch(m, 8)
+            red = NativeReducer(force=True) if seg else None
+            t = Trainer(m, 8, constant_lr(0.002), reducer=red, world_size=1, use_graph=True, graph_warmup=2,
+                        force_overlap=seg)
+            # no host sync between steps (as in bench.py): losses are traced device-side
+            tr = torch.zeros(8, device="cuda")
+            for i in range(8):
+                tr[i:i + 1].copy_(t.step(img, lab))
+            losses = tr.tolist()
+            if seg:
+                # collectives captured in the step graph: one graph, >= 2 segments reduced in it
+                assert t._g_all is not None and t._segs is None and len(t._seg_ranges) >= 2
+                cover = torch.zeros(m.ps.grad.numel(), dtype=torch.int32)
+                for rng in t._seg_ranges.values():
+                    for off, n in rng:
+                        cover[off:off + n] += 1
+                # every gradient exactly once (the buffer carries alignment padding between tensors)
+                assert int(cover.max()) == 1 and int(cover.sum()) >= m.num_params() - 64
+                red.close()
+            else:
+                assert t._g_all is not None
+            runs.append(losses)
+            masters.append(m.ps.master.detach().cpu().clone())
+    finally:
+        Fn.set_deterministic(False)
     a, b = torch.tensor(runs[0]), torch.tensor(runs[1])
     assert torch.isfinite(b).all()
-    # run-to-run spread of this non-deterministic step (tools/pc_noise_probe.py, 3 runs each, single
-    # and dp graphs): <= 0.3% at step 0 growing to ~4% at step 3 (4.62-4.80) as the tiny batch is
-    # memorised; 3% at step 3 failed a correct pair (4.754 vs 4.569)
-    assert torch.allclose(a[:3], b[:3], rtol=3e-2, atol=3e-2), (runs[0], runs[1])
-    assert torch.allclose(a[3], b[3], rtol=8e-2), (runs[0], runs[1])
-    assert b[-1] < 0.9 * b[0] and a[-1] < 0.9 * a[0], (runs[0], runs[1])
+    assert torch.equal(a, b), (runs[0], runs[1])
+    assert torch.equal(masters[0], masters[1])
+    assert b[-1] < 0.9 * b[0], runs[1]
 
 
 def _xgmi_worker(rank, world, port, q):

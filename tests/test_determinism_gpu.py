@@ -36,19 +36,24 @@ def test_deterministic_mode_is_bitwise_reproducible():
 
 
 def test_deterministic_mode_trains_like_default():
+    """Deterministic mode changes only the ORDER of fp32 sums (no split-K, one accumulator slot per
+    tile), so its trajectory must look like one more default-mode run. The bound is the run-to-run
+    spread of the default mode itself, measured here (4 runs: their atomics reorder between runs),
+    not an observed constant: this tiny-batch bf16 net amplifies any rounding-order difference
+    chaotically (a 1-ulp change of the stem BN's coefficients moved step 3 by ~4%:
+    profiles/r5_stem_prologue_determinism.txt), and a fixed 3% band failed correct code."""
     Fn.set_deterministic(True)
     try:
         _, _, trd = _run(steps=6, lr=0.01)
     finally:
         Fn.set_deterministic(False)
-    _, _, trn = _run(steps=6, lr=0.01)
-    # (a stable learning rate: at 0.05 this tiny-batch run diverges and amplifies the
-    # rounding-order difference chaotically). The default run's atomics make its trajectory vary
-    # from run to run; past step 4 the two drift apart by up to ~0.14 in loss (observed), so the
-    # first steps are compared tightly and the end point within 10%.
-    assert torch.allclose(trd[:4], trn[:4], rtol=3e-2, atol=3e-2), (trd.tolist(), trn.tolist())
-    assert abs(float(trd[-1]) - float(trn[-1])) < 0.1 * float(trn[-1]), (trd.tolist(), trn.tolist())
-    assert float(trd[-1]) < float(trd[0]) - 2.0 and float(trn[-1]) < float(trn[0]) - 2.0
+    runs = torch.stack([_run(steps=6, lr=0.01)[2] for _ in range(4)]).cpu()
+    trd = trd.cpu()
+    lo, hi = runs.min(0).values, runs.max(0).values
+    band = 2.0 * (hi - lo) + 2e-3 * hi.abs()
+    assert bool(((trd >= lo - band) & (trd <= hi + band)).all()), (trd.tolist(), runs.tolist())
+    # (a stable learning rate: at 0.05 this tiny-batch run diverges)
+    assert float(trd[-1]) < float(trd[0]) - 2.0 and float(runs[:, -1].max()) < float(runs[:, 0].min()) - 2.0
 
 
 def _shallow(device, **kw):

@@ -479,3 +479,38 @@ def _xgmi_validation(hvd):
 
 def test_xgmi_startup_validation_disables_on_any_rank_failure():
     run(2, _xgmi_validation)
+
+
+def _xgmi_construction_failure(hvd):
+    """XgmiAllreduce construction when the region export fails on ONE rank: every rank
+    still joins the handle all-gather and every rank raises, so the next collective (the startup
+    cross-check's RCCL reduction) is issued by all ranks -- no rank left waiting in a collective
+    its peers never enter. Fake native library on gloo."""
+    from azure_hc_intel_tf_amd.parallel import xgmi
+
+    class FakeCC:
+        def xgmi_create(self, rank, world, cap, dev):
+            if rank == 1:
+                raise RuntimeError("hipIpcGetMemHandle: invalid argument")
+            return 7
+
+        def xgmi_handle(self, h):
+            return torch.arange(64, dtype=torch.uint8)
+
+        def xgmi_open(self, h, handles):
+            raise AssertionError("must not open after a failed exchange")
+
+        def xgmi_destroy(self, h):
+            pass
+
+    xgmi.load = lambda: FakeCC()
+    xgmi.torch.cuda.current_device = lambda: 0
+    with pytest.raises(RuntimeError, match=r"rank\(s\) \[1\]"):
+        xgmi.XgmiAllreduce(capacity_bytes=1024)
+    t = torch.ones(3)
+    dist.all_reduce(t)  # both ranks arrive here: the collectives stayed matched
+    assert torch.all(t == hvd.size())
+
+
+def test_xgmi_construction_failure_keeps_collectives_matched():
+    run(2, _xgmi_construction_failure)

@@ -428,6 +428,32 @@ def test_sgd_momentum_flat():
     assert abs(l2.item() - l2c.item()) / l2c.item() < 1e-4
 
 
+def test_sgd_l2_partials_deterministic_and_summed_by_loss_total():
+    """The trainer's form: per-block w^2 partials (one slot per optimizer block, every slot written,
+    the slots past the grid cleared) summed in a fixed order by loss_total -- bitwise equal on
+    repeats (no atomics), equal to the fp64 sum; a skipped (non-finite) step reports l2 = 0."""
+    torch.manual_seed(4)
+    n, nd = 1_000_003, 700_000
+    hyper = torch.tensor([0.0, 0.9, 4e-5, 1.0, 0.0], device=DEV)  # lr 0: w unchanged between repeats
+    w, g = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+    row = torch.rand(16, device=DEV)
+    outs = []
+    for rep in range(3):
+        m = torch.zeros(n, device=DEV)
+        l2 = torch.full((4096,), float("nan"), device=DEV)  # stale garbage: must all be overwritten
+        Fn.sgd_momentum(w, m, g, nd, hyper, l2)
+        out = torch.empty(1, device=DEV)
+        Fn.loss_total(row, 16, l2, 0.5, out)
+        outs.append(out.item())
+    assert outs[0] == outs[1] == outs[2]
+    ref = row.double().mean() + 0.5 * (w[:nd].double() ** 2).sum()
+    assert abs(outs[0] - ref.item()) <= 2e-6 * abs(ref.item())
+    hyper[4] = 1.0  # found_inf: the update is skipped, the l2 term reads 0
+    l2 = torch.full((4096,), 7.0, device=DEV)
+    Fn.sgd_momentum(w, torch.zeros(n, device=DEV), g, nd, hyper, l2)
+    assert float(l2.abs().sum()) == 0.0
+
+
 @pytest.mark.parametrize("cin,cout,k", [(16, 24, 3), (136, 200, 3), (64, 128, 1), (256, 1001, 1), (8, 64, 7)])
 def test_weight_pack_transposed_flip(cin, cout, k):
     """Vector copy + LDS-tiled transpose of the weight pack kernel (partial and full 64x64
