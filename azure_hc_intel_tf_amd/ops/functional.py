@@ -286,29 +286,16 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
                12: (128, 128), 13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (64, 128),
                # 3x3 / stride-1 kernels with the input patch resident in LDS (conv3x3_patch.hip)
                17: (128, 128), 18: (256, 128), 19: (256, 64), 20: (128, 64), 21: (128, 128),
-               # LDS-DMA rings with two 64-deep k-steps per stage (one barrier per 128 of K)
-               22: (64, 128), 23: (128, 128), 24: (128, 128), 25: (64, 128), 26: (64, 64),
-               # two-slot rings sized for two / three workgroups per CU
-               27: (128, 128), 28: (128, 128), 29: (128, 64), 30: (64, 128),
-               # register-pipelined LDS-DMA loop on cfg 4, 5, 7, 12, 13, 14, 16's tiles
-               31: (128, 128), 32: (128, 64), 33: (64, 128), 34: (128, 128), 35: (128, 128), 36: (256, 128),
-               37: (64, 128)}
-# 100 + i: the plane-GEMM kernel (conv_p3_fwd.h cfg i) on one 16-bit plane (conv_s1.hip); filled in
-# below from _P3_TILES
+               }
+# (cfg 22-37 -- two k-steps per stage, occupancy-sized two-slot rings, the register-pipelined loop --
+# and 100-117, the plane kernel on one 16-bit plane, were measured without a step gain and removed in
+# round 5: profiles/r5_prune_variants.txt)
 PATCH_CFG0 = 17
 PATCH_CFGS = (17, 18, 19, 20, 21)
-TUNE_KU2 = False  # offer cfg 22-26 to the autotuner (see fwd_candidates)
-TUNE_OCC = False  # offer cfg 27-30 to the autotuner (see fwd_candidates)
-# offer cfg 31-37 (register-pipelined LDS-DMA loop) to the autotuner: a full bf16 retune with them
-# picked none of them for ResNet-50's 45 problems (profiles/r4ab_bf16_pipe_retune.txt)
-TUNE_PIPE = False
-# weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-9 LDS-DMA ring, 100-107 slot rings
+# weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-14 LDS-DMA rings
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
-                12: (64, 128), 13: (128, 64), 14: (64, 128),
-                # 100-107: the fp32 path's slot-ring kernel on one 16-bit plane (conv_wgrad_s1.hip)
-                100: (128, 128), 101: (128, 128), 102: (128, 128), 103: (256, 128), 104: (128, 64),
-                105: (64, 64), 106: (64, 128), 107: (128, 128)}
+                12: (64, 128), 13: (128, 64), 14: (64, 128)}
 N_CU = 256
 _tuned: dict = {}
 
@@ -333,21 +320,9 @@ def fwd_candidates(N: int, patch: bool = False):
     """Tile configs worth timing for a GEMM with N output columns; ``patch``: the problem is a
     3x3 / stride-1 / pad-1 conv over a multiple of 64 channels (patch_eligible), so the
     LDS-resident-patch kernels are candidates too."""
-    # cfg 22-26 (two k-steps per LDS-DMA stage) only with the module switch TUNE_KU2: under
-    # back-to-back timing they win per layer (stage-3 3x3 23.2 vs 24.3 us) yet the step runs 1.2%
-    # slower with them, and equal under per-launch isolated timing (profiles/r3x_ku2_cache_ab.txt)
-    ku2 = [22, 23, 24, 25, 26] if TUNE_KU2 else []
-    # cfg 27-30 (two-slot rings for two / three workgroups per CU) likewise: the per-layer tuner
-    # picks them for 25 of ResNet-50's 45 bf16 problems, and the step then runs 0.7% SLOWER
-    # (9436 vs 9507 img/s, interleaved A/B on one box: profiles/r4x_bf16_occ_ab.txt) -- unlike
-    # the fp32 plane GEMMs, whose occupancy tiles win in the step too
-    occ = [27, 28, 29, 30] if TUNE_OCC else []
-    pipe = [31, 32, 33, 34, 35, 36, 37] if TUNE_PIPE else []
-    s1 = [CONV_S1_BASE + c for c, (bm, bn) in _P3_TILES.items() if bn <= max(64, N)] if TUNE_S1 else []
     if N <= 64:
-        return ([1, 2, 5, 6, 10] + ([26] if ku2 else []) + ([29] if occ else []) + ([32] if pipe else [])
-                + ([19, 20] if patch else []) + s1)
-    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16] + ku2 + occ + pipe + s1
+        return [1, 2, 5, 6, 10] + ([19, 20] if patch else [])
+    c = [0, 3, 1, 2, 4, 7, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16]
     c = c + [15] if N > 128 else c
     return c + ([17, 18, 19, 20, 21] if patch else [])
 
@@ -365,8 +340,6 @@ def wgrad_candidates(Nout: int, K: int, M: int):
     ksteps = math.ceil(M / 64)
     out = []
     for c, (bm, bn) in _WGRAD_TILES.items():
-        if c >= 100 and ((Nout <= 64 and bm > 64) or (K <= 64 and bn > 64) or (Nout < 256 and bm > 128)):
-            continue
         tiles = math.ceil(Nout / bm) * math.ceil(K / bn)
         for s in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512):
             if s > 1 and ksteps // s < 2:
@@ -469,12 +442,7 @@ def set_tuned(table: dict) -> None:
 _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
              7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
              13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64)}
-_CONV_TILES.update({100 + c: t for c, t in _P3_TILES.items()})
-CONV_S1_BASE = 100
-# offer the one-plane slot-ring kernel (cfg 100-117) to the bf16 / fp16 autotuner: a retune picks it for 19
-# of ResNet-50's 45 problems and the step is unchanged (profiles/r4s1_bf16_slot_ring_fwd.txt)
-TUNE_S1 = False
-# workgroups per CU each plane-GEMM cfg is built for (its stream-K grid: N_CU x occupancy)
+# workgroups per CU each plane-GEMM cfg is built for
 _P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3}
 # wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles),
 # 12-15 32-deep slots, two / three workgroups per CU
@@ -496,7 +464,8 @@ def p3_candidates(M: int, N: int, K: int):
     """(cfg, splits) worth timing for an fp32 (Planes) forward / data-grad GEMM: every tile, with
     split-K factors that bring the grid close to whole rounds of the 256 CUs (one workgroup fits per
     CU: 144 KB of LDS) -- a 196-tile layer leaves 60 CUs idle, 4 splits run it in 3.06 rounds --
-    while every split keeps >= 2 64-deep k-steps."""
+    while every split keeps >= 2 64-deep k-steps. (Stream-K shares were measured 11-30% slower per
+    layer and removed: profiles/r4v_streamk_probe.txt, profiles/r5_prune_variants.txt.)"""
     out = []
     ksteps = math.ceil(K / 64)
     for c, (bm, bn) in _P3_TILES.items():
@@ -508,19 +477,6 @@ def p3_candidates(M: int, N: int, K: int):
             if tiles * s > 6 * N_CU or ksteps // s < 2 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
                 break
             out.append((c, s))
-        # stream-K: one or two rounds of the resident workgroups, each an even share of every
-        # (tile, k-slot) iteration (no quantization of e.g. 196 tiles on 256 CUs)
-        nk = ksteps * 64 // (64 if c <= 6 else 32)
-        if tiles % N_CU == 0:
-            continue
-        for rounds in (1, 2):
-            G = N_CU * _P3_OCC.get(c, 1) * rounds
-            q = tiles * nk // G
-            if G >= tiles * nk or q < 4:
-                continue
-            smax = min(G, -(-nk // q) + 1)
-            if tiles * smax * bm * bn <= SPLITK_WS_FLOATS:
-                out.append((c, -G))
     return out
 
 
@@ -582,12 +538,10 @@ def _plan3(cfg, M, N, K, device, taps: int = 1):
         cfg, splits = cfg
     else:
         splits = 1
-    splits = int(splits)
-    if splits >= 0:
-        splits = max(1, min(splits, max(K // 64, 1)))
+    splits = max(1, min(int(splits), max(K // 64, 1)))
     if _DET[0]:
         splits = 1
-    if splits != 1:  # split-K, or stream-K (splits = -G workgroups)
+    if splits != 1:
         ensure_splitk_workspace(device)
     return int(cfg), int(splits)
 

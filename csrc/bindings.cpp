@@ -316,11 +316,6 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArra
   p.dw = dw.data_ptr<float>();
   p.dy_bytes = (uint32_t)yb;
   p.x_bytes = (uint32_t)xb;
-  if (cfg >= hcb::WGRAD_S1_BASE) {  // the slot-ring weight-grad kernel on one 16-bit plane (conv_wgrad_s1.hip)
-    TORCH_CHECK(!f32 && cfg < hcb::WGRAD_S1_BASE + hcb::N_WS1_CFG, "hcb.conv_wgrad: bad s1 cfg");
-    hcb::launch_wgrad_s1(p, (int)cfg - hcb::WGRAD_S1_BASE, eff_splits, cur_stream());
-    return;
-  }
   hcb::launch_conv_wgrad(p, (int)cfg, eff_splits, cur_stream());
 }
 
@@ -1026,23 +1021,10 @@ hcb::ConvParams p3_params(const Tensor& x, const Tensor& w, const Tensor& w_lo, 
   const int64_t splits = g1.size() > 30 ? g1[30] : 1;
   if (g1.size() > 30) g1[30] = 1;
   hcb::ConvParams p = conv_params(x.select(0, 0), w, y, yres, bias, c10::nullopt, g1, 0);
-  // splits < 0: stream-K over -splits workgroups (an even share of every (tile, k-slot) iteration each)
   const int bm = hcb::p3_tile_m((int)cfg), bn = hcb::p3_tile_n((int)cfg);
   const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * ((p.Nout + bn - 1) / bn);
-  if (splits < 0) {
-    const int64_t nk = p.Kpad / hcb::p3_slot_k((int)cfg), T = tiles * nk;
-    const int64_t G = std::min<int64_t>(-splits, T);  // no more workgroups than iterations
-    TORCH_CHECK(p.Kpad % hcb::p3_slot_k((int)cfg) == 0, "hcb.conv_p3: Kpad vs slot depth");
-    TORCH_CHECK(G >= 1 && G <= (1 << 20) && T < (1 << 30), "hcb.conv_p3: stream-K grid out of range");
-    const int64_t q = T / G;  // every share has q or q + 1 iterations
-    TORCH_CHECK(q >= 1, "hcb.conv_p3: stream-K needs >= 1 k-slot per workgroup");
-    p.sk_grid = (int)G;
-    p.sk_smax = (int)std::min<int64_t>(G, (nk + q - 1) / q + 1);  // shares one tile can have
-    p.splits = 1;
-  } else {
-    p.splits = (int)splits;
-    TORCH_CHECK(p.splits >= 1 && p.splits <= p.Kpad / 64, "hcb.conv_p3: 1 <= splits <= k-steps");
-  }
+  p.splits = (int)splits;
+  TORCH_CHECK(p.splits >= 1 && p.splits <= p.Kpad / 64, "hcb.conv_p3: 1 <= splits <= k-steps");
   TORCH_CHECK(p.out_f32 && y.scalar_type() == at::kFloat, "hcb.conv_p3: fp32 output");
   check_range(x, 2 * xps * 2 + (int64_t)p.x_bytes, "x planes");
   TORCH_CHECK(2 * xps * 2 < (1ll << 32), "hcb.conv_p3: plane stride exceeds the 32-bit offset range");
@@ -1065,10 +1047,9 @@ hcb::ConvParams p3_params(const Tensor& x, const Tensor& w, const Tensor& w_lo, 
   }
   TORCH_CHECK(!stats_shift.has_value() || p.stats != nullptr, "hcb.conv_p3: stats_shift without stats");
   p.stats_shift = opt_f32(stats_shift, p.Nout, "stats_shift");
-  if (p.splits > 1 || p.sk_grid > 0) {
+  if (p.splits > 1) {
     TORCH_CHECK(g_splitk_ws != nullptr && g_splitk_cnt != nullptr, "hcb.conv_p3: split-K workspace not set");
-    const int64_t slabs = p.sk_grid > 0 ? p.sk_smax : p.splits;
-    TORCH_CHECK(tiles * slabs * bm * bn * 4 <= g_splitk_ws_bytes, "hcb.conv_p3: split-K workspace too small");
+    TORCH_CHECK(tiles * p.splits * bm * bn * 4 <= g_splitk_ws_bytes, "hcb.conv_p3: split-K workspace too small");
     TORCH_CHECK(tiles <= g_splitk_cnt_n, "hcb.conv_p3: split-K counter array too small");
     p.ws = g_splitk_ws;
     p.cnt = g_splitk_cnt;

@@ -112,41 +112,6 @@ __device__ __forceinline__ void mfma_tile_step(const u32x4* Ab, const u32x4* Bb,
   }
 }
 
-// One 64-deep k-step's fragments in registers (both 32-deep halves), and its MFMAs: the
-// register-pipelined LDS-DMA loop (PIPE) reads step k+1's fragments while step k's MFMAs run.
-template <int TM, int TN>
-struct GFrags {
-  act16x8 a[2][TM / 16], b[2][TN / 16];
-};
-template <int WM, int WN, int TM, int TN>
-__device__ __forceinline__ void gfrag_read(const u32x4* Ab, const u32x4* Bb, GFrags<TM, TN>& f, int wm, int wn,
-                                           int lane) {
-  const int frow = lane & 15, fq = lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int ch = ks * 4 + fq;
-#pragma unroll
-    for (int i = 0; i < TM / 16; ++i) {
-      const int row = wm * TM + i * 16 + frow;
-      f.a[ks][i] = __builtin_bit_cast(act16x8, Ab[row * 8 + (ch ^ ((row >> 1) & 7))]);
-    }
-#pragma unroll
-    for (int j = 0; j < TN / 16; ++j) {
-      const int row = wn * TN + j * 16 + frow;
-      f.b[ks][j] = __builtin_bit_cast(act16x8, Bb[row * 8 + (ch ^ ((row >> 1) & 7))]);
-    }
-  }
-}
-template <int TM, int TN>
-__device__ __forceinline__ void gfrag_mma(const GFrags<TM, TN>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int i = 0; i < TM / 16; ++i)
-#pragma unroll
-      for (int j = 0; j < TN / 16; ++j) acc[i][j] = mfma16(f.a[ks][i], f.b[ks][j], acc[i][j]);
-}
-
 // ============================================================== register-staged main loop
 // (16-bit operands; fp32 runs on the plane GEMMs, conv_p3.hip)
 template <int WM, int WN, int TM, int TN, bool CBIG, bool LHSDIL, bool BNB>
@@ -228,27 +193,22 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvParams p) {
 }
 
 // ============================================================== LDS-DMA multi-stage main loop
-// KU: 64-deep k-steps per ring stage (one wait + barrier per stage: KU = 2 halves the barriers
-// and doubles the MFMA run between them; a block's last stage may carry an all-zero k-step)
-// OCC: workgroups per CU the config is built for (its LDS fits OCC rings; __launch_bounds__ caps the
-// registers at 512 / (OCC x waves per SIMD)), so one workgroup's barrier / DMA waits overlap another's MFMAs
-// PIPE (KU = 1): register double-buffered fragments -- after the barrier of step k the wave issues
-// step k+1's fragment reads, then step k's MFMAs; one barrier per step, which both publishes step
-// k+1's DMA and retires every wave's reads of step k, whose stage is refilled with step k+NST.
-template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB, int KU = 1, int OCC = 1,
-          bool PIPE = false>
-__global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_glds_kernel(ConvParams p) {
-  constexpr int BM = WM * TM, BN = WN * TN, BK = 64;
+// NST-stage ring of 64-deep k-steps, NST - 1 in flight; the refill of step k + NST - 1 is issued
+// right after the barrier of step k. (Spreading that refill among step k's MFMAs -- the plane GEMMs'
+// ilv_schedule, +1.4% fp32 -- measured neutral here: bf16 9,698-9,704 vs 9,707-9,728 img/s,
+// profiles/r5_prune_variants.txt; the register-pipelined, two-k-step and occupancy-ring variants of
+// this loop were removed in round 5 for the same reason.)
+template <int WM, int WN, int TM, int TN, int NST, bool CBIG, bool LHSDIL, bool BNB>
+__global__ __launch_bounds__(WM * WN * 64, WM * WN / 4) void conv_igemm_glds_kernel(ConvParams p) {
+  constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, RP = NT / 8;  // threads; tile rows per load pass
   constexpr int AV = BM / RP, BV = BN / RP;
-  constexpr int LOADS = KU * (AV + BV);  // LDS-DMA instructions per thread per stage
-  constexpr int SUB = (BM + BN) * 128;   // one k-step's A + B image
-  constexpr int STAGE = KU * SUB;
-  static_assert((WM * WN == 4 || WM * WN == 8) && NST >= 2 && NST <= 6 && (KU == 1 || KU == 2), "config");
+  constexpr int LOADS = AV + BV;                // LDS-DMA instructions per thread per stage
+  constexpr int STAGE = (BM + BN) * 128;        // one k-step's A + B image
+  static_assert((WM * WN == 4 || WM * WN == 8) && NST >= 2 && NST <= 6, "config");
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 2) <= 63, "vmcnt range");
-  static_assert(!PIPE || (KU == 1 && LOADS * (NST - 1) <= 63), "PIPE: one k-step per stage");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -281,80 +241,29 @@ __global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_gl
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk_all = p.Kpad / BK;
-  const int kb = split * nk_all / S, nk_steps = (split + 1) * nk_all / S - kb;  // this block's k-steps
-  // stage g holds k-steps kb + g*KU + u; one past the block's range (odd count, KU = 2) is
-  // loaded as zeros (out-of-range offsets), so its MFMAs add nothing
-  auto issue = [&](int stage, int g) {
+  const int nk_all = p.Kpad / 64;
+  const int kb = split * nk_all / S, nk = (split + 1) * nk_all / S - kb;  // this block's k-steps
+  auto issue = [&](int stage, int kl) {
+    const bool live = kl < nk;
+    const int kt = kb + kl;
+    uint32_t off[AV];
+    al.offsets(p, kt, chunk, off);  // k-steps are issued strictly in order
+    char* sbase = smem + stage * STAGE;
 #pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const int kl = g * KU + u;
-      const bool live = KU == 1 || kl < nk_steps;
-      const int kt = kb + kl;
-      uint32_t off[AV];
-      if (live) al.offsets(p, kt, chunk, off);
-      char* sbase = smem + stage * STAGE + u * SUB;
+    for (int v = 0; v < AV; ++v) glds16(xr, sbase + (wid * 8 + RP * v) * 128, live ? off[v] : HCB_OOB);
 #pragma unroll
-      for (int v = 0; v < AV; ++v) glds16(xr, sbase + (wid * 8 + RP * v) * 128, live ? off[v] : HCB_OOB);
-#pragma unroll
-      for (int v = 0; v < BV; ++v)
-        glds16(wr, sbase + BM * 128 + (wid * 8 + RP * v) * 128,
-               (!live || b_off[v] == HCB_OOB) ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
-    }
+    for (int v = 0; v < BV; ++v)
+      glds16(wr, sbase + BM * 128 + (wid * 8 + RP * v) * 128,
+             (!live || b_off[v] == HCB_OOB) ? HCB_OOB : b_off[v] + (uint32_t)kt * 128u);
   };
-  const int nk = (nk_steps + KU - 1) / KU;  // ring stages of this block
   if (kb > 0) al.seek(p, kb);
   EpiPrefetch<WM, WN, TM, TN, BNB> pre;
   pre.load_shift(p, n0, wn, lane);
-  constexpr size_t PARAM_OFF = glds_param_off(BM, BN, WM, NST * KU);
+  constexpr size_t PARAM_OFF = glds_param_off(BM, BN, WM, NST);
   constexpr bool PARAM_LDS = PARAM_OFF + bnb_param_lds(BN) <= 160 * 1024;
   if constexpr (BNB && PARAM_LDS) stage_bnb_params<BN, NT>(p, n0, smem + PARAM_OFF);  // published by the first barrier
-  const bool early = BNB && S == 1 && nk_steps <= EARLY_EPI_KSTEPS;
+  const bool early = BNB && S == 1 && nk <= EARLY_EPI_KSTEPS;
   if (early) pre.load(p, 0, m0, n0, tid);
-  if constexpr (PIPE) {
-    // NST stages in flight from the start; at step k at most the stages after k+1 may be pending
-    auto wait_ahead = [&](int ahead) {
-      if (ahead >= 4)
-        wait_vmcnt<(NST >= 5 ? 4 : 0) * LOADS>();
-      else if (ahead == 3)
-        wait_vmcnt<(NST >= 4 ? 3 : 0) * LOADS>();
-      else if (ahead == 2)
-        wait_vmcnt<(NST >= 3 ? 2 : 0) * LOADS>();
-      else if (ahead == 1)
-        wait_vmcnt<LOADS>();
-      else
-        wait_vmcnt<0>();
-    };
-    auto read = [&](int k, GFrags<TM, TN>& f) {
-      const char* sb = smem + (k % NST) * STAGE;
-      gfrag_read<WM, WN, TM, TN>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + BM * 128), f,
-                                 wm, wn, lane);
-    };
-#pragma unroll
-    for (int s = 0; s < NST; ++s)
-      if (s < nk) issue(s, s);
-    GFrags<TM, TN> fr[2];
-    if (nk > 0) {
-      wait_ahead(min(NST - 1, nk - 1));
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      read(0, fr[0]);
-    }
-    auto body = [&](int k, GFrags<TM, TN>& cur, GFrags<TM, TN>& nxt) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of step k are done
-      if (k + 1 < nk) wait_ahead(min(NST - 2, nk - 2 - k));  // step k+1 landed for this thread
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (k + NST < nk) issue(k % NST, k + NST);
-      if (k + 1 < nk) read(k + 1, nxt);
-      __builtin_amdgcn_sched_barrier(0);
-      gfrag_mma<TM, TN>(cur, acc);
-    };
-    for (int k = 0; k < nk; k += 2) {
-      body(k, fr[0], fr[1]);
-      if (k + 1 < nk) body(k + 1, fr[1], fr[0]);
-    }
-  } else {
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
     if (s < nk) issue(s, s);
@@ -375,13 +284,9 @@ __global__ __launch_bounds__(WM * WN * 64, OCC * WM * WN / 4) void conv_igemm_gl
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, kt + NST - 1);
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const char* sb = smem + (kt % NST) * STAGE + u * SUB;
-      mfma_tile_step<WM, WN, TM, TN, true>(reinterpret_cast<const u32x4*>(sb),
-                                                     reinterpret_cast<const u32x4*>(sb + BM * 128), acc, wm, wn, lane);
-    }
-  }
+    const char* sb = smem + (kt % NST) * STAGE;
+    mfma_tile_step<WM, WN, TM, TN, true>(reinterpret_cast<const u32x4*>(sb),
+                                         reinterpret_cast<const u32x4*>(sb + BM * 128), acc, wm, wn, lane);
   }
   __syncthreads();  // every wave is done reading the ring before the epilogue reuses LDS
   if (S > 1 && !splitk_gather<MI, NI, NT>(p, acc, smem, tile, split, S, tid)) return;
@@ -426,42 +331,38 @@ static void launch_reg(const ConvParams& p, hipStream_t st) {
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, TM, TN, false, true, BNB>), dim3(tiles), dim3(256), lds, st, p);
 }
 
-template <int WM, int WN, int TM, int TN, int NST, bool BNB, int KU = 1, int OCC = 1, bool PIPE = false>
+template <int WM, int WN, int TM, int TN, int NST, bool BNB>
 static void launch_glds(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
   int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN) * p.splits;
-  // a block never touches more ring stages than it has: short-K layers (1x1 over 64-256
-  // channels: 1-4 k-steps) get the LDS of the stages they use, so more workgroups fit per CU
+  // a block never touches more ring stages than it has k-steps (short-K layers: 1x1 over 64-256
+  // channels, 1-4 k-steps, get the LDS they use, so more workgroups fit per CU)
   const int ksteps = (p.Kpad / 64 + p.splits - 1) / p.splits;
-  const int groups = (ksteps + KU - 1) / KU;
-  const int stages = groups < NST ? (groups > 0 ? groups : 1) : NST;
-  size_t lds_main = (size_t)stages * KU * (BM + BN) * 128;
+  const int stages = ksteps < NST ? (ksteps > 0 ? ksteps : 1) : NST;
+  size_t lds_main = (size_t)stages * (BM + BN) * 128;
   size_t lds_epi = igemm_epilogue_lds(BM, BN, WM, igemm_stage16(p));
   size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-  if (BNB && glds_param_off(BM, BN, WM, NST * KU) + bnb_param_lds(BN) <= 160 * 1024)
-    lds = glds_param_off(BM, BN, WM, NST * KU) + bnb_param_lds(BN);
+  if (BNB && glds_param_off(BM, BN, WM, NST) + bnb_param_lds(BN) <= 160 * 1024)
+    lds = glds_param_off(BM, BN, WM, NST) + bnb_param_lds(BN);
   bool cbig = (p.C % 64) == 0;
   bool lhs = p.idil_h > 1 || p.idil_w > 1;
   static bool once = false;
   if (!once) {
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC, PIPE>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC, PIPE>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC, PIPE>);
-    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC, PIPE>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>);
+    set_lds_once(conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>);
     once = true;
   }
   if (cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT), lds,
-                       st, p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, false, BNB>), dim3(tiles), dim3(NT), lds, st, p);
   else if (cbig && lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT), lds,
-                       st, p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, true, true, BNB>), dim3(tiles), dim3(NT), lds, st, p);
   else if (!cbig && !lhs)
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT),
-                       lds, st, p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, false, BNB>), dim3(tiles), dim3(NT), lds, st,
+                       p);
   else
-    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB, KU, OCC, PIPE>), dim3(tiles), dim3(NT), lds,
-                       st, p);
+    hipLaunchKernelGGL((conv_igemm_glds_kernel<WM, WN, TM, TN, NST, false, true, BNB>), dim3(tiles), dim3(NT), lds, st, p);
 }
 
 // cfg: 0..3 register-staged {128x128, 128x64, 64x64, 64x128}; 4..7 the same tiles on the
@@ -470,24 +371,18 @@ static void launch_glds(const ConvParams& p, hipStream_t st) {
 // waves per SIMD when a layer has only ~1 tile per CU): 128x128 as 2x4 waves of 64x32 and as
 // 4x2 of 32x64, 256x128 (4x2 of 64x64), 128x256 (2x4 of 64x64), 64x128 (2x4 of 32x32);
 // 17..21 the 3x3 patch kernels (conv3x3_patch.hip): 128x128, 256x128, 256x64, 128x64, 128x128;
-// 22..26 LDS-DMA rings with two k-steps per stage (KU = 2): 64x128 (1x4 waves of 64x32),
-// 128x128 (4x2 of 32x64), 128x128 (2x4 of 64x32), 64x128 (2x4 of 32x32), 64x64 (2x2 of 32x32);
-// 27..30 two-slot rings sized for two / three workgroups per CU: 128x128 (2x2 of 64x64, OCC 2),
-// 128x128 (2x4 of 64x32, OCC 2), 128x64 (2x2 of 64x32, OCC 3), 64x128 (2x2 of 32x64, OCC 3);
-// 31..37 the register-pipelined loop (PIPE) on cfg 4, 5, 7, 12, 13, 14, 16's tiles and rings
-constexpr int N_CONV_CFG = 38;
+// (round 5: the rejected variants -- two k-steps per stage, cfg 22-26; occupancy-sized two-slot
+// rings, 27-30; the register-pipelined loop, 31-37; the plane kernel on one 16-bit plane, 100-117 --
+// were measured without a step gain and removed: profiles/r5_prune_variants.txt)
+constexpr int N_CONV_CFG = 22;
 int conv_tile_m(int cfg) {
-  if (cfg >= CONV_S1_BASE) return p3_tile_m(cfg - CONV_S1_BASE);
-  static const int t[N_CONV_CFG] = {128, 128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 256, 128,
-                                    64,  128, 256, 256, 128, 128, 64,  128, 128, 64,  64,  128, 128, 128, 64,
-                                    128, 128, 64,  128, 128, 256, 64};
+  static const int t[N_CONV_CFG] = {128, 128, 64, 64, 128, 128, 64, 64, 128, 128, 128,
+                                    64,  128, 128, 256, 128, 64, 128, 256, 256, 128, 128};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 int conv_tile_n(int cfg) {
-  if (cfg >= CONV_S1_BASE) return p3_tile_n(cfg - CONV_S1_BASE);
-  static const int t[N_CONV_CFG] = {128, 64,  64,  128, 128, 64,  64,  128, 128, 128, 64, 128, 128, 128, 128, 256,
-                                    128, 128, 128, 64,  64,  128, 128, 128, 128, 128, 64,  128, 128, 64,  128,
-                                    128, 64,  128, 128, 128, 128, 128};
+  static const int t[N_CONV_CFG] = {128, 64,  64,  128, 128, 64,  64, 128, 128, 128, 64,
+                                    128, 128, 128, 128, 256, 128, 128, 128, 64, 64, 128};
   return (cfg >= 0 && cfg < N_CONV_CFG) ? t[cfg] : 128;
 }
 
@@ -511,31 +406,11 @@ static void launch_cfg(const ConvParams& p, int cfg, hipStream_t st) {
     case 14: launch_glds<4, 2, 64, 64, 3, BNB>(p, st); break;
     case 15: launch_glds<2, 4, 64, 64, 3, BNB>(p, st); break;
     case 16: launch_glds<2, 4, 32, 32, 4, BNB>(p, st); break;
-    case 22: launch_glds<1, 4, 64, 32, 2, BNB, 2>(p, st); break;
-    case 23: launch_glds<4, 2, 32, 64, 2, BNB, 2>(p, st); break;
-    case 24: launch_glds<2, 4, 64, 32, 2, BNB, 2>(p, st); break;
-    case 25: launch_glds<2, 4, 32, 32, 2, BNB, 2>(p, st); break;
-    case 26: launch_glds<2, 2, 32, 32, 3, BNB, 2>(p, st); break;
-    case 27: launch_glds<2, 2, 64, 64, 2, BNB, 1, 2>(p, st); break;
-    case 28: launch_glds<2, 4, 64, 32, 2, BNB, 1, 2>(p, st); break;
-    case 29: launch_glds<2, 2, 64, 32, 2, BNB, 1, 3>(p, st); break;
-    case 30: launch_glds<2, 2, 32, 64, 2, BNB, 1, 3>(p, st); break;
-    case 31: launch_glds<2, 2, 64, 64, 3, BNB, 1, 1, true>(p, st); break;
-    case 32: launch_glds<4, 1, 32, 64, 3, BNB, 1, 1, true>(p, st); break;
-    case 33: launch_glds<1, 4, 64, 32, 3, BNB, 1, 1, true>(p, st); break;
-    case 34: launch_glds<2, 4, 64, 32, 3, BNB, 1, 1, true>(p, st); break;
-    case 35: launch_glds<4, 2, 32, 64, 3, BNB, 1, 1, true>(p, st); break;
-    case 36: launch_glds<4, 2, 64, 64, 3, BNB, 1, 1, !BNB>(p, st); break;  // BNB: spills with PIPE
-    case 37: launch_glds<2, 4, 32, 32, 4, BNB, 1, 1, true>(p, st); break;
     default: launch_reg<2, 2, 64, 64, BNB>(p, st); break;
   }
 }
 
 void launch_conv_igemm(const ConvParams& p, int cfg, hipStream_t st) {
-  if (cfg >= CONV_S1_BASE) {
-    launch_conv_s1(p, cfg - CONV_S1_BASE, st);
-    return;
-  }
   if (cfg >= CONV_PATCH_CFG0 && cfg < CONV_PATCH_CFG0 + 5) {
     if (launch_conv3x3_patch(p, cfg, st)) return;
     // not a 3x3 / stride-1 problem (or its patch does not fit LDS): an LDS-DMA kernel of the

@@ -35,14 +35,10 @@ int p3_tile_n(int cfg) {
 }
 
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st) {
-  if (p.sk_grid > 0) {
-    launch_conv_p3_sk(p, cfg, st);
-    return;
-  }
   if (p.bnb_acc != nullptr)
-    launch_p3_cfg<true, false>(p, cfg, st);
+    launch_p3_cfg<true>(p, cfg, st);
   else
-    launch_p3_cfg<false, false>(p, cfg, st);
+    launch_p3_cfg<false>(p, cfg, st);
 }
 // p3 wgrad cfg (block tile, waves x wave tile, slots x pixel rows):
 //   0 128x64 (2x2 of 64x32, 2x64), 1 64x128 (2x2 of 32x64, 2x64), 2 64x64 (2x2 of 32x32, 3x64),

@@ -1,5 +1,5 @@
-// Weight-gradient plane GEMM (conv_wgrad_p3_kernel) and its launcher, shared by conv_p3.hip (fp32
-// on three bf16 planes) and conv_wgrad_s1.hip (the same kernel on one plane: bf16 / fp16 builds).
+// Weight-gradient plane GEMM (conv_wgrad_p3_kernel, fp32 on three bf16 planes) and its launcher,
+// instantiated in conv_p3.hip.
 #pragma once
 #include "conv_p3_fwd.h"
 
@@ -19,10 +19,8 @@ __device__ __forceinline__ int p3w_swz(int row) {
 // BK: pixel rows (reduction depth) per ring slot, 64 or 32 (32: half the LDS per slot, so 128x128 /
 // 256x128 block tiles fit); NST slots with early release; PIPE (when two fragment sets fit the
 // register budget): slot k+1's transposed fragment reads in flight during slot k's MFMAs, one
-// barrier per slot.
-// NPL: operand planes -- 3 (fp32 as bf16 hi / mid / lo, six MFMA products) or 1 (a plain 16-bit
-// activation of this build: bf16, or IEEE fp16 in the f16 library; one MFMA product).
-template <int WM, int WN, int TM, int TN, int NST, int BK, bool CBIG, int OCC = 1, int NPL = 3>
+// barrier per slot. The refill issues are interleaved with the MFMAs (ilv_schedule).
+template <int WM, int WN, int TM, int TN, int NST, int BK, bool CBIG, int OCC = 1>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_kernel(WgradParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16, KS = BK / 32;
@@ -55,11 +53,11 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   const char* db = reinterpret_cast<const char*>(p.dy);
   const char* xb = reinterpret_cast<const char*>(p.x);
   const __amdgpu_buffer_rsrc_t dyr0 = make_rsrc(db, p.dy_bytes);
-  const __amdgpu_buffer_rsrc_t dyr1 = make_rsrc(db + (NPL > 1 ? p.dy_plane : 0), p.dy_bytes);
-  const __amdgpu_buffer_rsrc_t dyr2 = make_rsrc(db + (NPL > 1 ? 2 * (size_t)p.dy_plane : 0), p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t dyr1 = make_rsrc(db + p.dy_plane, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t dyr2 = make_rsrc(db + 2 * (size_t)p.dy_plane, p.dy_bytes);
   const __amdgpu_buffer_rsrc_t xr0 = make_rsrc(xb, p.x_bytes);
-  const __amdgpu_buffer_rsrc_t xr1 = make_rsrc(xb + (NPL > 1 ? p.x_plane : 0), p.x_bytes);
-  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(xb + (NPL > 1 ? 2 * (size_t)p.x_plane : 0), p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr1 = make_rsrc(xb + p.x_plane, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(xb + 2 * (size_t)p.x_plane, p.x_bytes);
 
   int a_row[AI], a_col[AI];
 #pragma unroll
@@ -92,9 +90,9 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
     b_ok[v] = col < p.K;
   }
 
-  // HCB_P3_ILV: every slot issue is made, also past the last k-step (rows >= mend read as zeros
-  // into a slot nobody reads again), so the vmcnt arithmetic is uniform and the issue can be
-  // interleaved with the MFMAs of the same basic block (conv_p3_fwd.h p3_ilv)
+  // every slot issue is made, also past the last k-step (rows >= mend read as zeros into a slot
+  // nobody reads again), so the vmcnt arithmetic is uniform and the issue can be interleaved with
+  // the MFMAs of the same basic block (igemm_loader.h ilv_schedule)
   auto issue = [&](int stage, int kl) {
     const int mb = mbeg + kl * BK;
     char* sA = smem + stage * STAGE;
@@ -106,10 +104,8 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
       const uint32_t off = ((uint32_t)(m * p.ldy + a_col[v]) * 2u) | ((uint32_t)!ok << 31);
       char* d = sA + (wid * AI + v) * ARPI * BM * 2;
       glds16(dyr0, d, off);
-      if constexpr (NPL > 1) {
-        glds16(dyr1, d + AIMG, off);
-        glds16(dyr2, d + 2 * AIMG, off);
-      }
+      glds16(dyr1, d + AIMG, off);
+      glds16(dyr2, d + 2 * AIMG, off);
     }
 #pragma unroll
     for (int v = 0; v < BI; ++v) {
@@ -126,10 +122,8 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
       const uint32_t off = raw | ((uint32_t)!ok << 31);  // >= HCB_OOB: out of range
       char* d = sB + (wid * BI + v) * BRPI * BN * 2;
       glds16(xr0, d, off);
-      if constexpr (NPL > 1) {
-        glds16(xr1, d + BIMG, off);
-        glds16(xr2, d + 2 * BIMG, off);
-      }
+      glds16(xr1, d + BIMG, off);
+      glds16(xr2, d + 2 * BIMG, off);
     }
   };
 
@@ -153,7 +147,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
     short8 t = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
     return __builtin_bit_cast(u32x4, t);
   };
-  using Fr = P3Frags<TM, TN, KS, NPL>;
+  using Fr = P3Frags<TM, TN, KS>;
   auto read = [&](int k, Fr& f) {
     const char* Ab = smem + (k % NST) * STAGE;
     const char* Bb = Ab + NPL * AIMG;
@@ -169,61 +163,32 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
         for (int t = 0; t < NPL; ++t) f.b[ks][t][j] = frag(Bb + t * BIMG, BN, ks * 32 + 8 * g, wn * TN + j * 16);
     }
   };
-  auto wait_ahead = [&](int ahead) {
-    if (ahead >= 2)
-      wait_vmcnt<(NST >= 3 ? 2 : 0) * LOADS>();
-    else if (ahead == 1)
-      wait_vmcnt<LOADS>();
-    else
-      wait_vmcnt<0>();
-  };
 
   const int nk = (mend - mbeg + BK - 1) / BK;
+  // every slot issue is made, also past the last k-step (its rows read as zeros), so slot k has
+  // landed for this thread once at most the NST - 1 (PIPE: slot k+1 once NST - 2) slots after it are
+  // outstanding
 #pragma unroll
-  for (int s = 0; s < NST; ++s)
-    if (HCB_P3_ILV || s < nk) issue(s, s);
+  for (int s = 0; s < NST; ++s) issue(s, s);
   constexpr int FREGS = (MI + NI) * NPL * 4 * KS, AREGS = MI * NI * 4;
   constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 88 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 88 : 400;
   constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET;
-  constexpr int NMF = KS * MI * NI * (NPL == 3 ? 6 : 1), NRD = 2 * KS * (MI + NI) * NPL;
-  if constexpr (PIPE && HCB_P3_ILV) {
+  constexpr int NMF = KS * MI * NI * 6, NRD = 2 * KS * (MI + NI) * NPL;
+  if constexpr (PIPE) {
     Fr fr[2];
-    wait_ahead(NST - 1);
+    wait_vmcnt<(NST - 1) * LOADS>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     read(0, fr[0]);
     auto body = [&](int k, Fr& cur, Fr& nxt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot k are done
-      wait_ahead(NST - 2);                                 // slot k+1 landed for this thread
+      wait_vmcnt<(NST - 2) * LOADS>();                     // slot k+1 landed for this thread
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       issue(k % NST, k + NST);
       read(k + 1, nxt);
-      p3_mma<TM, TN, KS, NPL>(cur, acc);
-      p3_ilv<NMF, LOADS, NRD>();
-    };
-    for (int k = 0; k < nk; k += 2) {
-      body(k, fr[0], fr[1]);
-      if (k + 1 < nk) body(k + 1, fr[1], fr[0]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy pieces have landed before LDS reuse
-  } else if constexpr (PIPE) {
-    Fr fr[2];
-    if (nk > 0) {
-      wait_ahead(min(NST - 1, nk - 1));
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      read(0, fr[0]);
-    }
-    auto body = [&](int k, Fr& cur, Fr& nxt) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot k are done
-      if (k + 1 < nk) wait_ahead(min(NST - 2, nk - 2 - k));  // slot k+1 landed for this thread
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (k + NST < nk) issue(k % NST, k + NST);
-      if (k + 1 < nk) read(k + 1, nxt);
-      __builtin_amdgcn_sched_barrier(0);
-      p3_mma<TM, TN, KS, NPL>(cur, acc);
+      p3_mma<TM, TN, KS>(cur, acc);
+      ilv_schedule<NMF, LOADS, NRD>();
     };
     for (int k = 0; k < nk; k += 2) {
       body(k, fr[0], fr[1]);
@@ -232,22 +197,19 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   } else {
     Fr fr;
     for (int k = 0; k < nk; ++k) {
-      if constexpr (HCB_P3_ILV) wait_ahead(NST - 1);
-      else wait_ahead(min(NST - 1, nk - 1 - k));
+      wait_vmcnt<(NST - 1) * LOADS>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       read(k, fr);
-      if (HCB_P3_ILV || k + NST < nk) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
-        __builtin_amdgcn_s_barrier();                        // ... and every other wave's
-        asm volatile("" ::: "memory");
-        issue(k % NST, k + NST);
-      }
-      p3_mma<TM, TN, KS, NPL>(fr, acc);
-      if constexpr (HCB_P3_ILV) p3_ilv<NMF, LOADS, 0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+      __builtin_amdgcn_s_barrier();                        // ... and every other wave's
+      asm volatile("" ::: "memory");
+      issue(k % NST, k + NST);
+      p3_mma<TM, TN, KS>(fr, acc);
+      ilv_schedule<NMF, LOADS, 0>();
     }
-    if constexpr (HCB_P3_ILV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy pieces have landed before LDS reuse
   __syncthreads();  // every wave is done with the ring before the epilogue reuses LDS
 
   constexpr int LDC = BN + 4;
@@ -274,7 +236,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   }
 }
 
-template <int WM, int WN, int TM, int TN, int NST, int BK, int OCC = 1, int NPL = 3>
+template <int WM, int WN, int TM, int TN, int NST, int BK, int OCC = 1>
 static void wlaunch_p3(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
@@ -283,15 +245,15 @@ static void wlaunch_p3(const WgradParams& p, int splits, hipStream_t st) {
   const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   static bool once = false;
   if (!once) {
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC, NPL>);
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC, NPL>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC>);
     once = true;
   }
   const dim3 grid(tiles * splits);
   if ((p.C % BN) == 0)
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC, NPL>), grid, dim3(WM * WN * 64), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC>), grid, dim3(WM * WN * 64), lds, st, p);
   else
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC, NPL>), grid, dim3(WM * WN * 64), lds, st, p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC>), grid, dim3(WM * WN * 64), lds, st, p);
 }
 
 }  // namespace hcb

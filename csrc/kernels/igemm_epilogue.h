@@ -113,12 +113,11 @@ __device__ __forceinline__ void stage_bnb_params(const ConvParams& p, int n0, ch
 // agent-scope release + ticket; the last arriver acquires and sums ALL slabs in index order into
 // acc and returns true (it then runs the epilogue), the others return false. Call after the main
 // loop's final barrier (smem word 0 is used as the broadcast flag).
-// sstride: slabs reserved per tile (S for split-K; the maximum share count for stream-K).
 template <int MI, int NI, int NT>
 __device__ __forceinline__ bool splitk_gather(const ConvParams& p, f32x4 (&acc)[MI][NI], char* smem, int tile,
-                                              int split, int S, int tid, int sstride = 0) {
+                                              int split, int S, int tid) {
   constexpr int FR = MI * NI;  // f32x4 fragments per thread
-  f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)tile * (sstride > 0 ? sstride : S) * FR * NT;
+  f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)tile * S * FR * NT;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -143,8 +142,8 @@ __device__ __forceinline__ bool splitk_gather(const ConvParams& p, f32x4 (&acc)[
   __syncthreads();  // the flag word is epilogue staging space next
   if (!last) return false;
   // the sum in FIXED slab order 0..S-1 (the last arriver re-reads its own slab too): the fp32
-  // result does not depend on which split arrived last, so split-K / stream-K are run-to-run
-  // deterministic; one extra slab read per tile
+  // result does not depend on which split arrived last, so split-K is run-to-run deterministic
+  // (ADVICE r4); one extra slab read per tile
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll

@@ -70,9 +70,6 @@ struct ConvParams {
   int splits;
   float* ws;
   unsigned* cnt;
-  // stream-K (plane GEMMs): sk_grid > 0 workgroups each take an even share of all (tile, k-slot)
-  // iterations; a tile's shares meet in ws slabs [tile][sk_smax][tile elems] (splits == 1)
-  int sk_grid, sk_smax;
   // plane GEMMs (conv_p3.hip, the fp32 path): the mid and lo bf16 weight packs beside w (hi)
   const void* w_lo;
   const void* w_lo2;
@@ -122,18 +119,9 @@ void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st);
 int p3_tile_m(int cfg);
 int p3_tile_n(int cfg);
 int p3_slot_k(int cfg);
-void launch_conv_p3_sk(const ConvParams& p, int cfg, hipStream_t st);
-// the plane-GEMM kernel on one 16-bit plane (conv_s1.hip): cfg CONV_S1_BASE + i of the 16-bit ops
-constexpr int CONV_S1_BASE = 100;
-void launch_conv_s1(const ConvParams& p, int cfg, hipStream_t st);
 void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st);
 int wgrad_p3_tile_m(int cfg);
 int wgrad_p3_tile_n(int cfg);
-// weight-grad on ONE 16-bit plane with the plane kernel's slot rings (conv_wgrad_s1.hip): cfg
-// WGRAD_S1_BASE + i of the bf16 / fp16 conv_wgrad op
-constexpr int WGRAD_S1_BASE = 100;
-constexpr int N_WS1_CFG = 8;
-void launch_wgrad_s1(const WgradParams& p, int cfg, int splits, hipStream_t st);
 // fp32 [rows][ldx] <-> bf16 planes [3][rows][ldo] (plane stride `plane` elements)
 void launch_split_planes(const float* x, int ldx, int64_t rows, int C, uint16_t* out, int ldo, int64_t plane,
                          hipStream_t st);

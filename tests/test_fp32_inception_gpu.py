@@ -59,7 +59,7 @@ def _conv(cin, cout, kh, kw, s, mode, H):
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}x{c[3]}s{c[4]}{c[5]}")
-@pytest.mark.parametrize("cfg", [None, 4, 7, 14, 17, (2, 3), (13, -256)], ids=str)
+@pytest.mark.parametrize("cfg", [None, 4, 7, 14, 17, (2, 3), (13, 2)], ids=str)
 def test_fp32_inception_conv_classes_match_fp64(fp32_mode, case, cfg):
     cin, cout, kh, kw, s, mode, H = case
     spec, p, pk = _conv(cin, cout, kh, kw, s, mode, H)

@@ -91,7 +91,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
     dz = bf(torch.randn(N, P, Q, cout, device=DEV))
     dref = torch.empty(N, H, H, cpad)
     Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), dref, False)
-    for cfg in list(range(4, 17)) + [22, 23, 24, 25, 26]:
+    for cfg in list(range(4, 17)):
         y = torch.empty(N, P, Q, cout, dtype=torch.bfloat16, device=DEV)
         slab = torch.empty(math.ceil(N * P * Q / Fn._CONV_TILES[cfg][0]) * 2 * cout, device=DEV)
         Fn.conv_forward(x, spec, pk.pack, p.data, y, stats=slab, cfg=cfg)
@@ -102,7 +102,7 @@ def test_conv_lds_dma_kernels_all_geometries(case):
             assert rel_err(dx, dref) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("cfg", list(range(38)) + list(range(100, 118)))
+@pytest.mark.parametrize("cfg", list(range(22)))
 def test_conv_fwd_all_tile_configs(cfg):
     torch.manual_seed(1)
     spec, p, pk = make_conv(128, 192, 3, 3, 1, 1, (1, 1, 1, 1))
@@ -179,7 +179,7 @@ def test_conv_dgrad(case, accumulate):
                          ids=["1x1", "3x3", "1x1s2", "cin80"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [2, 4, 12, 23, 26, 27, 28, 29, 30, 31, 34, 36, 37, 100, 107, 109, 114, 117])
+@pytest.mark.parametrize("cfg", [2, 4, 5, 7, 12, 13, 14, 16])
 def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
     """data-grad GEMM with the consuming BN layer's ReLU gating and backward sums fused into
     its epilogue (ConvParams::bnb_*), vs the CPU gating + fp32 reductions."""
@@ -240,11 +240,10 @@ def test_conv_wgrad(case):
     assert rel_err(dw, ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(15)) + list(range(100, 108)))
+@pytest.mark.parametrize("cfg", list(range(15)))
 def test_conv_wgrad_all_configs(cfg):
     """Every weight-grad tile config (register-staged 0-2 and 13-14, LDS-DMA ring 3-9,
-    intra-workgroup k-split 10-12; 100-107: the plane kernel's slot rings on one 16-bit plane,
-    conv_wgrad_s1.hip) with split-K on
+    intra-workgroup k-split 10-12) with split-K on
     1x1 / 3x3 / strided / odd-channel geometries (partial tiles in Nout, K and pixels)."""
     torch.manual_seed(6)
     for cin, cout, k, s, pads, H, splits in [(64, 256, 1, 1, (0, 0, 0, 0), 14, 3),
