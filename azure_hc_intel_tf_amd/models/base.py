@@ -54,9 +54,12 @@ class CNNModel:
         # a GPU in the fp32 reference-precision mode) the PyTorch path of ops/functional.py
         from ..ops import functional as Fn
 
+        # HCB_F32_NATIVE=0: fp32 through the PyTorch (MIOpen / rocBLAS) path even where the HIP
+        # kernels exist -- the comparison point of the fp32 numbers
+        f32_ok = self.F32_NATIVE_OK and os.environ.get("HCB_F32_NATIVE", "1") != "0"
         self.native = self.device.type == "cuda" and (
             self.compute_dtype == "bf16" or (self.compute_dtype == "fp16" and Fn.F16_NATIVE)
-            or (self.compute_dtype == "fp32" and self.F32_NATIVE_OK))
+            or (self.compute_dtype == "fp32" and f32_ok))
         if image_channels is None:
             image_channels = 8 if self.native else 3
         assert image_channels in (3, 8) and (not self.native or image_channels == 8)

@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--retune", action="store_true")
+    ap.add_argument("--kinds", default="", help="comma-separated key kinds to step-tune (e.g. wgrad3); default all")
     ap.add_argument("--budget_s", type=float, default=900.0)
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
     a = ap.parse_args()
@@ -144,7 +145,8 @@ def main():
         v = Fn._tuned[k]
         return json.dumps(list(v) if isinstance(v, tuple) else v)
 
-    order = sorted(probs, key=lambda k: -iso[k][cur_s(k)] * probs[k][0])
+    kinds = [k for k in a.kinds.split(",") if k]
+    order = sorted((k for k in probs if not kinds or k[0] in kinds), key=lambda k: -iso[k][cur_s(k)] * probs[k][0])
 
     images, labels = synthetic_batch(model, a.batch)
     trainer = Trainer(model, a.batch, resnet_lr_schedule(a.batch), use_graph=True)
@@ -164,7 +166,7 @@ def main():
             break
         cur = cur_s(k)
         shortlist = [c for c in sorted(iso[k], key=iso[k].get) if c != cur][:a.cands]
-        best_c, best_gain = None, 0.0
+        best_c, best_gain, best_i = None, 0.0, -1
         for c in shortlist:
             ta, tb = ab(timer, k, json.loads(cur), json.loads(c), a.rounds)
             gain = ta - tb
@@ -174,14 +176,14 @@ def main():
             log(f"  {k} x{probs[k][0]}: {cur} -> {c}: iso {iso[k][cur] * 1000:.1f} -> {iso[k][c] * 1000:.1f} us; "
                 f"step {ta:.4f} -> {tb:.4f} ms")
             if gain > max(noise, 0.0005 * ta) and gain > best_gain:
-                best_c, best_gain = c, gain
+                best_c, best_gain, best_i = c, gain, len(trials) - 1
         if best_c is not None:
             # re-confirm the winner before keeping it
             ta, tb = ab(timer, k, json.loads(cur), json.loads(best_c), a.rounds + 1)
             if ta - tb > max(noise, 0.0005 * ta):
                 Fn._tuned[k] = json.loads(best_c)
                 log(f"  ACCEPT {k}: {cur} -> {best_c} ({ta:.4f} -> {tb:.4f} ms)")
-                trials[-1]["accepted"] = True
+                trials[best_i]["accepted"] = True
             else:
                 log(f"  reject {k}: {best_c} not confirmed ({ta:.4f} -> {tb:.4f} ms)")
 
