@@ -442,7 +442,14 @@ class StemS2D(ConvBN):
         assert self.spec.pt == 3 and self.spec.pl == 3 and not self.need_dx
         P, Q, _ = self.out_shape
         self.fold_shape = (P + 3, Q + 3, 16)
-        self.fold_spec = ConvSpec(cin=16, cin_pad=16, cout=cout, kh=4, kw=4, sh=1, sw=1, pt=0, pl=0, pb=0, pr=0)
+        # the GEMM of the 4x4 / stride-1 conv over the 16-channel fold, read as a 4x1 conv over ROW
+        # WINDOWS of 64 channels (pixel w's window = the 16 channels of pixels w .. w+3, the input's
+        # pixel stride staying 16; csrc/bindings.cpp x_span_bytes): K = 4 x 64 keeps the weight layout
+        # [cout][r][s][16] = [cout][r][64], and every k-step reads one contiguous 64-channel row (the
+        # kernels' channels-multiple-of-64 fast path) instead of a gather of 16-channel pieces of two
+        # or four taps. pr = -3: the windows of the last three fold columns reach past the row and are
+        # never an output's.
+        self.fold_spec = ConvSpec(cin=64, cin_pad=64, cout=cout, kh=4, kw=1, sh=1, sw=1, pt=0, pl=0, pb=0, pr=-3)
         self._wfold = None
         self._wpack = None
         self._dwfold = None

@@ -441,9 +441,14 @@ def set_tuned(table: dict) -> None:
 # 14-17 32-deep slots sized for two / three workgroups per CU
 _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
              7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
-             13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64)}
+             13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64),
+             18: (64, 128), 19: (128, 64), 20: (64, 64), 21: (64, 64), 22: (128, 128)}
 # workgroups per CU each plane-GEMM cfg is built for
-_P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3}
+_P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3, 18: 2, 19: 2, 20: 2, 21: 3}
+# persistent short-K twins (conv_p3_persist.h): one workgroup per resident slot walks its tiles with
+# the LDS-DMA ring running across tile boundaries and a register epilogue; no split-K (a problem
+# with an epilogue they do not serve -- fused BN backward, beta, bias -- runs the twin)
+_P3_PERSIST = {18: 15, 19: 14, 20: 16, 21: 17, 22: 7}
 # wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles),
 # 12-15 32-deep slots, two / three workgroups per CU
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),
@@ -473,6 +478,8 @@ def p3_candidates(M: int, N: int, K: int):
             continue
         tiles = math.ceil(M / bm) * math.ceil(N / bn)
         out.append((c, 1))
+        if c in _P3_PERSIST:
+            continue
         for s in (2, 3, 4, 5, 6, 8, 12, 16):
             if tiles * s > 6 * N_CU or ksteps // s < 2 or tiles * s * bm * bn > SPLITK_WS_FLOATS:
                 break

@@ -89,6 +89,15 @@ int64_t check_planes(const Tensor& t, const char* name) {
   return t.stride(0);  // elements between planes
 }
 
+// Bytes of an NHWC conv input that the kernels may address. ldx < C is a ROW WINDOW: pixel w's C
+// "channels" are the ldx channels of pixels w, w+1, ... (the space-to-depth stem's 4x4 filter read as
+// 4x1 over 64-channel windows of 16-channel pixels: one contiguous 128-byte row per filter row,
+// StemS2D.fold_spec); the buffer then ends with the tensor and the windows of the last pixels, which
+// no output reads, run out of range (zeros).
+static int64_t x_span_bytes(int64_t N, int64_t H, int64_t W, int64_t C, int64_t ldx, int64_t e) {
+  return ldx >= C ? ((N * H * W - 1) * ldx + C) * e : N * H * W * ldx * e;
+}
+
 // geom = [N,H,W,C,ldx, P,Q,R,S, sh,sw,ph,pw,dh,dw,idh,idw, Nout,K,Kpad,ldy,
 //         remap,OH,OW,osh,osw, beta,out_f32]
 hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
@@ -113,14 +122,15 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   p.oh0 = g.size() > 31 ? (int)g[31] : 0;
   p.ow0 = g.size() > 32 ? (int)g[32] : 0;
   p.M = p.N * p.P * p.Q;
-  TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0 && p.ldx >= p.C, "hcb.conv_igemm: C, ldx must be multiples of 8");
+  TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0 && (p.ldx >= p.C || p.C % p.ldx == 0),
+              "hcb.conv_igemm: C, ldx must be multiples of 8 (ldx < C: a row window, C a multiple of ldx)");
   TORCH_CHECK(p.Kpad % 64 == 0 && p.Kpad >= p.K && p.K == p.R * p.S * p.C,
               "hcb.conv_igemm: Kpad must be a multiple of 64 >= K = R*S*C");
   TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= ((p.Nout + 7) / 8) * 8, "hcb.conv_igemm: bad ldy");
   TORCH_CHECK(p.idil_h >= 1 && p.idil_w >= 1 && p.dil_h >= 1 && p.dil_w >= 1, "hcb.conv_igemm: bad dilation");
   TORCH_CHECK(p.M > 0 && p.Nout > 0, "hcb.conv_igemm: empty problem");
   const int64_t xe = f32 ? 4 : 2;
-  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * xe + (int64_t)p.C * xe;
+  int64_t xb = x_span_bytes(p.N, p.H, p.W, p.C, p.ldx, xe);
   int64_t wb = (int64_t)p.Nout * p.Kpad * 2;
   TORCH_CHECK(xb < (1ll << 31) && wb < (1ll << 31), "hcb.conv_igemm: operand exceeds 2 GiB buffer range");
   check_range(x, xb, "x");
@@ -295,7 +305,7 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntArra
   TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0, "hcb.conv_wgrad: C, ldx multiples of 8");
   TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= p.Nout, "hcb.conv_wgrad: bad ldy");
   TORCH_CHECK(splits >= 1, "hcb.conv_wgrad: splits >= 1");
-  int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * e + (int64_t)p.C * e;
+  int64_t xb = x_span_bytes(p.N, p.H, p.W, p.C, p.ldx, e);
   int64_t yb = ((int64_t)p.M - 1) * p.ldy * e + (int64_t)((p.Nout + 7) / 8) * 8 * e;
   TORCH_CHECK(xb < (1ll << 31) && yb < (1ll << 31), "hcb.conv_wgrad: operand exceeds 2 GiB");
   check_range(x, xb, "x");
@@ -1014,7 +1024,7 @@ hcb::ConvParams p3_params(const Tensor& x, const Tensor& w, const Tensor& w_lo, 
                           const c10::optional<Tensor>& stats, at::IntArrayRef g, int64_t cfg,
                           const c10::optional<Tensor>& stats_shift) {
   const int64_t xps = check_planes(x, "x");
-  TORCH_CHECK(cfg >= 0 && cfg < 18, "hcb.conv_p3: cfg 0..17");
+  TORCH_CHECK(cfg >= 0 && cfg < 23, "hcb.conv_p3: cfg 0..22");
   // conv_params validates geometry and byte ranges on plane 0 (a bf16 tensor of this build's type);
   // split-K is validated here against the p3 tiles
   std::vector<int64_t> g1(g.begin(), g.end());
@@ -1093,7 +1103,7 @@ void conv_wgrad_p3(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntA
   TORCH_CHECK(p.C % 8 == 0 && p.ldx % 8 == 0, "hcb.conv_wgrad_p3: C, ldx multiples of 8");
   TORCH_CHECK(p.ldy % 8 == 0 && p.ldy >= p.Nout, "hcb.conv_wgrad_p3: bad ldy");
   TORCH_CHECK(splits >= 1, "hcb.conv_wgrad_p3: splits >= 1");
-  const int64_t xb = ((int64_t)p.N * p.H * p.W - 1) * p.ldx * 2 + (int64_t)p.C * 2;
+  const int64_t xb = x_span_bytes(p.N, p.H, p.W, p.C, p.ldx, 2);
   const int64_t yb = ((int64_t)p.M - 1) * p.ldy * 2 + (int64_t)((p.Nout + 7) / 8) * 8 * 2;
   TORCH_CHECK(xb < (1ll << 31) && yb < (1ll << 31), "hcb.conv_wgrad_p3: operand exceeds 2 GiB");
   TORCH_CHECK(2 * xps * 2 < (1ll << 32) && 2 * dps * 2 < (1ll << 32), "hcb.conv_wgrad_p3: plane stride range");

@@ -19,22 +19,40 @@
 // workgroup per CU). Each stage carries 6x the MFMA time of a bf16 k-step (1536 cycles per wave at
 // 64x32 wave tiles), which covers the next stage's DMA latency, so double buffering is enough.
 #include "conv_p3_fwd.h"
+#include "conv_p3_persist.h"
 #include "conv_p3_wgrad.h"
 
 namespace hcb {
 
-constexpr int N_P3_CFG = 18;
+// cfg 0-17: conv_igemm_p3_kernel (conv_p3_fwd.h); 18-22: the persistent short-K kernel
+// (conv_p3_persist.h), twins of 15, 14, 16, 17 and 7
+constexpr int N_P3_CFG = 23;
 int p3_tile_m(int cfg) {
-  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 128, 128, 64, 64, 64};
+  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128,
+                                  64,  128, 128, 64, 64, 64, 64, 128, 64, 64, 128};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 128;
 }
 int p3_slot_k(int cfg) { return (cfg >= 0 && cfg <= 6) ? 64 : 32; }
 int p3_tile_n(int cfg) {
-  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256, 128, 64, 64, 128, 64, 64};
+  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256,
+                                  128, 64, 64, 128, 64, 64, 128, 64, 64, 64, 128};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 64;
 }
 
+// the persistent cfg, or (a problem with an epilogue it does not serve) its twin
+static int launch_p3_persist(const ConvParams& p, int cfg, hipStream_t st) {
+  switch (cfg) {
+    case 18: return launch_p3p<2, 2, 32, 64, 32, 2, 2>(p, st) ? -1 : 15;
+    case 19: return launch_p3p<2, 2, 64, 32, 32, 2, 2>(p, st) ? -1 : 14;
+    case 20: return launch_p3p<2, 2, 32, 32, 32, 3, 2>(p, st) ? -1 : 16;
+    case 21: return launch_p3p<2, 2, 32, 32, 32, 2, 3>(p, st) ? -1 : 17;
+    case 22: return launch_p3p<2, 4, 64, 32, 32, 3, 1>(p, st) ? -1 : 7;
+    default: return cfg;
+  }
+}
+
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st) {
+  if (cfg >= 18 && (cfg = launch_p3_persist(p, cfg, st)) < 0) return;
   if (p.bnb_acc != nullptr)
     launch_p3_cfg<true>(p, cfg, st);
   else

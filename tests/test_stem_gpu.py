@@ -18,8 +18,9 @@ def _stem(size):
     return st, ps
 
 
-@pytest.mark.parametrize("size", [224, 64, 30])
-def test_s2d_forward_matches_direct_conv(size):
+@pytest.mark.parametrize("size,cfg", [(224, None), (64, None), (30, None), (64, 4), (64, 11), (64, 16), (64, 7)],
+                         ids=str)
+def test_s2d_forward_matches_direct_conv(size, cfg):
     import azure_hc_intel_tf_amd.ops.functional as Fn
 
     st, ps = _stem(size)
@@ -30,7 +31,7 @@ def test_s2d_forward_matches_direct_conv(size):
     P, Q, C = st.out_shape
     z = torch.empty(4, P, Q, C, device="cuda", dtype=torch.bfloat16)
     xf = st.fold_input(x)
-    Fn.conv_forward(xf, st.fold_spec, st._folded_weight(x.device), st.w.data, z)
+    Fn.conv_forward(xf, st.fold_spec, st._folded_weight(x.device), st.w.data, z, cfg=cfg)
     w = st.w.data[..., :3].permute(0, 3, 1, 2).float().cpu()
     ref = F.conv2d(x[..., :3].permute(0, 3, 1, 2).float().cpu(), w.bfloat16().float(), stride=2, padding=3)
     got = z.float().permute(0, 3, 1, 2).cpu()
@@ -75,12 +76,16 @@ def fp32_stem():
     set_gpu_compute_dtype(torch.bfloat16)
 
 
-def test_s2d_fp32_planes_match_fp64(fp32_stem):
+@pytest.mark.parametrize("cfg", [None, 14, 7, 16, 10, 4], ids=str)
+def test_s2d_fp32_planes_match_fp64(fp32_stem, cfg):
     """fp32 path: the image split into planes and folded (three planes as one 3N batch), the folded
-    weight as planes, the bf16x6 plane GEMM -- forward and weight gradient to fp32 accuracy."""
+    weight as planes, the bf16x6 plane GEMM over 64-channel row windows (fold_spec: a 4x1 conv whose
+    pixel stride, 16, is below its channel count) -- forward (every tile shape class) and weight
+    gradient (the tuned plan and the candidate tiles) to fp32 accuracy."""
     import azure_hc_intel_tf_amd.ops.functional as Fn
 
     st = fp32_stem
+    assert st.fold_spec.cin_pad == 64 and st.fold_spec.kh * st.fold_spec.kw == 4
     torch.manual_seed(2)
     x = torch.zeros(2, 64, 64, 8, device="cuda")
     x[..., :3] = torch.randn(2, 64, 64, 3, device="cuda")
@@ -88,19 +93,31 @@ def test_s2d_fp32_planes_match_fp64(fp32_stem):
     xf = st.fold_input(x)
     assert Fn.is_planes(xf)
     z = torch.empty(2, P, Q, C, device="cuda")
-    Fn.conv_forward(xf, st.fold_spec, st._folded_weight(x.device), st.w.data, z)
+    Fn.conv_forward(xf, st.fold_spec, st._folded_weight(x.device), st.w.data, z, cfg=cfg)
     xd = x[..., :3].permute(0, 3, 1, 2).double().cpu()
     wd = st.w.data[..., :3].permute(0, 3, 1, 2).double().cpu()
     ref = F.conv2d(xd, wd, stride=2, padding=3)
     got = z.permute(0, 3, 1, 2).double().cpu()
     assert ((got - ref).norm() / ref.norm()).item() < 3e-6
     dz = torch.randn(2, P, Q, C, device="cuda")
+    gref = torch.nn.grad.conv2d_weight(xd, (64, 3, 7, 7), dz.permute(0, 3, 1, 2).double().cpu(), stride=2, padding=3)
     st.w.grad.zero_()
     st._wgrad(Fn.to_planes(dz), xf)
     torch.cuda.synchronize()
-    gref = torch.nn.grad.conv2d_weight(xd, (64, 3, 7, 7), dz.permute(0, 3, 1, 2).double().cpu(), stride=2, padding=3)
     g = st.w.grad[..., :3].permute(0, 3, 1, 2).double().cpu()
     assert ((g - gref).norm() / gref.norm()).item() < 3e-6
+    if cfg is None:  # the weight-gradient tiles over the row windows, split-K included
+        fs = st.fold_spec
+        per_tile = {}
+        for c, sp in Fn.wgrad_p3_candidates(C, fs.K, 2 * P * Q):
+            per_tile[c] = (c, sp)  # each tile class with its largest split
+        for wcfg in per_tile.values():
+            dwf = torch.zeros(C, fs.K, device="cuda")
+            Fn.conv_wgrad(Fn.to_planes(dz), xf, fs, dwf, cfg=tuple(wcfg))
+            st.w.grad.zero_()
+            Fn._ext.ops().stem_wgrad_unfold(dwf, st.w.grad)
+            g = st.w.grad[..., :3].permute(0, 3, 1, 2).double().cpu()
+            assert ((g - gref).norm() / gref.norm()).item() < 3e-6, wcfg
 
 
 def test_resnet_uses_s2d_stem_and_trains():

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--fp32", action="store_true")
     ap.add_argument("--cfg", default=None, help="cfg[,splits] (default: tuned)")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--stats_r", type=int, default=8,
+                    help="fwd: BN-statistics replicas of the epilogue (-1: no statistics, 0: per-tile slab)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     m = create_model(a.model, device=dev, compute_dtype="fp32" if a.fp32 else None)
@@ -45,8 +47,10 @@ def main():
         cfg = (v[0], v[1] if len(v) > 1 else 1)
     if a.op == "fwd":
         x, y = mk((N, H, W, C)), torch.empty(N, P, Q, K, device=dev, dtype=odt)
-        acc = torch.zeros(8 * 2 * K, device=dev)
-        fn = lambda: Fn.conv_forward(x, s, l.pack.pack, None, y, stats=acc, stats_R=8, cfg=cfg)
+        R = a.stats_r
+        acc = torch.zeros(max(R, 1) * 2 * K if R != 0 else (N * P * Q // 16 + 1) * 2 * K, device=dev)
+        fn = lambda: Fn.conv_forward(x, s, l.pack.pack, None, y, stats=acc if R >= 0 else None, stats_R=max(R, 0),
+                                     cfg=cfg)
     elif a.op == "dgrad":
         dz, dx = mk((N, P, Q, K)), torch.zeros(N, H, W, C, device=dev, dtype=odt)
         fn = lambda: Fn.conv_dgrad(dz, s, l.pack.tr, None, dx, False, cfg=cfg)
