@@ -88,6 +88,9 @@ FUSE_BN_BWD = True
 # projection blocks: the shortcut's BN is applied inside the block output's BN pass
 # (act(BN3(z3) + BN_sc(z_sc)) in one kernel), so the shortcut's normalised tensor is never written
 FUSE_RES_BN = True
+# ... and in the backward the shortcut BN's reduction (sum(g), sum(g * xhat_sc): it sees the same
+# gradient g as the block's last BN) rides in the data-grad epilogue that produces g
+FUSE_RES_BN_BWD = True
 # shifted single-pass BN statistics: the conv epilogue sums (v - K), (v - K)^2 with K = the
 # layer's previous batch mean, so E[x^2] - E[x]^2 does not cancel in fp32 when |mean| >> std
 # (False: K = 0, the plain single-pass form)
@@ -168,6 +171,7 @@ class ConvBN(Layer):
         self._saved = None
         self._acc = None  # (fwd acc, bwd acc, replicas) of the current step
         self._pre_reduced = False
+        self._res_bn = None  # the deferred residual BN normalised in this layer's BN pass (forward)
         self.training = True  # False: inference BN from the moving statistics (forward-only)
 
     def flops(self, batch: int) -> int:
@@ -248,6 +252,7 @@ class ConvBN(Layer):
                 saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
                                       self.decay, self.eps, y, self.relu, residual=residual)
             self._saved = (x, z, y, saved, residual is not None)
+            self._res_bn = residual_bn
             return y
         assert residual is None or not self.relu, "conv without BN: residual add only without ReLU"
         y = out if out is not None else empty_act((N, P, Q, C), dev)
@@ -326,7 +331,16 @@ class ConvBN(Layer):
         mode = (1 if had_res else 2) if self.relu else 0
         self._pre_reduced = True
         _, acc_b, R = self._acc if self._acc is not None else (None, self.acc_b.data, STAT_R)
-        return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, acc_b, R)
+        res = None
+        rb = self._res_bn
+        if FUSE_RES_BN_BWD and rb is not None and rb._saved is not None and rb._acc is not None \
+                and rb._acc[2] == R and not rb._pre_reduced:
+            _, z2, _, saved2, _ = rb._saved
+            if z2.dtype == z.dtype and z2.shape == z.shape and z2.is_contiguous() and z.is_contiguous():
+                # the shortcut BN sees the same g (relu(bn3 + bn_sc)): its reduction rides along
+                res = (z2, saved2, rb._acc[1])
+                rb._pre_reduced = True
+        return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, acc_b, R, res=res)
 
     def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False, dx_bn=None):
         """Returns (dx or None, gres or None). gres = gradient w.r.t. the residual input.
@@ -373,6 +387,7 @@ class ConvBN(Layer):
                 Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
                 gres = dz
+        self._res_bn = None
         run_wgrad(self, dz, x)
         if self.need_dx:
             H, W, Cin = self.in_shape
@@ -387,6 +402,7 @@ class ConvBN(Layer):
 
     def clear(self):
         self._saved = None
+        self._res_bn = None
         self._pre_reduced = False
 
 
@@ -452,7 +468,9 @@ class StemS2D(ConvBN):
         self.fold_spec = ConvSpec(cin=64, cin_pad=64, cout=cout, kh=4, kw=1, sh=1, sw=1, pt=0, pl=0, pb=0, pr=-3)
         self._wfold = None
         self._wpack = None
-        self._dwfold = None
+        # the folded weight gradient [cout][256]: per-step scratch in the statistics buffer, so the
+        # step-start clear zeroes it (no allocation + fill per step)
+        self.dwfold = ps.add_stat(f"{name}/dw_fold", (cout, 256))
 
     def _folded_weight(self, dev):
         """The folded GEMM weight [cout][256]: the 16-bit pack, or on the fp32 path the hi pack of
@@ -501,7 +519,7 @@ class StemS2D(ConvBN):
 
         if x.shape[1:] != self.fold_shape:  # direct-form training path (forward() not forward_maxpool)
             x = self.fold_input(x)
-        dwf = torch.zeros((self.spec.cout, 256), dtype=torch.float32, device=dz.device)
+        dwf = self.dwfold.data.view(self.spec.cout, 256)
         Fn.conv_wgrad(dz, x, self.fold_spec, dwf)
         _ext.ops().stem_wgrad_unfold(dwf, self.w.grad)
 

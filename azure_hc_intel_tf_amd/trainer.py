@@ -152,9 +152,13 @@ class Trainer:
         if hasattr(self.model, "activate"):
             self.model.activate()
         ps = self.ps
-        if not self.forward_only:
-            ps.zero_grad()
-        ps.zero_stats()
+        if ps.statbuf.is_cuda and ps.statbuf.numel() % 4 == 0 and ps.grad.numel() % 4 == 0:
+            # one HIP launch clears the gradient and the per-step statistics scratch
+            Fn.zero_bufs([ps.statbuf] if self.forward_only else [ps.grad, ps.statbuf])
+        else:
+            if not self.forward_only:
+                ps.zero_grad()
+            ps.zero_stats()
         ps.repack()
         with range_("forward"):
             logits = self.model.forward(images)

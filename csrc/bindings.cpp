@@ -267,6 +267,33 @@ void set_bnb(hcb::ConvParams& p, const Tensor& z, const c10::optional<Tensor>& y
   p.bnb_acc = acc.data_ptr<float>();
   p.bnb_mode = (int)mode;
   p.bnb_R = (int)R;
+  p.bnb2_z = nullptr;
+  p.bnb2_mean = p.bnb2_invstd = nullptr;
+  p.bnb2_acc = nullptr;
+}
+
+// the second BN's reduction on the same gradient (ConvParams::bnb2_*): z2 like z, acc2 like acc
+void set_bnb2(hcb::ConvParams& p, const c10::optional<Tensor>& z2, const c10::optional<Tensor>& mean2,
+              const c10::optional<Tensor>& invstd2, const c10::optional<Tensor>& acc2, bool f32) {
+  if (!z2.has_value()) return;
+  TORCH_CHECK(mean2.has_value() && invstd2.has_value() && acc2.has_value(), "hcb: z2 needs mean2, invstd2, acc2");
+  const int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
+  if (f32)
+    check_f32(*z2, "z2");
+  else
+    check_act(*z2, "z2");
+  check_range(*z2, ((rows - 1) * p.bnb_ld + ((p.Nout + 7) / 8) * 8) * (f32 ? 4 : 2), "z2");
+  check_align16(z2->data_ptr(), "z2");
+  for (const Tensor* t : {&*mean2, &*invstd2}) {
+    check_f32(*t, "bn2 param");
+    TORCH_CHECK(t->numel() >= p.Nout, "hcb: second-BN per-channel tensor too small");
+  }
+  check_f32(*acc2, "acc2");
+  TORCH_CHECK(acc2->numel() >= (int64_t)p.bnb_R * 2 * p.Nout, "hcb: acc2 too small");
+  p.bnb2_z = z2->data_ptr();
+  p.bnb2_mean = mean2->data_ptr<float>();
+  p.bnb2_invstd = invstd2->data_ptr<float>();
+  p.bnb2_acc = acc2->data_ptr<float>();
 }
 
 // data-grad conv whose output is the dy of a BN layer: the epilogue gates it with the
@@ -275,9 +302,12 @@ void set_bnb(hcb::ConvParams& p, const Tensor& z, const c10::optional<Tensor>& y
 void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                     at::IntArrayRef g, int64_t cfg, const Tensor& z, const c10::optional<Tensor>& yact,
                     int64_t ld, const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
-                    const Tensor& acc, int64_t R, int64_t mode) {
+                    const Tensor& acc, int64_t R, int64_t mode, const c10::optional<Tensor>& z2,
+                    const c10::optional<Tensor>& mean2, const c10::optional<Tensor>& invstd2,
+                    const c10::optional<Tensor>& acc2) {
   hcb::ConvParams p = conv_params(x, w, y, yres, c10::nullopt, c10::nullopt, g, cfg);
   set_bnb(p, z, yact, ld, mean, invstd, gamma, beta, acc, R, mode, false);
+  set_bnb2(p, z2, mean2, invstd2, acc2, false);
   hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
 }
 
@@ -617,6 +647,21 @@ void loss_scale_update(const Tensor& hyper, double world, bool dynamic) {
   check_f32(hyper, "hyper");
   TORCH_CHECK(hyper.numel() >= 8 && hyper.is_contiguous(), "hcb.loss_scale_update: hyper[8]");
   hcb::launch_loss_scale_update(hyper.data_ptr<float>(), (float)world, dynamic ? 1 : 0, cur_stream());
+}
+
+// zero up to ZERO_BUFS contiguous fp32 tensors (16-byte aligned) in one launch
+void zero_bufs(at::TensorList ts) {
+  TORCH_CHECK(ts.size() >= 1 && ts.size() <= (size_t)hcb::ZERO_BUFS, "hcb.zero_bufs: 1..", hcb::ZERO_BUFS, " tensors");
+  float* ptrs[hcb::ZERO_BUFS];
+  int64_t ns[hcb::ZERO_BUFS];
+  for (size_t i = 0; i < ts.size(); ++i) {
+    check_f32(ts[i], "zero_bufs");
+    TORCH_CHECK(ts[i].is_contiguous(), "hcb.zero_bufs: contiguous tensors only");
+    check_align16(ts[i].data_ptr(), "zero_bufs");
+    ptrs[i] = ts[i].data_ptr<float>();
+    ns[i] = ts[i].numel();
+  }
+  hcb::launch_zero_bufs(ptrs, ns, (int)ts.size(), cur_stream());
 }
 
 void colsum(const Tensor& g, int64_t ld, int64_t M, int64_t N, const Tensor& out) {
@@ -1079,9 +1124,12 @@ void conv_p3(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor&
 void conv_p3_bnb(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor& y,
                  const c10::optional<Tensor>& yres, at::IntArrayRef g, int64_t cfg, const Tensor& z,
                  const c10::optional<Tensor>& yact, int64_t ld, const Tensor& mean, const Tensor& invstd,
-                 const Tensor& gamma, const Tensor& beta, const Tensor& acc, int64_t R, int64_t mode) {
+                 const Tensor& gamma, const Tensor& beta, const Tensor& acc, int64_t R, int64_t mode,
+                 const c10::optional<Tensor>& z2, const c10::optional<Tensor>& mean2,
+                 const c10::optional<Tensor>& invstd2, const c10::optional<Tensor>& acc2) {
   hcb::ConvParams p = p3_params(x, w, w_lo, y, yres, c10::nullopt, c10::nullopt, g, cfg, c10::nullopt);
   set_bnb(p, z, yact, ld, mean, invstd, gamma, beta, acc, R, mode, true);
+  set_bnb2(p, z2, mean2, invstd2, acc2, true);
   hcb::launch_conv_p3(p, (int)cfg, cur_stream());
 }
 
@@ -1168,7 +1216,7 @@ void set_deterministic(bool on) { hcb::set_deterministic(on); }
 
 HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None, Tensor? w_lo=None) -> ()");
-  m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
+  m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode, Tensor? z2=None, Tensor? mean2=None, Tensor? invstd2=None, Tensor(c!)? acc2=None) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
@@ -1189,6 +1237,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("loss_total(Tensor row_loss, int B, Tensor? l2, float half_wd, Tensor(a!) loss) -> ()");
   m.def("loss_scale_update(Tensor(a!) hyper, float world, bool dynamic) -> ()");
   m.def("colsum(Tensor g, int ld, int M, int N, Tensor(a!) out) -> ()");
+  m.def("zero_bufs(Tensor(a!)[] ts) -> ()");
   m.def("sgd_momentum(Tensor(a!) w, Tensor(b!) mom, Tensor g, int n_decay, Tensor hyper, Tensor(c!)? l2, bool nesterov) -> ()");
   m.def("weight_pack(Tensor master, Tensor(a!) pack, Tensor table, int max_work, int lo=0) -> ()");
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()");
@@ -1215,7 +1264,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("stem_wgrad_unfold(Tensor dwp, Tensor(a!) dw) -> ()");
   m.def("conv_p3(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
   m.def("conv_wgrad_p3(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
-  m.def("conv_p3_bnb(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
+  m.def("conv_p3_bnb(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode, Tensor? z2=None, Tensor? mean2=None, Tensor? invstd2=None, Tensor(c!)? acc2=None) -> ()");
   m.def("split_planes(Tensor x, int ldx, int rows, int C, Tensor(a!) out, int ldo) -> ()");
   m.def("merge_planes(Tensor x, int ldi, int rows, int C, Tensor(a!) y, int ldy) -> ()");
   m.def("gap_fwd_p3(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
@@ -1242,6 +1291,7 @@ HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("gap_bwd", gap_bwd);
   m.impl("softmax_xent", softmax_xent);
   m.impl("colsum", colsum);
+  m.impl("zero_bufs", zero_bufs);
   m.impl("sgd_momentum", sgd_momentum);
   m.impl("weight_pack", weight_pack);
   m.impl("cast_f32_bf16", cast_f32_bf16);

@@ -21,7 +21,8 @@
 // tile's epilogue was issued after slot g+1's DMA (the first NST-1 steps of a tile).
 //
 // Not served (the host falls back to the twin cfg of conv_igemm_p3_kernel): the fused
-// BN-backward epilogue, split-K, beta-accumulate, bias and the strided-output remap.
+// BN-backward epilogue, split-K, beta-accumulate, bias, the strided-output remap and the
+// input-dilated (strided data-gradient) loader.
 // The reference's role: the MKL-DNN fp32 Conv2D forward primitive, driven by
 // /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81.
 #pragma once
@@ -280,7 +281,8 @@ static bool launch_p3p(const ConvParams& p, hipStream_t st) {
   const int nk = p.Kpad / KW;
   const size_t ring = p3p_ring_bytes<BM, BN, KW, NST>();
   const size_t lds = ring + (stats ? (size_t)p.Nout * 4 : 0);
-  if (p.bnb_acc != nullptr || p.remap || p.splits != 1 || p.beta || p.bias != nullptr || !p.out_f32 ||
+  if (p.bnb_acc != nullptr || p.remap || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || p.beta ||
+      p.bias != nullptr || !p.out_f32 ||
       (stats && p.stats_R <= 0) || nk < NST - 1 || p.Kpad % KW != 0 || lds > 160 * 1024 ||
       (size_t)p.M * p.ldy * 4 >= (1ull << 31))
     return false;

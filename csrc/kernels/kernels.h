@@ -63,6 +63,12 @@ struct ConvParams {
   const float *bnb_mean, *bnb_invstd, *bnb_gamma, *bnb_beta;
   float* bnb_acc;
   int bnb_mode, bnb_R, bnb_ld;
+  // A second BN on the same gradient (ResNet projection blocks: the shortcut's BN, whose output is
+  // added to the block's last BN before the ReLU, sees the same g): when bnb2_z is set the epilogue
+  // also accumulates sum(g) and sum(g * xhat2) into bnb2_acc ([bnb_R][2][Nout]); z2 rows like z.
+  const void* bnb2_z;
+  const float *bnb2_mean, *bnb2_invstd;
+  float* bnb2_acc;
   // In-launch split-K (LDS-DMA kernels): `splits` blocks per output tile each reduce a
   // contiguous k-step range; all but the last arriver park fp32 partials in ws slabs
   // [tile][split][tile elems], the last one (agent-scope ticket in cnt[tile], self-resetting)
@@ -227,6 +233,8 @@ void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t 
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
                          float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
                          hipStream_t st, bool f32 = false, float* dl32 = nullptr);
+constexpr int ZERO_BUFS = 6;
+void launch_zero_bufs(float* const* ptrs, const int64_t* ns, int nb, hipStream_t st);
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st);
 
 // ---------------------------------------------------------------- optimizer / weights

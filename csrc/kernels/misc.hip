@@ -73,6 +73,40 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
 __global__ void zero_f32_kernel(float* out, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = 0.f;
 }
+// Step-start clears in ONE launch (the flat gradient, the BN statistic accumulators, scratch
+// accumulators): up to ZERO_BUFS fp32 buffers, 16-byte stores over each buffer's 4-float body and
+// dword stores over its tail. Replaces the per-buffer torch fill kernels of the captured step (and
+// never a memset node: see colsum below).
+struct ZeroBufs {
+  float* p[ZERO_BUFS];
+  int64_t n[ZERO_BUFS];
+  int nb;
+};
+__global__ __launch_bounds__(256) void zero_bufs_kernel(ZeroBufs z) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int b = 0; b < z.nb; ++b) {
+    float* p = z.p[b];
+    const int64_t n = z.n[b], n4 = n >> 2;
+    f32x4* p4 = reinterpret_cast<f32x4*>(p);
+    for (int64_t i = t0; i < n4; i += stride) p4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t i = (n4 << 2) + t0; i < n; i += stride) p[i] = 0.f;
+  }
+}
+void launch_zero_bufs(float* const* ptrs, const int64_t* ns, int nb, hipStream_t st) {
+  ZeroBufs z{};
+  int64_t tot = 0;
+  for (int b = 0; b < nb; ++b) {
+    z.p[b] = ptrs[b];
+    z.n[b] = ns[b];
+    tot += ns[b];
+  }
+  z.nb = nb;
+  int64_t blocks = (tot / 4 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  hipLaunchKernelGGL(zero_bufs_kernel, dim3((unsigned)blocks), dim3(256), 0, st, z);
+}
+
 __global__ __launch_bounds__(256) void colsum_kernel(const void* g, int ld, int M, int N, int is_f32,
                                                      float* out, int direct) {
   __shared__ float part[8][257];
