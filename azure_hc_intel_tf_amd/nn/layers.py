@@ -495,9 +495,12 @@ class StemS2D(ConvBN):
         from ..ops import _ext
 
         if Fn.is_planes(x) or (x.is_cuda and x.dtype == torch.float32):
-            xp = Fn.to_planes(x)
             N = x.shape[0]
             xf = Fn.Planes.empty((N,) + self.fold_shape, x.device)
+            if not Fn.is_planes(x) and x.is_contiguous():  # split while folding: one pass over the image
+                _ext.ops().stem_s2d(x, xf.t, self.PAD)
+                return xf
+            xp = Fn.to_planes(x)
             _ext.ops().stem_s2d(xp.t.view((3 * N,) + tuple(xp.shape[1:])), xf.t.view((3 * N,) + self.fold_shape),
                                 self.PAD)
             return xf

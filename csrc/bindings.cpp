@@ -1025,6 +1025,19 @@ void bucket_unpack(const Tensor& src, const Tensor& dst, double scale) {
 void stem_s2d(const Tensor& x, const Tensor& out, int64_t pad) {
   check_cuda(x, "x");
   check_cuda(out, "out");
+  if (x.scalar_type() == at::kFloat) {  // fp32 image -> the folded tensor's three bf16 planes [3][N][Hs][Ws][16]
+    const int64_t ops = check_planes(out, "out");
+    TORCH_CHECK(x.dim() == 4 && out.dim() == 5 && x.is_contiguous() && out.select(0, 0).is_contiguous() &&
+                    x.size(3) >= 4 && x.size(3) % 4 == 0 && out.size(4) == 16 && out.size(1) == x.size(0),
+                "hcb.stem_s2d: fp32 x [N][H][W][>=4, multiple of 4] -> planes [3][N][Hs][Ws][16]");
+    const int64_t H = x.size(1), W = x.size(2), Hs = out.size(2), Ws = out.size(3);
+    TORCH_CHECK(2 * Hs - 1 - pad < H + 8 && 2 * Ws - 1 - pad < W + 8 && x.numel() < (1ll << 31),
+                "hcb.stem_s2d: folded extent");
+    hcb::launch_stem_s2d_f32(x.data_ptr<float>(), (int)x.size(0), (int)H, (int)W, (int)x.size(3),
+                             reinterpret_cast<uint16_t*>(out.data_ptr()), ops, (int)Hs, (int)Ws, (int)pad,
+                             cur_stream());
+    return;
+  }
   TORCH_CHECK(x.dim() == 4 && out.dim() == 4 && x.scalar_type() == kAct && out.scalar_type() == kAct,
               "hcb.stem_s2d: 16-bit NHWC tensors");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.size(3) >= 4 && x.size(3) % 4 == 0 && out.size(3) == 16 &&

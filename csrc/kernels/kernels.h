@@ -280,6 +280,8 @@ void launch_preprocess_images(const uint8_t* src, const int64_t* desc, int B, vo
                               const float* scale, const float* bias, hipStream_t st);
 
 // ---------------------------------------------------------------- space-to-depth stem (stem.hip)
+void launch_stem_s2d_f32(const float* x, int N, int H, int W, int ldx, uint16_t* out, int64_t plane, int Hs, int Ws,
+                         int pad, hipStream_t st);
 void launch_stem_s2d(const uint16_t* x, int N, int H, int W, int ldx, uint16_t* out, int Hs, int Ws, int pad,
                      hipStream_t st);
 void launch_stem_wfold(const float* w, int cout, int cs, uint16_t* wp, hipStream_t st, bool p3 = false);

@@ -42,6 +42,39 @@ __global__ __launch_bounds__(256) void stem_s2d_kernel(const uint16_t* __restric
   }
 }
 
+// fp32 path: the fold straight from the fp32 image into the three bf16 planes of the folded
+// tensor (plane stride `plane` elements): the split of each value (split3_8) happens here, so the
+// image is read once and no full-size planes copy of it is written and re-read
+__global__ __launch_bounds__(256) void stem_s2d_f32_kernel(const float* __restrict__ x, int N, int H, int W, int ldx,
+                                                           uint16_t* __restrict__ out, int64_t plane, int Hs, int Ws,
+                                                           int pad) {
+  const int64_t total = (int64_t)N * Hs * Ws;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int Q = (int)(t % Ws);
+    const int64_t r = t / Ws;
+    const int P = (int)(r % Hs);
+    const int n = (int)(r / Hs);
+    u32x4 v[4];
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab) {
+      const int h = 2 * P + (ab >> 1) - pad, w = 2 * Q + (ab & 1) - pad;
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+        v[ab] = *reinterpret_cast<const u32x4*>(x + (((int64_t)n * H + h) * W + w) * ldx);
+      else
+        v[ab] = u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {  // source pixels (0, 1), then (2, 3): 8 values each
+      u32x4 hi, mid, lo;
+      split3_8(v[2 * hf], v[2 * hf + 1], hi, mid, lo);
+      uint16_t* o = out + t * 16 + hf * 8;
+      *reinterpret_cast<u32x4*>(o) = hi;
+      *reinterpret_cast<u32x4*>(o + plane) = mid;
+      *reinterpret_cast<u32x4*>(o + 2 * plane) = lo;
+    }
+  }
+}
+
 // folded bf16 GEMM operand W'[cout][256] from the fp32 master w[cout][7][7][cs] (cs = stored
 // channels, the first 3 real)
 // P3 (fp32 path): the folded weight as bf16 hi / mid / lo planes (plane stride cout * 256)
@@ -84,6 +117,13 @@ void launch_stem_s2d(const uint16_t* x, int N, int H, int W, int ldx, uint16_t* 
   int64_t g = (total + 255) / 256;
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(stem_s2d_kernel, dim3((int)g), dim3(256), 0, st, x, N, H, W, ldx, out, Hs, Ws, pad);
+}
+void launch_stem_s2d_f32(const float* x, int N, int H, int W, int ldx, uint16_t* out, int64_t plane, int Hs, int Ws,
+                         int pad, hipStream_t st) {
+  const int64_t total = (int64_t)N * Hs * Ws;
+  int64_t g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(stem_s2d_f32_kernel, dim3((int)g), dim3(256), 0, st, x, N, H, W, ldx, out, plane, Hs, Ws, pad);
 }
 void launch_stem_wfold(const float* w, int cout, int cs, uint16_t* wp, hipStream_t st, bool p3) {
   if (p3)

@@ -17,7 +17,14 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 def test_shortcut_bn_reduction_rides_in_the_dgrad_epilogue(dtype, monkeypatch):
+    """Deterministic mode (this tiny-batch net amplifies atomic-order noise: two default-mode runs of
+    the SAME code differ by 100% (bf16) / 1.5% (fp32) in these gradients, tools/diag/res_bn_probe.py,
+    profiles/r5_res_bn_fusion.txt). fp32: fused = unfused to ~1e-6. bf16: the fused sums take the
+    epilogue's unrounded fp32 g where the separate pass reads the bf16-rounded tensor; the difference
+    (2e-3 on the first fused shortcut in backward order, stage 4) grows through the later BN
+    backwards to ~1.5e-2 on stage 1."""
     out = {}
+    Fn.set_deterministic(True)
     try:
         for fuse in (False, True):
             monkeypatch.setattr(L, "FUSE_RES_BN_BWD", fuse)
@@ -43,15 +50,16 @@ def test_shortcut_bn_reduction_rides_in_the_dgrad_epilogue(dtype, monkeypatch):
             out[fuse] = (m.ps.grad.float().cpu().clone(), sc, unfused[0])
             del m, t
     finally:
+        Fn.set_deterministic(False)
         Fn.set_f32_native(False)
         set_gpu_compute_dtype(torch.bfloat16)
     g0, sc0, n0 = out[False]
     g1, sc1, n1 = out[True]
     assert n0 - n1 == 4, (n0, n1)  # ResNet-50's four projection shortcuts
     assert len(sc0) == 8
-    tol = 1e-4 if dtype == "fp32" else 1e-2
     for name in sc0:
         rel = ((sc1[name] - sc0[name]).norm() / sc0[name].norm()).item()
+        tol = 1e-5 if dtype == "fp32" else (1e-2 if name.startswith("stage4") else 5e-2)
         assert rel < tol, (name, rel)
     rel = ((g1 - g0).norm() / g0.norm()).item()
-    assert rel < (1e-3 if dtype == "fp32" else 5e-2), rel
+    assert rel < (1e-4 if dtype == "fp32" else 5e-2), rel
