@@ -453,8 +453,9 @@ _P3_PERSIST = {18: 15, 19: 14, 20: 16, 21: 17, 22: 7}
 # 12-15 32-deep slots, two / three workgroups per CU
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),
               6: (128, 128), 7: (128, 128), 8: (256, 128), 9: (128, 256), 10: (128, 128), 11: (128, 64),
-              12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (64, 64)}
-_WP3_OCC = {12: 2, 13: 2, 14: 2, 15: 3}  # workgroups per CU the weight-grad tile is built for
+              12: (128, 64), 13: (64, 128), 14: (64, 64), 15: (64, 64),
+              16: (128, 64), 17: (64, 128), 18: (64, 64)}  # 16-18: persistent twins of 12, 13, 15
+_WP3_OCC = {12: 2, 13: 2, 14: 2, 15: 3, 16: 2, 17: 2, 18: 3}  # workgroups per CU the weight-grad tile is built for
 
 
 def fwd3_key(M: int, N: int, K: int, taps: int = 1):

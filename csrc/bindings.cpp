@@ -1151,7 +1151,7 @@ void conv_wgrad_p3(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntA
                    int64_t splits) {
   TORCH_CHECK(g.size() == 17, "hcb.conv_wgrad_p3: geom must have 17 entries");
   const int64_t dps = check_planes(dy, "dy"), xps = check_planes(x, "x");
-  TORCH_CHECK(cfg >= 0 && cfg < 16, "hcb.conv_wgrad_p3: cfg 0..15");
+  TORCH_CHECK(cfg >= 0 && cfg < 19, "hcb.conv_wgrad_p3: cfg 0..18");
   check_f32(dw, "dw");
   hcb::WgradParams p{};
   p.N = g[0]; p.H = g[1]; p.W = g[2]; p.C = g[3]; p.ldx = g[4];

@@ -65,18 +65,22 @@ void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st) {
 //   9 128x256 (2x4 of 64x64, 2x32), 10 128x128 (2x2 of 64x64, 3x32), 11 128x64 (2x2 of 64x32, 3x32),
 //   two per CU: 12 128x64 (2x2 of 64x32, 2x32), 13 64x128 (2x2 of 32x64, 2x32), 14 64x64 (2x2 of 32x32, 3x32),
 //   three per CU: 15 64x64 (2x2 of 32x32, 2x32)
-constexpr int N_WP3_CFG = 16;
+//   persistent (conv_p3_persist.h, twins of 12, 13, 15): 16 128x64, 17 64x128, 18 64x64
+constexpr int N_WP3_CFG = 19;
 int wgrad_p3_tile_m(int cfg) {
-  static const int t[N_WP3_CFG] = {128, 64, 64, 128, 64, 64, 128, 128, 256, 128, 128, 128, 128, 64, 64, 64};
+  static const int t[N_WP3_CFG] = {128, 64, 64, 128, 64, 64, 128, 128, 256, 128, 128, 128, 128, 64, 64, 64, 128, 64, 64};
   return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
 }
 int wgrad_p3_tile_n(int cfg) {
-  static const int t[N_WP3_CFG] = {64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 64, 128, 64, 64};
+  static const int t[N_WP3_CFG] = {64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 64, 128, 64, 64, 64, 128, 64};
   return (cfg >= 0 && cfg < N_WP3_CFG) ? t[cfg] : 64;
 }
 
 void launch_wgrad_p3(const WgradParams& p, int cfg, int splits, hipStream_t st) {
   switch (cfg) {
+    case 16: wlaunch_p3p<2, 2, 64, 32, 2>(p, splits, st); break;
+    case 17: wlaunch_p3p<2, 2, 32, 64, 2>(p, splits, st); break;
+    case 18: wlaunch_p3p<2, 2, 32, 32, 3>(p, splits, st); break;
     case 0: wlaunch_p3<2, 2, 64, 32, 2, 64>(p, splits, st); break;
     case 1: wlaunch_p3<2, 2, 32, 64, 2, 64>(p, splits, st); break;
     case 3: wlaunch_p3<4, 2, 32, 32, 2, 64>(p, splits, st); break;

@@ -27,6 +27,7 @@
 // /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81.
 #pragma once
 #include "conv_p3_fwd.h"
+#include "conv_p3_wgrad.h"
 
 namespace hcb {
 
@@ -317,6 +318,318 @@ static bool launch_p3p(const ConvParams& p, hipStream_t st) {
     hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, OCC>), dim3(grid), b, lds, st,
                        p);
   return true;
+}
+
+}  // namespace hcb
+
+namespace hcb {
+
+// ============================================================== persistent weight gradient
+// The weight-gradient plane GEMM (conv_p3_wgrad.h) as a persistent kernel: a workgroup walks the
+// (tile, split) work items first, first + grid, ... with its LDS-DMA ring running across item
+// boundaries, and adds each finished item into dW straight from the accumulator registers (one
+// buffer atomic per element; masked elements add to an out-of-range offset, so every epilogue is
+// exactly EOPS vector-memory instructions and the ring's vmcnt waits stay compile-time counts, as
+// in conv_p3_persist_kernel). One atomic per element and item: with one split (the deterministic
+// mode) every element receives a single add. NST = 2 only: the last split of a tile may own a
+// single 32-row k-step, and the wait arithmetic allows one epilogue per window of NST-1 steps.
+template <int WM, int WN, int TM, int TN, bool CBIG, int OCC>
+__global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_persist_kernel(WgradParams p, int nsplit) {
+  constexpr int NST = 2, BK = 32;
+  constexpr int BM = WM * TM, BN = WN * TN;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int ACPR = BM / 8, BCPR = BN / 8;
+  constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;
+  constexpr int AI = BK / ARPI / NW, BI = BK / BRPI / NW;
+  constexpr int LOADS = NPL * (AI + BI);
+  constexpr int AIMG = BK * BM * 2, BIMG = BK * BN * 2;
+  constexpr int STAGE = NPL * (AIMG + BIMG);
+  constexpr int EOPS = MI * NI * 4;
+  static_assert(AI * ARPI * NW == BK && BI * BRPI * NW == BK && AI >= 1 && BI >= 1, "tile / wave mapping");
+  static_assert(LOADS * (NST - 1) + EOPS <= 63 && NST * STAGE <= 160 * 1024, "vmcnt range / ring");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = wave_id_uniform();
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_m = (p.Nout + BM - 1) / BM;
+  const int tiles_n = (p.K + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int items = ntiles * nsplit;
+  const int grid = gridDim.x;
+  const int first = xcd_remap(blockIdx.x, grid);
+  if (first >= items) return;  // uniform
+  const int mine = (items - 1 - first) / grid + 1;
+  const int rows_per = p.ksteps_per_split * 64;
+
+  const char* db = reinterpret_cast<const char*>(p.dy);
+  const char* xb = reinterpret_cast<const char*>(p.x);
+  const __amdgpu_buffer_rsrc_t dyr0 = make_rsrc(db, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t dyr1 = make_rsrc(db + p.dy_plane, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t dyr2 = make_rsrc(db + 2 * (size_t)p.dy_plane, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr0 = make_rsrc(xb, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr1 = make_rsrc(xb + p.x_plane, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(xb + 2 * (size_t)p.x_plane, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t dwr = make_rsrc(p.dw, (uint32_t)((size_t)p.Nout * p.K * 4));
+
+  // per-thread LDS image positions (fixed) and the column chunk each lane fetches
+  int a_row[AI], a_chunk[AI], b_row[BI], b_chunk[BI];
+#pragma unroll
+  for (int v = 0; v < AI; ++v) {
+    const int row = (wid * AI + v) * ARPI + lane / ACPR, pos = lane % ACPR;
+    a_row[v] = row;
+    a_chunk[v] = (((pos >> 1) ^ p3w_swz<BM / 16>(row)) << 1) | (pos & 1);
+  }
+#pragma unroll
+  for (int v = 0; v < BI; ++v) {
+    const int row = (wid * BI + v) * BRPI + lane / BCPR, pos = lane % BCPR;
+    b_row[v] = row;
+    b_chunk[v] = (((pos >> 1) ^ p3w_swz<BN / 16>(row)) << 1) | (pos & 1);
+  }
+  auto item_rows = [&](int i, int& mbeg, int& mend) {
+    const int t = first + i * grid;
+    const int split = t / ntiles;
+    mbeg = split * rows_per;
+    mend = min(mbeg + rows_per, p.M);
+  };
+
+  // ---- issue cursor (item ci, k-step ck)
+  int ci = 0, ck = 0, c_nk = 0, c_mbeg = 0, c_mend = 0;
+  int a_col[AI], b_c[BI], b_dh[BI], b_dw[BI];
+  bool b_ok[BI];
+  auto cursor_item = [&](int i) {
+    const int t = first + i * grid;
+    const int tile = t % ntiles;
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int i0 = tm * BM, j0 = tn * BN;
+    item_rows(i, c_mbeg, c_mend);
+    c_nk = (c_mend - c_mbeg + BK - 1) / BK;
+#pragma unroll
+    for (int v = 0; v < AI; ++v) a_col[v] = i0 + a_chunk[v] * 8;
+#pragma unroll
+    for (int v = 0; v < BI; ++v) {
+      const int col = j0 + b_chunk[v] * 8;
+      int tap, c;
+      if constexpr (CBIG) {
+        tap = j0 / p.C;
+        c = j0 - tap * p.C + b_chunk[v] * 8;
+      } else {
+        tap = (int)fdiv((uint32_t)col, p.fd_c);
+        c = col - tap * p.C;
+      }
+      const int r = (int)fdiv((uint32_t)tap, p.fd_s), s = tap - r * p.S;
+      b_c[v] = c;
+      b_dh[v] = r * p.dil_h - p.pad_h;
+      b_dw[v] = s * p.dil_w - p.pad_w;
+      b_ok[v] = col < p.K;
+    }
+  };
+  cursor_item(0);
+  auto issue = [&](int stage) {
+    const bool live = ci < mine;
+    const int mb = c_mbeg + ck * BK;
+    char* sA = smem + stage * STAGE;
+    char* sB = sA + NPL * AIMG;
+#pragma unroll
+    for (int v = 0; v < AI; ++v) {
+      const int m = mb + a_row[v];
+      const bool ok = live & (a_col[v] < p.Nout) & (m < c_mend);
+      const uint32_t off = ((uint32_t)(m * p.ldy + a_col[v]) * 2u) | ((uint32_t)!ok << 31);
+      char* d = sA + (wid * AI + v) * ARPI * BM * 2;
+      glds16(dyr0, d, off);
+      glds16(dyr1, d + AIMG, off);
+      glds16(dyr2, d + 2 * AIMG, off);
+    }
+#pragma unroll
+    for (int v = 0; v < BI; ++v) {
+      const int m = mb + b_row[v];
+      const int n = (int)fdiv((uint32_t)m, p.fd_pq);
+      const int rem = m - n * p.P * p.Q;
+      const int pp = (int)fdiv((uint32_t)rem, p.fd_q);
+      const int qq = rem - pp * p.Q;
+      const int h = pp * p.stride_h + b_dh[v], w = qq * p.stride_w + b_dw[v];
+      const bool ok = live & b_ok[v] & (m < c_mend) & ((unsigned)h < (unsigned)p.H) & ((unsigned)w < (unsigned)p.W);
+      const uint32_t raw = (uint32_t)(((n * p.H + h) * p.W + w) * p.ldx + b_c[v]) * 2u;
+      const uint32_t off = raw | ((uint32_t)!ok << 31);
+      char* d = sB + (wid * BI + v) * BRPI * BN * 2;
+      glds16(xr0, d, off);
+      glds16(xr1, d + BIMG, off);
+      glds16(xr2, d + 2 * BIMG, off);
+    }
+  };
+  auto advance = [&]() {
+    if (++ck == c_nk) {
+      ck = 0;
+      if (++ci < mine) cursor_item(ci);
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int li = lane & 15, g = lane >> 4, q4 = li >> 2, p4 = li & 3;
+  auto epilogue = [&](int i) {
+    const int t = first + i * grid;
+    const int tile = t % ntiles;
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int rbase = tm * BM + wm * TM + g * 4, cbase = tn * BN + wn * TN + li;
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rbase + ii * 16 + e;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = cbase + j * 16;
+          const bool ok = (row < p.Nout) & (col < p.K);
+          buf_atomic_add_f32(dwr, ok ? (uint32_t)(row * p.K + col) * 4u : HCB_OOB, acc[ii][j][e]);
+        }
+      }
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // transposed fragment reads, as conv_wgrad_p3_kernel
+  auto frag = [&](const char* base, int ncols, int krow, int col) -> u32x4 {
+    short4v v[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rr = krow + 4 * h + q4, cb = (col + 4 * p4) * 2;
+      const int sw = ncols == BM ? p3w_swz<BM / 16>(rr) : p3w_swz<BN / 16>(rr);
+      const int slot = (cb >> 5) ^ sw;
+      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((short4v HCB_LDS*)(base + rr * ncols * 2 + slot * 32 + (cb & 31)));
+    }
+    short8 t = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
+    return __builtin_bit_cast(u32x4, t);
+  };
+  using Fr = P3Frags<TM, TN, 1>;
+  auto read = [&](int gstep, Fr& f) {
+    const char* Ab = smem + (gstep % NST) * STAGE;
+    const char* Bb = Ab + NPL * AIMG;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int t = 0; t < NPL; ++t) f.a[0][t][i] = frag(Ab + t * AIMG, BM, 8 * g, wm * TM + i * 16);
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int t = 0; t < NPL; ++t) f.b[0][t][j] = frag(Bb + t * BIMG, BN, 8 * g, wn * TN + j * 16);
+  };
+
+#pragma unroll
+  for (int s = 0; s < NST; ++s) {
+    issue(s);
+    advance();
+  }
+  int nsteps = 0;
+  for (int i = 0; i < mine; ++i) {
+    int mb, me;
+    item_rows(i, mb, me);
+    nsteps += (me - mb + BK - 1) / BK;
+  }
+  int i = 0, k = 0, nk_cur;
+  {
+    int mb, me;
+    item_rows(0, mb, me);
+    nk_cur = (me - mb + BK - 1) / BK;
+  }
+  auto post = [&]() {
+    if (++k == nk_cur) {
+      epilogue(i);
+      k = 0;
+      if (++i < mine) {
+        int mb, me;
+        item_rows(i, mb, me);
+        nk_cur = (me - mb + BK - 1) / BK;
+      }
+    }
+  };
+  constexpr int FREGS = (MI + NI) * NPL * 4, AREGS = MI * NI * 4;
+  constexpr int RBUDGET = p3_regs_per_wave<OCC, NW>() - 88 < 400 ? p3_regs_per_wave<OCC, NW>() - 88 : 400;
+  constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET;
+  constexpr int NMF = MI * NI * 6, NRD = 2 * (MI + NI) * NPL;
+  if constexpr (PIPE) {
+    Fr fr[2];
+    wait_vmcnt<(NST - 1) * LOADS>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(0, fr[0]);
+    auto body = [&](int gs, Fr& cur, Fr& nxt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (i > 0 && k == 0)  // the previous item's epilogue was issued after slot gs+1's DMA
+        wait_vmcnt<EOPS>();
+      else
+        wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue(gs % NST);
+      read(gs + 1, nxt);
+      p3_mma<TM, TN, 1>(cur, acc);
+      ilv_schedule<NMF, LOADS, NRD>();
+      advance();
+      post();
+    };
+    for (int gs = 0; gs < nsteps; gs += 2) {
+      body(gs, fr[0], fr[1]);
+      if (gs + 1 < nsteps) body(gs + 1, fr[1], fr[0]);
+    }
+  } else {
+    Fr fr;
+    for (int gs = 0; gs < nsteps; ++gs) {
+      // slot gs landed: one later slot issue, plus an epilogue issued after slot gs's DMA (the first
+      // two steps of an item; two epilogues in the window only make the count conservative)
+      if (i > 0 && k <= 1)
+        wait_vmcnt<LOADS + EOPS>();
+      else
+        wait_vmcnt<LOADS>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read(gs, fr);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue(gs % NST);
+      p3_mma<TM, TN, 1>(fr, acc);
+      ilv_schedule<NMF, LOADS, 0>();
+      advance();
+      post();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy pieces have landed before the LDS is freed
+}
+
+template <int WM, int WN, int TM, int TN, int OCC>
+static void wlaunch_p3p(const WgradParams& p, int splits, hipStream_t st) {
+  constexpr int BM = WM * TM, BN = WN * TN;
+  const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
+  const size_t lds = (size_t)2 * NPL * 32 * (BM + BN) * 2;
+  static bool once = false;
+  if (!once) {
+    p3_set_lds_once(conv_wgrad_p3_persist_kernel<WM, WN, TM, TN, true, OCC>);
+    p3_set_lds_once(conv_wgrad_p3_persist_kernel<WM, WN, TM, TN, false, OCC>);
+    once = true;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int items = tiles * splits;
+  const int per_cu = (int)((160 * 1024) / lds) < OCC ? (int)((160 * 1024) / lds) : OCC;
+  const int slots = cus * (per_cu > 0 ? per_cu : 1);
+  const int grid = items < slots ? items : slots;
+  const dim3 b(WM * WN * 64);
+  if ((p.C % BN) == 0)
+    hipLaunchKernelGGL((conv_wgrad_p3_persist_kernel<WM, WN, TM, TN, true, OCC>), dim3(grid), b, lds, st, p, splits);
+  else
+    hipLaunchKernelGGL((conv_wgrad_p3_persist_kernel<WM, WN, TM, TN, false, OCC>), dim3(grid), b, lds, st, p, splits);
 }
 
 }  // namespace hcb

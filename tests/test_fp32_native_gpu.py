@@ -82,7 +82,7 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     if isinstance(cfg, tuple):  # split-K case: the weight-gradient configs once
         return
     for wcfg in ((2, 1), (0, 4), (3, 8), (1, 2), (4, 1), (5, 2), (6, 1), (7, 2), (8, 1), (9, 3), (10, 4), (11, 2),
-                 (12, 1), (13, 2), (14, 3), (15, 2)):
+                 (12, 1), (13, 2), (14, 3), (15, 2), (16, 1), (16, 3), (17, 2), (18, 5)):
         dw = torch.zeros(cout, spec.K, device=DEV)
         Fn.conv_wgrad(dz, x, spec, dw, cfg=wcfg)
         assert rel_err(dw.view(cout, k, k, cin), wr.grad.permute(0, 2, 3, 1)) < 3e-6, wcfg
@@ -118,6 +118,18 @@ def test_fp32_persistent_short_k_gemm(fp32_mode, cfg, shape):
     y2 = torch.empty_like(y)
     Fn.conv_forward(x, spec, pk.pack, p.data, y2, cfg=cfg, relu=True)
     assert rel_err(y2, ref.clamp(min=0)) < 3e-6
+    if cfg == 18:  # the persistent weight gradient (wgrad cfg 16-18): many (tile, split) items per workgroup
+        dz = torch.randn(N, H, H, cout, device=DEV)
+        xr = xd.clone().requires_grad_(True)
+        wr = wd.clone().requires_grad_(True)
+        torch.nn.functional.conv2d(xr, wr, padding=pad).backward(dz.double().cpu().permute(0, 3, 1, 2))
+        ksteps = (M + 63) // 64
+        for wc in (16, 17, 18):
+            for sp in (1, max(1, ksteps // 2), 7):
+                dw = torch.zeros(cout, spec.K, device=DEV)
+                Fn.conv_wgrad(dz, x, spec, dw, cfg=(wc, sp))
+                # (one split sums up to 50,176 rows in one fp32 chain: ~sqrt(n) * 2^-24 = 1.3e-5)
+                assert rel_err(dw.view(cout, k, k, cin), wr.grad.permute(0, 2, 3, 1)) < 2e-5, (wc, sp)
     Rd = Fn.det_replicas(M)
     runs = []
     for _ in range(2):
