@@ -20,8 +20,19 @@ from . import _ext
 from . import functional as Fn
 
 _DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuned")
-# HCB_TUNED_TABLE: another table file (A/B timing of two tunings on one box)
-DEFAULT_CACHE = os.environ.get("HCB_TUNED_TABLE") or os.path.join(_DIR, "mi355x.json")
+# HCB_TUNED_TABLE: another table file (A/B timing of two tunings on one box); a relative path that
+# does not exist from the working directory is taken from the repository root (tools that run the
+# bench from another directory, e.g. rocprofv3 under /tmp, would otherwise silently re-tune)
+
+
+def _table_path(v):
+    if not v or os.path.isabs(v) or os.path.exists(v):
+        return v
+    alt = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), v)
+    return alt if os.path.exists(alt) else v
+
+
+DEFAULT_CACHE = _table_path(os.environ.get("HCB_TUNED_TABLE")) or os.path.join(_DIR, "mi355x.json")
 # bump whenever the kernel config set changes: entries of another version are re-tuned
 CACHE_VERSION = 5  # 5: keys carry the filter tap count
 

@@ -1,0 +1,65 @@
+"""CPU checks of the GEMM plan tables and helpers the GPU paths rely on: the persistent plane-GEMM
+twins (conv_p3_persist.h) in the candidate sets and the step tuner's twin map, the stem's row-window
+GEMM geometry, the second-BN arguments of a fused BN-backward request, and the step-start clear."""
+import os
+import sys
+
+import torch
+
+from azure_hc_intel_tf_amd.nn.layers import StemS2D
+from azure_hc_intel_tf_amd.nn.params import ParamStore
+from azure_hc_intel_tf_amd.ops import functional as Fn
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+
+
+def test_persistent_twins_in_candidate_sets():
+    fwd = Fn.p3_candidates(200704, 256, 64)
+    cfgs = {c for c, _ in fwd}
+    assert {18, 19, 20, 21, 22} <= cfgs
+    assert all(s == 1 for c, s in fwd if c >= 18), "persistent forward twins run without split-K"
+    assert Fn._P3_TILES[18] == Fn._P3_TILES[15] and Fn._P3_TILES[19] == Fn._P3_TILES[14]
+    assert Fn._P3_TILES[22] == Fn._P3_TILES[7]
+    wg = Fn.wgrad_p3_candidates(256, 2304, 12544)
+    assert {16, 17, 18} <= {c for c, _ in wg}
+    assert Fn._WP3_TILES[16] == Fn._WP3_TILES[12] and Fn._WP3_TILES[18] == Fn._WP3_TILES[15]
+
+
+def test_step_tuner_twin_map():
+    import step_tune as st
+
+    assert st.twin_plans(("fwd3", 200704, 256, 64, 1), [15, 1]) == [[18, 1]]
+    assert st.twin_plans(("fwd3", 12544, 256, 2304, 9), [8, 1]) == []
+    assert st.twin_plans(("wgrad3", 256, 2304, 12544, 9), [12, 7]) == [[16, 7]]
+    for src, dst in st.FWD_TWIN.items():
+        assert Fn._P3_TILES[src] == Fn._P3_TILES[dst]
+    for src, dst in st.WGRAD_TWIN.items():
+        assert Fn._WP3_TILES[src] == Fn._WP3_TILES[dst]
+
+
+def test_stem_row_window_geometry():
+    """fold_spec reads the 16-channel fold as a 4x1 conv over 64-channel windows: the same K and
+    weight layout as the 4x4 form, the same 112x112 output (pr = -3 trims the windows that run past
+    a fold row)."""
+    ps = ParamStore(seed=1)
+    st = StemS2D(ps, "conv0", (224, 224, 8), 64, relu=True, need_dx=False, logical_cin=3)
+    fs = st.fold_spec
+    assert (fs.cin_pad, fs.kh, fs.kw, fs.K) == (64, 4, 1, 256)
+    Hs, Ws, C = st.fold_shape
+    assert C == 16 and fs.out_hw(Hs, Ws) == st.out_shape[:2] == (112, 112)
+
+
+def test_bnb_res_args_and_zero_bufs():
+    z = torch.zeros(2, 4, 4, 8)
+    saved = Fn.BNSaved(torch.zeros(8), torch.ones(8))
+    acc = torch.zeros(8, 2, 8)
+    plain = Fn.BNBwdFuse(z, None, saved, torch.ones(8), torch.zeros(8), 2, acc, 8)
+    assert plain.res_args() == (None, None, None, None)
+    z2, acc2 = torch.ones(2, 4, 4, 8), torch.zeros(8, 2, 8)
+    saved2 = Fn.BNSaved(torch.full((8,), 0.5), torch.full((8,), 2.0))
+    fused = Fn.BNBwdFuse(z, None, saved, torch.ones(8), torch.zeros(8), 2, acc, 8, res=(z2, saved2, acc2))
+    a = fused.res_args()
+    assert a[0] is z2 and a[1] is saved2.mean and a[2] is saved2.invstd and a[3] is acc2
+    bufs = [torch.randn(37), torch.randn(5, 3)]
+    Fn.zero_bufs(bufs)
+    assert all(float(b.abs().sum()) == 0.0 for b in bufs)

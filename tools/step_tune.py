@@ -97,6 +97,21 @@ def ab(timer, key, cur, cand, rounds):
     return statistics.median(a), statistics.median(b)
 
 
+# persistent twins (conv_p3.hip launch_p3_persist / launch_wgrad_p3): forward / data-grad tile cfg ->
+# persistent cfg (single split), weight-grad cfg -> persistent cfg (same splits)
+FWD_TWIN = {15: 18, 14: 19, 16: 20, 17: 21, 7: 22}
+WGRAD_TWIN = {12: 16, 13: 17, 15: 18}
+
+
+def twin_plans(key, cur):
+    c, sp = (cur[0], cur[1]) if isinstance(cur, list) else (cur, 1)
+    if key[0] == "fwd3" and c in FWD_TWIN:
+        return [[FWD_TWIN[c], 1]]
+    if key[0] == "wgrad3" and c in WGRAD_TWIN:
+        return [[WGRAD_TWIN[c], sp]]
+    return []
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="fp32")
@@ -108,6 +123,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--retune", action="store_true")
     ap.add_argument("--kinds", default="", help="comma-separated key kinds to step-tune (e.g. wgrad3); default all")
+    ap.add_argument("--twins", action="store_true",
+                    help="fp32: try only the persistent twin of each problem's current tile (conv_p3_persist.h)")
     ap.add_argument("--budget_s", type=float, default=900.0)
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
     a = ap.parse_args()
@@ -166,6 +183,8 @@ def main():
             break
         cur = cur_s(k)
         shortlist = [c for c in sorted(iso[k], key=iso[k].get) if c != cur][:a.cands]
+        if a.twins:
+            shortlist = [json.dumps(t) for t in twin_plans(k, json.loads(cur))]
         best_c, best_gain, best_i = None, 0.0, -1
         for c in shortlist:
             ta, tb = ab(timer, k, json.loads(cur), json.loads(c), a.rounds)
