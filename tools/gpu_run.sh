@@ -20,7 +20,8 @@
 #   readme           tools/gpu_readme_numbers.sh
 #   race             tools/race_full.py (serialised vs async bitwise race check at full size)
 #   py:SCRIPT[,args] python SCRIPT args (a probe / diagnostic)
-# env: TAG (output prefix), PYTEST_X (default -x; PYTEST_X= runs every test), PYTEST_K (-k filter)
+# env: TAG (output prefix), PYTEST_X (default -x; PYTEST_X= runs every test), PYTEST_K (-k filter),
+#      BENCH_ARGS (extra bench.py arguments of benchab, e.g. "--model inception3 --secondary none")
 # Outputs go to gpurun_out/${TAG}_<step>.*
 set -o pipefail
 mkdir -p gpurun_out
@@ -50,7 +51,7 @@ for step in "$@"; do
     benchab)
       for r in 1 2; do for v in base var; do
         if [ $v = base ]; then e=""; else e="$args"; fi
-        env $e timeout -k 10 400 python bench.py --steps 40 --warmup 10 > ${O}_ab.json 2> ${O}_ab.err || fail benchab ${O}_ab.err
+        env $e timeout -k 10 400 python bench.py --steps 40 --warmup 10 $BENCH_ARGS > ${O}_ab.json 2> ${O}_ab.err || fail benchab ${O}_ab.err
         echo "$v [$e] $(python -c "import json;d=json.load(open('${O}_ab.json'));print(d['value'], d['ms_per_step'], 'bf16', d.get('bf16_value'), d.get('bf16_ms_per_step'))")"
       done; done ;;
     convab)
