@@ -18,7 +18,7 @@ from typing import List
 
 import torch
 
-from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_op
+from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_act, empty_op
 from .base import CNNModel
 
 BN_KW = dict(eps=1e-3, decay=0.999, scale=False)
@@ -80,6 +80,7 @@ class InceptionModule:
         self._fuse_src = {id(n) for n in self.nodes
                           if n.src is not None and cons.get(id(n.src)) == 1
                           and isinstance(n.layer, ConvBN) and isinstance(n.src.layer, ConvBN) and n.src.layer.bn}
+        self._fp32_out = any(isinstance(t.layer, ConvBN) and not t.layer.bn for t in self.terminals)
         outs = [t.layer.out_shape for t in self.terminals]
         H, W = outs[0][0], outs[0][1]
         assert all(o[0] == H and o[1] == W for o in outs), f"{name}: branch spatial mismatch {outs}"
@@ -95,8 +96,9 @@ class InceptionModule:
 
     def forward(self, x):
         N = x.shape[0]
-        # the concat buffer: bf16, or on the fp32 path the Planes the next module's GEMMs read
-        out = empty_op((N,) + self.out_shape, x.device)
+        # the concat buffer: bf16, or on the fp32 path the Planes the next module's GEMMs read -- fp32
+        # when a branch ends in a conv without BN (GoogLeNet: its conv epilogue writes fp32)
+        out = (empty_act if self._fp32_out else empty_op)((N,) + self.out_shape, x.device)
         term_slot = {id(t): (off, t.layer.out_shape[2]) for t, off in zip(self.terminals, self.offsets)}
         for n in self.nodes:
             inp = x if n.src is None else n.src.out

@@ -49,6 +49,10 @@ class SequentialCNN(CNNModel):
     ('inception', cols) | ('gap',) | ('flatten',) | ('affine', N) | ('dropout',)."""
 
     specs: List[Tuple] = []
+    # --compute_dtype fp32 on the HIP kernels: bf16x6 plane GEMMs with the bias + ReLU epilogue (fp32
+    # output; each fp32 activation / gradient split into planes once per consuming GEMM pair), fp32
+    # pools, dropout, ReLU backward and bias column sums
+    F32_NATIVE_OK = True
     dropout_keep = 0.5
     default_batch_size = 32
     default_lr = 0.005

@@ -14,6 +14,7 @@ class Trivial(CNNModel):
     name = "trivial"
     default_image_size = 227
     default_batch_size = 32
+    F32_NATIVE_OK = True  # the affine layers are 1x1 plane GEMMs with the bias + ReLU epilogue
 
     def build(self):
         ps = self.ps

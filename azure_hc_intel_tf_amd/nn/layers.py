@@ -256,6 +256,10 @@ class ConvBN(Layer):
             return y
         assert residual is None or not self.relu, "conv without BN: residual add only without ReLU"
         y = out if out is not None else empty_act((N, P, Q, C), dev)
+        if Fn.planes_mode() and Fn.native(x) and not Fn.is_planes(x):
+            # fp32 path, conv + bias + ReLU layers (the zoo): the fp32 input split into the GEMM's
+            # planes once, for the forward and the weight gradient
+            x = Fn.to_planes(x)
         Fn.conv_forward(x, self.spec, self.pack.pack if Fn.native(x) else None, self.w.data, y,
                         bias=self.bias.data if self.bias is not None else None, relu=self.relu, residual=residual)
         self._saved = (x, None, y, None, False)
@@ -387,6 +391,8 @@ class ConvBN(Layer):
                 Fn.colsum(dz.reshape(-1, C), N * P * Q, C, self.bias.grad)
             if want_gres:
                 gres = dz
+            if Fn.planes_mode() and Fn.native(dz) and not Fn.is_planes(dz):
+                dz = Fn.to_planes(dz)  # one split for the data- and the weight-gradient GEMM
         self._res_bn = None
         run_wgrad(self, dz, x)
         if self.need_dx:

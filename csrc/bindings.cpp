@@ -903,17 +903,17 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
 }
 
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
-  check_act(dy, "dy");
-  check_act(y, "y");
-  check_act(dz, "dz");
+  const bool f32 = check_act_or_f32(dy, "dy");
+  same_act(dy, y, "y");
+  same_act(dy, dz, "dz");
   TORCH_CHECK(dy.numel() == y.numel() && dy.numel() == dz.numel() && dy.numel() % 8 == 0, "hcb.relu_bwd: sizes");
   TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dz.is_contiguous(), "hcb.relu_bwd: contiguous");
-  hcb::launch_relu_bwd(dy.data_ptr(), y.data_ptr(), dz.data_ptr(), dy.numel(), cur_stream());
+  hcb::launch_relu_bwd(dy.data_ptr(), y.data_ptr(), dz.data_ptr(), dy.numel(), cur_stream(), f32);
 }
 
 void dropout_fwd(const Tensor& x, const Tensor& y, const Tensor& mask, double keep, int64_t seed, const Tensor& step) {
-  check_act(x, "x");
-  check_act(y, "y");
+  const bool f32 = check_act_or_f32(x, "x");
+  same_act(x, y, "y");
   check_cuda(mask, "mask");
   check_cuda(step, "step");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && mask.is_contiguous(), "hcb.dropout_fwd: contiguous");
@@ -923,19 +923,20 @@ void dropout_fwd(const Tensor& x, const Tensor& y, const Tensor& mask, double ke
   TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() >= 1, "hcb.dropout_fwd: step int64");
   TORCH_CHECK(keep > 0.0 && keep <= 1.0, "hcb.dropout_fwd: 0 < keep <= 1");
   hcb::launch_dropout_fwd(x.data_ptr(), y.data_ptr(), mask.data_ptr<uint8_t>(), x.numel(), (float)keep, (uint64_t)seed,
-                          step.data_ptr<int64_t>(), cur_stream());
+                          step.data_ptr<int64_t>(), cur_stream(), f32);
 }
 
 void dropout_bwd(const Tensor& dy, const Tensor& mask, const Tensor& dx, double keep) {
-  check_act(dy, "dy");
-  check_act(dx, "dx");
+  const bool f32 = check_act_or_f32(dy, "dy");
+  same_act(dy, dx, "dx");
   check_cuda(mask, "mask");
   TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous() && mask.is_contiguous(), "hcb.dropout_bwd: contiguous");
   TORCH_CHECK(dy.numel() == dx.numel() && dy.numel() % 8 == 0 && mask.scalar_type() == at::kByte &&
                   mask.numel() * 8 >= dy.numel(),
               "hcb.dropout_bwd: sizes");
   TORCH_CHECK(keep > 0.0 && keep <= 1.0, "hcb.dropout_bwd: 0 < keep <= 1");
-  hcb::launch_dropout_bwd(dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), dy.numel(), (float)keep, cur_stream());
+  hcb::launch_dropout_bwd(dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), dy.numel(), (float)keep, cur_stream(),
+                          f32);
 }
 
 void scale_f32(const Tensor& x, double s) {

@@ -261,13 +261,14 @@ void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* e
                         int n_entries, int64_t max_work, hipStream_t st, int lo = 0, int64_t pstride = 0);
 // dropout on bf16 activations (n % 8 == 0): mask = 1 bit per element packed 8 per byte
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
-                        const int64_t* step, hipStream_t st);
-void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float keep, hipStream_t st);
+                        const int64_t* step, hipStream_t st, bool f32 = false);
+void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float keep, hipStream_t st,
+                        bool f32 = false);
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 void launch_add_bf16(const void* a, const void* b, void* y, int64_t n, hipStream_t st);
 void launch_scale_f32(float* x, int64_t n, float s, hipStream_t st);
-void launch_relu_bwd(const void* dy, const void* y, void* dz, int64_t n, hipStream_t st);
+void launch_relu_bwd(const void* dy, const void* y, void* dz, int64_t n, hipStream_t st, bool f32 = false);
 void launch_l2norm_sq(const float* x, int64_t n, float* out, hipStream_t st);
 
 // ---------------------------------------------------------------- data

@@ -341,14 +341,18 @@ __device__ __forceinline__ uint32_t dropout_mix32(uint64_t z) {
   return (uint32_t)((z ^ (z >> 31)) >> 32);
 }
 
-__global__ __launch_bounds__(256) void dropout_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+// T: the build's 16-bit activation type or fp32 (the zoo models' fp32 path)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ mask, int64_t n8, uint32_t thresh,
                                                           float inv_keep, uint64_t seed,
                                                           const int64_t* __restrict__ step) {
   const uint64_t base = seed * 0x9E3779B97F4A7C15ull + (uint64_t)(*step) * 0xD1B54A32D192ED03ull;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     float f[8];
-    unpack8(reinterpret_cast<const u32x4*>(x)[i], f);
+    Act8<T> v;
+    v.load(x + i * 8);
+    v.to_f(f);
     uint32_t bits = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -356,21 +360,23 @@ __global__ __launch_bounds__(256) void dropout_fwd_kernel(const uint16_t* __rest
       f[e] = keep ? f[e] * inv_keep : 0.f;
       bits |= (keep ? 1u : 0u) << e;
     }
-    reinterpret_cast<u32x4*>(y)[i] = pack8(f);
+    Act8<T>::store(y + i * 8, f);
     mask[i] = (uint8_t)bits;
   }
 }
 
-__global__ __launch_bounds__(256) void dropout_bwd_kernel(const uint16_t* __restrict__ dy,
-                                                          const uint8_t* __restrict__ mask, uint16_t* __restrict__ dx,
-                                                          int64_t n8, float inv_keep) {
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                          T* __restrict__ dx, int64_t n8, float inv_keep) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     float f[8];
-    unpack8(reinterpret_cast<const u32x4*>(dy)[i], f);
+    Act8<T> v;
+    v.load(dy + i * 8);
+    v.to_f(f);
     const uint32_t bits = mask[i];
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = ((bits >> e) & 1u) ? f[e] * inv_keep : 0.f;
-    reinterpret_cast<u32x4*>(dx)[i] = pack8(f);
+    Act8<T>::store(dx + i * 8, f);
   }
 }
 
@@ -395,16 +401,20 @@ __global__ void add_bf16_kernel(const uint16_t* a, const uint16_t* b, uint16_t* 
     reinterpret_cast<u32x4*>(y)[i] = pack8(fa);
   }
 }
-// dz = dy * (y > 0), bf16, 8 elements per thread
-__global__ void relu_bwd_kernel(const uint16_t* dy, const uint16_t* y, uint16_t* dz, int64_t n8) {
+// dz = dy * (y > 0), 8 elements per thread (16-bit or fp32)
+template <typename T>
+__global__ void relu_bwd_kernel(const T* dy, const T* y, T* dz, int64_t n8) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
        i += (int64_t)gridDim.x * blockDim.x) {
     float d[8], v[8];
-    unpack8(reinterpret_cast<const u32x4*>(dy)[i], d);
-    unpack8(reinterpret_cast<const u32x4*>(y)[i], v);
+    Act8<T> a, b;
+    a.load(dy + i * 8);
+    b.load(y + i * 8);
+    a.to_f(d);
+    b.to_f(v);
 #pragma unroll
     for (int e = 0; e < 8; ++e) d[e] = v[e] > 0.f ? d[e] : 0.f;
-    reinterpret_cast<u32x4*>(dz)[i] = pack8(d);
+    Act8<T>::store(dz + i * 8, d);
   }
 }
 
@@ -657,14 +667,23 @@ void launch_weight_pack(const float* master, uint16_t* pack, const WPackEntry* e
                        lo, (int64_t)0);
 }
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float keep, uint64_t seed,
-                        const int64_t* step, hipStream_t st) {
+                        const int64_t* step, hipStream_t st, bool f32) {
   const uint32_t thresh = keep >= 1.f ? 0xffffffffu : (uint32_t)((double)keep * 4294967296.0);
-  hipLaunchKernelGGL(dropout_fwd_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y,
-                     mask, n / 8, thresh, 1.f / keep, seed, step);
+  if (f32)
+    hipLaunchKernelGGL(dropout_fwd_kernel<float>, dim3(grid_for(n / 8)), dim3(256), 0, st, (const float*)x, (float*)y,
+                       mask, n / 8, thresh, 1.f / keep, seed, step);
+  else
+    hipLaunchKernelGGL(dropout_fwd_kernel<uint16_t>, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)x,
+                       (uint16_t*)y, mask, n / 8, thresh, 1.f / keep, seed, step);
 }
-void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float keep, hipStream_t st) {
-  hipLaunchKernelGGL(dropout_bwd_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)dy, mask,
-                     (uint16_t*)dx, n / 8, 1.f / keep);
+void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float keep, hipStream_t st,
+                        bool f32) {
+  if (f32)
+    hipLaunchKernelGGL(dropout_bwd_kernel<float>, dim3(grid_for(n / 8)), dim3(256), 0, st, (const float*)dy, mask,
+                       (float*)dx, n / 8, 1.f / keep);
+  else
+    hipLaunchKernelGGL(dropout_bwd_kernel<uint16_t>, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)dy,
+                       mask, (uint16_t*)dx, n / 8, 1.f / keep);
 }
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);
@@ -676,9 +695,13 @@ void launch_add_bf16(const void* a, const void* b, void* y, int64_t n, hipStream
   hipLaunchKernelGGL(add_bf16_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)a,
                      (const uint16_t*)b, (uint16_t*)y, n / 8);
 }
-void launch_relu_bwd(const void* dy, const void* y, void* dz, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)dy,
-                     (const uint16_t*)y, (uint16_t*)dz, n / 8);
+void launch_relu_bwd(const void* dy, const void* y, void* dz, int64_t n, hipStream_t st, bool f32) {
+  if (f32)
+    hipLaunchKernelGGL(relu_bwd_kernel<float>, dim3(grid_for(n / 8)), dim3(256), 0, st, (const float*)dy,
+                       (const float*)y, (float*)dz, n / 8);
+  else
+    hipLaunchKernelGGL(relu_bwd_kernel<uint16_t>, dim3(grid_for(n / 8)), dim3(256), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)y, (uint16_t*)dz, n / 8);
 }
 void launch_scale_f32(float* x, int64_t n, float s, hipStream_t st) {
   hipLaunchKernelGGL(scale_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, n, s);
