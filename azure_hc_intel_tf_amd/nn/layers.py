@@ -582,6 +582,10 @@ class Pool(Layer):
 
     def forward(self, x, out=None):
         N = x.shape[0]
+        if Fn.planes_mode() and Fn.native(x) and not Fn.is_planes(x) and (out is None or Fn.is_planes(out)):
+            # fp32 path after a BN-free conv (the zoo): the fp32 map split into planes here, where the
+            # consuming GEMM would split the pooled map anyway; the pool then runs on planes
+            x = Fn.to_planes(x)
         if out is not None:
             y = out
         elif Fn.is_planes(x):  # fp32 path: the pooled tensor is the next GEMM's operand
