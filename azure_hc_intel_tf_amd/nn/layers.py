@@ -88,9 +88,6 @@ FUSE_BN_BWD = True
 # projection blocks: the shortcut's BN is applied inside the block output's BN pass
 # (act(BN3(z3) + BN_sc(z_sc)) in one kernel), so the shortcut's normalised tensor is never written
 FUSE_RES_BN = True
-# ... and in the backward the shortcut BN's reduction (sum(g), sum(g * xhat_sc): it sees the same
-# gradient g as the block's last BN) rides in the data-grad epilogue that produces g
-FUSE_RES_BN_BWD = True
 # shifted single-pass BN statistics: the conv epilogue sums (v - K), (v - K)^2 with K = the
 # layer's previous batch mean, so E[x^2] - E[x]^2 does not cancel in fp32 when |mean| >> std
 # (False: K = 0, the plain single-pass form)
@@ -171,7 +168,6 @@ class ConvBN(Layer):
         self._saved = None
         self._acc = None  # (fwd acc, bwd acc, replicas) of the current step
         self._pre_reduced = False
-        self._res_bn = None  # the deferred residual BN normalised in this layer's BN pass (forward)
         self.training = True  # False: inference BN from the moving statistics (forward-only)
 
     def flops(self, batch: int) -> int:
@@ -252,7 +248,6 @@ class ConvBN(Layer):
                 saved = Fn.bn_forward(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data,
                                       self.decay, self.eps, y, self.relu, residual=residual)
             self._saved = (x, z, y, saved, residual is not None)
-            self._res_bn = residual_bn
             return y
         assert residual is None or not self.relu, "conv without BN: residual add only without ReLU"
         y = out if out is not None else empty_act((N, P, Q, C), dev)
@@ -335,16 +330,7 @@ class ConvBN(Layer):
         mode = (1 if had_res else 2) if self.relu else 0
         self._pre_reduced = True
         _, acc_b, R = self._acc if self._acc is not None else (None, self.acc_b.data, STAT_R)
-        res = None
-        rb = self._res_bn
-        if FUSE_RES_BN_BWD and rb is not None and rb._saved is not None and rb._acc is not None \
-                and rb._acc[2] == R and not rb._pre_reduced:
-            _, z2, _, saved2, _ = rb._saved
-            if z2.dtype == z.dtype and z2.shape == z.shape and z2.is_contiguous() and z.is_contiguous():
-                # the shortcut BN sees the same g (relu(bn3 + bn_sc)): its reduction rides along
-                res = (z2, saved2, rb._acc[1])
-                rb._pre_reduced = True
-        return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, acc_b, R, res=res)
+        return Fn.BNBwdFuse(z, y, saved, self.gamma.data, self.beta.data, mode, acc_b, R)
 
     def backward(self, dy, dx=None, accumulate: bool = False, want_gres: bool = False, dx_bn=None):
         """Returns (dx or None, gres or None). gres = gradient w.r.t. the residual input.
@@ -393,7 +379,6 @@ class ConvBN(Layer):
                 gres = dz
             if Fn.planes_mode() and Fn.native(dz) and not Fn.is_planes(dz):
                 dz = Fn.to_planes(dz)  # one split for the data- and the weight-gradient GEMM
-        self._res_bn = None
         run_wgrad(self, dz, x)
         if self.need_dx:
             H, W, Cin = self.in_shape
@@ -408,7 +393,6 @@ class ConvBN(Layer):
 
     def clear(self):
         self._saved = None
-        self._res_bn = None
         self._pre_reduced = False
 
 

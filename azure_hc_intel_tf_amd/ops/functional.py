@@ -659,20 +659,9 @@ class BNBwdFuse:
     g = dy * relu_mask; on the GPU sum(g) and sum(g * xhat) are added to ``acc`` replicas, so
     the BN backward only runs its apply pass (``bn_backward_acc(..., pre_reduced=True)``)."""
 
-    def __init__(self, z, y, saved: "BNSaved", gamma, beta, mode: int, acc, R: int, res=None):
+    def __init__(self, z, y, saved: "BNSaved", gamma, beta, mode: int, acc, R: int):
         self.z, self.y, self.saved, self.gamma, self.beta = z, y, saved, gamma, beta
         self.mode, self.acc, self.R = mode, acc, R
-        # res = (z2, saved2, acc2): a second BN fed the same g (a projection shortcut's BN beside the
-        # block's last BN: ResNet v1 relu(bn3(z3) + bn_sc(z_sc))); its sum(g), sum(g * xhat2) are
-        # reduced by the same epilogue (ConvParams::bnb2_*), so its backward is apply-only too
-        self.res = res
-
-    def res_args(self):
-        """Trailing (z2, mean2, invstd2, acc2) arguments of the hcb *_bnb ops."""
-        if self.res is None:
-            return (None, None, None, None)
-        z2, saved2, acc2 = self.res
-        return (z2, saved2.mean, saved2.invstd, acc2)
 
     def gate_cpu(self, g):
         """CPU semantics of the fused epilogue's gating (the reductions stay in bn_backward)."""
@@ -769,8 +758,7 @@ def dgrad_phase(dz, spec: ConvSpec, wtr, dx, accumulate: bool, phase, cfg=None, 
     if bnb is not None:
         _ext.ops().conv_igemm_bnb(dz, sub, dx, dx if accumulate else None, geom, cfg, bnb.z,
                                   bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
-                                  bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode,
-                                  *bnb.res_args())
+                                  bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
     else:
         _ext.ops().conv_igemm(dz, sub, dx, dx if accumulate else None, None, None, geom, cfg, None, None)
 
@@ -783,7 +771,7 @@ def _p3_dgrad_launch(dz: "Planes", w, w_lo, dx, accumulate: bool, geom, cfg: int
         return
     _ext.ops().conv_p3_bnb(dz.t, w, w_lo, dx, dx if accumulate else None, geom, cfg, bnb.z,
                            _pl(bnb.y) if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean, bnb.saved.invstd,
-                           bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode, *bnb.res_args())
+                           bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
 
 
 def uses_dgrad_phases(spec: ConvSpec, H: int, W: int) -> bool:
@@ -836,8 +824,7 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
         if bnb is not None:
             _ext.ops().conv_igemm_bnb(dz, wtr, dx, dx if accumulate else None, geom, cfg, bnb.z,
                                       bnb.y if bnb.mode == 1 else None, ld(bnb.z), bnb.saved.mean,
-                                      bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode,
-                                      *bnb.res_args())
+                                      bnb.saved.invstd, bnb.gamma, bnb.beta, bnb.acc, bnb.R, bnb.mode)
         else:
             _ext.ops().conv_igemm(dz, wtr, dx, dx if accumulate else None, None, None, geom, cfg, None, None)
         return dx

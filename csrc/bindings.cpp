@@ -267,34 +267,8 @@ void set_bnb(hcb::ConvParams& p, const Tensor& z, const c10::optional<Tensor>& y
   p.bnb_acc = acc.data_ptr<float>();
   p.bnb_mode = (int)mode;
   p.bnb_R = (int)R;
-  p.bnb2_z = nullptr;
-  p.bnb2_mean = p.bnb2_invstd = nullptr;
-  p.bnb2_acc = nullptr;
 }
 
-// the second BN's reduction on the same gradient (ConvParams::bnb2_*): z2 like z, acc2 like acc
-void set_bnb2(hcb::ConvParams& p, const c10::optional<Tensor>& z2, const c10::optional<Tensor>& mean2,
-              const c10::optional<Tensor>& invstd2, const c10::optional<Tensor>& acc2, bool f32) {
-  if (!z2.has_value()) return;
-  TORCH_CHECK(mean2.has_value() && invstd2.has_value() && acc2.has_value(), "hcb: z2 needs mean2, invstd2, acc2");
-  const int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
-  if (f32)
-    check_f32(*z2, "z2");
-  else
-    check_act(*z2, "z2");
-  check_range(*z2, ((rows - 1) * p.bnb_ld + ((p.Nout + 7) / 8) * 8) * (f32 ? 4 : 2), "z2");
-  check_align16(z2->data_ptr(), "z2");
-  for (const Tensor* t : {&*mean2, &*invstd2}) {
-    check_f32(*t, "bn2 param");
-    TORCH_CHECK(t->numel() >= p.Nout, "hcb: second-BN per-channel tensor too small");
-  }
-  check_f32(*acc2, "acc2");
-  TORCH_CHECK(acc2->numel() >= (int64_t)p.bnb_R * 2 * p.Nout, "hcb: acc2 too small");
-  p.bnb2_z = z2->data_ptr();
-  p.bnb2_mean = mean2->data_ptr<float>();
-  p.bnb2_invstd = invstd2->data_ptr<float>();
-  p.bnb2_acc = acc2->data_ptr<float>();
-}
 
 // data-grad conv whose output is the dy of a BN layer: the epilogue gates it with the
 // layer's ReLU mask (mode 1: y > 0, 2: recomputed from z, 0: none), stores g and adds
@@ -302,12 +276,9 @@ void set_bnb2(hcb::ConvParams& p, const c10::optional<Tensor>& z2, const c10::op
 void conv_igemm_bnb(const Tensor& x, const Tensor& w, const Tensor& y, const c10::optional<Tensor>& yres,
                     at::IntArrayRef g, int64_t cfg, const Tensor& z, const c10::optional<Tensor>& yact,
                     int64_t ld, const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
-                    const Tensor& acc, int64_t R, int64_t mode, const c10::optional<Tensor>& z2,
-                    const c10::optional<Tensor>& mean2, const c10::optional<Tensor>& invstd2,
-                    const c10::optional<Tensor>& acc2) {
+                    const Tensor& acc, int64_t R, int64_t mode) {
   hcb::ConvParams p = conv_params(x, w, y, yres, c10::nullopt, c10::nullopt, g, cfg);
   set_bnb(p, z, yact, ld, mean, invstd, gamma, beta, acc, R, mode, false);
-  set_bnb2(p, z2, mean2, invstd2, acc2, false);
   hcb::launch_conv_igemm(p, (int)cfg, cur_stream());
 }
 
@@ -1138,12 +1109,9 @@ void conv_p3(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor&
 void conv_p3_bnb(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor& y,
                  const c10::optional<Tensor>& yres, at::IntArrayRef g, int64_t cfg, const Tensor& z,
                  const c10::optional<Tensor>& yact, int64_t ld, const Tensor& mean, const Tensor& invstd,
-                 const Tensor& gamma, const Tensor& beta, const Tensor& acc, int64_t R, int64_t mode,
-                 const c10::optional<Tensor>& z2, const c10::optional<Tensor>& mean2,
-                 const c10::optional<Tensor>& invstd2, const c10::optional<Tensor>& acc2) {
+                 const Tensor& gamma, const Tensor& beta, const Tensor& acc, int64_t R, int64_t mode) {
   hcb::ConvParams p = p3_params(x, w, w_lo, y, yres, c10::nullopt, c10::nullopt, g, cfg, c10::nullopt);
   set_bnb(p, z, yact, ld, mean, invstd, gamma, beta, acc, R, mode, true);
-  set_bnb2(p, z2, mean2, invstd2, acc2, true);
   hcb::launch_conv_p3(p, (int)cfg, cur_stream());
 }
 
@@ -1172,6 +1140,8 @@ void conv_wgrad_p3(const Tensor& dy, const Tensor& x, const Tensor& dw, at::IntA
   check_range(x, 2 * xps * 2 + xb, "x planes");
   check_range(dy, 2 * dps * 2 + yb, "dy planes");
   check_range(dw, (int64_t)p.Nout * p.K * 4, "dw");
+  TORCH_CHECK(cfg < 16 || (int64_t)p.Nout * p.K * 4 < (1ll << 31),
+              "hcb.conv_wgrad_p3: the persistent configs address dW through a 32-bit buffer offset");
   const int nkt = (p.M + 63) / 64;
   const int per = (nkt + (int)splits - 1) / (int)splits;
   p.ksteps_per_split = per;
@@ -1230,7 +1200,7 @@ void set_deterministic(bool on) { hcb::set_deterministic(on); }
 
 HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None, Tensor? w_lo=None) -> ()");
-  m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode, Tensor? z2=None, Tensor? mean2=None, Tensor? invstd2=None, Tensor(c!)? acc2=None) -> ()");
+  m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
@@ -1278,7 +1248,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("stem_wgrad_unfold(Tensor dwp, Tensor(a!) dw) -> ()");
   m.def("conv_p3(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, Tensor? bias, Tensor(b!)? stats, int[] geom, int cfg, Tensor? stats_shift=None) -> ()");
   m.def("conv_wgrad_p3(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
-  m.def("conv_p3_bnb(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode, Tensor? z2=None, Tensor? mean2=None, Tensor? invstd2=None, Tensor(c!)? acc2=None) -> ()");
+  m.def("conv_p3_bnb(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("split_planes(Tensor x, int ldx, int rows, int C, Tensor(a!) out, int ldo) -> ()");
   m.def("merge_planes(Tensor x, int ldi, int rows, int C, Tensor(a!) y, int ldy) -> ()");
   m.def("gap_fwd_p3(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");

@@ -53,7 +53,6 @@ struct EpiPrefetch {
   static constexpr int CH = BNB ? (ITER < CHMAX ? ITER : CHMAX) : 1;
   u32x4 pr[CH], pz[CH], py[CH];
   u32x4 pr2[F32 ? CH : 1], pz2[F32 ? CH : 1];
-  u32x4 pq[BNB ? CH : 1], pq2[BNB && F32 ? CH : 1];  // z2 of the second BN (ConvParams::bnb2_z)
   // forward GEMMs: the BN statistic shift of each of the lane's accumulator columns, loaded
   // before the main loop so the epilogue does not wait on it
   static constexpr int NKC = BNB ? 1 : TN / 16;
@@ -82,17 +81,10 @@ struct EpiPrefetch {
           const u32x4* z = reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(p.bnb_z) + o * p.bnb_ld + col);
           pz[k] = z[0];
           pz2[k] = z[1];
-          if (BNB && p.bnb2_z != nullptr) {
-            const u32x4* q = reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(p.bnb2_z) + o * p.bnb_ld + col);
-            pq[k] = q[0];
-            pq2[k] = q[1];
-          }
         } else {
           if (p.beta)
             pr[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.yres) + o * p.ldy + col);
           pz[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_z) + o * p.bnb_ld + col);
-          if (BNB && p.bnb2_z != nullptr)
-            pq[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb2_z) + o * p.bnb_ld + col);
         }
         if (p.bnb_mode == 1)
           py[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.bnb_y) + o * p.bnb_ld + col);
@@ -354,14 +346,9 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
   } else {
     // 16-bit (fp32 on the F32 path) output, no bias / relu (checked on the host)
     float bmu[8], bis[8], bsc[8], bsh[8], bs1[8], bs2[8];
-    const bool two = p.bnb2_z != nullptr;  // the second BN's sum(g * xhat2) (bs3)
-    float qmu[8], qis[8], bs3[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const bool okc = col + e < p.Nout;
-      qmu[e] = two && okc ? p.bnb2_mean[col + e] : 0.f;
-      qis[e] = two && okc ? p.bnb2_invstd[col + e] : 0.f;
-      bs3[e] = 0.f;
       if (bnb_params != nullptr) {
         const float4 q = reinterpret_cast<const float4*>(bnb_params)[cs * 8 + e];  // zeros past Nout
         bmu[e] = q.x;
@@ -425,15 +412,6 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
           bs1[e] += v[e];
           bs2[e] += v[e] * ((zf[e] - bmu[e]) * bis[e]);
         }
-        if (two) {
-          float qf[8];
-          if constexpr (F32)
-            f32x8(pre.pq[k], pre.pq2[k], qf);
-          else
-            unpack8(pre.pq[k], qf);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bs3[e] += v[e] * ((qf[e] - qmu[e]) * qis[e]);
-        }
         if constexpr (F32) {
           f32x4* yo = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + orow * p.ldy + col);
           yo[0] = f32x4{v[0], v[1], v[2], v[3]};
@@ -444,36 +422,31 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
       }
     }
     // threads sharing a column segment: LDS partials [NT/SEGS][BN] (x2), column sums, atomics
-    // (a second pass with the second BN's pair: sum(g) again and sum(g * xhat2))
     constexpr int PR = NT / SEGS;
     static_assert(2 * PR * BN <= BM * LDC, "partials fit in the staging buffer");
     float* part = Cs;
+    __syncthreads();  // all Cs reads of the store pass are done
     const int r = tid / SEGS;
-    auto reduce_pair = [&](const float* sa, const float* sb, float* acc) {
-      __syncthreads();  // all earlier reads of the staging buffer are done
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        part[r * BN + cs * 8 + e] = sa[e];
-        part[PR * BN + r * BN + cs * 8 + e] = sb[e];
-      }
-      __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
-        float a = 0.f, b = 0.f;
+    for (int e = 0; e < 8; ++e) {
+      part[r * BN + cs * 8 + e] = bs1[e];
+      part[PR * BN + r * BN + cs * 8 + e] = bs2[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float a = 0.f, b = 0.f;
 #pragma unroll 4
-        for (int rr = 0; rr < PR; ++rr) {
-          a += part[rr * BN + c];
-          b += part[PR * BN + rr * BN + c];
-        }
-        const int gc = n0 + c;
-        if (gc < p.Nout) {
-          float* dst = acc + (size_t)(tm % p.bnb_R) * 2 * p.Nout;
-          atomicAdd(dst + gc, a);
-          atomicAdd(dst + p.Nout + gc, b);
-        }
+      for (int rr = 0; rr < PR; ++rr) {
+        a += part[rr * BN + c];
+        b += part[PR * BN + rr * BN + c];
       }
-    };
-    reduce_pair(bs1, bs2, p.bnb_acc);
-    if (two) reduce_pair(bs1, bs3, p.bnb2_acc);
+      const int gc = n0 + c;
+      if (gc < p.Nout) {
+        float* dst = p.bnb_acc + (size_t)(tm % p.bnb_R) * 2 * p.Nout;
+        atomicAdd(dst + gc, a);
+        atomicAdd(dst + p.Nout + gc, b);
+      }
+    }
   }
 }
 

@@ -63,12 +63,6 @@ struct ConvParams {
   const float *bnb_mean, *bnb_invstd, *bnb_gamma, *bnb_beta;
   float* bnb_acc;
   int bnb_mode, bnb_R, bnb_ld;
-  // A second BN on the same gradient (ResNet projection blocks: the shortcut's BN, whose output is
-  // added to the block's last BN before the ReLU, sees the same g): when bnb2_z is set the epilogue
-  // also accumulates sum(g) and sum(g * xhat2) into bnb2_acc ([bnb_R][2][Nout]); z2 rows like z.
-  const void* bnb2_z;
-  const float *bnb2_mean, *bnb2_invstd;
-  float* bnb2_acc;
   // In-launch split-K (LDS-DMA kernels): `splits` blocks per output tile each reduce a
   // contiguous k-step range; all but the last arriver park fp32 partials in ws slabs
   // [tile][split][tile elems], the last one (agent-scope ticket in cnt[tile], self-resetting)

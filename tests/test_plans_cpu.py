@@ -1,6 +1,6 @@
 """CPU checks of the GEMM plan tables and helpers the GPU paths rely on: the persistent plane-GEMM
 twins (conv_p3_persist.h) in the candidate sets and the step tuner's twin map, the stem's row-window
-GEMM geometry, the second-BN arguments of a fused BN-backward request, and the step-start clear."""
+GEMM geometry and the step-start clear."""
 import os
 import sys
 
@@ -49,17 +49,7 @@ def test_stem_row_window_geometry():
     assert C == 16 and fs.out_hw(Hs, Ws) == st.out_shape[:2] == (112, 112)
 
 
-def test_bnb_res_args_and_zero_bufs():
-    z = torch.zeros(2, 4, 4, 8)
-    saved = Fn.BNSaved(torch.zeros(8), torch.ones(8))
-    acc = torch.zeros(8, 2, 8)
-    plain = Fn.BNBwdFuse(z, None, saved, torch.ones(8), torch.zeros(8), 2, acc, 8)
-    assert plain.res_args() == (None, None, None, None)
-    z2, acc2 = torch.ones(2, 4, 4, 8), torch.zeros(8, 2, 8)
-    saved2 = Fn.BNSaved(torch.full((8,), 0.5), torch.full((8,), 2.0))
-    fused = Fn.BNBwdFuse(z, None, saved, torch.ones(8), torch.zeros(8), 2, acc, 8, res=(z2, saved2, acc2))
-    a = fused.res_args()
-    assert a[0] is z2 and a[1] is saved2.mean and a[2] is saved2.invstd and a[3] is acc2
+def test_zero_bufs():
     bufs = [torch.randn(37), torch.randn(5, 3)]
     Fn.zero_bufs(bufs)
     assert all(float(b.abs().sum()) == 0.0 for b in bufs)

@@ -18,6 +18,8 @@ run c2_resnet50_bs256 400 python bench.py --batch_size 256 --compute_dtype bf16 
 run c2_resnet50_bs256_fp32 400 python bench.py --batch_size 256 --compute_dtype fp32 --secondary none --steps 10 --warmup 3
 run c4_inception3_bs64 400 python bench.py --model inception3 --batch_size 64 --compute_dtype bf16 --secondary none \
     --steps 20 --warmup 5
+run c4_inception3_bs64_fp32 400 python bench.py --model inception3 --batch_size 64 --compute_dtype fp32 --secondary none \
+    --steps 20 --warmup 5
 run c5_resnet152_fp16_bs128 600 python tf_cnn_benchmarks.py --model=resnet152 --batch_size=128 --num_batches=30 \
     --num_warmup_batches=10 --display_every=10 --optimizer=momentum --variable_update=horovod --use_fp16 \
     --fp16_enable_auto_loss_scale --device=gpu
@@ -25,5 +27,9 @@ run miopen_eager_resnet50_bs64 400 python tools/torch_resnet_baseline.py --batch
 for spec in ${MODELS:-resnet101:64 resnet50_v1.5:64 resnet50_v2:64 vgg16:64 googlenet:128 alexnet:512 overfeat:128}; do
   IFS=: read m b <<< "$spec"
   run zoo_$m 400 python bench.py --model $m --batch_size $b --compute_dtype bf16 --secondary none --steps 20 --warmup 5
+done
+for spec in ${FP32_MODELS:-vgg16:64 googlenet:128 alexnet:512}; do  # the zoo at fp32 on the HIP kernels
+  IFS=: read m b <<< "$spec"
+  run zoo32_$m 400 python bench.py --model $m --batch_size $b --compute_dtype fp32 --secondary none --steps 20 --warmup 5
 done
 echo "readme numbers done" >> $OUT
