@@ -382,9 +382,8 @@ class ConvBN(Layer):
         run_wgrad(self, dz, x)
         if self.need_dx:
             H, W, Cin = self.in_shape
-            if dx is None:
-                strided_1x1 = (self.spec.sh > 1 or self.spec.sw > 1) and self.spec.kh == 1 and self.spec.kw == 1
-                dx = empty_act((N, H, W, Cin), dev, zero=strided_1x1 and Fn.native(dz))
+            if dx is None:  # (a strided 1x1 data gradient writes its stride cells' gaps itself)
+                dx = empty_act((N, H, W, Cin), dev)
                 accumulate = False
             bnb = dx_bn.bwd_fuse_request() if dx_bn is not None else None
             Fn.conv_dgrad(dz, self.spec, self.pack.tr, self.w.data, dx, accumulate, bnb=bnb)

@@ -673,6 +673,10 @@ class BNBwdFuse:
         return g
 
 
+# strided 1x1 data gradients zero their stride cells' gaps in the GEMM epilogue (False: a separate
+# zero-fill of dx first; the A/B switch HCB_REMAP_FILL=0)
+REMAP_FILL = os.environ.get("HCB_REMAP_FILL", "1") != "0"
+
 # strided k x k data gradients as sh*sw stride-phase GEMMs (module switch, False: one GEMM over the
 # zero-dilated dz, which spends (sh*sw - 1)/(sh*sw) of its MFMA work on the inserted zeros)
 DGRAD_PHASES = True
@@ -780,9 +784,10 @@ def uses_dgrad_phases(spec: ConvSpec, H: int, W: int) -> bool:
 
 
 def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None, bnb: "BNBwdFuse" = None):
-    """dx[N,H,W,cin] (+)= conv_transpose(dz, W). dx must be zero-filled by the caller when
-    not accumulating and the conv is a strided 1x1 (remap path leaves gaps). With ``bnb`` the
-    result is gated by the consuming BN layer's ReLU mask and its backward sums are fused."""
+    """dx[N,H,W,cin] (+)= conv_transpose(dz, W). A strided 1x1 writes every pixel of dx when not
+    accumulating: its GEMM rows (one per dz pixel) also zero the rest of their stride cell (remap
+    2, igemm_epilogue.h epi_fill_cell), so dx needs no zero-fill. With ``bnb`` the result is gated
+    by the consuming BN layer's ReLU mask and its backward sums are fused."""
     N, P, Q, _ = dz.shape
     _, H, W, _ = dx.shape
     if native(dz):
@@ -799,8 +804,11 @@ def conv_dgrad(dz, spec: ConvSpec, wtr, w_master, dx, accumulate: bool, cfg=None
         if strided and spec.kh == 1 and spec.kw == 1 and spec.pt == 0 and spec.pl == 0:
             # 1x1 strided: dense GEMM over dz pixels, scatter rows to (p*sh, q*sw)
             M = N * P * Q
+            fill = REMAP_FILL and not accumulate and P * spec.sh >= H and Q * spec.sw >= W
+            if not accumulate and not fill:
+                dx.zero_()  # cells that do not tile dx: pixels past the last cell stay 0
             geom = [N, P, Q, Cdz, ld(dz), P, Q, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, spec.cin_pad, K, Kpad,
-                    ld(dx), 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, _f32o(dx)]
+                    ld(dx), 2 if fill else 1, H, W, spec.sh, spec.sw, 1 if accumulate else 0, _f32o(dx)]
         else:
             M = N * H * W
             pt = spec.dh * (spec.kh - 1) - spec.pt

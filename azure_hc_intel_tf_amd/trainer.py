@@ -113,6 +113,7 @@ class Trainer:
         if self.loss_scaling:
             h += [0.0, S, 0.0, float(loss_scale_interval)]
         self.hyper = torch.tensor(h, dtype=torch.float32, device=self.dev)
+        self._lr_dev = None  # the learning rate last written to hyper[0]
         self.row_loss = torch.zeros(batch_size, dtype=torch.float32, device=self.dev)
         self.dlogits = torch.zeros((batch_size, ld), dtype=model.act_dtype, device=self.dev)
         # 16-bit dlogits on the HIP path: the loss kernel also writes them unrounded, the
@@ -388,7 +389,10 @@ class Trainer:
             L.WGRAD_SIDE["keep"].clear()
 
     def _step_body(self, images, labels):
-        self.hyper[0:1].fill_(float(self.lr_fn(self.steps_done)))  # host write, outside the graph
+        lr = float(self.lr_fn(self.steps_done))
+        if lr != self._lr_dev:  # host write outside the graph, only when the schedule moves
+            self.hyper[0:1].fill_(lr)
+            self._lr_dev = lr
         if not self.use_graph:
             self._eager_step(images, labels)
         else:

@@ -136,9 +136,13 @@ hcb::ConvParams conv_params(const Tensor& x, const Tensor& w, const Tensor& y, c
   check_range(x, xb, "x");
   check_range(w, wb, "w");
   int64_t rows = p.remap ? (int64_t)p.N * p.OH * p.OW : (int64_t)p.M;
+  TORCH_CHECK(p.remap >= 0 && p.remap <= 2, "hcb.conv_igemm: remap is 0, 1 or 2");
   if (p.remap) {
     TORCH_CHECK(p.oh0 >= 0 && p.ow0 >= 0 && (p.P - 1) * p.osh + p.oh0 < p.OH && (p.Q - 1) * p.osw + p.ow0 < p.OW,
                 "hcb.conv_igemm: remap out of range");
+    // remap 2 zeroes each GEMM pixel's whole stride cell: the cells must cover the output
+    TORCH_CHECK(p.remap != 2 || (!p.beta && p.oh0 == 0 && p.ow0 == 0 && p.P * p.osh >= p.OH && p.Q * p.osw >= p.OW),
+                "hcb.conv_igemm: remap 2 needs cells covering the output and no beta");
   } else {
     TORCH_CHECK(p.oh0 == 0 && p.ow0 == 0, "hcb.conv_igemm: a remap origin needs remap");
   }

@@ -37,6 +37,32 @@ __device__ __forceinline__ size_t epi_out_row(const ConvParams& p, int m) {
   return ((size_t)n * p.OH + (size_t)pp * p.osh + p.oh0) * p.OW + (size_t)qq * p.osw + p.ow0;
 }
 
+// remap == 2: a strided 1x1 data gradient that writes ALL of dx -- GEMM row m = (n, p, q) also
+// stores zeros to the other pixels of its stride cell, (p*osh + a, q*osw + b) for (a, b) != (0, 0)
+// (the host checks that the cells tile the output), so dx needs no zero-fill pass of its own
+template <bool F32OUT>
+__device__ __forceinline__ void epi_fill_cell(const ConvParams& p, int m, int col) {
+  const int PQ = p.P * p.Q;
+  const int n = m / PQ, r = m - n * PQ;
+  const int pp = r / p.Q, qq = r - pp * p.Q;
+  for (int a = 0; a < p.osh; ++a) {
+    const int h = pp * p.osh + a;
+    if (h >= p.OH) break;
+    for (int b = (a == 0 ? 1 : 0); b < p.osw; ++b) {
+      const int w = qq * p.osw + b;
+      if (w >= p.OW) break;
+      const size_t o = ((size_t)n * p.OH + h) * p.OW + w;
+      if constexpr (F32OUT) {
+        f32x4* yo = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.y) + o * p.ldy + col);
+        yo[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        yo[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + o * p.ldy + col) = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+}
+
 // Register prefetch of the fused BN-backward epilogue operands (z, y and the beta source) for
 // one chunk of CH output segments per thread. A kernel with a short main loop issues the first
 // chunk BEFORE its main loop, so these loads share one memory latency with the A/B tiles
@@ -305,6 +331,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
           v = pack8(f);
         }
         *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + out_row(m) * p.ldy + col) = v;
+        if (p.remap == 2) epi_fill_cell<false>(p, m, col);
       }
       return;
     }
@@ -332,6 +359,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
         }
         reinterpret_cast<f32x4*>(yo)[0] = f32x4{v[0], v[1], v[2], v[3]};
         reinterpret_cast<f32x4*>(yo)[1] = f32x4{v[4], v[5], v[6], v[7]};
+        if (p.remap == 2) epi_fill_cell<true>(p, m, col);
       } else {
         uint16_t* yo = reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col;
         if (p.beta) {
@@ -341,6 +369,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
           for (int e = 0; e < 8; ++e) v[e] += o[e];
         }
         *reinterpret_cast<u32x4*>(yo) = pack8(v);
+        if (p.remap == 2) epi_fill_cell<false>(p, m, col);
       }
     }
   } else {
@@ -419,6 +448,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams& p, f32x4 (&acc)
         } else {
           *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.y) + orow * p.ldy + col) = pack8(v);
         }
+        if (p.remap == 2) epi_fill_cell<F32>(p, m, col);
       }
     }
     // threads sharing a column segment: LDS partials [NT/SEGS][BN] (x2), column sums, atomics

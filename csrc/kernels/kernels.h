@@ -47,7 +47,7 @@ struct ConvParams {
   int stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, idil_h, idil_w;
   int Nout, K, Kpad, ldy;
   int M;
-  int remap, OH, OW, osh, osw;
+  int remap, OH, OW, osh, osw;  // remap 2: also zero the rest of each stride cell (igemm_epilogue.h)
   int oh0, ow0;  // remap origin: GEMM pixel (p, q) -> output pixel (p*osh + oh0, q*osw + ow0)
   int beta, out_f32;
   int relu;     // fused ReLU in the epilogue (affine layers without BN)

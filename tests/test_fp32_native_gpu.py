@@ -76,7 +76,7 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     xr = xd.clone().requires_grad_(True)
     wr = wd.clone().requires_grad_(True)
     torch.nn.functional.conv2d(xr, wr, stride=s, padding=pad).backward(dz.double().cpu().permute(0, 3, 1, 2))
-    dx = torch.zeros(N, H, H, cin, dtype=torch.float32, device=DEV)
+    dx = torch.full((N, H, H, cin), float("nan"), dtype=torch.float32, device=DEV)  # every pixel written
     Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, False, cfg=cfg)
     assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 3e-6
     if isinstance(cfg, tuple):  # split-K case: the weight-gradient configs once
@@ -86,6 +86,39 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
         dw = torch.zeros(cout, spec.K, device=DEV)
         Fn.conv_wgrad(dz, x, spec, dw, cfg=wcfg)
         assert rel_err(dw.view(cout, k, k, cin), wr.grad.permute(0, 2, 3, 1)) < 3e-6, wcfg
+
+
+@pytest.mark.parametrize("H", [13, 14])
+@pytest.mark.parametrize("f32", [True, False], ids=["fp32", "bf16"])
+def test_strided_1x1_dgrad_zeroes_its_cells(H, f32):
+    """A strided 1x1 data gradient (remap 2) writes ALL of dx: the GEMM row of dz pixel (p, q) also
+    zeroes the other pixels of its 2x2 stride cell (odd H: the last cell is cut by the border), so
+    the step allocates dx without a fill kernel. dx starts as NaN."""
+    if f32:
+        set_gpu_compute_dtype(torch.float32)
+        Fn.set_f32_native(True)
+    try:
+        spec, p, pk, ps = _conv(64, 128, 1, 2, 0)
+        N = 3
+        P, Q = spec.out_hw(H, H)
+        torch.manual_seed(6)
+        dz = torch.randn(N, P, Q, 128, device=DEV)
+        dt = torch.float32 if f32 else torch.bfloat16
+        dz = dz.to(dt)
+        dx = torch.full((N, H, H, 64), float("nan"), dtype=dt, device=DEV)
+        Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, False)
+        wd = p.data.double().cpu().permute(0, 3, 1, 2)
+        if not f32:
+            wd = wd.to(torch.bfloat16).double()
+        xr = torch.zeros(N, 64, H, H, dtype=torch.float64, requires_grad=True)
+        torch.nn.functional.conv2d(xr, wd, stride=2).backward(dz.double().cpu().permute(0, 3, 1, 2))
+        ref = xr.grad.permute(0, 2, 3, 1)
+        assert not torch.isnan(dx).any()
+        assert float(dx[:, 1::2].abs().max()) == 0.0 and float(dx[:, :, 1::2].abs().max()) == 0.0
+        assert rel_err(dx, ref) < (3e-6 if f32 else 1e-2)
+    finally:
+        Fn.set_f32_native(False)
+        set_gpu_compute_dtype(torch.bfloat16)
 
 
 @pytest.mark.parametrize("cfg", [18, 19, 20, 21, 22])

@@ -165,8 +165,8 @@ def test_conv_dgrad(case, accumulate):
     P, Q = spec.out_hw(H, H)
     dz = bf(torch.randn(N, P, Q, cout, device=DEV))
     base = bf(torch.randn(N, H, H, cin, device=DEV))
-    strided_1x1 = s > 1 and kh == 1 and kw == 1
-    dx = base.clone() if accumulate else (torch.zeros_like(base) if strided_1x1 else torch.empty_like(base))
+    # not accumulating: every pixel written (a strided 1x1 zeroes its stride cells' gaps itself)
+    dx = base.clone() if accumulate else torch.full_like(base, float("nan"))
     Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate)
     ref = torch.empty(N, H, H, cin)
     Fn.conv_dgrad(dz.float().cpu(), spec, None, bf(p.data).float().cpu(), ref, False)
@@ -205,7 +205,7 @@ def test_conv_dgrad_fused_bn_backward(case, mode, accumulate, cfg):
         keep = torch.zeros(1, H, H, 1, dtype=torch.bool, device=DEV)
         keep[:, ::s, ::s] = True
         base = base * keep
-    dx = base.clone() if accumulate else (torch.zeros_like(base) if strided_1x1 else torch.empty_like(base))
+    dx = base.clone() if accumulate else torch.full_like(base, float("nan"))
     bnb = Fn.BNBwdFuse(z, yact, saved, gamma, beta, mode, acc, R)
     Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate, cfg=cfg, bnb=bnb)
     ref = torch.empty(N, H, H, cin)

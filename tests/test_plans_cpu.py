@@ -53,3 +53,20 @@ def test_zero_bufs():
     bufs = [torch.randn(37), torch.randn(5, 3)]
     Fn.zero_bufs(bufs)
     assert all(float(b.abs().sum()) == 0.0 for b in bufs)
+
+
+def test_learning_rate_written_only_when_it_moves():
+    """The step writes hyper[0] (the device-side learning rate) only when the schedule changes it:
+    a constant schedule adds no fill kernel between graph replays."""
+    from azure_hc_intel_tf_amd.models import create_model
+    from azure_hc_intel_tf_amd.trainer import Trainer, synthetic_batch
+
+    m = create_model("trivial", image_size=16, device="cpu", seed=5)
+    t = Trainer(m, 4, lambda s: 0.1 if s < 2 else 0.05)
+    img, lab = synthetic_batch(m, 4, seed=1)
+    seen = []
+    for _ in range(4):
+        t.step(img, lab)
+        seen.append(round(float(t.hyper[0]), 6))
+    assert seen == [0.1, 0.1, 0.05, 0.05]
+    assert t._lr_dev == 0.05

@@ -5,7 +5,7 @@ import argparse
 import csv
 import re
 
-CLASSES = [("conv fwd/dgrad (igemm)", r"conv_igemm"), ("conv wgrad", r"wgrad"), ("stem", r"stem"),
+CLASSES = [("conv fwd/dgrad (igemm)", r"conv_igemm|conv_p3_persist|conv3x3"), ("conv wgrad", r"wgrad"), ("stem", r"stem"),
            ("BN fwd apply", r"bn_apply|bn_relu_maxpool"), ("BN bwd", r"bn_bwd"), ("pool", r"pool|gap_"),
            ("optimizer / pack", r"sgd|weight_pack|nonfinite"), ("torch fills / misc", r"at::|at6native|rocclr"),
            ("loss / fc", r"softmax|colsum")]
