@@ -33,7 +33,8 @@ size, batch = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (64
 if len(sys.argv) > 5 and sys.argv[5] == "tuned":  # the autotuned kernel configs bench.py runs
     from azure_hc_intel_tf_amd.ops import autotune
     autotune.load_cache()
-m = create_model("resnet50", image_size=size, device="cuda", seed=5)
+dt = os.environ.get("RACE_DTYPE")  # fp32: the headline precision (plane GEMMs, persistent kernels)
+m = create_model("resnet50", image_size=size, device="cuda", seed=5, **({"compute_dtype": dt} if dt else {}))
 img, lab = synthetic_batch(m, batch, seed=3)
 red = None
 if dp:
@@ -60,7 +61,7 @@ def _run(mode, serialize, extra_env=None):
     env.update(extra_env or {})
     if serialize:
         env.update(AMD_SERIALIZE_KERNEL="3", AMD_SERIALIZE_COPY="3", HIP_LAUNCH_BLOCKING="1")
-    if mode == "dp":
+    if mode.startswith("dp"):
         env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29650 + int(serialize)), RANK="0", WORLD_SIZE="1",
                    LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
     out = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, mode.split("+")[0]], env=env, capture_output=True, text=True,
@@ -69,11 +70,13 @@ def _run(mode, serialize, extra_env=None):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("mode", ["single", "dp"])
+@pytest.mark.parametrize("mode", ["single", "dp", "single+fp32", "dp+fp32"])
 def test_serialised_run_equals_async_run(mode):
-    a = _run(mode, serialize=False)
-    s = _run(mode, serialize=True)
-    assert a["graph"] and a["overlap"] == (mode == "dp")
+    """bf16 and the fp32 headline path (plane GEMMs incl. the persistent short-K kernels, fp32 BN)."""
+    env = {"RACE_DTYPE": "fp32"} if mode.endswith("+fp32") else None
+    a = _run(mode, serialize=False, extra_env=env)
+    s = _run(mode, serialize=True, extra_env=env)
+    assert a["graph"] and a["overlap"] == mode.startswith("dp")
     assert a["losses"] == s["losses"], (a["losses"], s["losses"])
     assert a["master"] == s["master"], "weights differ between the asynchronous and the serialised run"
 

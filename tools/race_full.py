@@ -31,13 +31,16 @@ def run(mode, serialize, port):
 
 def main():
     ok = True
-    for i, mode in enumerate(("single", "dp")):
-        a = run(mode, False, 29670 + 2 * i)
-        s = run(mode, True, 29671 + 2 * i)
-        same = a["losses"] == s["losses"] and a["master"] == s["master"]
-        ok &= same
-        print(json.dumps({"mode": mode, "size": 224, "batch": 64, "tuned": True, "overlap": a["overlap"],
-                          "bitwise_equal": same}), flush=True)
+    dts = os.environ.get("RACE_DTYPES", "bf16,fp32").split(",")  # fp32: the headline precision
+    for j, dt in enumerate(dts):
+        os.environ["RACE_DTYPE"] = dt
+        for i, mode in enumerate(("single", "dp")):
+            a = run(mode, False, 29670 + 4 * j + 2 * i)
+            s = run(mode, True, 29671 + 4 * j + 2 * i)
+            same = a["losses"] == s["losses"] and a["master"] == s["master"]
+            ok &= same
+            print(json.dumps({"mode": mode, "dtype": dt, "size": 224, "batch": 64, "tuned": True,
+                              "overlap": a["overlap"], "bitwise_equal": same}), flush=True)
     sys.exit(0 if ok else 1)
 
 
