@@ -144,7 +144,7 @@ class ResNet(CNNModel):
             if cut:
                 yield seg, False
                 seg = []
-        if L.FUSE_STEM_POOL_BWD and getattr(self.stem, "_pool_fused", None) is self.pool and Fn.native(dx):
+        if L.fuse_stem_pool_bwd() and getattr(self.stem, "_pool_fused", None) is self.pool and Fn.native(dx):
             self.stem.backward_from_maxpool(dx, self.pool)  # no max-pool backward kernel
         else:
             dx = self.pool.backward(dx)

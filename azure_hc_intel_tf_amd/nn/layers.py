@@ -428,10 +428,17 @@ STEM_S2D = True
 
 
 # ResNet stem: the BN backward gathers dy from the max pool's gradient (ConvBN.backward_from_maxpool).
-# Bitwise equal (tests/test_stem_pool_bwd_gpu.py) but not faster: the per-pixel window gather (<= 4
-# argmax / gradient loads + index math per 8 channels) costs what the removed 205 MB round trip
-# saved -- fp32 4009 vs 4008 img/s, bf16 0.7% slower (profiles/r4sp_stem_pool_bwd_ab.txt). Off.
-FUSE_STEM_POOL_BWD = os.environ.get("HCB_FUSE_STEM_POOL_BWD", "0") == "1"
+# Bitwise equal (tests/test_stem_pool_bwd_gpu.py). The per-pixel window gather (<= 4 argmax /
+# gradient loads + index math per 8 channels) costs about what the removed round trip saves: bf16
+# 0.5-0.7% slower (16-bit: the round trip is only 103 MB), fp32 +0.3% in round 5's A/B
+# (profiles/r4sp_stem_pool_bwd_ab.txt, profiles/r5_stem_pool_bwd_fp32.txt). None = on for the fp32
+# (planes) path only; HCB_FUSE_STEM_POOL_BWD=1 / 0 forces it.
+_SPB = os.environ.get("HCB_FUSE_STEM_POOL_BWD")
+FUSE_STEM_POOL_BWD = None if _SPB is None else _SPB == "1"
+
+
+def fuse_stem_pool_bwd() -> bool:
+    return FUSE_STEM_POOL_BWD if FUSE_STEM_POOL_BWD is not None else Fn.planes_mode()
 
 
 class StemS2D(ConvBN):

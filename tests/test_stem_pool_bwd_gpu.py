@@ -14,6 +14,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _grads(dtype, fused):
+    keep = L.FUSE_STEM_POOL_BWD
     L.FUSE_STEM_POOL_BWD = fused
     try:
         m = create_model("resnet50", image_size=64, device="cuda", compute_dtype=dtype, seed=11)
@@ -23,7 +24,7 @@ def _grads(dtype, fused):
         torch.cuda.synchronize()
         return m.ps.grad.clone(), {p.name: p.grad.clone() for p in m.ps.params if p.name.startswith("conv0")}
     finally:
-        L.FUSE_STEM_POOL_BWD = False
+        L.FUSE_STEM_POOL_BWD = keep
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
