@@ -173,7 +173,7 @@ def noop_flags_set(p: Params) -> Dict[str, Any]:
 # (bf16x6 plane GEMMs, fp32 BN / pool / loss): their classes set F32_NATIVE_OK. Kept here, torch-free,
 # for the launcher's config echo; tests/test_cli.py checks it against the model classes.
 FP32_NATIVE_MODELS = frozenset({"resnet50", "resnet50_v1.5", "resnet101", "resnet101_v1.5", "resnet152",
-                                "resnet152_v1.5", "inception3", "vgg11", "vgg16", "vgg19", "alexnet", "overfeat",
+                                "resnet152_v1.5", "resnet50_v2", "resnet101_v2", "resnet152_v2", "inception3", "vgg11", "vgg16", "vgg19", "alexnet", "overfeat",
                                 "lenet", "googlenet", "trivial"})
 
 

@@ -16,12 +16,15 @@ TORCH_DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.flo
 
 
 def check_compute_dtype(compute_dtype, device) -> str:
-    """Validate a requested compute precision; never substitute one precision for another."""
+    """Validate a requested compute precision; never substitute one precision for another. The
+    default is fp32 on every device: the reference's precision (tf_cnn_benchmarks with MKL-DNN,
+    /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16), the
+    same default as tf_cnn_benchmarks.py, the runners and bench.py; bf16 / fp16 are opt-in."""
     if torch.device(device).type != "cuda":
         if compute_dtype not in (None, "fp32"):
             raise ValueError(f"the CPU path computes in fp32, not {compute_dtype}")
         return "fp32"
-    cd = compute_dtype or "bf16"
+    cd = compute_dtype or "fp32"
     if cd not in GPU_COMPUTE_DTYPES:
         raise NotImplementedError(f"compute dtype {cd!r} is not implemented on the GPU path "
                                   f"(available: {', '.join(GPU_COMPUTE_DTYPES)})")

@@ -156,7 +156,12 @@ class ResNet(CNNModel):
 class PreActBottleneck:
     """tf_cnn_benchmarks ``bottleneck_block_v2`` (pre-activation ResNet): preact = relu(BN(x));
     shortcut = x (identity) or a bias-free 1x1 projection of preact; 1x1 (stride) conv+BN+ReLU
-    -> 3x3 conv+BN+ReLU -> bias-free 1x1 conv whose GEMM epilogue adds the shortcut."""
+    -> 3x3 conv+BN+ReLU -> bias-free 1x1 conv whose GEMM epilogue adds the shortcut.
+
+    Backward as the v1 block: conv2's / conv1's BN-backward reductions run in the epilogues of the
+    data-grad GEMMs of conv3 / conv2 (``dx_bn``); the projection's data gradient and conv1's are
+    summed by beta-accumulate; the identity shortcut's gradient is added inside the pre-activation
+    BN's backward apply."""
 
     def __init__(self, ps, name, in_shape, depth, bottleneck, stride):
         H, W, C = in_shape
@@ -185,23 +190,24 @@ class PreActBottleneck:
         return self.c3.forward(h, residual=sc)
 
     def backward(self, dy):
-        d2, gres = self.c3.backward(dy, want_gres=True)  # gres = dy: the shortcut's gradient
-        d1, _ = self.c2.backward(d2)
+        d2, gres = self.c3.backward(dy, want_gres=True, dx_bn=self.c2)  # gres = dy: the shortcut's gradient
+        d1, _ = self.c2.backward(d2, dx_bn=self.c1)
         if self.proj:
             da, _ = self.sc.backward(gres)
             self.c1.backward(d1, dx=da, accumulate=True)
             return self.pre.backward(da)
         da, _ = self.c1.backward(d1)
-        dx = self.pre.backward(da)
-        return Fn.add(dx, gres)  # identity shortcut: d(x) += dy
+        return self.pre.backward(da, add=gres)  # identity shortcut: d(x) = BN'(da) + dy, one pass
 
 
 class ResNetV2(CNNModel):
     """ResNet v2 (``--model=resnet50_v2`` / 101 / 152): stem conv+BN+ReLU, max pool, the
     pre-activation bottleneck stages (stride on the first 1x1, as tf_cnn_benchmarks), a final
-    BN + ReLU, spatial mean, affine."""
+    BN + ReLU, spatial mean, affine. fp32 (``--compute_dtype fp32``) runs on the HIP kernels like
+    v1: plane GEMMs, the S2D stem, acc-replica BN passes."""
 
     default_image_size = 224
+    F32_NATIVE_OK = True
 
     def __init__(self, depth: int = 50, **kw):
         self.depth = depth
@@ -211,8 +217,12 @@ class ResNetV2(CNNModel):
     def build(self):
         ps = self.ps
         S = self.image_size
-        self.stem = ConvBN(ps, "conv0", (S, S, self.image_channels), 64, 7, 7, 2, 2, "SAME_RESNET", relu=True,
-                           need_dx=False, logical_cin=3)
+        if self.native and L.STEM_S2D:
+            self.stem = StemS2D(ps, "conv0", (S, S, self.image_channels), 64, relu=True, need_dx=False,
+                                logical_cin=3)
+        else:
+            self.stem = ConvBN(ps, "conv0", (S, S, self.image_channels), 64, 7, 7, 2, 2, "SAME_RESNET", relu=True,
+                               need_dx=False, logical_cin=3)
         self.pool = Pool("mpool0", self.stem.out_shape, 3, 3, 2, 2, "SAME", is_max=True)
         shape = self.pool.out_shape
         self.blocks = []
@@ -229,20 +239,31 @@ class ResNetV2(CNNModel):
         self.layers = ([self.stem, self.pool] + [l for b in self.blocks for l in b.layers()]
                        + [self.post, self.gap, self.fc])
 
+    def _stem_pool(self, images):
+        if Fn.native(images) and L.FUSE_STEM_POOL and self.stem.training:
+            # the pooled map feeds a BN (the first pre-activation), not a GEMM: fp32, not planes
+            return self.stem.forward_maxpool(images, self.pool, out_planes=False)
+        return self.pool.forward(self.stem.forward(images))
+
     def forward(self, images):
-        x = ResNet._stem_pool(self, images)
+        x = self._stem_pool(images)
         for b in self.blocks:
             x = b.forward(x)
         return self.fc.forward(self.gap.forward(self.post.forward(x)))
 
+    def _stem_backward(self, dx):
+        if L.fuse_stem_pool_bwd() and getattr(self.stem, "_pool_fused", None) is self.pool and Fn.native(dx):
+            self.stem.backward_from_maxpool(dx, self.pool)  # no max-pool backward kernel
+        else:
+            self.stem.backward(self.pool.backward(dx))
+        return None
+
     def backward_segments(self, dlogits):
         dx = self.post.backward(self.gap.backward(self.fc.backward(dlogits)))
         units = [(b.backward, b.layers()) for b in reversed(self.blocks)]
-        units.append((lambda d: self.stem.backward(self.pool.backward(d)), [self.pool, self.stem]))
+        units.append((self._stem_backward, [self.pool, self.stem]))
         yield from self._segments_from_units(dx, [self.fc, self.gap, self.post], units)
 
     def backward(self, dlogits):
-        dx = self.post.backward(self.gap.backward(self.fc.backward(dlogits)))
-        for b in reversed(self.blocks):
-            dx = b.backward(dx)
-        self.stem.backward(self.pool.backward(dx))
+        for _ in self.backward_segments(dlogits):
+            pass

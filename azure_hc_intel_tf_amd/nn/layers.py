@@ -260,17 +260,19 @@ class ConvBN(Layer):
         self._saved = (x, None, y, None, False)
         return y
 
-    def forward_maxpool(self, x, pool: "Pool"):
+    def forward_maxpool(self, x, pool: "Pool", out_planes: bool = True):
         """GPU training forward of conv -> BN -> ReLU -> max pool (the ResNet stem) in two
         launches: the conv (BN statistics in its epilogue) and one BN+ReLU+pool kernel. The
         full-size BN+ReLU activation is never written; ``pool`` keeps the argmax for its
-        backward and this layer recomputes the ReLU mask from z."""
+        backward and this layer recomputes the ReLU mask from z. ``out_planes=False``: on the fp32
+        path the pooled map is written as an fp32 tensor, not as GEMM planes (its consumer is a
+        BN -- ResNet v2's first pre-activation)."""
         assert self.bn and self.relu and Fn.native(x) and pool.is_max and self.training
         N = x.shape[0]
         P, Q, C = self.out_shape
         z = empty_act((N, P, Q, C), x.device)
         x = self._conv_fwd_stats(x, z)
-        y = empty_op((N,) + tuple(pool.out_shape), x.device)
+        y = (empty_op if out_planes else empty_act)((N,) + tuple(pool.out_shape), x.device)
         amax = torch.empty((N,) + tuple(pool.out_shape), dtype=torch.uint8, device=x.device)
         acc_f, _, R = self._acc
         saved = Fn.bn_relu_maxpool_acc(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
@@ -606,8 +608,11 @@ class Pool(Layer):
 class BNReLU(Layer):
     """Standalone training-mode BatchNorm (+ ReLU) on an activation: the pre-activation of
     ResNet v2 blocks (tf_cnn_benchmarks ``bottleneck_block_v2``: preact = relu(batch_norm(x)))
-    and its final BN. Statistics come from a reduction kernel over the input (there is no
-    producing GEMM epilogue to fuse them into)."""
+    and its final BN. There is no producing GEMM epilogue to fuse the statistics into: on the GPU
+    one reduction pass accumulates them (shifted sums into the R replicas, ``bn_stats_acc``) and
+    the finalize-free apply writes the next GEMMs' operand (Planes on the fp32 path); the backward
+    is the acc-replica reduce + apply, with the identity shortcut's gradient added in the apply
+    (``backward(dy, add=)``)."""
 
     def __init__(self, ps: ParamStore, name: str, in_shape, relu: bool = True, eps: float = 1e-5,
                  decay: float = 0.9):
@@ -622,27 +627,58 @@ class BNReLU(Layer):
         self.beta = ps.add(f"{name}/batchnorm/beta", (C,), False, ParamStore.const(0.0))
         self.rmean = ps.add_buffer(f"{name}/batchnorm/moving_mean", (C,), 0.0)
         self.rvar = ps.add_buffer(f"{name}/batchnorm/moving_variance", (C,), 1.0)
+        self.acc_f = ps.add_stat(f"{name}/bn_acc_fwd", (STAT_R, 2, C))
+        self.acc_b = ps.add_stat(f"{name}/bn_acc_bwd", (STAT_R, 2, C))
+        self.sv_mean = ps.add_stat(f"{name}/bn_mean", (C,))
+        self.sv_invstd = ps.add_stat(f"{name}/bn_invstd", (C,))
+        self.shift = ps.add_persist(f"{name}/bn_shift", (C,)) if BN_SHIFT else None
         self._saved = None
+        self._acc = None
         self.training = True
 
     def params(self):
         return [self.beta, self.gamma]
 
+    _stat_bufs = ConvBN._stat_bufs
+    _shift = ConvBN._shift
+
     def forward(self, x):
-        y = empty_act(tuple(x.shape), x.device)
+        if Fn.is_planes(x):  # (the fp32 path's pooled stem output when not produced in fp32)
+            x = Fn.from_planes(x)
         if not self.training:
+            y = empty_act(tuple(x.shape), x.device)
             return Fn.bn_inference(x, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.eps, y,
                                    self.relu)
-        saved = Fn.bn_forward(x, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
-                              self.eps, y, self.relu)
+        if Fn.native(x):
+            N, H, W, C = x.shape
+            acc_f, _, R = self._stat_bufs(N, x.device)
+            Fn.bn_stats_acc(x, acc_f, R, self._shift())
+            y = empty_op(tuple(x.shape), x.device)
+            saved = Fn.bn_forward_acc(x, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
+                                      self.eps, y, self.relu, acc_f, R, self.sv_mean.data, self.sv_invstd.data,
+                                      shift=self._shift())
+        else:
+            y = empty_act(tuple(x.shape), x.device)
+            saved = Fn.bn_forward(x, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.decay,
+                                  self.eps, y, self.relu)
         self._saved = (x, y, saved)
         return y
 
-    def backward(self, dy):
+    def backward(self, dy, add=None):
+        """dx = BN'(dy) (+ ``add``, the identity shortcut's gradient, summed in the same pass)."""
         x, y, saved = self._saved
         dx = empty_act(tuple(x.shape), dy.device)
-        Fn.bn_backward(dy if dy.is_contiguous() else dy.contiguous(), y, x, saved, self.gamma.data, self.beta.data,
-                       1 if self.relu else 0, self.gamma.grad, self.beta.grad, dx)
+        dy = dy if dy.is_contiguous() else dy.contiguous()
+        if Fn.native(dy):
+            _, acc_b, R = self._acc
+            Fn.bn_backward_acc(dy, None, x, saved, self.gamma.data, self.beta.data, 2 if self.relu else 0,
+                               self.gamma.grad, self.beta.grad, dx, acc_b, R, None, shift_out=self._shift(),
+                               add=add)
+        else:
+            Fn.bn_backward(dy, y, x, saved, self.gamma.data, self.beta.data, 1 if self.relu else 0, self.gamma.grad,
+                           self.beta.grad, dx)
+            if add is not None:
+                dx.add_(add)
         self._saved = None
         return dx
 

@@ -976,15 +976,38 @@ def bn_relu_maxpool_acc(z, gamma, beta, running_mean, running_var, momentum, eps
     return BNSaved(saved_mean, saved_invstd)
 
 
+def bn_stats_acc(x, acc, R: int, shift=None):
+    """GPU BN statistics of ``x`` [N, H, W, C] (fp32 or 16-bit, rows of C channels, row stride ld(x))
+    accumulated into ``acc`` (R replicas of [2][C], zeroed per step): sums of (v - shift) and
+    (v - shift)^2 -- what a producing conv's epilogue leaves for bn_forward_acc, for a BN whose
+    input is not a GEMM output (ResNet v2's pre-activation / final BN)."""
+    C = x.shape[-1]
+    _ext.ops().bn_stats_acc(x, ld(x), x.numel() // C, C, acc, R, shift)
+
+
+def from_planes(x):
+    """Planes -> the fp32 tensor (hi + mid + lo, exact; one launch on the GPU)."""
+    if not isinstance(x, Planes):
+        return x
+    C = x.shape[-1]
+    out = torch.empty(tuple(x.shape), dtype=torch.float32, device=x.device)
+    if x.is_cuda:
+        _ext.ops().merge_planes(x.t, ld(x), x.numel() // C, C, out, C)
+        return out
+    out.copy_(x.float())
+    return out
+
+
 def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamma, dbeta, dz, acc, R: int,
-                    gres=None, pre_reduced: bool = False, shift_out=None, pool=None):
+                    gres=None, pre_reduced: bool = False, shift_out=None, pool=None, add=None):
     """GPU BN(+ReLU) backward with the dgamma/dbeta reduction accumulated in ``acc`` replicas
     (zeroed per step) and consumed directly by the apply kernel. ``pre_reduced``: dy is already
     the gated g and ``acc`` already holds its sums (a BNBwdFuse data-grad epilogue produced it),
     so only the apply pass runs. ``shift_out``: receives this step's batch mean, the statistics
     shift of the layer's next forward. ``pool`` = (amax, [H, W, P, Q, k, s, pt, pl]): dy is the
     gradient of the max pool that followed this BN+ReLU (the ResNet stem) and both passes gather
-    the full-size dy from it through the pool's argmax (it is never materialised)."""
+    the full-size dy from it through the pool's argmax (it is never materialised). ``add``: a tensor of
+    dz's layout added to dz in the apply pass (dz = BN'(dy) + add; plain dz, not planes)."""
     N, H, W, C = z.shape
     M = N * H * W
     hcb = _ext.ops()
@@ -998,7 +1021,8 @@ def bn_backward_acc(dy, y, z, saved: BNSaved, gamma, beta, relu_mode: int, dgamm
     hcb.bn_bwd_reduce_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), M, C, saved.mean, saved.invstd,
                           gamma, beta, relu_mode, acc, R, gres, ld(gres) if gres is not None else 0, pa, pg)
     hcb.bn_bwd_apply_acc(dy, ld(dy), ym, ld(y) if relu_mode == 1 else 0, z, ld(z), _pl(dz), ld(dz), M, C, saved.mean,
-                         saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode, shift_out, pa, pg)
+                         saved.invstd, gamma, beta, acc, R, dgamma, dbeta, relu_mode, shift_out, pa, pg, add,
+                         ld(add) if add is not None else 0)
     return dz
 
 

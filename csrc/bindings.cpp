@@ -838,7 +838,7 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
                       const Tensor& mean, const Tensor& invstd, const Tensor& gamma, const Tensor& beta,
                       const Tensor& acc, int64_t R, const Tensor& dgamma, const Tensor& dbeta, int64_t relu,
                       const c10::optional<Tensor>& shift_out, const c10::optional<Tensor>& pool_amax,
-                      at::OptionalIntArrayRef pool_geom) {
+                      at::OptionalIntArrayRef pool_geom, const c10::optional<Tensor>& add, int64_t ldadd) {
   const bool f32 = check_act_or_f32(dy, "dy");
   same_act(dy, x, "x");
   // fp32 dy with a bf16 dx: dx is written as [3, ...] bf16 planes (the data / weight-gradient
@@ -847,6 +847,11 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
   const int64_t dxps = dp3 ? check_planes(dx, "dx") : 0;
   if (!dp3) same_act(dy, dx, "dx");
   const int64_t e = f32 ? 4 : 2;
+  if (add.has_value()) {  // dx = BN'(dy) + add: plain dx (no planes), no pooled dy
+    same_act(dy, *add, "add");
+    TORCH_CHECK(!dp3 && !pool_amax.has_value() && ldadd % 8 == 0, "hcb.bn_bwd_apply_acc: add needs a plain dx");
+    check_range(*add, ((M - 1) * ldadd + C) * e, "add");
+  }
   check_f32(acc, "acc");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && R >= 1 && acc.numel() >= R * 2 * C, "hcb.bn_bwd_apply_acc: C/R");
   hcb::PoolSrc ps{};
@@ -874,7 +879,19 @@ void bn_bwd_apply_acc(const Tensor& dy, int64_t lddy, const c10::optional<Tensor
                                gamma.data_ptr<float>(), beta.data_ptr<float>(), acc.data_ptr<float>(), (int)R,
                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), (int)relu,
                                const_cast<float*>(opt_f32(shift_out, C, "shift_out")), cur_stream(), f32, yh, dxps,
-                               pool_amax.has_value() ? &ps : nullptr);
+                               pool_amax.has_value() ? &ps : nullptr, add.has_value() ? add->data_ptr() : nullptr,
+                               (int)ldadd);
+}
+
+void bn_stats_acc(const Tensor& x, int64_t ldx, int64_t M, int64_t C, const Tensor& acc, int64_t R,
+                  const c10::optional<Tensor>& shift) {
+  const bool f32 = check_act_or_f32(x, "x");
+  check_f32(acc, "acc");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && ldx % 8 == 0 && ldx >= C && R >= 1 && M >= 1, "hcb.bn_stats_acc: C/ld/R");
+  TORCH_CHECK(acc.numel() >= R * 2 * C, "hcb.bn_stats_acc: acc too small");
+  check_range(x, ((M - 1) * ldx + C) * (f32 ? 4 : 2), "x");
+  hcb::launch_bn_stats_acc(x.data_ptr(), (int)ldx, (int)M, (int)C, opt_f32(shift, C, "shift"), acc.data_ptr<float>(),
+                           (int)R, cur_stream(), f32);
 }
 
 void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dz) {
@@ -1234,7 +1251,8 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("relu_bwd(Tensor dy, Tensor y, Tensor(a!) dz) -> ()");
   m.def("bn_apply_acc(Tensor x, int ldx, Tensor(a!) y, int ldy, Tensor? res, int ldr, int M, int C, Tensor acc, int R, float eps, float momentum, Tensor gamma, Tensor beta, int relu, Tensor(b!) saved_mean, Tensor(c!) saved_invstd, Tensor(d!)? running_mean, Tensor(e!)? running_var, Tensor? shift=None, Tensor? res_acc=None, Tensor? res_gamma=None, Tensor? res_beta=None, Tensor(g!)? res_saved_mean=None, Tensor(h!)? res_saved_invstd=None, Tensor(i!)? res_running_mean=None, Tensor(j!)? res_running_var=None, Tensor? res_shift=None) -> ()");
   m.def("bn_bwd_reduce_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, int relu, Tensor(a!) acc, int R, Tensor(b!)? gout, int ldg, Tensor? pool_amax=None, int[]? pool_geom=None) -> ()");
-  m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu, Tensor(d!)? shift_out=None, Tensor? pool_amax=None, int[]? pool_geom=None) -> ()");
+  m.def("bn_bwd_apply_acc(Tensor dy, int lddy, Tensor? y, int ldyv, Tensor x, int ldx, Tensor(a!) dx, int lddx, int M, int C, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor acc, int R, Tensor(b!) dgamma, Tensor(c!) dbeta, int relu, Tensor(d!)? shift_out=None, Tensor? pool_amax=None, int[]? pool_geom=None, Tensor? add=None, int ldadd=0) -> ()");
+  m.def("bn_stats_acc(Tensor x, int ldx, int M, int C, Tensor(a!) acc, int R, Tensor? shift=None) -> ()");
   m.def("l2norm_sq(Tensor x, Tensor(a!) out) -> ()");
   m.def("preprocess_images(Tensor src, Tensor desc, Tensor desc_host, Tensor(a!) out, float[] scale, float[] bias) -> ()");
   m.def("bn_relu_maxpool_acc(Tensor z, Tensor(a!) y, Tensor(b!) amax, int[] geom, Tensor acc, int R, float eps, "
@@ -1289,6 +1307,7 @@ HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("bn_apply_acc", bn_apply_acc);
   m.impl("bn_bwd_reduce_acc", bn_bwd_reduce_acc);
   m.impl("bn_bwd_apply_acc", bn_bwd_apply_acc);
+  m.impl("bn_stats_acc", bn_stats_acc);
   m.impl("l2norm_sq", l2norm_sq);
   m.impl("synth_images", synth_images);
   m.impl("dropout_fwd", dropout_fwd);

@@ -889,12 +889,15 @@ __device__ __forceinline__ void bn_coef_bwd(const float* __restrict__ acc, int R
 
 // P3 (fp32 path): dx is written as bf16 hi / mid / lo planes (plane stride dxps elements), the
 // operand format of the data- and weight-gradient GEMMs that consume it
-template <typename T = uint16_t, typename TY = T, bool P3 = false, bool POOL = false>
+// ADD: dx = BN-backward(dy) + addend (row stride ldadd, T) -- a pre-activation BN on an identity
+// shortcut (ResNet v2: d(block input) = BN'(d preact) + d(block output)) in the same pass
+template <typename T = uint16_t, typename TY = T, bool P3 = false, bool POOL = false, bool ADD = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
     const T* __restrict__ dy, int lddy, const TY* __restrict__ y, int ldyv,
     const T* __restrict__ x, int ldx, void* __restrict__ dxv, int lddx, int M, int C, int CVB,
     const float* mean, const float* invstd, const float* gamma, const float* beta, const float* __restrict__ acc,
-    int R, float* dgamma, float* dbeta, int relu, float* shift_out, int64_t dxps, PoolSrc pool) {
+    int R, float* dgamma, float* dbeta, int relu, float* shift_out, int64_t dxps, PoolSrc pool,
+    const T* __restrict__ addp, int ldadd) {
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [6][CB]: mean invstd scale shift k1 k2
   const GroupMap gm = groupmap(CVB);
   const bool active = gm.r0 < gm.rows;
@@ -928,10 +931,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
   lds_read8(coef + 3 * gm.CB + cl, sh);
   lds_read8(coef + 4 * gm.CB + cl, k1);
   lds_read8(coef + 5 * gm.CB + cl, k2);
+  const __amdgpu_buffer_rsrc_t adr = make_rsrc(ADD ? (const void*)addp : (const void*)x,
+                                               rsrc_bytes(M, ADD ? ldadd : ldx, E));
   for (int m0 = mfirst; m0 < M; m0 += BN_UB * stride) {
     if (m0 != mfirst) {
 #pragma unroll
       for (int u = 0; u < BN_UB; ++u) src.load(m0 + u * stride, M, relu, dv[u], xv[u], yv[u]);
+    }
+    Act8<T> av[ADD ? BN_UB : 1];
+    if constexpr (ADD) {
+#pragma unroll
+      for (int u = 0; u < BN_UB; ++u) {
+        const int m = m0 + u * stride;
+        av[u].load(adr, m < M ? (uint32_t)((size_t)m * ldadd + gm.cv * 8) * E : HCB_OOB);
+      }
     }
 #pragma unroll
     for (int u = 0; u < BN_UB; ++u) {
@@ -940,6 +953,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_acc_kernel(
       bwd_math_t<T, TY>(dv[u], xv[u], yv[u], relu, mu, is, sc, sh, g, xh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = sc[e] * (g[e] - k1[e] - xh[e] * k2[e]);
+      if constexpr (ADD) {
+        float a[8];
+        av[u].to_f(a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += a[e];
+      }
       if (m < M) {
         if constexpr (P3)
           store_p3(reinterpret_cast<uint16_t*>(dxv) + (size_t)m * lddx + gm.cv * 8, dxps, o);
@@ -1169,37 +1188,124 @@ void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv,
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu,
-                             float* shift_out, hipStream_t st, bool f32, bool yh, int64_t dxps, const PoolSrc* pool) {
+                             float* shift_out, hipStream_t st, bool f32, bool yh, int64_t dxps, const PoolSrc* pool,
+                             const void* add, int ldadd) {
   int cvb;
   dim3 grid = bn_grid_groups(M, C, &cvb);
   const size_t lds = (size_t)6 * cvb * 8 * 4;
   const PoolSrc ps = pool != nullptr ? *pool : PoolSrc{};
-  if (pool != nullptr && f32 && dxps > 0) {
+  if (add != nullptr) {  // addend: plain (non-plane) dx, no pooled dy (checked on the host)
+    if (f32)
+      hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, float, false, false, true>), grid, dim3(256), lds, st,
+                         (const float*)dy, lddy, (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb,
+                         mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps,
+                         (const float*)add, ldadd);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<uint16_t, uint16_t, false, false, true>), grid, dim3(256), lds, st,
+                         (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, dx, lddx, M, C,
+                         cvb, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps,
+                         (const uint16_t*)add, ldadd);
+  } else if (pool != nullptr && f32 && dxps > 0) {
     hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, float, true, true>), grid, dim3(256), lds, st,
                        (const float*)dy, lddy, (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean,
-                       invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps);
+                       invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps, (const float*)nullptr, 0);
   } else if (pool != nullptr && !f32) {
     hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<uint16_t, uint16_t, false, true>), grid, dim3(256), lds, st,
                        (const uint16_t*)dy, lddy, (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, dx, lddx, M, C,
-                       cvb, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps);
+                       cvb, mean, invstd, gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps,
+                       (const uint16_t*)nullptr, 0);
   } else if (f32 && dxps > 0) {
     if (yh)
       hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, uint16_t, true>), grid, dim3(256), lds, st, (const float*)dy,
                          lddy, (const uint16_t*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd,
-                         gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps);
+                         gamma, beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps, (const float*)nullptr, 0);
     else
       hipLaunchKernelGGL((bn_bwd_apply_acc_kernel<float, float, true>), grid, dim3(256), lds, st, (const float*)dy,
                          lddy, (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma,
-                         beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps);
+                         beta, acc, R, dgamma, dbeta, relu, shift_out, dxps, ps, (const float*)nullptr, 0);
   } else if (f32) {
     hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<float>, grid, dim3(256), lds, st, (const float*)dy, lddy,
                        (const float*)y, ldyv, (const float*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma, beta, acc,
-                       R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps);
+                       R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps, (const float*)nullptr, 0);
   } else {
     hipLaunchKernelGGL(bn_bwd_apply_acc_kernel<uint16_t>, grid, dim3(256), lds, st, (const uint16_t*)dy, lddy,
                        (const uint16_t*)y, ldyv, (const uint16_t*)x, ldx, dx, lddx, M, C, cvb, mean, invstd, gamma,
-                       beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps);
+                       beta, acc, R, dgamma, dbeta, relu, shift_out, (int64_t)0, ps, (const uint16_t*)nullptr, 0);
   }
+}
+
+// Standalone BN statistics into the R accumulator replicas, for a BN whose input has no producing
+// GEMM epilogue to fuse them into (ResNet v2's pre-activation and final BN: the input is a block
+// output, conv + shortcut): sums of (v - K) and (v - K)^2 per channel, K = the layer's previous batch
+// mean (shift; 0 when null), block partials through LDS, then atomics into replica blockIdx.x % R --
+// exactly what a conv epilogue leaves for bn_apply_acc.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_acc_kernel(const T* __restrict__ x, int ldx, int M, int C, int CVB,
+                                                           const float* __restrict__ shift, float* acc, int R) {
+  constexpr uint32_t E = Act8<T>::ESZ;
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];  // [2][rows][CB]
+  const GroupMap gm = groupmap(CVB);
+  const bool active = gm.r0 < gm.rows;
+  const int cl = (threadIdx.x % CVB) * 8;
+  float s1[8] = {0}, s2[8] = {0};
+  if (active) {
+    float k[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) k[e] = shift != nullptr ? shift[gm.cv * 8 + e] : 0.f;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, rsrc_bytes(M, ldx, E));
+    const int stride = gridDim.x * gm.rows;
+    for (int m0 = blockIdx.x * gm.rows + gm.r0; m0 < M; m0 += BN_U * stride) {
+      Act8<T> v[BN_U];
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const int m = m0 + u * stride;
+        v[u].load(xr, m < M ? (uint32_t)((size_t)m * ldx + gm.cv * 8) * E : HCB_OOB);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        if (m0 + u * stride >= M) continue;  // an out-of-range zero row would add (-K)^2
+        float f[8];
+        v[u].to_f(f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = f[e] - k[e];
+          s1[e] += d;
+          s2[e] += d * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      lds_f[gm.r0 * gm.CB + cl + e] = s1[e];
+      lds_f[gm.rows * gm.CB + gm.r0 * gm.CB + cl + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  float* dst = acc + (size_t)(blockIdx.x % R) * 2 * C;
+  for (int i = threadIdx.x; i < gm.CB; i += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < gm.rows; ++r) {
+      a += lds_f[r * gm.CB + i];
+      b += lds_f[gm.rows * gm.CB + r * gm.CB + i];
+    }
+    atomicAdd(dst + gm.c0 + i, a);
+    atomicAdd(dst + C + gm.c0 + i, b);
+  }
+}
+
+void launch_bn_stats_acc(const void* x, int ldx, int M, int C, const float* shift, float* acc, int R, hipStream_t st,
+                         bool f32) {
+  int cvb;
+  dim3 grid = bn_grid_groups(M, C, &cvb);
+  // deterministic mode: at most R row blocks, so each replica slot receives a single add
+  if (deterministic() && (int)grid.x > R) grid.x = R;
+  const size_t lds = (size_t)2 * (256 / cvb) * cvb * 8 * 4;
+  if (f32)
+    hipLaunchKernelGGL(bn_stats_acc_kernel<float>, grid, dim3(256), lds, st, (const float*)x, ldx, M, C, cvb, shift,
+                       acc, R);
+  else
+    hipLaunchKernelGGL(bn_stats_acc_kernel<uint16_t>, grid, dim3(256), lds, st, (const uint16_t*)x, ldx, M, C, cvb,
+                       shift, acc, R);
 }
 
 }  // namespace hcb

@@ -204,7 +204,11 @@ void launch_bn_bwd_reduce_acc(const void* dy, int lddy, const void* y, int ldyv,
 void launch_bn_bwd_apply_acc(const void* dy, int lddy, const void* y, int ldyv, const void* x, int ldx, void* dx,
                              int lddx, int M, int C, const float* mean, const float* invstd, const float* gamma,
                              const float* beta, const float* acc, int R, float* dgamma, float* dbeta, int relu, float* shift_out, hipStream_t st,
-                             bool f32 = false, bool yh = false, int64_t dxps = 0, const PoolSrc* pool = nullptr);
+                             bool f32 = false, bool yh = false, int64_t dxps = 0, const PoolSrc* pool = nullptr,
+                             const void* add = nullptr, int ldadd = 0);
+// BN statistics of x (no producing GEMM epilogue) into R replicas of [2][C]: sums of (v - K), (v - K)^2
+void launch_bn_stats_acc(const void* x, int ldx, int M, int C, const float* shift, float* acc, int R, hipStream_t st,
+                         bool f32);
 // fp32 path, plane-stored tensors: (yps / rps / dxps > 0) outputs / residuals as bf16 hi / mid / lo
 // planes with that plane stride in elements; yh: the ReLU-mask source y is the bf16 hi plane
 

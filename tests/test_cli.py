@@ -229,3 +229,25 @@ def test_flavors_differ_like_the_reference_runners():
     out = subprocess.run([os.path.join(ROOT, "benchmark-scripts", "run-tf-sing-ucx-openmpi.sh"), "1", "1", "32",
                           "ib"], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and "--no_pin" not in out.stdout and "HOROVOD_MPI_THREADS_DISABLE=1" in out.stdout
+
+
+def test_api_default_gpu_precision_is_fp32():
+    """create_model(..., device="cuda") trains at the reference's precision, fp32, like the CLI,
+    the runners and bench.py; bf16 / fp16 are opt-in. Checked on the CPU
+    through the dtype resolution itself (no GPU needed)."""
+    from azure_hc_intel_tf_amd.models.base import check_compute_dtype
+
+    assert check_compute_dtype(None, "cuda") == "fp32"
+    assert check_compute_dtype(None, "cuda:0") == "fp32"
+    assert check_compute_dtype("bf16", "cuda") == "bf16"
+    assert check_compute_dtype(None, "cpu") == "fp32"
+
+
+def test_resnet_v2_is_fp32_native():
+    from azure_hc_intel_tf_amd.bench.flags import FP32_NATIVE_MODELS, parse_flags, precision_label
+    from azure_hc_intel_tf_amd.models.resnet import ResNetV2
+
+    assert ResNetV2.F32_NATIVE_OK
+    for n in ("resnet50_v2", "resnet101_v2", "resnet152_v2"):
+        assert n in FP32_NATIVE_MODELS
+        assert precision_label(parse_flags([f"--model={n}"])) == "fp32 (HIP kernels)"

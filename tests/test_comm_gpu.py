@@ -80,7 +80,7 @@ def test_segmented_overlap_step_matches_single_graph(model_name):
     try:
         for seg in (False, True):
             torch.manual_seed(0)
-            m = create_model(model_name, image_size=size, device="cuda")
+            m = create_model(model_name, image_size=size, device="cuda", compute_dtype="bf16")
             img, lab = synthetic_batch(m, 8)
             red = NativeReducer(force=True) if seg else None
             t = Trainer(m, 8, constant_lr(0.002), reducer=red, world_size=1, use_graph=True, graph_warmup=2,
@@ -209,7 +209,7 @@ def test_comm_profile_on_forced_dp_path():
     from azure_hc_intel_tf_amd.parallel.native import NativeReducer
     from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 
-    m = create_model("resnet50", image_size=64, device="cuda")
+    m = create_model("resnet50", image_size=64, device="cuda", compute_dtype="bf16")
     img, lab = synthetic_batch(m, 8)
     red = NativeReducer(force=True, bucket_bytes=4 << 20)
     t = Trainer(m, 8, constant_lr(0.01), reducer=red, world_size=1, use_graph=True, force_overlap=True)

@@ -53,7 +53,7 @@ def test_loader_feeds_graph_captured_training(tmp_path):
     from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 
     make_fake_imagenet.make(str(tmp_path), shards=2, per_shard=16, seed=3)
-    m = create_model("resnet50", image_size=64, device="cuda:0")
+    m = create_model("resnet50", image_size=64, device="cuda:0", compute_dtype="bf16")
     img, lab = synthetic_batch(m, 8)
     ld = ImageNetLoader(str(tmp_path), 8, 64, 8, "cuda:0", seed=1, reader_threads=2, decode_threads=4, depth=2)
     t = Trainer(m, 8, constant_lr(0.01), use_graph=True)

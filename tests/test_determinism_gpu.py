@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 def _run(steps=4, size=96, batch=16, lr=0.05):
     torch.manual_seed(0)
-    m = create_model("resnet50", image_size=size, device="cuda", seed=21)
+    m = create_model("resnet50", image_size=size, device="cuda", seed=21, compute_dtype="bf16")
     img, lab = synthetic_batch(m, batch, seed=3)
     t = Trainer(m, batch, constant_lr(lr), use_graph=True, graph_warmup=1)
     tr = torch.zeros(steps, device="cuda")

@@ -77,7 +77,7 @@ def test_inception_backward_with_phase_dgrads_matches_dilated(monkeypatch):
     try:
         for phases in (True, False):
             monkeypatch.setattr(Fn, "DGRAD_PHASES", phases)
-            m = create_model("inception3", image_size=107, device=DEV, seed=4)
+            m = create_model("inception3", image_size=107, device=DEV, seed=4, compute_dtype="bf16")
             img, lab = synthetic_batch(m, 8, seed=2)
             t = Trainer(m, 8, constant_lr(0.0), weight_decay=0.0, use_graph=False)
             t._forward_backward(img, lab)

@@ -25,7 +25,7 @@ def test_model_gpu_forward_and_descent(name, size, batch):
     forward (loss, logits) against the fp32 CPU path, the classifier gradient (depends on the
     forward only), and that the hand-written GPU gradient is a descent direction."""
     kw = dict(image_size=size, image_channels=8, seed=11)
-    mg = create_model(name, device="cuda", **kw)
+    mg = create_model(name, device="cuda", compute_dtype="bf16", **kw)
     mc = create_model(name, device="cpu", **kw)
     assert torch.equal(mg.ps.master.cpu(), mc.ps.master)
     img_c, lab_c = synthetic_batch(mc, batch, seed=5)
@@ -59,7 +59,7 @@ def test_graph_training_step_runs_and_learns():
     # Loss on one repeated batch plateaus near ln(#labels in batch) for a few steps before it
     # drops; seed the init and run long enough to leave the plateau.
     torch.manual_seed(0)
-    m = create_model("resnet50", image_size=96, device="cuda")
+    m = create_model("resnet50", image_size=96, device="cuda", compute_dtype="bf16")
     img, lab = synthetic_batch(m, 16)
     t = Trainer(m, 16, constant_lr(0.02), use_graph=True, graph_warmup=2)
     losses = [float(t.step(img, lab)) for _ in range(28)]
@@ -70,7 +70,7 @@ def test_graph_training_step_runs_and_learns():
 
 
 def test_full_size_resnet50_step_bs64():
-    m = create_model("resnet50", device="cuda")
+    m = create_model("resnet50", device="cuda", compute_dtype="bf16")
     img, lab = synthetic_batch(m, 64)
     t = Trainer(m, 64, constant_lr(0.01), use_graph=True)
     for _ in range(4):

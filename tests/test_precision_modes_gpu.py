@@ -1,7 +1,9 @@
 """Reference-precision compute modes on the GPU. fp32 is the reference's precision
-(run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16): on ResNet it runs the HIP kernels
-(bf16x6 GEMMs, fp32 BN / pool; kernel checks in test_fp32_native_gpu.py), on the other models
-the PyTorch path (MIOpen / rocBLAS) of ops/functional.py -- as does IEEE fp16 with
+(run-tf-sing-ucx-openmpi.sh:62-81 passes no --use_fp16) and the default of create_model on every
+device: every model of the zoo runs it on the HIP kernels (bf16x6 plane GEMMs, fp32 BN / pool;
+kernel checks in test_fp32_native_gpu.py, models in test_fp32_zoo_gpu.py / test_fp32_inception_gpu.py
+/ test_fp32_resnet_v2_gpu.py). The PyTorch path (MIOpen / rocBLAS) of ops/functional.py is only the
+comparison arm (HCB_F32_NATIVE=0, or F32_NATIVE_OK patched off as below) -- as is IEEE fp16 with
 Fn.F16_NATIVE off (the default fp16 mode runs the HIP kernels: test_fp16_native_gpu.py)."""
 import pytest
 import torch
@@ -61,5 +63,5 @@ def test_bf16_and_fp32_models_coexist():
     """A bf16 (HIP) and an fp32 (reference) GPU model in one process keep their own
     activation dtypes."""
     a = create_model("resnet50", image_size=64, device="cuda", compute_dtype="fp32")
-    b = create_model("resnet50", image_size=64, device="cuda")
+    b = create_model("resnet50", image_size=64, device="cuda", compute_dtype="bf16")
     assert b.native and b.act_dtype == torch.bfloat16 and a.act_dtype == torch.float32

@@ -126,7 +126,7 @@ def test_resnet_uses_s2d_stem_and_trains():
     from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 
     torch.manual_seed(0)
-    m = create_model("resnet50", image_size=96, device="cuda")
+    m = create_model("resnet50", image_size=96, device="cuda", compute_dtype="bf16")
     assert isinstance(m.stem, StemS2D)
     img, lab = synthetic_batch(m, 16)
     t = Trainer(m, 16, constant_lr(0.02), use_graph=True, graph_warmup=2)

@@ -21,7 +21,7 @@ def _no_dropout(m):
 @pytest.mark.parametrize("name", sorted(SIZES))
 def test_zoo_gpu_forward_and_descent(name):
     kw = dict(image_size=SIZES[name], image_channels=8, seed=3)
-    mg = create_model(name, device="cuda", **kw)
+    mg = create_model(name, device="cuda", compute_dtype="bf16", **kw)
     mc = create_model(name, device="cpu", **kw)
     _no_dropout(mg)
     _no_dropout(mc)
@@ -63,7 +63,7 @@ def test_dropout_kernel():
 
 @pytest.mark.parametrize("name,batch", [("vgg16", 16), ("googlenet", 32), ("alexnet", 64)])
 def test_zoo_full_size_graph_steps(name, batch):
-    m = create_model(name, device="cuda")
+    m = create_model(name, device="cuda", compute_dtype="bf16")
     img, lab = synthetic_batch(m, batch)
     t = Trainer(m, batch, constant_lr(1e-4), use_graph=True)
     losses = [float(t.step(img, lab)) for _ in range(5)]

@@ -32,7 +32,7 @@ def main():
     from azure_hc_intel_tf_amd.ops import autotune
 
     autotune.load_cache()  # --cfg omitted: the autotuned config of this shape
-    m = create_model(a.model, device=dev)
+    m = create_model(a.model, device=dev, compute_dtype="bf16" if str(dev).startswith("cuda") else None)
     m.ps.repack()
     layer = next(l for l in m.all_layers() if isinstance(l, ConvBN) and l.name == a.layer)
     s = layer.spec

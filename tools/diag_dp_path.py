@@ -32,7 +32,7 @@ def main():
     for mode in a.modes.split(","):
         torch.manual_seed(0)
         red = NativeReducer(compression=a.compression, force=True) if (mode == "dp" and a.reducer_first) else None
-        m = create_model("resnet50", device="cuda")
+        m = create_model("resnet50", device="cuda", compute_dtype="bf16")
         img, lab = synthetic_batch(m, 64)
         if mode == "dp" and red is None:
             red = NativeReducer(compression=a.compression, force=True)

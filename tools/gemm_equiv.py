@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     a = ap.parse_args()
     dev = torch.device("cuda")
-    m = create_model("resnet50", device=dev)
+    m = create_model("resnet50", device=dev, compute_dtype="bf16" if str(dev).startswith("cuda") else None)
     m.ps.repack()
     autotune.load_cache()
     seen = set()

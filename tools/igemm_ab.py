@@ -31,7 +31,7 @@ def main():
     variants = [int(v) for v in (sys.argv[1:] or ["0"])]
     dev = torch.device("cuda")
     autotune.load_cache()
-    m = create_model("resnet50", device=dev)
+    m = create_model("resnet50", device=dev, compute_dtype="bf16" if str(dev).startswith("cuda") else None)
     m.ps.repack()
     probs = []
     seen = set()

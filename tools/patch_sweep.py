@@ -46,7 +46,7 @@ def main():
     only_cfgs = None if a.cfgs is None else {int(c) for c in a.cfgs.split(",")}
     only_stages = None if a.stages is None else {f"stage{s}/" for s in a.stages.split(",")}
     dev = torch.device("cuda")
-    m = create_model("resnet50", device=dev)
+    m = create_model("resnet50", device=dev, compute_dtype="bf16" if str(dev).startswith("cuda") else None)
     m.ps.repack()
     seen = set()
     for layer in m.all_layers():

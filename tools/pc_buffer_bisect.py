@@ -34,7 +34,7 @@ os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = os.environ["HCB_PC_WANT"]
 Fn.set_deterministic(True)
 steps = int(sys.argv[2])
 dp = sys.argv[3] == "dp"
-m = create_model("resnet50", image_size=64, device="cuda", seed=5)
+m = create_model("resnet50", image_size=64, device="cuda", seed=5, compute_dtype="bf16")
 img, lab = synthetic_batch(m, 8, seed=3)
 red = None
 if dp:  # the data-parallel step graph: forked comm branch, 1-rank RCCL communicator

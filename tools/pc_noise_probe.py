@@ -17,7 +17,7 @@ from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = os.environ["HCB_PC_WANT"]
 seg = sys.argv[2] == "dp"
 torch.manual_seed(0)
-m = create_model("resnet50", image_size=96, device="cuda")
+m = create_model("resnet50", image_size=96, device="cuda", compute_dtype="bf16")
 img, lab = synthetic_batch(m, 8)
 red = None
 if seg:

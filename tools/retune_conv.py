@@ -35,7 +35,7 @@ def main():
         if name not in only:
             continue
         t0 = time.time()
-        m = create_model(name, device="cuda")
+        m = create_model(name, device="cuda", compute_dtype="bf16")
         n = autotune.tune_model(m, b, verbose=True, save=False)
         del m
         torch.cuda.empty_cache()

@@ -27,7 +27,7 @@ def main():
         if only and name not in only:
             continue
         t0 = time.time()
-        m = create_model(name, device="cuda")
+        m = create_model(name, device="cuda", compute_dtype="bf16")
         n = autotune.tune_model(m, b, verbose=True, save=True)
         del m
         torch.cuda.empty_cache()

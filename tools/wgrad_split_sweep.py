@@ -29,7 +29,7 @@ def tm(fn, reps=20):
 def main():
     dev = torch.device("cuda")
     autotune.load_cache()
-    m = create_model("resnet50", device=dev)
+    m = create_model("resnet50", device=dev, compute_dtype="bf16" if str(dev).startswith("cuda") else None)
     N = 64
     done = set()
     for l in m.all_layers():

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--layers", default="")
     a = ap.parse_args()
     dev = torch.device("cuda")
-    m = create_model("resnet50", device=dev)
+    m = create_model("resnet50", device=dev, compute_dtype="bf16" if str(dev).startswith("cuda") else None)
     seen = set()
     want = set(a.layers.split(",")) if a.layers else None
     for l in m.all_layers():
