@@ -19,6 +19,7 @@ from typing import List
 import torch
 
 from ..nn.layers import ConvBN, GlobalAvgPool, Logits, Pool, empty_act, empty_op
+from ..ops import functional as Fn
 from .base import CNNModel
 
 BN_KW = dict(eps=1e-3, decay=0.999, scale=False)
@@ -100,6 +101,12 @@ class InceptionModule:
         # when a branch ends in a conv without BN (GoogLeNet: its conv epilogue writes fp32)
         out = (empty_act if self._fp32_out else empty_op)((N,) + self.out_shape, x.device)
         term_slot = {id(t): (off, t.layer.out_shape[2]) for t, off in zip(self.terminals, self.offsets)}
+        heads = [n for n in self.nodes if n.src is None]
+        if len(heads) > 1 and Fn.planes_mode() and Fn.native(x) and not Fn.is_planes(x) and not (
+                self._fp32_out and any(isinstance(n.layer, Pool) and id(n) in term_slot for n in heads)):
+            # fp32 path, an fp32 module input (GoogLeNet: the previous concat is fp32) read by several
+            # branch heads: split it into the GEMM planes once instead of once per branch
+            x = Fn.to_planes(x)
         for n in self.nodes:
             inp = x if n.src is None else n.src.out
             slot = term_slot.get(id(n))

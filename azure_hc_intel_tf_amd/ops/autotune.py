@@ -34,7 +34,16 @@ def _table_path(v):
 
 DEFAULT_CACHE = _table_path(os.environ.get("HCB_TUNED_TABLE")) or os.path.join(_DIR, "mi355x.json")
 # bump whenever the kernel config set changes: entries of another version are re-tuned
-CACHE_VERSION = 5  # 5: keys carry the filter tap count
+CACHE_VERSION = 6  # 5: keys carry the filter tap count; 6: round-5 pruned cfgs / stream-K plans gone
+
+
+def _entry_valid(key, val) -> bool:
+    """A cached plan whose cfg the current kernel set still has (and splits >= 1): entries of
+    removed configs would otherwise fall through to a kernel's default launcher, untuned."""
+    tiles = {"fwd": Fn._CONV_TILES, "dgb": Fn._CONV_TILES, "wgrad": Fn._WGRAD_TILES, "fwd3": Fn._P3_TILES,
+             "wgrad3": Fn._WP3_TILES}.get(key[0])
+    cfg, splits = (val[0], val[1]) if isinstance(val, (tuple, list)) else (val, 1)
+    return tiles is not None and int(cfg) in tiles and int(splits) >= 1
 
 
 def _key_str(k) -> str:
@@ -55,7 +64,9 @@ def load_cache(path: str = DEFAULT_CACHE) -> int:
         return 0
     table = {}
     for k, v in d.get("entries", {}).items():
-        table[_key_parse(k)] = tuple(v) if isinstance(v, list) else v
+        key, val = _key_parse(k), tuple(v) if isinstance(v, list) else v
+        if _entry_valid(key, val):
+            table[key] = val
     Fn.set_tuned(table)
     return len(table)
 

@@ -51,7 +51,22 @@ class XgmiAllreduce:
             self.close()
             raise RuntimeError(f"xgmi region export failed on rank(s) {failed}" + (f" (here: {err})" if err else ""))
         handles = torch.stack([torch.frombuffer(bytearray(b), dtype=torch.uint8) for b in got])
-        cc.xgmi_open(self.h, handles)
+        # mapping the peers' regions can also fail on one rank only: agree on the outcome (one
+        # more all-gather) so every rank either continues or closes and raises
+        err = ""
+        try:
+            cc.xgmi_open(self.h, handles)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        if self.world > 1:
+            oks = [None] * self.world
+            dist.all_gather_object(oks, not err, group=group)
+        else:
+            oks = [not err]
+        failed = [r for r, ok in enumerate(oks) if not ok]
+        if failed:
+            self.close()
+            raise RuntimeError(f"xgmi peer mapping failed on rank(s) {failed}" + (f" (here: {err})" if err else ""))
 
     def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
         if t.numel() > self.capacity:

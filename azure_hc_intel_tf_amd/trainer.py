@@ -471,6 +471,7 @@ class Trainer:
             for t, c in snap:
                 t.copy_(c)
             self.steps_done = steps
+            self._lr_dev = None  # hyper was restored: the next step rewrites hyper[0]
             ps.repack()
             torch.cuda.synchronize()
 

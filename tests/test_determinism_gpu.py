@@ -52,12 +52,20 @@ def test_deterministic_mode_trains_like_default():
     lo, hi = runs.min(0).values, runs.max(0).values
     band = 2.0 * (hi - lo) + 2e-3 * hi.abs()
     assert bool(((trd >= lo - band) & (trd <= hi + band)).all()), (trd.tolist(), runs.tolist())
+    # the first steps, before the chaos has amplified anything, against a tight fixed bound (a
+    # regression of the deterministic split-K / statistics path shows up here, whatever the band):
+    # step 0 is the forward of identical weights (only the fp32 summation order differs)
+    mean = runs.mean(0)
+    assert abs(float(trd[0] - mean[0])) <= 1e-3 * abs(float(mean[0])), (trd.tolist(), runs.tolist())
+    assert abs(float(trd[1] - mean[1])) <= 3e-2 * abs(float(mean[1])), (trd.tolist(), runs.tolist())
     # (a stable learning rate: at 0.05 this tiny-batch run diverges)
     assert float(trd[-1]) < float(trd[0]) - 2.0 and float(runs[:, -1].max()) < float(runs[:, 0].min()) - 2.0
 
 
 def _shallow(device, **kw):
     resnet.LAYER_COUNTS.setdefault(1, (1,))  # stem + max pool + ONE bottleneck block + classifier
+    if str(device).startswith("cuda"):
+        kw.setdefault("compute_dtype", "bf16")  # the 16-bit path (create_model defaults to fp32)
     return resnet.ResNet(depth=1, device=device, **kw)
 
 
@@ -149,7 +157,8 @@ def test_bf16_gradients_within_the_autocast_floor():
         sl = (lambda t: t[..., :3]) if name.startswith("conv0/conv2d") else (lambda t: t)
         e32, eac, ehip = (BF.rel(sl(d[name]).flatten(), sl(r).flatten()) for d in (f32, ac, hip))
         print("bf16 floor", name, e32, eac, ehip, ehip / eac)
-        # the fp32 mirror only has to sit far below the bf16 floor: MIOpen's fp32 algorithm choice
-        # varies by box (measured 1.8e-3 on the stem weight gradient on one box, < 1e-4 on others)
-        assert e32 < 5e-3 and e32 < 0.1 * eac, (name, e32, eac)
+        # the fp32 mirror pins the MIRROR (not the HIP kernels): it only has to sit an order of
+        # magnitude below the bf16 floor it calibrates. No absolute bound: MIOpen's fp32 algorithm
+        # choice varies by box (1.8e-3 on the stem weight gradient on one box, < 1e-4 on others)
+        assert e32 < 0.1 * eac, (name, e32, eac)
         assert ehip < 1.5 * eac, (name, ehip, eac)

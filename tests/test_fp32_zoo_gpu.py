@@ -51,13 +51,40 @@ def test_fp32_zoo_gpu_step_matches_fp32_cpu_step(name, size, batch, monkeypatch)
         lc = float(tc.step(img_c, lab_c))
         assert abs(lg - lc) <= 1e-4 * abs(lc), (lg, lc)
         gg, gc = mg.ps.grad.cpu(), mc.ps.grad
-        # fp32-level agreement except where a ReLU / max-pool decision sits within rounding of its
-        # threshold and flips between the two summation orders (measured: 5.2e-3 AlexNet, 1.4e-3
-        # LeNet, < 1e-3 the others; cosine > 0.9999 everywhere)
         assert float(gg @ gc / (gg.norm() * gc.norm())) > 0.9999
-        assert ((gg - gc).norm() / gc.norm()).item() < 1e-2
+        if name not in MIRRORED:
+            assert ((gg - gc).norm() / gc.norm()).item() < 1e-3
+        # (the plain sequential nets are held to fp32 rounding given their ReLU / max-pool decisions
+        # by test_fp32_zoo_gpu_gradient_given_its_decisions below: AlexNet / LeNet each flip ONE ReLU
+        # decision against the CPU, which alone moves the whole gradient by 5.2e-3 / 1.4e-3)
     finally:
         _reset()
+
+
+# the sequential nets the fp64 decision-forced mirror of tools/zoo_flip_probe.py covers
+MIRRORED = {"vgg11", "alexnet", "overfeat", "lenet"}
+
+
+@pytest.mark.parametrize("name,size,batch", [z for z in ZOO if z[0] in MIRRORED], ids=[z[0] for z in ZOO if z[0] in MIRRORED])
+def test_fp32_zoo_gpu_gradient_given_its_decisions(name, size, batch):
+    """The GPU gradient against an fp64 autograd mirror of the network whose ReLU masks and
+    max-pool argmaxes are forced to the GPU's own decisions: what remains is the kernels' fp32
+    rounding (measured 3.5e-7 - 7.1e-7). The GPU-vs-CPU gap is then bounded GIVEN the number of
+    decisions that differ from the CPU's (profiles/r6_zoo_fp32_flip_probe.txt: one ReLU flip in
+    AlexNet's last affine layer / LeNet's second conv accounts for the whole 5.2e-3 / 1.4e-3)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import zoo_flip_probe as ZP
+
+    r = ZP.probe(name, size, batch, seed=9, img_seed=4)  # the inputs of the step test above
+    flips = sum(f for _, _, f, _ in r["flips"])
+    assert r["gpu_vs_mirror_gpu"] < 1e-5, r
+    assert r["cpu_vs_mirror_cpu"] < 1e-5, r  # the mirror itself reproduces the CPU step
+    assert flips <= 2, r["flips"]
+    if flips == 0:
+        assert r["gpu_vs_cpu"] < 1e-5, r
 
 
 @pytest.mark.parametrize("name,size,batch", [("alexnet", 67, 8), ("googlenet", 64, 8)], ids=["alexnet", "googlenet"])

@@ -29,6 +29,8 @@ BATCH = 32
 
 def shallow(device, **kw):
     resnet.LAYER_COUNTS.setdefault(1, (1,))  # stem + max pool + ONE bottleneck block + classifier
+    if str(device).startswith("cuda"):
+        kw.setdefault("compute_dtype", "bf16")  # the 16-bit path (create_model defaults to fp32)
     return resnet.ResNet(depth=1, device=device, **KW, **kw)
 
 

@@ -64,6 +64,8 @@ def conv_ops():
 
 def shallow(device, **kw):
     resnet.LAYER_COUNTS.setdefault(1, (1,))
+    if str(device).startswith("cuda"):
+        kw.setdefault("compute_dtype", "bf16")  # the 16-bit path (create_model defaults to fp32)
     return resnet.ResNet(depth=1, device=device, **kw)
 
 
