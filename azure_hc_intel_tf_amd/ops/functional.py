@@ -442,13 +442,20 @@ def set_tuned(table: dict) -> None:
 _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128),
              7: (128, 128), 8: (128, 128), 9: (128, 128), 10: (256, 128), 11: (128, 256), 12: (64, 128),
              13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64),
-             18: (64, 128), 19: (128, 64), 20: (64, 64), 21: (64, 64), 22: (128, 128)}
+             18: (64, 128), 19: (128, 64), 20: (64, 64), 21: (64, 64), 22: (128, 128),
+             23: (64, 128), 24: (128, 64), 25: (64, 64), 26: (64, 64), 27: (128, 128), 28: (128, 128),
+             29: (256, 128), 30: (128, 256)}
 # workgroups per CU each plane-GEMM cfg is built for
-_P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3, 18: 2, 19: 2, 20: 2, 21: 3}
+_P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3, 18: 2, 19: 2, 20: 2, 21: 3, 23: 2, 24: 2, 25: 2, 26: 3}
 # persistent short-K twins (conv_p3_persist.h): one workgroup per resident slot walks its tiles with
 # the LDS-DMA ring running across tile boundaries and a register epilogue; no split-K (a problem
 # with an epilogue they do not serve -- fused BN backward, beta, bias -- runs the twin)
-_P3_PERSIST = {18: 15, 19: 14, 20: 16, 21: 17, 22: 7}
+_P3_PERSIST = {18: 15, 19: 14, 20: 16, 21: 17, 22: 7, 23: 15, 24: 14, 25: 16, 26: 17, 27: 7, 28: 8,
+               29: 10, 30: 11}
+# their STREAM-K form (conv_p3_persist.h SK): every workgroup a contiguous, equal share of all (tile,
+# k-step) iterations -- no wave-quantization tail; split tiles meet through the split-K workspace.
+# sk cfg -> the cfg it falls back to (the whole-tile persistent form; 28 -- cfg 8's geometry -- cfg 8)
+_P3_STREAMK = {23: 18, 24: 19, 25: 20, 26: 21, 27: 22, 28: 8, 29: 10, 30: 11}
 # wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles),
 # 12-15 32-deep slots, two / three workgroups per CU
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),
@@ -549,7 +556,7 @@ def _plan3(cfg, M, N, K, device, taps: int = 1):
     splits = max(1, min(int(splits), max(K // 64, 1)))
     if _DET[0]:
         splits = 1
-    if splits != 1:
+    if splits != 1 or int(cfg) in _P3_STREAMK:
         ensure_splitk_workspace(device)
     return int(cfg), int(splits)
 

@@ -25,23 +25,35 @@
 namespace hcb {
 
 // cfg 0-17: conv_igemm_p3_kernel (conv_p3_fwd.h); 18-22: the persistent short-K kernel
-// (conv_p3_persist.h), twins of 15, 14, 16, 17 and 7
-constexpr int N_P3_CFG = 23;
+// (conv_p3_persist.h), twins of 15, 14, 16, 17 and 7; 23-27: its stream-K form (tiles of 18-22);
+// 28-30: stream-K with cfg 8's, 10's and 11's geometry (4 x 2 waves of 32 x 64; 256 x 128 and
+// 128 x 256 of 64 x 64 wave tiles: 25% fewer operand bytes per MFMA than 128 x 128, and with
+// stream-K no quantization tail however few tiles)
+constexpr int N_P3_CFG = 31;
 int p3_tile_m(int cfg) {
-  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128,
-                                  64,  128, 128, 64, 64, 64, 64, 128, 64, 64, 128};
+  static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 128, 128, 64,
+                                  64, 64, 64, 128, 64, 64, 128, 64, 128, 64, 64, 128, 128, 256, 128};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 128;
 }
 int p3_slot_k(int cfg) { return (cfg >= 0 && cfg <= 6) ? 64 : 32; }
 int p3_tile_n(int cfg) {
-  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256,
-                                  128, 64, 64, 128, 64, 64, 128, 64, 64, 64, 128};
+  static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256, 128, 64, 64, 128,
+                                  64, 64, 128, 64, 64, 64, 128, 128, 64, 64, 64, 128, 128, 128, 256};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 64;
 }
 
-// the persistent cfg, or (a problem with an epilogue it does not serve) its twin
+// the persistent cfg, or (a problem with an epilogue it does not serve) its twin; the stream-K cfg,
+// else its whole-tile persistent form
 static int launch_p3_persist(const ConvParams& p, int cfg, hipStream_t st) {
   switch (cfg) {
+    case 23: return launch_p3sk<2, 2, 32, 64, 32, 2, 2>(p, st) ? -1 : launch_p3_persist(p, 18, st);
+    case 24: return launch_p3sk<2, 2, 64, 32, 32, 2, 2>(p, st) ? -1 : launch_p3_persist(p, 19, st);
+    case 25: return launch_p3sk<2, 2, 32, 32, 32, 3, 2>(p, st) ? -1 : launch_p3_persist(p, 20, st);
+    case 26: return launch_p3sk<2, 2, 32, 32, 32, 2, 3>(p, st) ? -1 : launch_p3_persist(p, 21, st);
+    case 27: return launch_p3sk<2, 4, 64, 32, 32, 3, 1>(p, st) ? -1 : launch_p3_persist(p, 22, st);
+    case 28: return launch_p3sk<4, 2, 32, 64, 32, 3, 1>(p, st) ? -1 : 8;
+    case 29: return launch_p3sk<4, 2, 64, 64, 32, 2, 1>(p, st) ? -1 : 10;
+    case 30: return launch_p3sk<2, 4, 64, 64, 32, 2, 1>(p, st) ? -1 : 11;
     case 18: return launch_p3p<2, 2, 32, 64, 32, 2, 2>(p, st) ? -1 : 15;
     case 19: return launch_p3p<2, 2, 64, 32, 32, 2, 2>(p, st) ? -1 : 14;
     case 20: return launch_p3p<2, 2, 32, 32, 32, 3, 2>(p, st) ? -1 : 16;

@@ -26,6 +26,8 @@
 // The reference's role: the MKL-DNN fp32 Conv2D forward primitive, driven by
 // /root/reference/benchmark-scripts/run-tf-sing-ucx-openmpi.sh:62-81.
 #pragma once
+#include <cstdlib>
+
 #include "conv_p3_fwd.h"
 #include "conv_p3_wgrad.h"
 
@@ -44,10 +46,23 @@ constexpr size_t p3p_ring_bytes() {
   return (size_t)NST * p3_stage_bytes<BM, BN, KW>();
 }
 
-// STATS: BN statistics into p.stats_R replicas. WM <= 2: a replica slot of a tile receives one add
-// per wave row, and two fp32 adds commute exactly, so the deterministic mode's one-replica-per-tile
-// statistics stay bitwise reproducible.
-template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool STATS, int OCC>
+// STATS: BN statistics into p.stats_R replicas, replica = the wave's 64-row block (mod R). TM >= 32:
+// a replica slot receives at most two adds per tile (the two 32-row waves of a 64-row block), and
+// two fp32 adds commute exactly, so the deterministic mode's one-replica-per-64-rows statistics stay
+// bitwise reproducible.
+//
+// SK (stream-K, cfg 23-27): instead of whole tiles first, first + grid, ... every workgroup owns a
+// CONTIGUOUS share [x0, x0 + nsteps) of all ntiles x nk (tile, k-step) iterations, equal to within
+// one k-step, so the launch has no wave-quantization tail (196 tiles of 128 x 128 on 256 CUs leave
+// 60 CUs idle for the whole launch; here every CU runs ~0.77 tile). The ring runs across the share's
+// tile boundaries as in the whole-tile form (no per-share ramp: round 4's stream-K paid one per
+// share, profiles/r4v_streamk_probe.txt). A tile split between workgroups (its shares: the workgroups
+// of its first .. last iteration, at most p.splits of them) meets through the split-K hand-off
+// (splitk_gather's protocol: slab in p.ws, agent-scope release + ticket in p.cnt[tile]; the last
+// arriver acquires, sums every share's slab in share order -- run-to-run deterministic -- and runs
+// the epilogue). Only a share's first and last segments can be split tiles, so a workgroup pays at
+// most two hand-offs, and the spin-free protocol cannot deadlock whatever the residency.
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool STATS, int OCC, bool SK = false>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
@@ -57,12 +72,18 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   constexpr int LOADS = NPL * (AV + BV);
   constexpr int AIMG = BM * RB, BIMG = BN * RB;
   constexpr int STAGE = (int)p3_stage_bytes<BM, BN, KW>();
-  constexpr int EOPS = MI * NI * 4 + (STATS ? 2 * NI : 0);  // epilogue vector-memory instructions
-  static_assert(WM <= 2, "at most two adds per statistics slot and tile (deterministic mode)");
+  // epilogue vector-memory instructions; EDRAIN (64 x 64 wave tiles: more than the vmcnt field can
+  // count beside the ring): the epilogue drains itself instead and the ring's waits count 0 for it
+  constexpr int EOPS_N = MI * NI * 4 + (STATS ? 2 * NI : 0);
+  constexpr bool EDRAIN = LOADS * (NST - 1) + EOPS_N > 63;
+  constexpr int EOPS = EDRAIN ? 0 : EOPS_N;
+  static_assert(TM >= 32, "at most two adds per statistics slot and tile (deterministic mode)");
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 1) + EOPS <= 63 && NST >= 2 && NST <= 4, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* ktab = reinterpret_cast<float*>(smem + p3p_ring_bytes<BM, BN, KW, NST>());
+  // SK: the last-arriver broadcast word, after the shift table
+  int* skflag = reinterpret_cast<int*>(smem + p3p_ring_bytes<BM, BN, KW, NST>() + (STATS ? (size_t)p.Nout * 4 : 0));
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = wave_id_uniform();
@@ -72,9 +93,20 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   const int ntiles = ((p.M + BM - 1) / BM) * tiles_n;
   const int grid = gridDim.x;
   const int first = xcd_remap(blockIdx.x, grid);  // concurrent neighbours (same M rows) share an XCD
-  if (first >= ntiles) return;                     // uniform (the host sizes grid <= ntiles)
-  const int mine = (ntiles - 1 - first) / grid + 1;
   const int nk = p.Kpad / KW;
+  // the work: SK -- iterations [x0, x0 + nsteps) of the tile-major (tile, k-step) space; otherwise
+  // `mine` whole tiles first, first + grid, ...
+  int mine = 0, x0 = 0, nsteps = 0;
+  if constexpr (SK) {  // 32-bit: the host checks ntiles * nk * grid < 2^32
+    const uint32_t T = (uint32_t)ntiles * (uint32_t)nk;
+    x0 = (int)((uint32_t)first * T / (uint32_t)grid);
+    nsteps = (int)((uint32_t)(first + 1) * T / (uint32_t)grid) - x0;
+    if (nsteps <= 0) return;  // uniform (the host sizes grid <= ntiles * nk)
+  } else {
+    if (first >= ntiles) return;  // uniform (the host sizes grid <= ntiles)
+    mine = (ntiles - 1 - first) / grid + 1;
+    nsteps = mine * nk;
+  }
   const int chunk = (tid % CPR) ^ p3_swz<KW>(tid / CPR);
 
   const char* xb = reinterpret_cast<const char*>(p.x);
@@ -95,22 +127,28 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   // MFMAs; its loader state follows it across tile boundaries
   ALoader<AV, CBIG, false, RP, 2, KW> al;
   uint32_t b_off[BV];
-  int ci = 0, ck = 0;
-  auto cursor_tile = [&](int i) {
-    const int t = first + i * grid;
+  int ci = 0, ck = 0;  // the next issue: local tile (whole-tile form) / local step (SK), and k-step
+  auto cursor_at = [&](int t, int k0) {
     const int tm = t / tiles_n, tn = t - tm * tiles_n;
     al.init(p, tm * BM, tid, chunk);
+    if (k0 > 0) al.seek(p, k0);
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const int j = tn * BN + tid / CPR + RP * v;
       b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
     }
   };
-  cursor_tile(0);
+  auto cursor_tile = [&](int i) { cursor_at(first + i * grid, 0); };
+  if constexpr (SK) {
+    ck = x0 % nk;
+    cursor_at(x0 / nk, ck);
+  } else {
+    cursor_tile(0);
+  }
   constexpr int WROWS = 64 / CPR;
   // branch-free: past the last tile every piece is out of range (lands zeros in a slot nobody reads)
   auto issue = [&](int stage) {
-    const bool live = ci < mine;
+    const bool live = SK ? ci < nsteps : ci < mine;
     uint32_t off[AV];
     al.offsets(p, ck, chunk, off);
     char* sa = smem + stage * STAGE + wid * WROWS * RB;
@@ -131,9 +169,17 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
     }
   };
   auto advance = [&]() {
-    if (++ck == nk) {
-      ck = 0;
-      if (++ci < mine) cursor_tile(ci);
+    if constexpr (SK) {
+      ++ci;
+      if (++ck == nk) {
+        ck = 0;
+        if (ci < nsteps) cursor_at((x0 + ci) / nk, 0);
+      }
+    } else {
+      if (++ck == nk) {
+        ck = 0;
+        if (++ci < mine) cursor_tile(ci);
+      }
     }
   };
 
@@ -143,15 +189,14 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- register epilogue of local tile i: exactly EOPS vector-memory instructions per thread
-  auto epilogue = [&](int i) {
-    const int t = first + i * grid;
+  // ---- register epilogue of tile t: exactly EOPS vector-memory instructions per thread
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int tm = t / tiles_n, tn = t - tm * tiles_n;
     const int rbase = tm * BM + wm * TM;           // the wave's first row
     const int cbase = tn * BN + wn * TN + frow;    // the lane's column in fragment j = 0
     if constexpr (STATS) {
       const int wrows = p.M - rbase;
-      const uint32_t rep = (uint32_t)(tm % p.stats_R) * 2u * (uint32_t)p.Nout;
+      const uint32_t rep = (uint32_t)((rbase >> 6) % p.stats_R) * 2u * (uint32_t)p.Nout;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = cbase + j * 16;
@@ -192,10 +237,75 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
           buf_store_f32(yr, o, relu ? fmaxf(v, 0.f) : v);
         }
       }
+    if constexpr (EDRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int ii = 0; ii < MI; ++ii)
 #pragma unroll
       for (int j = 0; j < NI; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // ---- SK: a split tile's segment ends here. Park the partial, take a ticket; the last of the
+  // tile's S shares sums every slab in share order and runs the epilogue. Drains this thread's
+  // vector memory (the ring's in-flight slots included: the later counted waits only get stricter)
+  auto partial = [&](int t) __attribute__((always_inline)) {
+    constexpr int FR = MI * NI;
+    if (p.cnt == nullptr) {  // timing probe only (HCB_SK_PROBE=1): no hand-off, the split tiles' output is wrong
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
+    const uint32_t T = (uint32_t)ntiles * (uint32_t)nk;
+    // the share holding iteration x: the largest w with w * T / grid <= x
+    auto owner = [&](uint32_t x) { return (int)(((x + 1) * (uint32_t)grid - 1) / T); };
+    const int w0 = owner((uint32_t)(t * nk)), S = owner((uint32_t)((t + 1) * nk - 1)) - w0 + 1;
+    f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (size_t)t * p.splits * FR * NT;
+    // the partial leaves by sc1 (write-through) stores, drained by every storing wave before the
+    // ticket: no agent-scope release, whose L2 write-back of EVERY dirty line of the XCD (this
+    // launch's whole output stream) cost ~6x the kernel's time (MI355X guide, publish-large); the
+    // last arriver still acquires before reading the slabs
+    const __amdgpu_buffer_rsrc_t wsr = make_rsrc(p.ws, (uint32_t)(p.ws_floats * 4 < 0x7fffffff ? p.ws_floats * 4 : 0x7fffffff));
+    const uint32_t sbase = (uint32_t)(((size_t)t * p.splits + (first - w0)) * FR * NT + tid) * 16u;
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const f32x4 a = acc[ii][j];
+        const u32x4 v = {__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]), __float_as_uint(a[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, wsr, sbase + (uint32_t)((ii * NI + j) * NT) * 16u, 0, 16 /* sc1 */);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned got = __hip_atomic_fetch_add(p.cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = got == (unsigned)(S - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.cnt + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *skflag = last;
+    }
+    __syncthreads();
+    if (*skflag != 0) {
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[ii][j] = slab[(size_t)(ii * NI + j) * NT + tid];
+      for (int sh = 1; sh < S; ++sh) {
+#pragma unroll
+        for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[ii][j] += slab[((size_t)sh * FR + ii * NI + j) * NT + tid];
+      }
+      epilogue(t);
+    } else {
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   };
 
   auto read = [&](int g, P3Frags<TM, TN, KW / 32>& f) {
@@ -209,20 +319,39 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
     issue(s);
     advance();
   }
-  const int nsteps = mine * nk;
   constexpr int FREGS = (MI + NI) * NPL * 4 * (KW / 32), AREGS = MI * NI * 4;
   constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 64 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 64 : 400;
   constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET;
   constexpr int NMF = (KW / 32) * MI * NI * 6, NRD = (KW / 32) * (MI + NI) * NPL;
-  int i = 0, k = 0;  // the compute side's local tile and k-step
-  // after the MFMAs of step g: the tile's epilogue once its last k-step is in
-  auto post = [&]() {
-    if (++k == nk) {
-      epilogue(i);
-      k = 0;
-      ++i;
+  int i = 0, k = 0;  // the compute side's local tile (SK: segment) and k-step
+  // SK: the first segment starts at k-step x0 % nk (a later one at 0); k counts the steps since the
+  // last segment end once one has ended (i > 0)
+  if constexpr (SK) k = x0 % nk;
+  // after the MFMAs of step g: the tile's epilogue once its last k-step is in (SK: the segment's
+  // epilogue or hand-off at a tile end or the share's end)
+  auto post = [&](int g) __attribute__((always_inline)) {
+    if constexpr (SK) {
+      const bool tile_end = ++k == nk;
+      if (tile_end || g + 1 == nsteps) {
+        const int t = (x0 + g) / nk;
+        if (tile_end && (i > 0 || x0 % nk == 0))  // the segment ran the whole tile
+          epilogue(t);
+        else
+          partial(t);
+        ++i;
+        k = 0;
+      }
+    } else {
+      if (++k == nk) {
+        epilogue(first + i * grid);
+        k = 0;
+        ++i;
+      }
     }
   };
+  // "an epilogue's EOPS instructions were issued after the awaited slot's DMA": the first steps after
+  // a segment end (after an SK hand-off every older instruction has drained: any count is safe)
+  auto after_epi = [&](int lim) { return i > 0 && k <= lim; };
   if constexpr (PIPE) {
     P3Frags<TM, TN, KW / 32> fr[2];
     wait_vmcnt<(NST - 1) * LOADS>();
@@ -232,7 +361,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
     auto body = [&](int g, P3Frags<TM, TN, KW / 32>& cur, P3Frags<TM, TN, KW / 32>& nxt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot g are done
       // slot g+1 has landed for this thread
-      if (i > 0 && k <= NST - 2)
+      if (after_epi(NST - 2))
         wait_vmcnt<(NST - 2) * LOADS + EOPS>();
       else
         wait_vmcnt<(NST - 2) * LOADS>();
@@ -243,7 +372,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
       p3_mma<TM, TN, KW / 32>(cur, acc);
       ilv_schedule<NMF, LOADS, NRD>();
       advance();
-      post();
+      post(g);
     };
     for (int g = 0; g < nsteps; g += 2) {
       body(g, fr[0], fr[1]);
@@ -253,7 +382,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
     P3Frags<TM, TN, KW / 32> fr;
     for (int g = 0; g < nsteps; ++g) {
       // slot g has landed: NST-1 later slot issues, plus the previous epilogue when it came after
-      if (i > 0 && k <= NST - 1)
+      if (after_epi(NST - 1))
         wait_vmcnt<(NST - 1) * LOADS + EOPS>();
       else
         wait_vmcnt<(NST - 1) * LOADS>();
@@ -267,7 +396,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
       p3_mma<TM, TN, KW / 32>(fr, acc);
       ilv_schedule<NMF, LOADS, 0>();
       advance();
-      post();
+      post(g);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy pieces have landed before the LDS is freed
@@ -317,6 +446,66 @@ static bool launch_p3p(const ConvParams& p, hipStream_t st) {
   else
     hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, OCC>), dim3(grid), b, lds, st,
                        p);
+  return true;
+}
+
+// cfg 23-27: the stream-K form of cfg 18-22 (same tiles and ring). False when the problem needs an
+// epilogue feature the persistent kernel does not have, or the split-K workspace cannot hold every
+// tile's shares (the caller then tries the whole-tile persistent cfg, then the twin).
+template <int WM, int WN, int TM, int TN, int KW, int NST, int OCC>
+static bool launch_p3sk(const ConvParams& p0, hipStream_t st) {
+  constexpr int BM = WM * TM, BN = WN * TN;
+  ConvParams p = p0;
+  const bool stats = p.stats != nullptr;
+  const int nk = p.Kpad / KW;
+  const size_t ring = p3p_ring_bytes<BM, BN, KW, NST>();
+  const size_t lds = ring + (stats ? (size_t)p.Nout * 4 : 0) + 16;  // + the last-arriver word
+  if (p.bnb_acc != nullptr || p.remap || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || p.beta ||
+      p.bias != nullptr || !p.out_f32 || p.ws == nullptr || p.cnt == nullptr ||
+      (stats && p.stats_R <= 0) || nk < NST - 1 || p.Kpad % KW != 0 || lds > 160 * 1024 ||
+      (size_t)p.M * p.ldy * 4 >= (1ull << 31))
+    return false;
+  const bool cbig = (p.C % KW) == 0;
+  static bool once = false;
+  if (!once) {
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, true, OCC, true>);
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, OCC, true>);
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, true, OCC, true>);
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, OCC, true>);
+    once = true;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int ntiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
+  const long long T = (long long)ntiles * nk;
+  const int per_cu = (int)((160 * 1024) / lds) < OCC ? (int)((160 * 1024) / lds) : OCC;
+  const int slots = cus * (per_cu > 0 ? per_cu : 1);
+  const int grid = (int)(T < slots ? T : slots);
+  if ((T + 1) * grid >= (1ll << 32)) return false;  // the kernel's share arithmetic is 32-bit
+  // shares of any tile: the shares meeting nk consecutive iterations, each share >= T / grid long
+  const int smax = (int)((nk - 1) / (T / grid) + 2);
+  if ((long long)ntiles * smax * BM * BN > p.ws_floats || ntiles > p.cnt_n) return false;
+  p.splits = smax;
+  static const bool probe = getenv("HCB_SK_PROBE") != nullptr && getenv("HCB_SK_PROBE")[0] == '1';
+  if (probe) p.cnt = nullptr;  // tools/diag/sk_probe.sh: the main loop alone, hand-offs skipped (wrong output)
+  const dim3 b(WM * WN * 64);
+  if (cbig && stats)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, true, OCC, true>), dim3(grid), b, lds, st,
+                       p);
+  else if (cbig)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, OCC, true>), dim3(grid), b, lds,
+                       st, p);
+  else if (stats)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, true, OCC, true>), dim3(grid), b, lds,
+                       st, p);
+  else
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, OCC, true>), dim3(grid), b, lds,
+                       st, p);
   return true;
 }
 

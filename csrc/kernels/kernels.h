@@ -70,6 +70,8 @@ struct ConvParams {
   int splits;
   float* ws;
   unsigned* cnt;
+  int64_t ws_floats;  // capacity of ws / cnt (set whenever the workspace is registered)
+  int cnt_n;
   // plane GEMMs (conv_p3.hip, the fp32 path): the mid and lo bf16 weight packs beside w (hi)
   const void* w_lo;
   const void* w_lo2;

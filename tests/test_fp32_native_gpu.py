@@ -49,7 +49,7 @@ CASES = [(64, 256, 1, 1, 0, 14), (64, 64, 3, 1, 1, 14), (128, 128, 3, 2, 1, 14),
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}s{c[3]}")
 @pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
-                                 (0, 2), (4, 3), (7, 2), (10, 3), (14, 3), (16, 5), (17, 6)],
+                                 23, 24, 25, 26, 27, 28, 29, 30, (0, 2), (4, 3), (7, 2), (10, 3), (14, 3), (16, 5), (17, 6)],
                          ids=str)
 def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     """bf16x6 on planes reproduces the fp32 convolution to fp32 accuracy (~1e-6): fwd, data grad
@@ -58,7 +58,7 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     planes by the ops themselves. cfg 7-13: 32-deep slots (64-byte LDS rows) and 128x128 / 256x128
     block tiles; (cfg, S): in-launch split-K (fixed-order slab sum); weight-grad cfg 6-11: 32-deep slots, up to 256x128 / 128x256; fwd cfg 14-17 / weight-grad 12-15: two or
     three workgroups per CU; 18-22: the persistent short-K kernel (conv_p3_persist.h; the strided
-    data gradients' remap form runs its twin)."""
+    data gradients' remap form runs its twin); 23-27: its stream-K form."""
     cin, cout, k, s, pad, H = case
     spec, p, pk, ps = _conv(cin, cout, k, s, pad)
     assert Fn.lo_pack(pk.pack) is not None and Fn.lo_pack(pk.tr) is not None
@@ -121,15 +121,18 @@ def test_strided_1x1_dgrad_zeroes_its_cells(H, f32):
         set_gpu_compute_dtype(torch.bfloat16)
 
 
-@pytest.mark.parametrize("cfg", [18, 19, 20, 21, 22])
-@pytest.mark.parametrize("shape", [(64, 256, 1, 56, 16), (256, 96, 1, 23, 5), (64, 64, 3, 30, 3)],
+@pytest.mark.parametrize("cfg", [18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30])
+@pytest.mark.parametrize("shape", [(64, 256, 1, 56, 16), (256, 96, 1, 23, 5), (64, 64, 3, 30, 3), (256, 256, 3, 14, 4)],
                          ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}H{c[3]}N{c[4]}")
 def test_fp32_persistent_short_k_gemm(fp32_mode, cfg, shape):
     """The persistent plane GEMM (conv_p3_persist.h): each workgroup walks several tiles with the
     LDS-DMA ring running across tile boundaries (16 x 56 x 56 rows: 3-6 tiles per workgroup), row
     and column tails (2645 rows, 96 outputs against 64 / 128-wide tiles), a 3x3 (18 k-steps); the
     register epilogue's output, ReLU and BN statistics (shifted sums in STAT_R replicas) against
-    fp64, and the deterministic mode's one-replica-per-64-rows statistics bitwise reproducible."""
+    fp64, and the deterministic mode's one-replica-per-64-rows statistics bitwise reproducible.
+    cfg 23-27: the stream-K form -- equal (tile, k-step) shares per workgroup, split tiles summed
+    through the workspace (256x256 3x3 at 14 x 14 x 4: 14 tiles x 72 k-steps over the grid, up to
+    ~20 shares per tile), bitwise reproducible output and statistics."""
     cin, cout, k, H, N = shape
     pad = k // 2
     spec, p, pk, ps = _conv(cin, cout, k, 1, pad)
@@ -168,8 +171,8 @@ def test_fp32_persistent_short_k_gemm(fp32_mode, cfg, shape):
     for _ in range(2):
         a = torch.zeros(Rd * 2 * cout, device=DEV)
         Fn.conv_forward(x, spec, pk.pack, p.data, y2, stats=a, stats_R=Rd, cfg=cfg, stats_shift=shift)
-        runs.append(a)
-    assert torch.equal(runs[0], runs[1])
+        runs.append((a, y2.clone()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
 
 
 @pytest.mark.parametrize("C", [64, 256, 2048])

@@ -70,3 +70,14 @@ def test_learning_rate_written_only_when_it_moves():
         seen.append(round(float(t.hyper[0]), 6))
     assert seen == [0.1, 0.1, 0.05, 0.05]
     assert t._lr_dev == 0.05
+
+
+def test_streamk_cfgs_share_the_persistent_tiles():
+    """cfg 23-27 are the stream-K form of the persistent cfg 18-22: same tiles / occupancy, no
+    split-K candidates of their own, and a plan that needs the split-K workspace."""
+    for sk, pc in Fn._P3_STREAMK.items():
+        assert Fn._P3_TILES[sk] == Fn._P3_TILES[pc] and Fn._P3_OCC.get(sk, 1) == Fn._P3_OCC.get(pc, 1)
+        assert Fn._P3_PERSIST[sk] == Fn._P3_PERSIST.get(pc, pc)
+    cands = Fn.p3_candidates(12544, 256, 2304)
+    assert {27} <= {c for c, _ in cands}
+    assert all(s == 1 for c, s in cands if c in Fn._P3_STREAMK)

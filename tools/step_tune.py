@@ -88,6 +88,22 @@ class StepTimer:
                     Fn._tuned[k] = v
 
 
+def aa_band(timer, rounds, reps=4):
+    """Interleaved A/A: the SAME table in both arms of an A/B with `rounds`
+    rounds (each measurement a fresh capture, as in ab()), repeated `reps` times. The band is the
+    largest |median(A) - median(A')|: the difference an A/B of two identical tables shows on this box,
+    in this process -- the drift of repeated captures included, which the old spread-of-6-captures
+    band (0.08%) missed (0.3-0.8% in round 5)."""
+    diffs = []
+    for _ in range(reps):
+        a, b = [], []
+        for _ in range(rounds):
+            a.append(timer.measure())
+            b.append(timer.measure())
+        diffs.append(abs(statistics.median(a) - statistics.median(b)))
+    return max(diffs), diffs
+
+
 def ab(timer, key, cur, cand, rounds):
     """Interleaved A/B of one problem's plan: medians (ms/step) of the current and the candidate."""
     a, b = [], []
@@ -126,6 +142,8 @@ def main():
     ap.add_argument("--twins", action="store_true",
                     help="fp32: try only the persistent twin of each problem's current tile (conv_p3_persist.h)")
     ap.add_argument("--budget_s", type=float, default=900.0)
+    ap.add_argument("--aa_only", action="store_true", help="measure and print the interleaved A/A band only")
+    ap.add_argument("--aa_reps", type=int, default=4)
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
     a = ap.parse_args()
     t_start = time.time()
@@ -148,7 +166,7 @@ def main():
 
     # isolated timing of every candidate (ranking and candidate shortlist)
     iso = {}
-    for k, (cnt, cands, run) in probs.items():
+    for k, (cnt, cands, run) in ([] if a.aa_only else probs.items()):
         iso[k] = {json.dumps(c): autotune._time(lambda: run(c)) for c in cands}
         cur = json.dumps(Fn._tuned[k] if not isinstance(Fn._tuned[k], tuple) else list(Fn._tuned[k]))
         if cur not in iso[k]:
@@ -163,7 +181,8 @@ def main():
         return json.dumps(list(v) if isinstance(v, tuple) else v)
 
     kinds = [k for k in a.kinds.split(",") if k]
-    order = sorted((k for k in probs if not kinds or k[0] in kinds), key=lambda k: -iso[k][cur_s(k)] * probs[k][0])
+    order = [] if a.aa_only else sorted((k for k in probs if not kinds or k[0] in kinds),
+                                        key=lambda k: -iso[k][cur_s(k)] * probs[k][0])
 
     images, labels = synthetic_batch(model, a.batch)
     trainer = Trainer(model, a.batch, resnet_lr_schedule(a.batch), use_graph=True)
@@ -171,10 +190,13 @@ def main():
         trainer.step(images, labels)
     timer = StepTimer(trainer, images, labels, a.reps)
     base = [timer.measure() for _ in range(6)]
-    noise = (max(base) - min(base)) / 2
     t0 = statistics.median(base)
-    log(f"[step_tune] start: {t0:.4f} ms/step (6 captures: {' '.join(f'{x:.4f}' for x in base)}; "
-        f"noise band {noise:.4f} ms)")
+    noise, diffs = aa_band(timer, a.rounds, a.aa_reps)
+    log(f"[step_tune] start: {t0:.4f} ms/step (6 captures: {' '.join(f'{x:.4f}' for x in base)}; spread "
+        f"{max(base) - min(base):.4f} ms); interleaved A/A band {noise:.4f} ms = {100 * noise / t0:.2f}% "
+        f"({a.aa_reps} A/As of {a.rounds} rounds: {' '.join(f'{d:.4f}' for d in diffs)})")
+    if a.aa_only:
+        return
 
     trials = []
     for k in order[:a.top]:
