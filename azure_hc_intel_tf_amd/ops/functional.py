@@ -57,6 +57,15 @@ def deterministic() -> bool:
     return _DET[0]
 
 
+def set_p3p_bnb(level: int) -> None:
+    """Fused BN-backward data gradients on the persistent plane GEMMs (conv_p3_persist.h BNB): 0
+    never (the non-persistent twin runs; the default: level 1 measured 0.38% slower in the fp32 step,
+    profiles/r6_persistent_bnb.txt), 1 ReLU modes 0 / 2, 2 every mode. Takes effect at the next
+    launch (a captured step graph must be re-captured). Env default: HCB_P3P_BNB."""
+    for ns in _ext.loaded_namespaces():
+        ns.set_p3p_bnb(int(level))
+
+
 def det_replicas(M: int) -> int:
     """Accumulator replicas for an M-row BN layer in deterministic mode: one per 64 rows covers
     every GEMM row tile (tiles are >= 64 rows) and every BN-backward row block."""

@@ -205,6 +205,11 @@ void set_splitk_workspace(const Tensor& ws, const Tensor& cnt) {
   g_splitk_cnt_n = cnt.numel();
 }
 
+void set_p3p_bnb(int64_t v) {
+  TORCH_CHECK(v >= 0 && v <= 2, "hcb.set_p3p_bnb: 0, 1 or 2");
+  hcb::set_p3p_bnb((int)v);
+}
+
 const float* opt_f32(const c10::optional<Tensor>& t, int64_t n, const char* what) {
   if (!t.has_value()) return nullptr;
   check_f32(*t, what);
@@ -1231,6 +1236,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_igemm_bnb(Tensor x, Tensor w, Tensor(a!) y, Tensor? yres, int[] geom, int cfg, Tensor z, Tensor? yact, int ld, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta, Tensor(b!) acc, int R, int mode) -> ()");
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
+  m.def("set_p3p_bnb(int v) -> ()", set_p3p_bnb);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
   m.def("bn_stats(Tensor x, int M, int C, int ldx, Tensor(a!) slab) -> ()");
   m.def("bn_partials(int M, int C) -> int", bn_partials);

@@ -63,6 +63,8 @@ static int launch_p3_persist(const ConvParams& p, int cfg, hipStream_t st) {
   }
 }
 
+void set_p3p_bnb(int v) { p3p_bnb_level() = v; }
+
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st) {
   if (cfg >= 18 && (cfg = launch_p3_persist(p, cfg, st)) < 0) return;
   if (p.bnb_acc != nullptr)

@@ -62,7 +62,15 @@ constexpr size_t p3p_ring_bytes() {
 // arriver acquires, sums every share's slab in share order -- run-to-run deterministic -- and runs
 // the epilogue). Only a share's first and last segments can be split tiles, so a workgroup pays at
 // most two hand-offs, and the spin-free protocol cannot deadlock whatever the residency.
-template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool STATS, int OCC, bool SK = false>
+//
+// BNB (a data gradient whose output is a BN layer's dy, conv_p3_fwd.h's fused BN-backward epilogue
+// from the registers): per tile, z (fp32), the ReLU-mask source (mode 1: the bf16 hi plane of y) and
+// the beta-accumulate source (fp32) of the lane's accumulator elements are loaded in two chunks of
+// wave rows (one memory round trip each), g = (acc [+ beta]) gated, stored fp32, and sum(g) /
+// sum(g * xhat) reduced per column by shuffles into one buffer atomic per column and wave (replica =
+// the wave's 64-row block, as the statistics) -- EOPS vector-memory instructions after the loads.
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool STATS, int OCC, bool SK = false,
+          bool BNB = false>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
@@ -74,7 +82,8 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   constexpr int STAGE = (int)p3_stage_bytes<BM, BN, KW>();
   // epilogue vector-memory instructions; EDRAIN (64 x 64 wave tiles: more than the vmcnt field can
   // count beside the ring): the epilogue drains itself instead and the ring's waits count 0 for it
-  constexpr int EOPS_N = MI * NI * 4 + (STATS ? 2 * NI : 0);
+  static_assert(!(STATS && BNB), "a data gradient has no forward statistics");
+  constexpr int EOPS_N = MI * NI * 4 + (STATS || BNB ? 2 * NI : 0);
   constexpr bool EDRAIN = LOADS * (NST - 1) + EOPS_N > 63;
   constexpr int EOPS = EDRAIN ? 0 : EOPS_N;
   static_assert(TM >= 32, "at most two adds per statistics slot and tile (deterministic mode)");
@@ -117,7 +126,13 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   const __amdgpu_buffer_rsrc_t wr1 = make_rsrc(p.w_lo, p.w_bytes);
   const __amdgpu_buffer_rsrc_t wr2 = make_rsrc(p.w_lo2, p.w_bytes);
   const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, (uint32_t)((size_t)p.M * p.ldy * 4));
-  const __amdgpu_buffer_rsrc_t sr = make_rsrc(p.stats, STATS ? (uint32_t)((size_t)p.stats_R * 2 * p.Nout * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t sr = BNB ? make_rsrc(p.bnb_acc, (uint32_t)((size_t)p.bnb_R * 2 * p.Nout * 4))
+                                       : make_rsrc(p.stats, STATS ? (uint32_t)((size_t)p.stats_R * 2 * p.Nout * 4) : 0u);
+  // BNB operands: z and the beta source fp32 (row strides bnb_ld / ldy), y's hi plane bf16 (bnb_ld)
+  const __amdgpu_buffer_rsrc_t zr = make_rsrc(BNB ? p.bnb_z : p.y, BNB ? (uint32_t)((size_t)p.M * p.bnb_ld * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t br = make_rsrc(BNB && p.beta ? p.yres : p.y, BNB && p.beta ? (uint32_t)((size_t)p.M * p.ldy * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t mr = make_rsrc(BNB && p.bnb_mode == 1 ? p.bnb_y : p.y,
+                                              BNB && p.bnb_mode == 1 ? (uint32_t)((size_t)p.M * p.bnb_ld * 2) : 0u);
 
   if constexpr (STATS) {  // published by the first barrier; older than every DMA (vmcnt order)
     for (int c = tid; c < p.Nout; c += NT) ktab[c] = p.stats_shift != nullptr ? p.stats_shift[c] : 0.f;
@@ -194,6 +209,87 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
     const int tm = t / tiles_n, tn = t - tm * tiles_n;
     const int rbase = tm * BM + wm * TM;           // the wave's first row
     const int cbase = tn * BN + wn * TN + frow;    // the lane's column in fragment j = 0
+    if constexpr (BNB) {
+      float mu[NI], is[NI], sc[NI], sh[NI], s1[NI], s2[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = cbase + j * 16;
+        const bool cok = col < p.Nout;
+        mu[j] = cok ? p.bnb_mean[col] : 0.f;
+        is[j] = cok ? p.bnb_invstd[col] : 0.f;
+        sc[j] = (cok ? p.bnb_gamma[col] : 0.f) * is[j];
+        sh[j] = (cok ? p.bnb_beta[col] : 0.f) - mu[j] * sc[j];
+        s1[j] = 0.f;
+        s2[j] = 0.f;
+      }
+      const int mode = p.bnb_mode;
+      const bool beta = p.beta != 0;
+      constexpr int HC = MI > 1 ? MI / 2 : 1;  // wave-row fragments per chunk
+#pragma unroll
+      for (int c0 = 0; c0 < MI; c0 += HC) {
+        float zf[HC][4][NI], rf[HC][4][NI];
+        uint32_t yb[HC][4][NI];
+#pragma unroll
+        for (int ii = 0; ii < HC; ++ii)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = rbase + (c0 + ii) * 16 + fq * 4 + e;
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+              const int col = cbase + j * 16;
+              const bool ok = (row < p.M) & (col < p.Nout);
+              zf[ii][e][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                  zr, ok ? (uint32_t)(row * p.bnb_ld + col) * 4u : HCB_OOB, 0, 0));
+              rf[ii][e][j] = beta ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                        br, ok ? (uint32_t)(row * p.ldy + col) * 4u : HCB_OOB, 0, 0))
+                                  : 0.f;
+              yb[ii][e][j] = mode == 1 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
+                                             mr, ok ? (uint32_t)(row * p.bnb_ld + col) * 2u : HCB_OOB, 0, 0)
+                                       : 0u;
+            }
+          }
+#pragma unroll
+        for (int ii = 0; ii < HC; ++ii)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = rbase + (c0 + ii) * 16 + fq * 4 + e;
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+              const int col = cbase + j * 16;
+              const bool ok = (row < p.M) & (col < p.Nout);
+              const float z = zf[ii][e][j];
+              float g = acc[c0 + ii][j][e] + rf[ii][e][j];
+              if (mode == 1)
+                g = __uint_as_float(yb[ii][e][j] << 16) > 0.f ? g : 0.f;  // the hi plane: > 0 exactly when y > 0
+              else if (mode == 2)
+                g = (z * sc[j] + sh[j]) > 0.f ? g : 0.f;
+              g = ok ? g : 0.f;
+              s1[j] += g;
+              s2[j] += g * ((z - mu[j]) * is[j]);
+              buf_store_f32(yr, ok ? (uint32_t)(row * p.ldy + col) * 4u : HCB_OOB, g);
+            }
+          }
+      }
+      const uint32_t rep = (uint32_t)((rbase >> 6) % p.bnb_R) * 2u * (uint32_t)p.Nout;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        float a = s1[j], b = s2[j];
+        a += __shfl_xor(a, 16, 64);
+        b += __shfl_xor(b, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        b += __shfl_xor(b, 32, 64);
+        const int col = cbase + j * 16;
+        const bool own = (fq == 0) & (col < p.Nout);
+        buf_atomic_add_f32(sr, own ? (rep + (uint32_t)col) * 4u : HCB_OOB, a);
+        buf_atomic_add_f32(sr, own ? (rep + (uint32_t)(p.Nout + col)) * 4u : HCB_OOB, b);
+      }
+      if constexpr (EDRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
     if constexpr (STATS) {
       const int wrows = p.M - rbase;
       const uint32_t rep = (uint32_t)((rbase >> 6) % p.stats_R) * 2u * (uint32_t)p.Nout;
@@ -402,8 +498,18 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy pieces have landed before the LDS is freed
 }
 
+// kernels.h set_p3p_bnb
+inline int& p3p_bnb_level() {
+  static int v = [] {
+    const char* e = std::getenv("HCB_P3P_BNB");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 // cfg 18-22 (persistent twins of cfg 15, 14, 16, 17, 7): false when the problem needs an epilogue
-// feature this kernel does not have (the caller then launches the twin)
+// feature this kernel does not have (the caller then launches the twin). A fused BN-backward data
+// gradient (bnb_acc) runs the BNB instantiation.
 template <int WM, int WN, int TM, int TN, int KW, int NST, int OCC>
 static bool launch_p3p(const ConvParams& p, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
@@ -411,14 +517,19 @@ static bool launch_p3p(const ConvParams& p, hipStream_t st) {
   const int nk = p.Kpad / KW;
   const size_t ring = p3p_ring_bytes<BM, BN, KW, NST>();
   const size_t lds = ring + (stats ? (size_t)p.Nout * 4 : 0);
-  if (p.bnb_acc != nullptr || p.remap || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || p.beta ||
-      p.bias != nullptr || !p.out_f32 ||
+  const bool bnb = p.bnb_acc != nullptr;
+  // the mode-1 mask is a 2-byte load per accumulator element (the hi plane of y): measured slower
+  // than the twin's vector prefetch, so only p3p_bnb_level() 2 runs it here
+  if ((bnb && (p3p_bnb_level() == 0 || (p.bnb_mode == 1 && p3p_bnb_level() < 2))) || p.remap || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || (p.beta && !bnb) ||
+      p.bias != nullptr || !p.out_f32 || (bnb && (stats || p.bnb_R <= 0 || p.bnb_mode < 0 || p.bnb_mode > 2)) ||
       (stats && p.stats_R <= 0) || nk < NST - 1 || p.Kpad % KW != 0 || lds > 160 * 1024 ||
-      (size_t)p.M * p.ldy * 4 >= (1ull << 31))
+      (size_t)p.M * p.ldy * 4 >= (1ull << 31) || (bnb && (size_t)p.M * p.bnb_ld * 4 >= (1ull << 31)))
     return false;
   const bool cbig = (p.C % KW) == 0;
   static bool once = false;
   if (!once) {
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, OCC, false, true>);
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, OCC, false, true>);
     p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, true, OCC>);
     p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, OCC>);
     p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, true, OCC>);
@@ -437,7 +548,13 @@ static bool launch_p3p(const ConvParams& p, hipStream_t st) {
   const int slots = cus * (per_cu > 0 ? per_cu : 1);
   const int grid = ntiles < slots ? ntiles : slots;
   const dim3 b(WM * WN * 64);
-  if (cbig && stats)
+  if (bnb && cbig)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, OCC, false, true>), dim3(grid), b,
+                       lds, st, p);
+  else if (bnb)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, OCC, false, true>), dim3(grid),
+                       b, lds, st, p);
+  else if (cbig && stats)
     hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, true, OCC>), dim3(grid), b, lds, st, p);
   else if (cbig)
     hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, OCC>), dim3(grid), b, lds, st, p);

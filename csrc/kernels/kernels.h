@@ -118,6 +118,10 @@ int wgrad_tile_n(int cfg);
 // fp32 convolutions on bf16 hi / mid / lo planes (conv_p3.hip): forward / data-gradient GEMM (x
 // planes, weight packs w / w_lo / w_lo2, fp32 output) and weight gradient (dy and x planes)
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st);
+// fused BN-backward data gradients on the persistent cfgs 18-27 (conv_p3_persist.h BNB): 0 never
+// (the twin runs; default -- 0.38% slower step with 1, profiles/r6_persistent_bnb.txt), 1 ReLU
+// modes 0 / 2, 2 every mode; initialised from HCB_P3P_BNB
+void set_p3p_bnb(int v);
 int p3_tile_m(int cfg);
 int p3_tile_n(int cfg);
 int p3_slot_k(int cfg);

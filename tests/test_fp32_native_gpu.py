@@ -398,3 +398,57 @@ def test_fp32_fused_bn_backward_matches_unfused(fp32_mode, case, mode):
     s2 = (g.view(-1, cin) * xhat).sum(0)
     a = acc.double().sum(0)
     assert rel_err(a[0], s1) < 1e-5 and rel_err(a[1], s2) < 1e-5
+
+
+@pytest.mark.parametrize("cfg", [18, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize("case", [(96, 64, 1, 23, 5, False), (64, 64, 3, 30, 3, True), (256, 128, 1, 14, 4, True)],
+                         ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}H{c[3]}N{c[4]}acc{int(c[5])}")
+def test_fp32_persistent_fused_bn_backward(fp32_mode, cfg, case):
+    """The persistent plane GEMM's BNB register epilogue (conv_p3_persist.h, a fused BN-backward data
+    gradient walking several tiles per workgroup; cfg 23 -- stream-K -- falls back to it): g for
+    modes 0 / 1 / 2 with and without the beta source, row tails (2645 rows) and a 96-column tail,
+    sum(g) / sum(g * xhat) against fp64, and the deterministic replicas bitwise reproducible."""
+    cin, cout, k, H, N, accumulate = case
+    pad = k // 2
+    spec, p, pk, ps = _conv(cin, cout, k, 1, pad)
+    torch.manual_seed(11)
+    dzf = torch.randn(N, H, H, cout, device=DEV)
+    dz = Fn.to_planes(dzf)
+    wd = p.data.double().cpu().permute(0, 3, 1, 2)
+    xr = torch.zeros(N, cin, H, H, dtype=torch.float64, requires_grad=True)
+    torch.nn.functional.conv2d(xr, wd, padding=pad).backward(dzf.double().cpu().permute(0, 3, 1, 2))
+    ref = xr.grad.permute(0, 2, 3, 1)
+    z = torch.randn(N, H, H, cin, device=DEV) * 1.5 + 0.2
+    mean, invstd = torch.randn(cin, device=DEV) * 0.1, torch.rand(cin, device=DEV) + 0.5
+    gamma, beta = torch.rand(cin, device=DEV) + 0.5, torch.randn(cin, device=DEV) * 0.1
+    yf = torch.relu(torch.randn(N, H, H, cin, device=DEV))
+    y = Fn.to_planes(yf)
+    base = torch.randn(N, H, H, cin, device=DEV) if accumulate else None
+    M = N * H * H
+    xh = ((z.double() - mean.double()) * invstd.double()).cpu()
+    Fn.set_p3p_bnb(2)  # every mode on the persistent kernel (the default, 0, runs the twin)
+    for mode in (0, 1, 2):
+        g = ref + (base.double().cpu() if accumulate else 0)
+        if mode == 1:
+            g = g * (yf.cpu() > 0).double()
+        elif mode == 2:
+            g = g * ((xh * gamma.double().cpu() + beta.double().cpu()) > 0).double()
+        R = 8
+        acc = torch.zeros(R, 2, cin, device=DEV)
+        dx = base.clone() if accumulate else torch.zeros(N, H, H, cin, device=DEV)
+        bnb = Fn.BNBwdFuse(z, y, Fn.BNSaved(mean, invstd), gamma, beta, mode, acc, R)
+        Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate, cfg=(cfg, 1), bnb=bnb)
+        assert rel_err(dx, g) < 3e-6, mode
+        a = acc.double().sum(0).cpu()
+        assert rel_err(a[0], g.reshape(-1, cin).sum(0)) < 1e-5, mode
+        assert rel_err(a[1], (g.reshape(-1, cin) * xh.reshape(-1, cin)).sum(0)) < 1e-5, mode
+    Rd = Fn.det_replicas(M)
+    runs = []
+    for _ in range(2):
+        a = torch.zeros(Rd, 2, cin, device=DEV)
+        dx = base.clone() if accumulate else torch.zeros(N, H, H, cin, device=DEV)
+        Fn.conv_dgrad(dz, spec, pk.tr, p.data, dx, accumulate, cfg=(cfg, 1),
+                      bnb=Fn.BNBwdFuse(z, y, Fn.BNSaved(mean, invstd), gamma, beta, 2, a, Rd))
+        runs.append((a, dx))
+    Fn.set_p3p_bnb(0)
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])

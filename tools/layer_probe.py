@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--stats_r", type=int, default=8,
                     help="fwd: BN-statistics replicas of the epilogue (-1: no statistics, 0: per-tile slab)")
+    ap.add_argument("--bnb", type=int, default=-1,
+                    help="dgrad: fuse the consuming BN's backward reduction (ReLU mode 0/1/2) into the epilogue")
     a = ap.parse_args()
     dev = torch.device("cuda")
     m = create_model(a.model, device=dev, compute_dtype="fp32" if a.fp32 else None)
@@ -53,7 +55,15 @@ def main():
                                      cfg=cfg)
     elif a.op == "dgrad":
         dz, dx = mk((N, P, Q, K)), torch.zeros(N, H, W, C, device=dev, dtype=odt)
-        fn = lambda: Fn.conv_dgrad(dz, s, l.pack.tr, None, dx, False, cfg=cfg)
+        bnb = None
+        if a.bnb >= 0:
+            z = torch.randn(N, H, W, C, device=dev)
+            yb = Fn.to_planes(torch.relu(z)) if a.fp32 else torch.relu(z).bfloat16()
+            st = Fn.BNSaved(torch.zeros(C, device=dev), torch.ones(C, device=dev))
+            bacc = torch.zeros(8, 2, C, device=dev)
+            bnb = Fn.BNBwdFuse(z if a.fp32 else z.bfloat16(), yb, st, torch.ones(C, device=dev),
+                               torch.zeros(C, device=dev), a.bnb, bacc, 8)
+        fn = lambda: Fn.conv_dgrad(dz, s, l.pack.tr, None, dx, False, cfg=cfg, bnb=bnb)
     else:
         x, dz = mk((N, H, W, C)), mk((N, P, Q, K))
         dw = torch.zeros(K, s.K, device=dev)

@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--budget_s", type=float, default=900.0)
     ap.add_argument("--aa_only", action="store_true", help="measure and print the interleaved A/A band only")
     ap.add_argument("--aa_reps", type=int, default=4)
+    ap.add_argument("--knob_ab", default="",
+                    help="interleaved in-step A/B of a kernel switch instead of tuning: p3p_bnb:A:B")
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
     a = ap.parse_args()
     t_start = time.time()
@@ -166,7 +168,7 @@ def main():
 
     # isolated timing of every candidate (ranking and candidate shortlist)
     iso = {}
-    for k, (cnt, cands, run) in ([] if a.aa_only else probs.items()):
+    for k, (cnt, cands, run) in ([] if a.aa_only or a.knob_ab else probs.items()):
         iso[k] = {json.dumps(c): autotune._time(lambda: run(c)) for c in cands}
         cur = json.dumps(Fn._tuned[k] if not isinstance(Fn._tuned[k], tuple) else list(Fn._tuned[k]))
         if cur not in iso[k]:
@@ -181,7 +183,7 @@ def main():
         return json.dumps(list(v) if isinstance(v, tuple) else v)
 
     kinds = [k for k in a.kinds.split(",") if k]
-    order = [] if a.aa_only else sorted((k for k in probs if not kinds or k[0] in kinds),
+    order = [] if a.aa_only or a.knob_ab else sorted((k for k in probs if not kinds or k[0] in kinds),
                                         key=lambda k: -iso[k][cur_s(k)] * probs[k][0])
 
     images, labels = synthetic_batch(model, a.batch)
@@ -195,6 +197,19 @@ def main():
     log(f"[step_tune] start: {t0:.4f} ms/step (6 captures: {' '.join(f'{x:.4f}' for x in base)}; spread "
         f"{max(base) - min(base):.4f} ms); interleaved A/A band {noise:.4f} ms = {100 * noise / t0:.2f}% "
         f"({a.aa_reps} A/As of {a.rounds} rounds: {' '.join(f'{d:.4f}' for d in diffs)})")
+    if a.knob_ab:
+        name, va, vb = a.knob_ab.split(":")
+        setter = {"p3p_bnb": Fn.set_p3p_bnb}[name]
+        ta, tb = [], []
+        for _ in range(a.aa_reps * a.rounds):
+            setter(int(va))
+            ta.append(timer.measure())
+            setter(int(vb))
+            tb.append(timer.measure())
+        ma, mb = statistics.median(ta), statistics.median(tb)
+        log(f"[step_tune] knob {name}: {va} {ma:.4f} ms/step vs {vb} {mb:.4f} ms/step ({100 * (ma - mb) / ma:+.2f}%; "
+            f"A/A band {100 * noise / t0:.2f}%) A: {' '.join(f'{x:.4f}' for x in ta)} B: {' '.join(f'{x:.4f}' for x in tb)}")
+        return
     if a.aa_only:
         return
 
