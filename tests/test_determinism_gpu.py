@@ -54,9 +54,12 @@ def test_deterministic_mode_trains_like_default():
     assert bool(((trd >= lo - band) & (trd <= hi + band)).all()), (trd.tolist(), runs.tolist())
     # the first steps, before the chaos has amplified anything, against a tight fixed bound (a
     # regression of the deterministic split-K / statistics path shows up here, whatever the band):
-    # step 0 is the forward of identical weights (only the fp32 summation order differs)
+    # step 0 is the forward of identical weights (only the fp32 summation order differs; bf16
+    # activations turn a reordered sum into an occasional 1-ulp flip, so the default runs themselves
+    # spread by up to ~3e-3 at step 0 on this 4-image batch): within that spread of their mean
     mean = runs.mean(0)
-    assert abs(float(trd[0] - mean[0])) <= 1e-3 * abs(float(mean[0])), (trd.tolist(), runs.tolist())
+    tol0 = max(1e-3 * abs(float(mean[0])), float(hi[0] - lo[0]))
+    assert abs(float(trd[0] - mean[0])) <= tol0, (trd.tolist(), runs.tolist())
     assert abs(float(trd[1] - mean[1])) <= 3e-2 * abs(float(mean[1])), (trd.tolist(), runs.tolist())
     # (a stable learning rate: at 0.05 this tiny-batch run diverges)
     assert float(trd[-1]) < float(trd[0]) - 2.0 and float(runs[:, -1].max()) < float(runs[:, 0].min()) - 2.0
