@@ -625,19 +625,6 @@ def _conv_forward_p3(x, spec: ConvSpec, wpack, out, stats, bias, cfg, relu, stat
     return out
 
 
-def conv_forward_af32(z, spec: ConvSpec, wpack, out, sc, sh, cfg: int, stats=None, stats_R: int = 0,
-                      stats_shift=None) -> bool:
-    """Prologue-side BN fusion PROTOTYPE (conv_p3_fwd.h AF32): out = conv(relu(z *
-    sc + sh), W) with z the fp32 pre-BN tensor of the consumer conv's input BN: the GEMM's A loader
-    stages fp32 z (4 B/element) and applies BN + ReLU + the plane split in registers, so no
-    normalised plane tensor is read. 1x1 / cin % 64 == 0, cfg 8 or 13-16. False: not launched."""
-    N, H, W, C = z.shape
-    P, Q = spec.out_hw(H, W)
-    geom = [N, H, W, spec.cin_pad, ld(z), P, Q, spec.kh, spec.kw, spec.sh, spec.sw, spec.pt, spec.pl,
-            spec.dh, spec.dw, 1, 1, spec.cout, spec.K, spec.Kpad, ld(out), 0, P, Q, 1, 1, 0, 1, 0, int(stats_R), 1]
-    return bool(_ext.ops().conv_p3_af32(z, wpack, lo_pack(wpack), out, geom, int(cfg), sc, sh, stats, stats_shift))
-
-
 def _plan(cfg, M, N, K, device, taps: int = 1):
     """Normalise a cfg argument (None = tuned / heuristic, int, or (cfg, splits))."""
     if cfg is None:

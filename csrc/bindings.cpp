@@ -1137,36 +1137,6 @@ void conv_p3(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor&
   hcb::launch_conv_p3(p, (int)cfg, cur_stream());
 }
 
-// prologue-side BN fusion prototype (conv_p3_fwd.h AF32): x is the fp32 PRE-BN tensor, the loader
-// applies relu(x * sc + sh) per input channel and splits to planes. Returns false (nothing launched)
-// when the problem / cfg does not fit the prototype (1x1 / C % 64 == 0, no split-K, cfg 8, 13-16).
-bool conv_p3_af32(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor& y, at::IntArrayRef g, int64_t cfg,
-                  const Tensor& sc, const Tensor& sh, const c10::optional<Tensor>& stats,
-                  const c10::optional<Tensor>& stats_shift) {
-  TORCH_CHECK(x.scalar_type() == at::kFloat, "hcb.conv_p3_af32: fp32 x");
-  hcb::ConvParams p = conv_params(x, w, y, c10::nullopt, c10::nullopt, c10::nullopt, g, 0);
-  TORCH_CHECK(p.out_f32 && y.scalar_type() == at::kFloat, "hcb.conv_p3_af32: fp32 output");
-  TORCH_CHECK(w_lo.dim() == 2 && w_lo.size(0) == 2 && w_lo.stride(1) == 1 && w_lo.scalar_type() == w.scalar_type() &&
-                  w_lo.size(1) >= (int64_t)p.Nout * p.Kpad,
-              "hcb.conv_p3_af32: w_lo must be [2][>= Nout*Kpad] of the pack's type");
-  const Tensor m = w_lo.select(0, 0), l = w_lo.select(0, 1);
-  check_align16(m.data_ptr(), "w_lo[0]");
-  check_align16(l.data_ptr(), "w_lo[1]");
-  p.w_lo = m.data_ptr();
-  p.w_lo2 = l.data_ptr();
-  p.af_sc = opt_f32(sc, p.C, "sc");
-  p.af_sh = opt_f32(sh, p.C, "sh");
-  p.stats = nullptr;
-  if (stats.has_value()) {
-    check_f32(*stats, "stats");
-    TORCH_CHECK(p.stats_R > 0 && stats->numel() >= (int64_t)p.stats_R * 2 * p.Nout, "hcb.conv_p3_af32: stats buffer");
-    p.stats = stats->data_ptr<float>();
-  }
-  TORCH_CHECK(!stats_shift.has_value() || p.stats != nullptr, "hcb.conv_p3_af32: stats_shift without stats");
-  p.stats_shift = opt_f32(stats_shift, p.Nout, "stats_shift");
-  return hcb::launch_conv_p3_af32(p, (int)cfg, cur_stream());
-}
-
 // fp32 data gradient with the fused BN-backward epilogue (see conv_igemm_bnb): z fp32, yact the
 // activation's planes (mode 1), output g fp32
 void conv_p3_bnb(const Tensor& x, const Tensor& w, const Tensor& w_lo, const Tensor& y,
@@ -1267,7 +1237,6 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("conv_tiles_m(int M, int cfg) -> int", conv_tiles_m);
   m.def("set_splitk_workspace(Tensor ws, Tensor cnt) -> ()");
   m.def("set_p3p_bnb(int v) -> ()", set_p3p_bnb);
-  m.def("conv_p3_af32(Tensor x, Tensor w, Tensor w_lo, Tensor(a!) y, int[] geom, int cfg, Tensor sc, Tensor sh, Tensor(b!)? stats=None, Tensor? stats_shift=None) -> bool");
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int[] geom, int cfg, int splits) -> ()");
   m.def("bn_stats(Tensor x, int M, int C, int ldx, Tensor(a!) slab) -> ()");
   m.def("bn_partials(int M, int C) -> int", bn_partials);
@@ -1367,7 +1336,6 @@ HCB_TORCH_LIBRARY_IMPL(hcb, CUDA, m) {
   m.impl("conv_p3", conv_p3);
   m.impl("conv_wgrad_p3", conv_wgrad_p3);
   m.impl("conv_p3_bnb", conv_p3_bnb);
-  m.impl("conv_p3_af32", conv_p3_af32);
   m.impl("split_planes", split_planes);
   m.impl("merge_planes", merge_planes);
   m.impl("gap_fwd_p3", gap_fwd_p3);

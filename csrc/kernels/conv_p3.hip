@@ -65,17 +65,6 @@ static int launch_p3_persist(const ConvParams& p, int cfg, hipStream_t st) {
 
 void set_p3p_bnb(int v) { p3p_bnb_level() = v; }
 
-bool launch_conv_p3_af32(const ConvParams& p, int cfg, hipStream_t st) {
-  switch (cfg) {
-    case 8: return launch_p3_af32<4, 2, 32, 64, 32, 3, 1>(p, st);
-    case 13: return launch_p3_af32<2, 2, 64, 32, 32, 4, 1>(p, st);
-    case 14: return launch_p3_af32<2, 2, 64, 32, 32, 2, 2>(p, st);
-    case 15: return launch_p3_af32<2, 2, 32, 64, 32, 2, 2>(p, st);
-    case 16: return launch_p3_af32<2, 2, 32, 32, 32, 3, 2>(p, st);
-    default: return false;
-  }
-}
-
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st) {
   if (cfg >= 18 && (cfg = launch_p3_persist(p, cfg, st)) < 0) return;
   if (p.bnb_acc != nullptr)

@@ -55,43 +55,6 @@ __device__ __forceinline__ void p3_read(const u32x4* A, const u32x4* B, P3Frags<
   }
 }
 
-// AF32 fragment read: A from the two fp32 half-row images, relu(z * sc + sh) per channel (prm: sc[C]
-// then sh[C]; c0: the slot's first channel), split into the three planes in registers; B as p3_read
-template <int WM, int WN, int TM, int TN, int KW>
-__device__ __forceinline__ void p3_read_af32(const u32x4* A, const u32x4* B, const float* prm, int C, int c0,
-                                             P3Frags<TM, TN, KW / 32>& f, int wm, int wn, int lane) {
-  constexpr int MI = TM / 16, NI = TN / 16, BM = WM * TM, BN = WN * TN, CPR = KW / 8;
-  constexpr int AIMG = BM * CPR, BIMG = BN * CPR;
-  const int frow = lane & 15, fq = lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < KW / 32; ++ks) {
-    const int ch = ks * 4 + fq;
-    const int c = c0 + ch * 8;
-    const float4* ps = reinterpret_cast<const float4*>(prm + c);
-    const float4* ph = reinterpret_cast<const float4*>(prm + C + c);
-    const float4 s0 = ps[0], s1 = ps[1], h0 = ph[0], h1 = ph[1];
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int row = wm * TM + i * 16 + frow, o = row * CPR + (ch ^ p3_swz<KW>(row));
-      u32x4 a = A[o], b = A[AIMG + o];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a[e] = __float_as_uint(fmaxf(fmaf(__uint_as_float(a[e]), sc[e], sh[e]), 0.f));
-        b[e] = __float_as_uint(fmaxf(fmaf(__uint_as_float(b[e]), sc[4 + e], sh[4 + e]), 0.f));
-      }
-      split3_8(a, b, f.a[ks][0][i], f.a[ks][1][i], f.a[ks][2][i]);
-    }
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int row = wn * TN + j * 16 + frow, o = row * CPR + (ch ^ p3_swz<KW>(row));
-#pragma unroll
-      for (int t = 0; t < NPL; ++t) f.b[ks][t][j] = B[t * BIMG + o];
-    }
-  }
-}
-
 // the KS x MI x NI x 6 MFMAs of the slot on register fragments (small terms first)
 template <int TM, int TN, int KS>
 __device__ __forceinline__ void p3_mma(const P3Frags<TM, TN, KS>& f, f32x4 (&acc)[TM / 16][TN / 16]) {
@@ -140,29 +103,20 @@ template <int OCC, int NW>
 constexpr int p3_regs_per_wave() {
   return 512 / (OCC * NW / 4 > 0 ? OCC * NW / 4 : 1);
 }
-//
-// AF32 (prologue-side BN fusion prototype): the A operand is the PRE-BN fp32
-// tensor z; the ring holds it as two 64-byte half-row images (channels 0-3 / 4-7 of each lane's
-// 8-channel chunk: 4 bytes/element in LDS and HBM instead of the planes' 6), and the fragment read
-// applies relu(z * sc[c] + sh[c]) (per-channel BN scale / shift staged in LDS) and splits the result
-// into the hi / mid / lo planes in registers. 1x1 / CBIG, no split-K, no BNB.
-template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool LHSDIL, bool BNB, int OCC = 1,
-          bool AF32 = false>
+template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool LHSDIL, bool BNB, int OCC = 1>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, CPR = KW / 8, RB = KW * 2;  // threads; chunks and bytes per LDS row
   constexpr int RP = NT / CPR;                                    // tile rows per load pass
   constexpr int AV = BM / RP, BV = BN / RP;
-  constexpr int NPA = AF32 ? 2 : NPL;  // A images per slot
-  constexpr int LOADS = NPA * AV + NPL * BV;  // LDS-DMA instructions per thread per slot
+  constexpr int LOADS = NPL * (AV + BV);  // LDS-DMA instructions per thread per slot
   constexpr int AIMG = BM * RB, BIMG = BN * RB;
-  constexpr int STAGE = AF32 ? (NPA * BM + NPL * BN) * RB : (int)p3_stage_bytes<BM, BN, KW>();
+  constexpr int STAGE = (int)p3_stage_bytes<BM, BN, KW>();
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 1) <= 63 && NST >= 2 && NST <= 4, "vmcnt range");
   static_assert(p3_param_off<BM, BN, WM, KW, NST>() + bnb_param_lds(BN) <= 160 * 1024,
                 "ring + BN parameters must fit LDS");
-  static_assert(!AF32 || (CBIG && !LHSDIL && !BNB), "AF32: the plain 1x1 / CBIG forward only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -180,14 +134,14 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
 
   const char* xb = reinterpret_cast<const char*>(p.x);
   const __amdgpu_buffer_rsrc_t xr0 = make_rsrc(xb, p.x_bytes);
-  const __amdgpu_buffer_rsrc_t xr1 = make_rsrc(xb + (AF32 ? 0 : p.x_plane), AF32 ? 0u : p.x_bytes);
-  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(xb + (AF32 ? 0 : 2 * (size_t)p.x_plane), AF32 ? 0u : p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr1 = make_rsrc(xb + p.x_plane, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t xr2 = make_rsrc(xb + 2 * (size_t)p.x_plane, p.x_bytes);
   const __amdgpu_buffer_rsrc_t wr0 = make_rsrc(p.w, p.w_bytes);
   const __amdgpu_buffer_rsrc_t wr1 = make_rsrc(p.w_lo, p.w_bytes);
   const __amdgpu_buffer_rsrc_t wr2 = make_rsrc(p.w_lo2, p.w_bytes);
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  ALoader<AV, CBIG, LHSDIL, RP, AF32 ? 4 : 2, KW> al;
+  ALoader<AV, CBIG, LHSDIL, RP, 2, KW> al;
   al.init(p, m0, tid, chunk);
   uint32_t b_off[BV];
 #pragma unroll
@@ -214,16 +168,11 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       if (!live) off[v] = HCB_OOB;
-      if constexpr (AF32) {  // the lane's 32 bytes (8 fp32 channels) as two 16-byte halves
-        glds16(xr0, sa + RP * v * RB, off[v]);
-        glds16(xr0, sa + AIMG + RP * v * RB, off[v] == HCB_OOB ? HCB_OOB : off[v] + 16u);
-      } else {
-        glds16(xr0, sa + RP * v * RB, off[v]);
-        glds16(xr1, sa + AIMG + RP * v * RB, off[v]);
-        glds16(xr2, sa + 2 * AIMG + RP * v * RB, off[v]);
-      }
+      glds16(xr0, sa + RP * v * RB, off[v]);
+      glds16(xr1, sa + AIMG + RP * v * RB, off[v]);
+      glds16(xr2, sa + 2 * AIMG + RP * v * RB, off[v]);
     }
-    char* sb = smem + stage * STAGE + NPA * AIMG + wid * WROWS * RB;
+    char* sb = smem + stage * STAGE + NPL * AIMG + wid * WROWS * RB;
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const uint32_t o = (b_off[v] == HCB_OOB || !live) ? HCB_OOB : b_off[v] + (uint32_t)kt * (uint32_t)RB;
@@ -232,14 +181,6 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
       glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
     }
   };
-  if constexpr (AF32) {  // BN scale / shift of every input channel, published by the first barrier
-    float* prm = reinterpret_cast<float*>(smem + (size_t)NST * STAGE);
-    for (int c = tid; c < p.C; c += NT) {
-      prm[c] = p.af_sc[c];
-      prm[p.C + c] = p.af_sh[c];
-    }
-    __syncthreads();
-  }
   if (kb > 0) al.seek(p, kb);
   EpiPrefetch<WM, WN, TM, TN, BNB, true> pre;
   pre.load_shift(p, n0, wn, lane);
@@ -256,13 +197,8 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
   };
   auto read = [&](int k, P3Frags<TM, TN, KW / 32>& f) {
     const char* sb = smem + (k % NST) * STAGE;
-    if constexpr (AF32)
-      p3_read_af32<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + NPA * AIMG),
-                                       reinterpret_cast<const float*>(smem + (size_t)NST * STAGE), p.C,
-                                       ((kb + k) * KW) % p.C, f, wm, wn, lane);
-    else
-      p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + NPL * AIMG), f,
-                                  wm, wn, lane);
+    p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + NPL * AIMG), f,
+                                wm, wn, lane);
   };
   // two register fragment sets when they fit (PIPE): slot k+1's fragment reads are in flight
   // while slot k's MFMAs run, and ONE barrier per slot both publishes slot k+1's DMA and retires
@@ -271,7 +207,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_igemm_p3_ke
   constexpr int FREGS = (MI + NI) * NPL * 4 * (KW / 32), AREGS = MI * NI * 4;
   constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 56 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 56 : 400;
   constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET && !(BNB && RBUDGET < 400);
-  constexpr int NMF = (KW / 32) * MI * NI * 6, NRD = (KW / 32) * (MI * NPA + NI * NPL + (AF32 ? 4 : 0));
+  constexpr int NMF = (KW / 32) * MI * NI * 6, NRD = (KW / 32) * (MI + NI) * NPL;
   if constexpr (PIPE) {
     // slot k+1 has landed for this thread once at most the NST - 2 slots after it are outstanding
     P3Frags<TM, TN, KW / 32> fr[2];
@@ -352,28 +288,6 @@ static void launch_p3(const ConvParams& p, hipStream_t st) {
   else
     hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, false, true, BNB, OCC>), dim3(tiles), dim3(NT),
                        lds, st, p);
-}
-
-// AF32 prototype launcher (1x1 / CBIG only; false when the problem does not fit it)
-template <int WM, int WN, int TM, int TN, int KW, int NST, int OCC = 1>
-static bool launch_p3_af32(const ConvParams& p, hipStream_t st) {
-  constexpr int BM = WM * TM, BN = WN * TN, NT = WM * WN * 64;
-  constexpr size_t STAGE = (size_t)(2 * BM + NPL * BN) * KW * 2;
-  const size_t lds_main = NST * STAGE + (size_t)p.C * 8;
-  const size_t lds_epi = igemm_epilogue_lds(BM, BN, WM);
-  const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
-  if ((p.C % 64) != 0 || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || p.bnb_acc != nullptr || p.remap ||
-      lds > 160 * 1024 || p.af_sc == nullptr || p.af_sh == nullptr)
-    return false;
-  static bool once = false;
-  if (!once) {
-    p3_set_lds_once(conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, false, OCC, true>);
-    once = true;
-  }
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.Nout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_igemm_p3_kernel<WM, WN, TM, TN, KW, NST, true, false, false, OCC, true>), dim3(tiles),
-                     dim3(NT), lds, st, p);
-  return true;
 }
 
 // p3 cfg (block tile, waves x wave tile, slot depth, ring slots):

@@ -63,9 +63,6 @@ struct ConvParams {
   const float *bnb_mean, *bnb_invstd, *bnb_gamma, *bnb_beta;
   float* bnb_acc;
   int bnb_mode, bnb_R, bnb_ld;
-  // prologue-side BN fusion prototype (conv_p3_fwd.h AF32): x is the fp32 pre-BN tensor, the A
-  // loader applies relu(x * af_sc[c] + af_sh[c]) per input channel and splits to planes
-  const float *af_sc, *af_sh;
   // In-launch split-K (LDS-DMA kernels): `splits` blocks per output tile each reduce a
   // contiguous k-step range; all but the last arriver park fp32 partials in ws slabs
   // [tile][split][tile elems], the last one (agent-scope ticket in cnt[tile], self-resetting)
@@ -121,8 +118,6 @@ int wgrad_tile_n(int cfg);
 // fp32 convolutions on bf16 hi / mid / lo planes (conv_p3.hip): forward / data-gradient GEMM (x
 // planes, weight packs w / w_lo / w_lo2, fp32 output) and weight gradient (dy and x planes)
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st);
-// the AF32 prototype (cfg 8, 13, 14, 15, 16); false when the problem or cfg does not fit it
-bool launch_conv_p3_af32(const ConvParams& p, int cfg, hipStream_t st);
 // fused BN-backward data gradients on the persistent cfgs 18-27 (conv_p3_persist.h BNB): 0 never
 // (the twin runs; default -- 0.38% slower step with 1, profiles/r6_persistent_bnb.txt), 1 ReLU
 // modes 0 / 2, 2 every mode; initialised from HCB_P3P_BNB
