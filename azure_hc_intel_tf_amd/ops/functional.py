@@ -301,13 +301,10 @@ _CONV_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128),
 # round 5: profiles/r5_prune_variants.txt)
 PATCH_CFG0 = 17
 PATCH_CFGS = (17, 18, 19, 20, 21)
-# weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-14 LDS-DMA rings; 15-22 the plane
-# weight-gradient kernel's one-plane form (conv_p3_wgrad.h NP = 1: LDS-DMA ring, transposed fragment
-# reads, double-buffered register fragments; 19-22 two per CU)
+# weight-grad cfg -> (Nout tile, K tile); 0-2 register-staged, 3-14 LDS-DMA rings
 _WGRAD_TILES = {0: (128, 128), 1: (64, 128), 2: (64, 64), 3: (128, 128), 4: (128, 128), 5: (256, 128),
                 6: (128, 256), 7: (64, 128), 8: (64, 64), 9: (64, 128), 10: (64, 64), 11: (128, 64),
-                12: (64, 128), 13: (128, 64), 14: (64, 128), 15: (128, 128), 16: (128, 128), 17: (256, 128),
-                18: (128, 256), 19: (128, 128), 20: (128, 64), 21: (64, 128), 22: (64, 64)}
+                12: (64, 128), 13: (128, 64), 14: (64, 128)}
 N_CU = 256
 _tuned: dict = {}
 

@@ -65,21 +65,6 @@ static int launch_p3_persist(const ConvParams& p, int cfg, hipStream_t st) {
 
 void set_p3p_bnb(int v) { p3p_bnb_level() = v; }
 
-// the 16-bit weight gradient on the plane kernel's one-plane form (conv_p3_wgrad.h NP = 1): LDS-DMA
-// ring, transposed fragment reads, register-double-buffered fragments; conv_wgrad.hip cfg 15-22
-void launch_wgrad_p1(const WgradParams& p, int cfg, int splits, hipStream_t st) {
-  switch (cfg) {
-    case 15: wlaunch_p3<2, 4, 64, 32, 3, 64, 1, 1>(p, splits, st); break;  // 128 x 128
-    case 16: wlaunch_p3<4, 2, 32, 64, 3, 64, 1, 1>(p, splits, st); break;  // 128 x 128
-    case 17: wlaunch_p3<4, 2, 64, 64, 2, 64, 1, 1>(p, splits, st); break;  // 256 x 128
-    case 18: wlaunch_p3<2, 4, 64, 64, 2, 64, 1, 1>(p, splits, st); break;  // 128 x 256
-    case 19: wlaunch_p3<2, 2, 64, 64, 3, 64, 1, 1>(p, splits, st); break;  // 128 x 128, 4 waves
-    case 20: wlaunch_p3<2, 2, 64, 32, 3, 64, 2, 1>(p, splits, st); break;  // 128 x 64, two per CU
-    case 21: wlaunch_p3<2, 2, 32, 64, 3, 64, 2, 1>(p, splits, st); break;  // 64 x 128, two per CU
-    default: wlaunch_p3<2, 2, 32, 32, 3, 64, 2, 1>(p, splits, st); break;  // 22: 64 x 64, two per CU
-  }
-}
-
 void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st) {
   if (cfg >= 18 && (cfg = launch_p3_persist(p, cfg, st)) < 0) return;
   if (p.bnb_acc != nullptr)

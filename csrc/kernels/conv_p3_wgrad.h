@@ -20,9 +20,7 @@ __device__ __forceinline__ int p3w_swz(int row) {
 // 256x128 block tiles fit); NST slots with early release; PIPE (when two fragment sets fit the
 // register budget): slot k+1's transposed fragment reads in flight during slot k's MFMAs, one
 // barrier per slot. The refill issues are interleaved with the MFMAs (ilv_schedule).
-// NP: operand planes -- 3 (fp32 as bf16x6) or 1 (the 16-bit weight gradient: dy / x of the build's
-// 16-bit type, one MFMA of that type per fragment pair; conv_wgrad.hip cfg 15-22)
-template <int WM, int WN, int TM, int TN, int NST, int BK, bool CBIG, int OCC = 1, int NP = NPL>
+template <int WM, int WN, int TM, int TN, int NST, int BK, bool CBIG, int OCC = 1>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_kernel(WgradParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16, KS = BK / 32;
@@ -30,10 +28,9 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   constexpr int ACPR = BM / 8, BCPR = BN / 8;        // 16-byte chunks per LDS row
   constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;  // LDS rows filled by one wave instruction
   constexpr int AI = BK / ARPI / NW, BI = BK / BRPI / NW;  // instructions per wave per plane and slot
-  static_assert(NP == NPL || NP == 1, "three planes or one 16-bit operand");
-  constexpr int LOADS = NP * (AI + BI);
+  constexpr int LOADS = NPL * (AI + BI);
   constexpr int AIMG = BK * BM * 2, BIMG = BK * BN * 2;
-  constexpr int STAGE = NP * (AIMG + BIMG);
+  constexpr int STAGE = NPL * (AIMG + BIMG);
   static_assert(AI * ARPI * NW == BK && BI * BRPI * NW == BK && AI >= 1 && BI >= 1, "tile / wave mapping");
   static_assert(NST >= 2 && NST <= 3 && LOADS * (NST - 1) <= 63 && NST * STAGE <= 160 * 1024, "ring");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -99,7 +96,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   auto issue = [&](int stage, int kl) {
     const int mb = mbeg + kl * BK;
     char* sA = smem + stage * STAGE;
-    char* sB = sA + NP * AIMG;
+    char* sB = sA + NPL * AIMG;
 #pragma unroll
     for (int v = 0; v < AI; ++v) {
       const int m = mb + a_row[v];
@@ -107,10 +104,8 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
       const uint32_t off = ((uint32_t)(m * p.ldy + a_col[v]) * 2u) | ((uint32_t)!ok << 31);
       char* d = sA + (wid * AI + v) * ARPI * BM * 2;
       glds16(dyr0, d, off);
-      if constexpr (NP == NPL) {
-        glds16(dyr1, d + AIMG, off);
-        glds16(dyr2, d + 2 * AIMG, off);
-      }
+      glds16(dyr1, d + AIMG, off);
+      glds16(dyr2, d + 2 * AIMG, off);
     }
 #pragma unroll
     for (int v = 0; v < BI; ++v) {
@@ -127,10 +122,8 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
       const uint32_t off = raw | ((uint32_t)!ok << 31);  // >= HCB_OOB: out of range
       char* d = sB + (wid * BI + v) * BRPI * BN * 2;
       glds16(xr0, d, off);
-      if constexpr (NP == NPL) {
-        glds16(xr1, d + BIMG, off);
-        glds16(xr2, d + 2 * BIMG, off);
-      }
+      glds16(xr1, d + BIMG, off);
+      glds16(xr2, d + 2 * BIMG, off);
     }
   };
 
@@ -157,31 +150,17 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   using Fr = P3Frags<TM, TN, KS>;
   auto read = [&](int k, Fr& f) {
     const char* Ab = smem + (k % NST) * STAGE;
-    const char* Bb = Ab + NP * AIMG;
+    const char* Bb = Ab + NPL * AIMG;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int t = 0; t < NP; ++t) f.a[ks][t][i] = frag(Ab + t * AIMG, BM, ks * 32 + 8 * g, wm * TM + i * 16);
+        for (int t = 0; t < NPL; ++t) f.a[ks][t][i] = frag(Ab + t * AIMG, BM, ks * 32 + 8 * g, wm * TM + i * 16);
 #pragma unroll
       for (int j = 0; j < NI; ++j)
 #pragma unroll
-        for (int t = 0; t < NP; ++t) f.b[ks][t][j] = frag(Bb + t * BIMG, BN, ks * 32 + 8 * g, wn * TN + j * 16);
-    }
-  };
-  auto mma = [&](const Fr& f) {
-    if constexpr (NP == NPL) {
-      p3_mma<TM, TN, KS>(f, acc);
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-            acc[i][j] = mfma16(__builtin_bit_cast(act16x8, f.a[ks][0][i]), __builtin_bit_cast(act16x8, f.b[ks][0][j]),
-                               acc[i][j]);
+        for (int t = 0; t < NPL; ++t) f.b[ks][t][j] = frag(Bb + t * BIMG, BN, ks * 32 + 8 * g, wn * TN + j * 16);
     }
   };
 
@@ -191,10 +170,10 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   // outstanding
 #pragma unroll
   for (int s = 0; s < NST; ++s) issue(s, s);
-  constexpr int FREGS = (MI + NI) * NP * 4 * KS, AREGS = MI * NI * 4;
+  constexpr int FREGS = (MI + NI) * NPL * 4 * KS, AREGS = MI * NI * 4;
   constexpr int RBUDGET = p3_regs_per_wave<OCC, WM * WN>() - 88 < 400 ? p3_regs_per_wave<OCC, WM * WN>() - 88 : 400;
   constexpr bool PIPE = 2 * FREGS + AREGS <= RBUDGET;
-  constexpr int NMF = KS * MI * NI * (NP == NPL ? 6 : 1), NRD = 2 * KS * (MI + NI) * NP;
+  constexpr int NMF = KS * MI * NI * 6, NRD = 2 * KS * (MI + NI) * NPL;
   if constexpr (PIPE) {
     Fr fr[2];
     wait_vmcnt<(NST - 1) * LOADS>();
@@ -208,7 +187,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
       asm volatile("" ::: "memory");
       issue(k % NST, k + NST);
       read(k + 1, nxt);
-      mma(cur);
+      p3_mma<TM, TN, KS>(cur, acc);
       ilv_schedule<NMF, LOADS, NRD>();
     };
     for (int k = 0; k < nk; k += 2) {
@@ -226,7 +205,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
       __builtin_amdgcn_s_barrier();                        // ... and every other wave's
       asm volatile("" ::: "memory");
       issue(k % NST, k + NST);
-      mma(fr);
+      p3_mma<TM, TN, KS>(fr, acc);
       ilv_schedule<NMF, LOADS, 0>();
     }
   }
@@ -257,26 +236,24 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_wgrad_p3_ke
   }
 }
 
-template <int WM, int WN, int TM, int TN, int NST, int BK, int OCC = 1, int NP = NPL>
+template <int WM, int WN, int TM, int TN, int NST, int BK, int OCC = 1>
 static void wlaunch_p3(const WgradParams& p, int splits, hipStream_t st) {
   constexpr int BM = WM * TM, BN = WN * TN;
   const int tiles = ((p.Nout + BM - 1) / BM) * ((p.K + BN - 1) / BN);
-  const size_t lds_main = (size_t)NST * NP * BK * (BM + BN) * 2;
+  const size_t lds_main = (size_t)NST * NPL * BK * (BM + BN) * 2;
   const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
   const size_t lds = lds_main > lds_epi ? lds_main : lds_epi;
   static bool once = false;
   if (!once) {
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC, NP>);
-    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC, NP>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC>);
+    p3_set_lds_once(conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC>);
     once = true;
   }
   const dim3 grid(tiles * splits);
   if ((p.C % BN) == 0)
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC, NP>), grid, dim3(WM * WN * 64), lds, st,
-                       p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, true, OCC>), grid, dim3(WM * WN * 64), lds, st, p);
   else
-    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC, NP>), grid, dim3(WM * WN * 64), lds,
-                       st, p);
+    hipLaunchKernelGGL((conv_wgrad_p3_kernel<WM, WN, TM, TN, NST, BK, false, OCC>), grid, dim3(WM * WN * 64), lds, st, p);
 }
 
 }  // namespace hcb

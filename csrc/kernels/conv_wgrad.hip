@@ -868,28 +868,19 @@ static void wlaunch(const WgradParams& p, int splits, hipStream_t st) {
 // NST 4)}
 // 10-12: intra-workgroup k-split 64x64, 128x64, 64x128; 13-14: register-staged 128x64 / 64x128 with
 // 64x32 / 32x64 wave tiles (twice the MFMAs per loaded row of the 64x64 tile)
-// 15-22: the plane weight-gradient kernel's one-plane form (conv_p3.hip launch_wgrad_p1): 128x128
-// (8 waves of 64x32 / 32x64), 256x128, 128x256, 128x128 (4 waves of 64x64), 128x64 / 64x128 / 64x64
-// two per CU; 64-row slots
-constexpr int N_WGRAD_CFG = 23;
+constexpr int N_WGRAD_CFG = 15;
 int wgrad_tile_m(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64, 64, 128,
-                                     64, 128, 64, 128, 128, 256, 128, 128, 128, 64, 64};
+  static const int t[N_WGRAD_CFG] = {128, 64, 64, 128, 128, 256, 128, 64, 64, 64, 64, 128, 64, 128, 64};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 int wgrad_tile_n(int cfg) {
-  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128, 64, 64,
-                                     128, 64, 128, 128, 128, 128, 256, 128, 64, 128, 64};
+  static const int t[N_WGRAD_CFG] = {128, 128, 64, 128, 128, 128, 256, 128, 64, 128, 64, 64, 128, 64, 128};
   return (cfg >= 0 && cfg < N_WGRAD_CFG) ? t[cfg] : 64;
 }
 
 void launch_conv_wgrad(const WgradParams& p, int cfg, int splits, hipStream_t st) {
   // the register-staged loaders keep a thread's 16-byte vector inside one filter tap (every
   // weight pack already requires C % 8 == 0; bindings.cpp checks it)
-  if (cfg >= 15 && cfg < N_WGRAD_CFG) {
-    launch_wgrad_p1(p, cfg, splits, st);
-    return;
-  }
   switch (cfg) {
     case 0: wlaunch<2, 2, 64, 64>(p, splits, st); break;  // 128 x 128
     case 1: wlaunch<1, 4, 64, 32>(p, splits, st); break;  // 64 x 128

@@ -122,8 +122,6 @@ void launch_conv_p3(const ConvParams& p, int cfg, hipStream_t st);
 // (the twin runs; default -- 0.38% slower step with 1, profiles/r6_persistent_bnb.txt), 1 ReLU
 // modes 0 / 2, 2 every mode; initialised from HCB_P3P_BNB
 void set_p3p_bnb(int v);
-// the 16-bit weight gradient's plane-kernel cfgs 15-22 (conv_p3.hip; called by launch_conv_wgrad)
-void launch_wgrad_p1(const WgradParams& p, int cfg, int splits, hipStream_t st);
 int p3_tile_m(int cfg);
 int p3_tile_n(int cfg);
 int p3_slot_k(int cfg);

@@ -240,12 +240,11 @@ def test_conv_wgrad(case):
     assert rel_err(dw, ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(23)))
+@pytest.mark.parametrize("cfg", list(range(15)))
 def test_conv_wgrad_all_configs(cfg):
     """Every weight-grad tile config (register-staged 0-2 and 13-14, LDS-DMA ring 3-9,
-    intra-workgroup k-split 10-12, the plane kernel's one-plane form 15-22) with split-K on
-    1x1 / 3x3 / strided / odd-channel geometries (partial tiles in Nout, K and pixels). The
-    reference sums the same bf16 products in fp32: the one-plane cfgs are held to 1e-5."""
+    intra-workgroup k-split 10-12) with split-K on
+    1x1 / 3x3 / strided / odd-channel geometries (partial tiles in Nout, K and pixels)."""
     torch.manual_seed(6)
     for cin, cout, k, s, pads, H, splits in [(64, 256, 1, 1, (0, 0, 0, 0), 14, 3),
                                              (128, 128, 3, 2, (1, 1, 1, 1), 15, 2),
@@ -260,7 +259,7 @@ def test_conv_wgrad_all_configs(cfg):
         Fn.conv_wgrad(dz, x, spec, dw, cfg=(cfg, splits))
         ref = torch.zeros(cout, k, k, cin)
         Fn.conv_wgrad(dz.float().cpu(), x.float().cpu(), spec, ref)
-        assert rel_err(dw, ref.view(cout, -1)) < (1e-5 if cfg >= 15 else 1e-2), (cfg, cin, cout, k)
+        assert rel_err(dw, ref.view(cout, -1)) < 1e-2, (cfg, cin, cout, k)
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 10, 11, 12, 13, 14])
