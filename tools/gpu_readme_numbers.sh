@@ -30,7 +30,7 @@ for spec in ${MODELS:-resnet101:64 resnet50_v1.5:64 resnet50_v2:64 vgg16:64 goog
   IFS=: read m b <<< "$spec"
   run zoo_$m 400 python bench.py --model $m --batch_size $b --compute_dtype bf16 --secondary none --steps 20 --warmup 5
 done
-for spec in ${FP32_MODELS:-vgg16:64 googlenet:128 alexnet:512}; do  # the zoo at fp32 on the HIP kernels
+for spec in ${FP32_MODELS:-resnet50_v2:64 resnet101:64 vgg16:64 googlenet:128 alexnet:512}; do  # the zoo at fp32 on the HIP kernels
   IFS=: read m b <<< "$spec"
   run zoo32_$m 400 python bench.py --model $m --batch_size $b --compute_dtype fp32 --secondary none --steps 20 --warmup 5
 done
