@@ -144,6 +144,9 @@ def main():
     ap.add_argument("--budget_s", type=float, default=900.0)
     ap.add_argument("--aa_only", action="store_true", help="measure and print the interleaved A/A band only")
     ap.add_argument("--aa_reps", type=int, default=4)
+    ap.add_argument("--try_plan", action="append", default=[],
+                    help="interleaved in-step A/B of one plan change instead of tuning: kind,M,N,K,taps=cfg,splits "
+                         "(repeatable; each tried alone against the current table)")
     ap.add_argument("--knob_ab", default="",
                     help="interleaved in-step A/B of a kernel switch instead of tuning: p3p_bnb:A:B")
     ap.add_argument("--out", default="gpurun_out/step_tune.json")
@@ -168,7 +171,7 @@ def main():
 
     # isolated timing of every candidate (ranking and candidate shortlist)
     iso = {}
-    for k, (cnt, cands, run) in ([] if a.aa_only or a.knob_ab else probs.items()):
+    for k, (cnt, cands, run) in ([] if a.aa_only or a.knob_ab or a.try_plan else probs.items()):
         iso[k] = {json.dumps(c): autotune._time(lambda: run(c)) for c in cands}
         cur = json.dumps(Fn._tuned[k] if not isinstance(Fn._tuned[k], tuple) else list(Fn._tuned[k]))
         if cur not in iso[k]:
@@ -183,7 +186,7 @@ def main():
         return json.dumps(list(v) if isinstance(v, tuple) else v)
 
     kinds = [k for k in a.kinds.split(",") if k]
-    order = [] if a.aa_only or a.knob_ab else sorted((k for k in probs if not kinds or k[0] in kinds),
+    order = [] if a.aa_only or a.knob_ab or a.try_plan else sorted((k for k in probs if not kinds or k[0] in kinds),
                                         key=lambda k: -iso[k][cur_s(k)] * probs[k][0])
 
     images, labels = synthetic_batch(model, a.batch)
@@ -197,6 +200,18 @@ def main():
     log(f"[step_tune] start: {t0:.4f} ms/step (6 captures: {' '.join(f'{x:.4f}' for x in base)}; spread "
         f"{max(base) - min(base):.4f} ms); interleaved A/A band {noise:.4f} ms = {100 * noise / t0:.2f}% "
         f"({a.aa_reps} A/As of {a.rounds} rounds: {' '.join(f'{d:.4f}' for d in diffs)})")
+    if a.try_plan:
+        for spec in a.try_plan:
+            ks, vs = spec.split("=")
+            kp = ks.split(",")
+            key = (kp[0],) + tuple(int(v) for v in kp[1:])
+            cand = [int(v) for v in vs.split(",")]
+            cur = Fn._tuned.get(key)
+            cur = list(cur) if isinstance(cur, (tuple, list)) else cur
+            ta, tb = ab(timer, key, cur, cand, a.aa_reps * a.rounds)
+            log(f"[step_tune] try {key}: {cur} {ta:.4f} ms/step vs {cand} {tb:.4f} ms/step ({100 * (ta - tb) / ta:+.2f}%; "
+                f"A/A band {100 * noise / t0:.2f}%)")
+        return
     if a.knob_ab:
         name, va, vb = a.knob_ab.split(":")
         setter = {"p3p_bnb": Fn.set_p3p_bnb}[name]
