@@ -12,6 +12,13 @@ transport, and the reference's quirks are fixed (``WORKERS_PER_SOCKET=0`` no lon
 Env overrides: MODEL, NUM_BATCHES, NUM_WARMUP_BATCHES, DISPLAY_EVERY, DEVICE (gpu|cpu),
 GPUS_PER_NODE, HOSTFILE (multi-node: one host per line; this node's rank = its line),
 DRY_RUN=1 (print the plan, launch nothing), LOG_DIR, EXTRA_ARGS.
+
+Multi-node from ONE shell (the reference's ``mpirun -hostfile``, run-tf-sing-ucx-openmpi.sh:99-103):
+``FANOUT=1`` on the hostfile's first node starts the same runner on every other host of the
+hostfile over ssh (``SSH``, default ``ssh -o BatchMode=yes``; the repo and the hostfile at the same
+paths on every node, as the reference assumes for ~/nodeips.txt), forwarding the overrides above and
+every ``HCB_*`` / ``NCCL_*`` / ``RCCL_*`` variable, runs its own node, and returns the worst exit
+code. Each node derives its rank from its line of the hostfile.
 """
 from __future__ import annotations
 
@@ -145,6 +152,28 @@ def node_rank_from_hostfile(path: str) -> (List[str], int):
     return hosts, 0
 
 
+FORWARD_ENV = ("MODEL", "NUM_BATCHES", "NUM_WARMUP_BATCHES", "DISPLAY_EVERY", "DEVICE", "GPUS_PER_NODE",
+               "HOSTFILE", "LOG_DIR", "EXTRA_ARGS")
+FORWARD_PREFIXES = ("HCB_", "NCCL_", "RCCL_")
+
+
+def fanout_commands(hosts: List[str], node_rank: int, argv: List[str], env=os.environ,
+                    repo: str = REPO) -> List[List[str]]:
+    """ssh command lines that start this runner (same arguments) on every host but this one."""
+    ssh = shlex.split(env.get("SSH", "ssh -o BatchMode=yes"))
+    fwd = {k: v for k, v in env.items() if k in FORWARD_ENV or k.startswith(FORWARD_PREFIXES)}
+    fwd["HCB_FANOUT_CHILD"] = "1"  # a child never fans out again
+    exports = " ".join(f"{k}={shlex.quote(v)}" for k, v in sorted(fwd.items()))
+    out = []
+    for i, h in enumerate(hosts):
+        if i == node_rank:
+            continue
+        remote = (f"cd {shlex.quote(repo)} && env {exports} {shlex.quote(sys.executable)} -m "
+                  f"azure_hc_intel_tf_amd.launch.run_tf_sing " + " ".join(shlex.quote(x) for x in argv))
+        out.append(ssh + [h, remote])
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="run-tf-sing")
     ap.add_argument("--flavor", default="ucx-openmpi", choices=["ucx-openmpi", "libfabric-intelmpi"])
@@ -152,6 +181,7 @@ def main(argv=None) -> int:
     ap.add_argument("workers_per_socket", type=int)
     ap.add_argument("batch_size", type=int)
     ap.add_argument("fabric", choices=["ib", "sock"])
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = ap.parse_args(argv)
     env = os.environ
     topo = lscpu_topology()
@@ -190,8 +220,17 @@ def main(argv=None) -> int:
           (f"  (unset {' '.join(fl['unset'])})" if fl["unset"] else "") +
           f"  PINNING: {'per-GPU NUMA cores' if fl['pin'] else 'none'}")
     print("COMMAND: " + " ".join(shlex.quote(c) for c in launcher), flush=True)
+    fan = []
+    if plan.num_nodes > 1 and env.get("FANOUT") == "1" and env.get("HCB_FANOUT_CHILD") != "1":
+        if node_rank != 0:
+            print("FANOUT=1 must be started on the hostfile's first node", file=sys.stderr)
+            return 2
+        fan = fanout_commands(hosts[:plan.num_nodes], node_rank, argv, env)
+        for c in fan:
+            print("FANOUT: " + " ".join(shlex.quote(x) for x in c), flush=True)
     if env.get("DRY_RUN") == "1":
         return 0
+    remotes = [subprocess.Popen(c) for c in fan]
     log_dir = env.get("LOG_DIR", os.path.join(REPO, "gpurun_out", "logs"))
     os.makedirs(log_dir, exist_ok=True)
     log = os.path.join(log_dir, f"tfmn-{plan.num_nodes}n-{plan.batch_size}b-synthetic-{plan.fabric}-r1.log")
@@ -206,6 +245,10 @@ def main(argv=None) -> int:
             sys.stdout.write(line)
             lf.write(line)
         rc = p.wait()
+    for r in remotes:  # the other nodes' runners (their output goes to their own logs and this terminal)
+        rr = r.wait()
+        if rc == 0 and rr != 0:
+            rc = rr
     print(f"log: {log}")
     return rc
 

@@ -251,3 +251,30 @@ def test_resnet_v2_is_fp32_native():
     for n in ("resnet50_v2", "resnet101_v2", "resnet152_v2"):
         assert n in FP32_NATIVE_MODELS
         assert precision_label(parse_flags([f"--model={n}"])) == "fp32 (HIP kernels)"
+
+
+def test_multi_node_fanout_from_one_shell(tmp_path, capsys, monkeypatch):
+    """FANOUT=1 on the hostfile's first node (the reference's mpirun -hostfile): one ssh command per
+    other host, starting the same runner with the overrides and HCB_* / NCCL_* variables forwarded,
+    marked as a child (no second fan-out); the child itself plans no fan-out."""
+    from azure_hc_intel_tf_amd.launch import run_tf_sing as R
+
+    hf = tmp_path / "nodeips.txt"
+    hf.write_text("127.0.0.1\nnode-b\nnode-c\n")
+    for k, v in {"HOSTFILE": str(hf), "FANOUT": "1", "DRY_RUN": "1", "DEVICE": "cpu", "MODEL": "resnet101",
+                 "HCB_X": "7", "NCCL_DEBUG": "WARN", "SSH": "fakessh -p 22"}.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.delenv("HCB_FANOUT_CHILD", raising=False)
+    assert R.main(["3", "1", "64", "ib"]) == 0
+    out = capsys.readouterr().out
+    fan = [l for l in out.splitlines() if l.startswith("FANOUT: ")]
+    assert len(fan) == 2 and "node-b" in fan[0] and "node-c" in fan[1], out
+    for l in fan:
+        assert l.startswith("FANOUT: fakessh -p 22 node-")
+        for tok in ("HCB_FANOUT_CHILD=1", "MODEL=resnet101", "HCB_X=7", "NCCL_DEBUG=WARN",
+                    "azure_hc_intel_tf_amd.launch.run_tf_sing 3 1 64 ib"):
+            assert tok in l, (tok, l)
+        assert "DRY_RUN" not in l and "FANOUT=1" not in l
+    monkeypatch.setenv("HCB_FANOUT_CHILD", "1")
+    assert R.main(["3", "1", "64", "ib"]) == 0
+    assert "FANOUT: " not in capsys.readouterr().out
