@@ -69,17 +69,24 @@ constexpr size_t p3p_ring_bytes() {
 // wave rows (one memory round trip each), g = (acc [+ beta]) gated, stored fp32, and sum(g) /
 // sum(g * xhat) reduced per column by shuffles into one buffer atomic per column and wave (replica =
 // the wave's 64-row block, as the statistics) -- EOPS vector-memory instructions after the loads.
+//
+// BRES (B resident, cfg 31-34): the WHOLE weight operand (one N tile: Nout <= BN; every k-step's
+// three plane images, nk * 3 * BN * 64 B) is DMA'd into LDS once per workgroup, and the ring streams
+// A only. For the stage-1 1x1 GEMMs the weight tile is as large as the activation tile (64 -> 256:
+// BN x K = 256 x 64 against BM x K = 64 x 64), so re-staging it for every tile doubled-to-quintupled
+// the L2 -> LDS operand traffic that bounds these launches.
 template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool STATS, int OCC, bool SK = false,
-          bool BNB = false>
+          bool BNB = false, bool BRES = false>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_kernel(ConvParams p) {
   constexpr int BM = WM * TM, BN = WN * TN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int NT = WM * WN * 64, CPR = KW / 8, RB = KW * 2;
   constexpr int RP = NT / CPR;
   constexpr int AV = BM / RP, BV = BN / RP;
-  constexpr int LOADS = NPL * (AV + BV);
+  static_assert(!(BRES && (SK || BNB)), "B-resident: the whole-tile forward form");
+  constexpr int LOADS = NPL * (AV + (BRES ? 0 : BV));
   constexpr int AIMG = BM * RB, BIMG = BN * RB;
-  constexpr int STAGE = (int)p3_stage_bytes<BM, BN, KW>();
+  constexpr int STAGE = BRES ? NPL * AIMG : (int)p3_stage_bytes<BM, BN, KW>();
   // epilogue vector-memory instructions; EDRAIN (64 x 64 wave tiles: more than the vmcnt field can
   // count beside the ring): the epilogue drains itself instead and the ring's waits count 0 for it
   static_assert(!(STATS && BNB), "a data gradient has no forward statistics");
@@ -90,9 +97,12 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 1) + EOPS <= 63 && NST >= 2 && NST <= 4, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* ktab = reinterpret_cast<float*>(smem + p3p_ring_bytes<BM, BN, KW, NST>());
+  // BRES: the resident weight images after the A ring, then the shift table
+  char* bres = smem + (size_t)NST * STAGE;
+  const size_t bres_bytes = BRES ? (size_t)(p.Kpad / KW) * NPL * BIMG : 0;
+  float* ktab = reinterpret_cast<float*>(smem + (size_t)NST * STAGE + bres_bytes);
   // SK: the last-arriver broadcast word, after the shift table
-  int* skflag = reinterpret_cast<int*>(smem + p3p_ring_bytes<BM, BN, KW, NST>() + (STATS ? (size_t)p.Nout * 4 : 0));
+  int* skflag = reinterpret_cast<int*>(smem + (size_t)NST * STAGE + bres_bytes + (STATS ? (size_t)p.Nout * 4 : 0));
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = wave_id_uniform();
@@ -174,13 +184,15 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
       glds16(xr1, sa + AIMG + RP * v * RB, o);
       glds16(xr2, sa + 2 * AIMG + RP * v * RB, o);
     }
-    char* sb = smem + stage * STAGE + NPL * AIMG + wid * WROWS * RB;
+    if constexpr (!BRES) {
+      char* sb = smem + stage * STAGE + NPL * AIMG + wid * WROWS * RB;
 #pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      const uint32_t o = (b_off[v] == HCB_OOB || !live) ? HCB_OOB : b_off[v] + (uint32_t)ck * (uint32_t)RB;
-      glds16(wr0, sb + RP * v * RB, o);
-      glds16(wr1, sb + BIMG + RP * v * RB, o);
-      glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
+      for (int v = 0; v < BV; ++v) {
+        const uint32_t o = (b_off[v] == HCB_OOB || !live) ? HCB_OOB : b_off[v] + (uint32_t)ck * (uint32_t)RB;
+        glds16(wr0, sb + RP * v * RB, o);
+        glds16(wr1, sb + BIMG + RP * v * RB, o);
+        glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
+      }
     }
   };
   auto advance = [&]() {
@@ -406,10 +418,25 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
 
   auto read = [&](int g, P3Frags<TM, TN, KW / 32>& f) {
     const char* sb = smem + (g % NST) * STAGE;
-    p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(sb + NPL * AIMG), f,
-                                wm, wn, lane);
+    const char* bb = BRES ? bres + (size_t)(g % nk) * NPL * BIMG : sb + NPL * AIMG;  // BRES: step g's k-step
+    p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(bb), f, wm, wn, lane);
   };
 
+  if constexpr (BRES) {  // every k-step's weight images, once (one N tile: cursor_tile(0)'s b_off serve all tiles)
+    for (int kt = 0; kt < nk; ++kt) {
+      char* sb = bres + (size_t)kt * NPL * BIMG + wid * WROWS * RB;
+#pragma unroll
+      for (int v = 0; v < BV; ++v) {
+        const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * (uint32_t)RB;
+        glds16(wr0, sb + RP * v * RB, o);
+        glds16(wr1, sb + BIMG + RP * v * RB, o);
+        glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
+      }
+    }
+    // landed before the ring starts (the ring's counted waits count ring pieces only); published to
+    // the other waves by the first barrier below
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 #pragma unroll
   for (int s = 0; s < NST; ++s) {
     issue(s);
@@ -563,6 +590,55 @@ static bool launch_p3p(const ConvParams& p, hipStream_t st) {
   else
     hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, OCC>), dim3(grid), b, lds, st,
                        p);
+  return true;
+}
+
+// cfg 31-34: the B-resident form (BRES above). False when the problem does not fit it (more than one
+// N tile, the weights + ring over the LDS, an epilogue feature the persistent kernel lacks): the
+// caller then runs the whole-tile persistent cfg.
+template <int WM, int WN, int TM, int TN, int KW, int NST>
+static bool launch_p3bres(const ConvParams& p, hipStream_t st) {
+  constexpr int BM = WM * TM, BN = WN * TN, NPLc = NPL;
+  const bool stats = p.stats != nullptr;
+  const int nk = p.Kpad / KW;
+  const size_t lds = (size_t)NST * NPLc * BM * KW * 2 + (size_t)nk * NPLc * BN * KW * 2 + (stats ? (size_t)p.Nout * 4 : 0);
+  if (p.Nout > BN || p.bnb_acc != nullptr || p.remap || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || p.beta ||
+      p.bias != nullptr || !p.out_f32 || (stats && p.stats_R <= 0) || nk < NST - 1 || p.Kpad % KW != 0 ||
+      lds > 160 * 1024 || (size_t)p.M * p.ldy * 4 >= (1ull << 31))
+    return false;
+  const bool cbig = (p.C % KW) == 0;
+  static bool once = false;
+  if (!once) {
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, true, 1, false, false, true>);
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, 1, false, false, true>);
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, true, 1, false, false, true>);
+    p3_set_lds_once(conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, 1, false, false, true>);
+    once = true;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int ntiles = (p.M + BM - 1) / BM;
+  const int per_cu = (int)((160 * 1024) / lds) < 1 ? 1 : (int)((160 * 1024) / lds);
+  const int slots = cus * per_cu;
+  const int grid = ntiles < slots ? ntiles : slots;
+  const dim3 b(WM * WN * 64);
+  if (cbig && stats)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, true, 1, false, false, true>), dim3(grid),
+                       b, lds, st, p);
+  else if (cbig)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, false, 1, false, false, true>), dim3(grid),
+                       b, lds, st, p);
+  else if (stats)
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, true, 1, false, false, true>), dim3(grid),
+                       b, lds, st, p);
+  else
+    hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, false, false, 1, false, false, true>), dim3(grid),
+                       b, lds, st, p);
   return true;
 }
 
