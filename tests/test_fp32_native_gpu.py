@@ -49,7 +49,8 @@ CASES = [(64, 256, 1, 1, 0, 14), (64, 64, 3, 1, 1, 14), (128, 128, 3, 2, 1, 14),
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}s{c[3]}")
 @pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
-                                 23, 24, 25, 26, 27, 28, 29, 30, (0, 2), (4, 3), (7, 2), (10, 3), (14, 3), (16, 5), (17, 6)],
+                                 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, (0, 2), (4, 3), (7, 2), (10, 3), (14, 3),
+                                 (16, 5), (17, 6)],
                          ids=str)
 def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     """bf16x6 on planes reproduces the fp32 convolution to fp32 accuracy (~1e-6): fwd, data grad
@@ -58,7 +59,8 @@ def test_fp32_conv_fwd_dgrad_wgrad_match_fp64(fp32_mode, case, cfg):
     planes by the ops themselves. cfg 7-13: 32-deep slots (64-byte LDS rows) and 128x128 / 256x128
     block tiles; (cfg, S): in-launch split-K (fixed-order slab sum); weight-grad cfg 6-11: 32-deep slots, up to 256x128 / 128x256; fwd cfg 14-17 / weight-grad 12-15: two or
     three workgroups per CU; 18-22: the persistent short-K kernel (conv_p3_persist.h; the strided
-    data gradients' remap form runs its twin); 23-27: its stream-K form."""
+    data gradients' remap form runs its twin); 23-27: its stream-K form; 31-34: its weights-resident
+    form (falling back where it does not fit)."""
     cin, cout, k, s, pad, H = case
     spec, p, pk, ps = _conv(cin, cout, k, s, pad)
     assert Fn.lo_pack(pk.pack) is not None and Fn.lo_pack(pk.tr) is not None

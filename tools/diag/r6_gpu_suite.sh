@@ -1,7 +1,7 @@
 #!/bin/bash
 # the whole GPU test tier in one pytest process, then smoke()
 set -o pipefail
-O=gpurun_out/r6n
+O=gpurun_out/${TAG:-r6n}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider \
   > $O/gpu_tests.txt 2>&1
