@@ -1080,7 +1080,7 @@ hcb::ConvParams p3_params(const Tensor& x, const Tensor& w, const Tensor& w_lo, 
                           const c10::optional<Tensor>& stats, at::IntArrayRef g, int64_t cfg,
                           const c10::optional<Tensor>& stats_shift) {
   const int64_t xps = check_planes(x, "x");
-  TORCH_CHECK(cfg >= 0 && cfg < 35, "hcb.conv_p3: cfg 0..34");
+  TORCH_CHECK(cfg >= 0 && cfg < 37, "hcb.conv_p3: cfg 0..36");
   // conv_params validates geometry and byte ranges on plane 0 (a bf16 tensor of this build's type);
   // split-K is validated here against the p3 tiles
   std::vector<int64_t> g1(g.begin(), g.end());

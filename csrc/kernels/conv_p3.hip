@@ -29,20 +29,21 @@ namespace hcb {
 // 28-30: stream-K with cfg 8's, 10's and 11's geometry (4 x 2 waves of 32 x 64; 256 x 128 and
 // 128 x 256 of 64 x 64 wave tiles: 25% fewer operand bytes per MFMA than 128 x 128, and with
 // stream-K no quantization tail however few tiles)
-// 31-34: the persistent kernel with the weights resident in LDS (BRES): 64x256 (4 waves of 64x64),
-// 128x256 (8 waves of 64x64), 64x64 (4 waves of 32x32), 128x64 (4 waves of 64x32)
-constexpr int N_P3_CFG = 35;
+// 31-36: the persistent kernel with the workgroup's weight slice resident in LDS (BRES): 64x256 (4
+// waves of 64x64), 128x256 (8 waves of 64x64), 64x64 (4 waves of 32x32), 128x64 (4 waves of 64x32),
+// 128x64 (8 waves of 32x32), 128x128 (8 waves of 32x64)
+constexpr int N_P3_CFG = 37;
 int p3_tile_m(int cfg) {
   static const int t[N_P3_CFG] = {128, 64, 128, 64, 64, 128, 64, 128, 128, 128, 256, 128, 64, 128, 128, 64,
                                   64, 64, 64, 128, 64, 64, 128, 64, 128, 64, 64, 128, 128, 256, 128,
-                                  64, 128, 64, 128};
+                                  64, 128, 64, 128, 128, 128};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 128;
 }
 int p3_slot_k(int cfg) { return (cfg >= 0 && cfg <= 6) ? 64 : 32; }
 int p3_tile_n(int cfg) {
   static const int t[N_P3_CFG] = {64, 128, 64, 128, 64, 64, 128, 128, 128, 128, 128, 256, 128, 64, 64, 128,
                                   64, 64, 128, 64, 64, 64, 128, 128, 64, 64, 64, 128, 128, 128, 256,
-                                  256, 256, 64, 64};
+                                  256, 256, 64, 64, 64, 128};
   return (cfg >= 0 && cfg < N_P3_CFG) ? t[cfg] : 64;
 }
 
@@ -62,6 +63,8 @@ static int launch_p3_persist(const ConvParams& p, int cfg, hipStream_t st) {
     case 32: return launch_p3bres<2, 4, 64, 64, 32, 2>(p, st) ? -1 : launch_p3_persist(p, 18, st);
     case 33: return launch_p3bres<2, 2, 32, 32, 32, 3>(p, st) ? -1 : launch_p3_persist(p, 20, st);
     case 34: return launch_p3bres<2, 2, 64, 32, 32, 2>(p, st) ? -1 : launch_p3_persist(p, 19, st);
+    case 35: return launch_p3bres<4, 2, 32, 32, 32, 2>(p, st) ? -1 : launch_p3_persist(p, 19, st);
+    case 36: return launch_p3bres<4, 2, 32, 64, 32, 2>(p, st) ? -1 : launch_p3_persist(p, 22, st);
     case 18: return launch_p3p<2, 2, 32, 64, 32, 2, 2>(p, st) ? -1 : 15;
     case 19: return launch_p3p<2, 2, 64, 32, 32, 2, 2>(p, st) ? -1 : 14;
     case 20: return launch_p3p<2, 2, 32, 32, 32, 3, 2>(p, st) ? -1 : 16;

@@ -70,11 +70,12 @@ constexpr size_t p3p_ring_bytes() {
 // sum(g * xhat) reduced per column by shuffles into one buffer atomic per column and wave (replica =
 // the wave's 64-row block, as the statistics) -- EOPS vector-memory instructions after the loads.
 //
-// BRES (B resident, cfg 31-34): the WHOLE weight operand (one N tile: Nout <= BN; every k-step's
-// three plane images, nk * 3 * BN * 64 B) is DMA'd into LDS once per workgroup, and the ring streams
-// A only. For the stage-1 1x1 GEMMs the weight tile is as large as the activation tile (64 -> 256:
-// BN x K = 256 x 64 against BM x K = 64 x 64), so re-staging it for every tile doubled-to-quintupled
-// the L2 -> LDS operand traffic that bounds these launches.
+// BRES (B resident, cfg 31-36): the workgroup's whole weight slice (its N tile's every k-step: three
+// plane images, nk * 3 * BN * 64 B) is DMA'd into LDS once, and the ring streams A only. The host
+// sizes the grid as a multiple of the N-tile count, so first, first + grid, ... all lie in the N tile
+// first % tiles_n. For the 1x1 GEMMs with K <= 256 the weight tile is as large as the activation
+// tile or larger (stage 1, 64 -> 256: BN x K = 256 x 64 against BM x K = 64 x 64), so re-staging it
+// for every tile doubled-to-quintupled the L2 -> LDS operand traffic that bounds these launches.
 template <int WM, int WN, int TM, int TN, int KW, int NST, bool CBIG, bool STATS, int OCC, bool SK = false,
           bool BNB = false, bool BRES = false>
 __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_kernel(ConvParams p) {
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   constexpr bool EDRAIN = LOADS * (NST - 1) + EOPS_N > 63;
   constexpr int EOPS = EDRAIN ? 0 : EOPS_N;
   static_assert(TM >= 32, "at most two adds per statistics slot and tile (deterministic mode)");
-  static_assert(AV * RP == BM && BV * RP == BN, "tile rows must be a multiple of the load pass");
+  static_assert(AV * RP == BM && (BRES || BV * RP == BN), "tile rows must be a multiple of the load pass");
   static_assert(LOADS * (NST - 1) + EOPS <= 63 && NST >= 2 && NST <= 4, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // BRES: the resident weight images after the A ring, then the shift table
@@ -151,14 +152,14 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
   // ---- issue cursor: the (local tile, k-step) whose slot is issued next, NST steps ahead of the
   // MFMAs; its loader state follows it across tile boundaries
   ALoader<AV, CBIG, false, RP, 2, KW> al;
-  uint32_t b_off[BV];
+  uint32_t b_off[BV > 0 ? BV : 1];
   int ci = 0, ck = 0;  // the next issue: local tile (whole-tile form) / local step (SK), and k-step
   auto cursor_at = [&](int t, int k0) {
     const int tm = t / tiles_n, tn = t - tm * tiles_n;
     al.init(p, tm * BM, tid, chunk);
     if (k0 > 0) al.seek(p, k0);
 #pragma unroll
-    for (int v = 0; v < BV; ++v) {
+    for (int v = 0; v < (BRES ? 0 : BV); ++v) {  // (BRES stages its weights itself)
       const int j = tn * BN + tid / CPR + RP * v;
       b_off[v] = (j < p.Nout) ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
     }
@@ -422,15 +423,19 @@ __global__ __launch_bounds__(WM* WN * 64, OCC* WM* WN / 4) void conv_p3_persist_
     p3_read<WM, WN, TM, TN, KW>(reinterpret_cast<const u32x4*>(sb), reinterpret_cast<const u32x4*>(bb), f, wm, wn, lane);
   };
 
-  if constexpr (BRES) {  // every k-step's weight images, once (one N tile: cursor_tile(0)'s b_off serve all tiles)
-    for (int kt = 0; kt < nk; ++kt) {
-      char* sb = bres + (size_t)kt * NPL * BIMG + wid * WROWS * RB;
-#pragma unroll
-      for (int v = 0; v < BV; ++v) {
-        const uint32_t o = b_off[v] == HCB_OOB ? HCB_OOB : b_off[v] + (uint32_t)kt * (uint32_t)RB;
-        glds16(wr0, sb + RP * v * RB, o);
-        glds16(wr1, sb + BIMG + RP * v * RB, o);
-        glds16(wr2, sb + 2 * BIMG + RP * v * RB, o);
+  if constexpr (BRES) {  // every k-step's weight images of this workgroup's N tile, once
+    const int n0 = (first % tiles_n) * BN;
+    // rows rb .. rb + WROWS - 1 per wave instruction (wave-uniform; a wave past BN issues nothing):
+    // the lane-linear images of issue()'s B part, row r's swizzle a function of tid as there
+    for (int rb = wid * WROWS; rb < BN; rb += RP) {
+      const int j = n0 + rb + lane / CPR;
+      const uint32_t bo = j < p.Nout ? (uint32_t)(j * p.Kpad + chunk * 8) * 2u : HCB_OOB;
+      for (int kt = 0; kt < nk; ++kt) {
+        char* sb = bres + (size_t)kt * NPL * BIMG + rb * RB;
+        const uint32_t o = bo == HCB_OOB ? HCB_OOB : bo + (uint32_t)kt * (uint32_t)RB;
+        glds16(wr0, sb, o);
+        glds16(wr1, sb + BIMG, o);
+        glds16(wr2, sb + 2 * BIMG, o);
       }
     }
     // landed before the ring starts (the ring's counted waits count ring pieces only); published to
@@ -602,7 +607,7 @@ static bool launch_p3bres(const ConvParams& p, hipStream_t st) {
   const bool stats = p.stats != nullptr;
   const int nk = p.Kpad / KW;
   const size_t lds = (size_t)NST * NPLc * BM * KW * 2 + (size_t)nk * NPLc * BN * KW * 2 + (stats ? (size_t)p.Nout * 4 : 0);
-  if (p.Nout > BN || p.bnb_acc != nullptr || p.remap || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || p.beta ||
+  if (p.bnb_acc != nullptr || p.remap || p.idil_h > 1 || p.idil_w > 1 || p.splits != 1 || p.beta ||
       p.bias != nullptr || !p.out_f32 || (stats && p.stats_R <= 0) || nk < NST - 1 || p.Kpad % KW != 0 ||
       lds > 160 * 1024 || (size_t)p.M * p.ldy * 4 >= (1ull << 31))
     return false;
@@ -622,10 +627,13 @@ static bool launch_p3bres(const ConvParams& p, hipStream_t st) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const int ntiles = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.Nout + BN - 1) / BN;
+  const int ntiles = ((p.M + BM - 1) / BM) * tiles_n;
   const int per_cu = (int)((160 * 1024) / lds) < 1 ? 1 : (int)((160 * 1024) / lds);
   const int slots = cus * per_cu;
-  const int grid = ntiles < slots ? ntiles : slots;
+  // a multiple of the N-tile count: each workgroup's tiles share one N tile (its resident slice)
+  const int grid = ((ntiles < slots ? ntiles : slots) / tiles_n) * tiles_n;
+  if (grid <= 0) return false;
   const dim3 b(WM * WN * 64);
   if (cbig && stats)
     hipLaunchKernelGGL((conv_p3_persist_kernel<WM, WN, TM, TN, KW, NST, true, true, 1, false, false, true>), dim3(grid),

@@ -84,12 +84,14 @@ def test_streamk_cfgs_share_the_persistent_tiles():
 
 
 def test_b_resident_cfgs_only_where_the_weights_fit():
-    """cfg 31-34 (weights resident in LDS) are candidates only for one-N-tile problems whose K x N
-    planes fit beside the A ring: the stage-1 1x1 GEMMs, not the 3x3 or the wide ones."""
+    """cfg 31-36 (a workgroup's weight slice resident in LDS) are candidates only where the K x BN
+    planes of one N tile fit beside the A ring: the 1x1 GEMMs with K <= 256, not the 3x3 ones."""
     c = {c for c, _ in Fn.p3_candidates(200704, 256, 64)}
-    assert {31, 32} <= c and not {33, 34} & c
+    assert {31, 32, 33, 34} <= c
     c = {c for c, _ in Fn.p3_candidates(200704, 64, 256)}
-    assert {33, 34} <= c
-    assert not {31, 32, 33, 34} & {c for c, _ in Fn.p3_candidates(200704, 64, 576)}
-    assert not {31, 32, 33, 34} & {c for c, _ in Fn.p3_candidates(12544, 1024, 256)}
+    assert {33, 34, 35} <= c and 36 not in c
+    assert not set(Fn._P3_BRES) & {c for c, _ in Fn.p3_candidates(200704, 64, 576)}
+    assert {33, 34, 35} <= {c for c, _ in Fn.p3_candidates(12544, 1024, 256)}
+    assert {36} <= {c for c, _ in Fn.p3_candidates(50176, 512, 128)}
+    assert not set(Fn._P3_BRES) & {c for c, _ in Fn.p3_candidates(3136, 2048, 512)}
     assert all(s == 1 for c, s in Fn.p3_candidates(200704, 256, 64) if c in Fn._P3_BRES)
