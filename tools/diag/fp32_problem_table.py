@@ -18,8 +18,9 @@ from azure_hc_intel_tf_amd.ops import functional as Fn  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--dtype", default="fp32", help="fp32 (plane GEMMs) or bf16")
     a = ap.parse_args()
-    m = create_model("resnet50", device="cuda", compute_dtype="fp32")
+    m = create_model("resnet50", device="cuda", compute_dtype=a.dtype)
     autotune.load_cache()
     m.ps.repack()
     probs = autotune.model_problems(m, a.batch)
@@ -27,7 +28,7 @@ def main():
     for k, (cnt, cands, run) in probs.items():
         cur = Fn._tuned.get(k)
         t = autotune._time(lambda: run(cur)) * 1000
-        if k[0] == "wgrad3":
+        if k[0] in ("wgrad3", "wgrad"):
             _, nout, kk, mm, taps = k
             fl = 2.0 * nout * kk * mm
         else:
@@ -38,7 +39,8 @@ def main():
     tot = sum(r[0] for r in rows)
     print(f"# {len(rows)} problems, isolated sum x launches = {tot / 1000:.3f} ms/step")
     for tt, k, cnt, cur, t, tf in rows:
-        print(f"{str(k):44s} x{cnt:2d} plan {str(cur):10s} {t:7.1f} us  {tf:5.0f} TF  x6 {6 * tf / 25:4.0f}%  "
+        x = 6 if a.dtype == "fp32" else 1
+        print(f"{str(k):44s} x{cnt:2d} plan {str(cur):10s} {t:7.1f} us  {tf:5.0f} TF  MFMA {x * tf / 25:4.0f}%  "
               f"step {tt / 1000:.3f} ms ({100 * tt / tot:4.1f}%)", flush=True)
 
 
