@@ -53,7 +53,9 @@ def test_reference_precision_training_learns(dtype, monkeypatch):
     img, lab = synthetic_batch(m, 8)
     assert img.dtype == {"fp32": torch.float32, "fp16": torch.float16}[dtype]
     img = (img.float() - 127.0).div(60.0).to(img.dtype)
-    t = Trainer(m, 8, constant_lr(0.02), dynamic_loss_scale=(dtype == "fp16"))
+    # (lr 0.02 on this 8-image batch occasionally diverged after learning on the fp16 MIOpen path:
+    # 6.99 -> 3.20 by step 3, then 10.9 at step 9; 0.01 learns as fast without the overshoot)
+    t = Trainer(m, 8, constant_lr(0.01), dynamic_loss_scale=(dtype == "fp16"))
     losses = [float(t.step(img, lab)) for _ in range(12)]
     assert all(l == l for l in losses)
     assert min(losses[-3:]) < 0.8 * losses[0], losses
