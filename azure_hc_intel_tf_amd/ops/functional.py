@@ -453,7 +453,7 @@ _P3_TILES = {0: (128, 64), 1: (64, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)
              13: (128, 64), 14: (128, 64), 15: (64, 128), 16: (64, 64), 17: (64, 64),
              18: (64, 128), 19: (128, 64), 20: (64, 64), 21: (64, 64), 22: (128, 128),
              23: (64, 128), 24: (128, 64), 25: (64, 64), 26: (64, 64), 27: (128, 128), 28: (128, 128),
-             29: (256, 128), 30: (128, 256), 31: (64, 256), 32: (128, 256), 33: (64, 64), 34: (128, 64),
+             31: (64, 256), 32: (128, 256), 33: (64, 64), 34: (128, 64),
              35: (128, 64), 36: (128, 128)}
 # workgroups per CU each plane-GEMM cfg is built for
 _P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3, 18: 2, 19: 2, 20: 2, 21: 3, 23: 2, 24: 2, 25: 2, 26: 3}
@@ -461,7 +461,7 @@ _P3_OCC = {14: 2, 15: 2, 16: 2, 17: 3, 18: 2, 19: 2, 20: 2, 21: 3, 23: 2, 24: 2,
 # the LDS-DMA ring running across tile boundaries and a register epilogue; no split-K (a problem
 # with an epilogue they do not serve -- fused BN backward, beta, bias -- runs the twin)
 _P3_PERSIST = {18: 15, 19: 14, 20: 16, 21: 17, 22: 7, 23: 15, 24: 14, 25: 16, 26: 17, 27: 7, 28: 8,
-               29: 10, 30: 11, 31: 15, 32: 15, 33: 16, 34: 14, 35: 14, 36: 7}
+               31: 15, 32: 15, 33: 16, 34: 14, 35: 14, 36: 7}
 # the persistent kernel with each workgroup's weight slice resident in LDS (conv_p3_persist.h BRES):
 # every k-step's planes of one N tile (K x BN x 6 B) beside the A ring; cfg -> ring slots
 _P3_BRES = {31: 3, 32: 2, 33: 3, 34: 2, 35: 2, 36: 2}
@@ -475,7 +475,7 @@ def p3_bres_fits(cfg: int, N: int, K: int) -> bool:
 # their STREAM-K form (conv_p3_persist.h SK): every workgroup a contiguous, equal share of all (tile,
 # k-step) iterations -- no wave-quantization tail; split tiles meet through the split-K workspace.
 # sk cfg -> the cfg it falls back to (the whole-tile persistent form; 28 -- cfg 8's geometry -- cfg 8)
-_P3_STREAMK = {23: 18, 24: 19, 25: 20, 26: 21, 27: 22, 28: 8, 29: 10, 30: 11}
+_P3_STREAMK = {23: 18, 24: 19, 25: 20, 26: 21, 27: 22, 28: 8}  # (29 / 30 retired: profiles/r6_quantization_streamk.txt)
 # wgrad cfg -> block tile: 0-5 64-deep slots, 6-11 32-deep slots (128x128 / 256x128 / 128x256 tiles),
 # 12-15 32-deep slots, two / three workgroups per CU
 _WP3_TILES = {0: (128, 64), 1: (64, 128), 2: (64, 64), 3: (128, 64), 4: (64, 128), 5: (64, 64),

@@ -26,9 +26,9 @@ namespace hcb {
 
 // cfg 0-17: conv_igemm_p3_kernel (conv_p3_fwd.h); 18-22: the persistent short-K kernel
 // (conv_p3_persist.h), twins of 15, 14, 16, 17 and 7; 23-27: its stream-K form (tiles of 18-22);
-// 28-30: stream-K with cfg 8's, 10's and 11's geometry (4 x 2 waves of 32 x 64; 256 x 128 and
-// 128 x 256 of 64 x 64 wave tiles: 25% fewer operand bytes per MFMA than 128 x 128, and with
-// stream-K no quantization tail however few tiles)
+// 28: stream-K with cfg 8's geometry (4 x 2 waves of 32 x 64); 29 / 30 (stream-K 256 x 128 / 128 x 256
+// of 64 x 64 wave tiles) are retired -- a 272-byte stack frame, 5x slower (profiles/r6_quantization_streamk.txt)
+// -- and launch cfg 10 / 11
 // 31-36: the persistent kernel with the workgroup's weight slice resident in LDS (BRES): 64x256 (4
 // waves of 64x64), 128x256 (8 waves of 64x64), 64x64 (4 waves of 32x32), 128x64 (4 waves of 64x32),
 // 128x64 (8 waves of 32x32), 128x128 (8 waves of 32x64)
@@ -57,8 +57,8 @@ static int launch_p3_persist(const ConvParams& p, int cfg, hipStream_t st) {
     case 26: return launch_p3sk<2, 2, 32, 32, 32, 2, 3>(p, st) ? -1 : launch_p3_persist(p, 21, st);
     case 27: return launch_p3sk<2, 4, 64, 32, 32, 3, 1>(p, st) ? -1 : launch_p3_persist(p, 22, st);
     case 28: return launch_p3sk<4, 2, 32, 64, 32, 3, 1>(p, st) ? -1 : 8;
-    case 29: return launch_p3sk<4, 2, 64, 64, 32, 2, 1>(p, st) ? -1 : 10;
-    case 30: return launch_p3sk<2, 4, 64, 64, 32, 2, 1>(p, st) ? -1 : 11;
+    case 29: return 10;
+    case 30: return 11;
     case 31: return launch_p3bres<1, 4, 64, 64, 32, 3>(p, st) ? -1 : launch_p3_persist(p, 18, st);
     case 32: return launch_p3bres<2, 4, 64, 64, 32, 2>(p, st) ? -1 : launch_p3_persist(p, 18, st);
     case 33: return launch_p3bres<2, 2, 32, 32, 32, 3>(p, st) ? -1 : launch_p3_persist(p, 20, st);
