@@ -97,19 +97,30 @@ def aa_band(timer, rounds, reps=4):
     diffs = []
     for _ in range(reps):
         a, b = [], []
-        for _ in range(rounds):
-            a.append(timer.measure())
-            b.append(timer.measure())
+        for r in range(rounds):  # ABBA: a drift between consecutive captures cancels
+            if r % 2 == 0:
+                a.append(timer.measure())
+                b.append(timer.measure())
+            else:
+                b.append(timer.measure())
+                a.append(timer.measure())
         diffs.append(abs(statistics.median(a) - statistics.median(b)))
     return max(diffs), diffs
 
 
 def ab(timer, key, cur, cand, rounds):
-    """Interleaved A/B of one problem's plan: medians (ms/step) of the current and the candidate."""
+    """Interleaved A/B of one problem's plan: medians (ms/step) of the current and the candidate, in
+    ABBA order (round 6: with A always first, the second capture of every pair measured ~0.1 ms
+    slower -- an identical table included, profiles/r6_step_tune_order.txt -- which biased every
+    in-step comparison against the candidate)."""
     a, b = [], []
-    for _ in range(rounds):
-        a.append(timer.measure({key: cur}))
-        b.append(timer.measure({key: cand}))
+    for r in range(rounds):
+        if r % 2 == 0:
+            a.append(timer.measure({key: cur}))
+            b.append(timer.measure({key: cand}))
+        else:
+            b.append(timer.measure({key: cand}))
+            a.append(timer.measure({key: cur}))
     return statistics.median(a), statistics.median(b)
 
 
@@ -216,11 +227,10 @@ def main():
         name, va, vb = a.knob_ab.split(":")
         setter = {"p3p_bnb": Fn.set_p3p_bnb}[name]
         ta, tb = [], []
-        for _ in range(a.aa_reps * a.rounds):
-            setter(int(va))
-            ta.append(timer.measure())
-            setter(int(vb))
-            tb.append(timer.measure())
+        for r in range(a.aa_reps * a.rounds):  # ABBA
+            for v, t in (((va, ta), (vb, tb)) if r % 2 == 0 else ((vb, tb), (va, ta))):
+                setter(int(v))
+                t.append(timer.measure())
         ma, mb = statistics.median(ta), statistics.median(tb)
         log(f"[step_tune] knob {name}: {va} {ma:.4f} ms/step vs {vb} {mb:.4f} ms/step ({100 * (ma - mb) / ma:+.2f}%; "
             f"A/A band {100 * noise / t0:.2f}%) A: {' '.join(f'{x:.4f}' for x in ta)} B: {' '.join(f'{x:.4f}' for x in tb)}")
@@ -261,9 +271,13 @@ def main():
     # final: start table vs tuned table, interleaved
     final_patch = {k: Fn._tuned[k] for k in probs}
     s_t, f_t = [], []
-    for _ in range(4):
-        s_t.append(timer.measure(start_table))
-        f_t.append(timer.measure(final_patch))
+    for r in range(4):  # ABBA
+        if r % 2 == 0:
+            s_t.append(timer.measure(start_table))
+            f_t.append(timer.measure(final_patch))
+        else:
+            f_t.append(timer.measure(final_patch))
+            s_t.append(timer.measure(start_table))
     changed = {str(k): [start_table[k], final_patch[k]] for k in probs if start_table[k] != final_patch[k]}
     res = {"model": a.model, "batch": a.batch, "dtype": a.dtype, "problems": len(probs),
            "start_ms": statistics.median(s_t), "final_ms": statistics.median(f_t), "noise_ms": noise,
