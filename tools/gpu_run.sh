@@ -48,8 +48,8 @@ for step in "$@"; do
     bench)
       timeout -k 10 400 python bench.py $args > ${O}_bench.json 2> ${O}_bench.err || fail bench ${O}_bench.err
       cut -c1-260 ${O}_bench.json ;;
-    benchab)
-      for r in 1 2; do for v in base var; do
+    benchab)  # ABBA: base var var base (a drift between consecutive runs cancels)
+      for r in 1 2; do if [ $r = 1 ]; then vs="base var"; else vs="var base"; fi; for v in $vs; do
         if [ $v = base ]; then e=""; else e="$args"; fi
         env $e timeout -k 10 400 python bench.py --steps 40 --warmup 10 $BENCH_ARGS > ${O}_ab.json 2> ${O}_ab.err || fail benchab ${O}_ab.err
         echo "$v [$e] $(python -c "import json;d=json.load(open('${O}_ab.json'));print(d['value'], d['ms_per_step'], 'bf16', d.get('bf16_value'), d.get('bf16_ms_per_step'))")"
