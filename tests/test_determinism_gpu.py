@@ -55,10 +55,12 @@ def test_deterministic_mode_trains_like_default():
     # the first steps, before the chaos has amplified anything, against a tight fixed bound (a
     # regression of the deterministic split-K / statistics path shows up here, whatever the band):
     # step 0 is the forward of identical weights (only the fp32 summation order differs; bf16
-    # activations turn a reordered sum into an occasional 1-ulp flip, so the default runs themselves
-    # spread by up to ~3e-3 at step 0 on this 4-image batch): within that spread of their mean
+    # activations turn a reordered sum into an occasional 1-ulp flip: the default runs spread by up
+    # to ~3e-3 at step 0 on this 4-image batch, and the deterministic run -- bitwise the same every
+    # time, 7.59103 -- sat 1.2e-3 above a tightly clustered set of default runs once): 3e-3 of their
+    # mean, or their own spread if larger
     mean = runs.mean(0)
-    tol0 = max(1e-3 * abs(float(mean[0])), float(hi[0] - lo[0]))
+    tol0 = max(3e-3 * abs(float(mean[0])), float(hi[0] - lo[0]))
     assert abs(float(trd[0] - mean[0])) <= tol0, (trd.tolist(), runs.tolist())
     assert abs(float(trd[1] - mean[1])) <= 3e-2 * abs(float(mean[1])), (trd.tolist(), runs.tolist())
     # (a stable learning rate: at 0.05 this tiny-batch run diverges)
