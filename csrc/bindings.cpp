@@ -966,7 +966,7 @@ void preprocess_images(const Tensor& src, const Tensor& desc, const Tensor& desc
                        at::ArrayRef<double> scale, at::ArrayRef<double> bias) {
   check_cuda(src, "src");
   check_cuda(desc, "desc");
-  check_act(out, "out");
+  const bool f32 = check_act_or_f32(out, "out");  // the fp32 path's input is fp32
   TORCH_CHECK(src.scalar_type() == at::kByte && src.is_contiguous(), "hcb.preprocess_images: src uint8 contiguous");
   TORCH_CHECK(desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 4 && desc.is_contiguous(),
               "hcb.preprocess_images: desc int64 [B][4]");
@@ -990,7 +990,7 @@ void preprocess_images(const Tensor& src, const Tensor& desc, const Tensor& desc
   const float bi[3] = {(float)bias[0], (float)bias[1], (float)bias[2]};
   if (B == 0) return;
   hcb::launch_preprocess_images(src.data_ptr<uint8_t>(), desc.data_ptr<int64_t>(), (int)B, out.data_ptr(),
-                                (int)out.size(1), (int)out.size(3), sc, bi, cur_stream());
+                                (int)out.size(1), (int)out.size(3), sc, bi, f32, cur_stream());
 }
 
 static int pack_mode(const Tensor& t, const char* what) {

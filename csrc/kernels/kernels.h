@@ -282,7 +282,7 @@ void launch_synth_labels(int64_t* out, int n, int ncls, uint64_t seed, hipStream
 // real data: batch of RGB uint8 crops (desc [B][4] = byte offset, h, w, flip) -> bilinear resize
 // to S x S, optional horizontal flip, x*scale[c]+bias[c], NHWC bf16 with Cpad channels
 void launch_preprocess_images(const uint8_t* src, const int64_t* desc, int B, void* out, int S, int Cpad,
-                              const float* scale, const float* bias, hipStream_t st);
+                              const float* scale, const float* bias, bool f32, hipStream_t st);
 
 // ---------------------------------------------------------------- space-to-depth stem (stem.hip)
 void launch_stem_s2d_f32(const float* x, int N, int H, int W, int ldx, uint16_t* out, int64_t plane, int Hs, int Ws,

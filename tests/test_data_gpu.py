@@ -1,6 +1,6 @@
 """GPU half of the real-data pipeline: the HIP preprocess kernel (resize / flip / normalise /
-NHWC bf16 pack) against the PyTorch fp32 reference, and the ImageNetLoader feeding a
-graph-captured training step from TFRecords."""
+NHWC bf16 or fp32 pack) against the PyTorch fp32 reference, and the ImageNetLoader feeding a
+graph-captured training step from TFRecords at bf16 and at fp32 (the default precision)."""
 import os
 import sys
 
@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 pytestmark = pytest.mark.gpu
 
 
-def test_preprocess_kernel_matches_reference():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_preprocess_kernel_matches_reference(dtype):
     from azure_hc_intel_tf_amd.data.imagenet import BIAS, SCALE, preprocess_reference
     from azure_hc_intel_tf_amd.ops import _ext
 
@@ -33,19 +34,22 @@ def test_preprocess_kernel_matches_reference():
         off += c.size + pad
     src = torch.from_numpy(np.concatenate(chunks)).cuda()
     desc_h = torch.tensor(desc, dtype=torch.int64)
-    out = torch.full((len(crops), S, S, 8), 7.0, dtype=torch.bfloat16, device="cuda")
+    out = torch.full((len(crops), S, S, 8), 7.0, dtype=dtype, device="cuda")
     _ext.ops().preprocess_images(src, desc_h.cuda(), desc_h, out, list(SCALE), list(BIAS))
     ref = torch.empty(len(crops), S, S, 8)
     preprocess_reference(crops, flips, ref)
     err = (out.float().cpu() - ref).abs().max().item()
-    assert err < 1e-2, err  # bf16 rounding of values in [-1, 1]
+    # bf16: rounding of values in [-1, 1]; fp32: the source coordinate y*(h/S) is formed in fp32 here and
+    # from a double ratio in the reference, a ~1e-5 px difference times pixel steps of up to 255/127.5
+    assert err < (1e-2 if dtype == torch.bfloat16 else 2e-4), err
     with pytest.raises(RuntimeError, match="outside the staging buffer"):
         bad = desc_h.clone()
         bad[0, 1] = 10_000
         _ext.ops().preprocess_images(src, bad.cuda(), bad, out, list(SCALE), list(BIAS))
 
 
-def test_loader_feeds_graph_captured_training(tmp_path):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_loader_feeds_graph_captured_training(tmp_path, dtype):
     import make_fake_imagenet
 
     from azure_hc_intel_tf_amd.data.imagenet import ImageNetLoader
@@ -53,9 +57,11 @@ def test_loader_feeds_graph_captured_training(tmp_path):
     from azure_hc_intel_tf_amd.trainer import Trainer, constant_lr, synthetic_batch
 
     make_fake_imagenet.make(str(tmp_path), shards=2, per_shard=16, seed=3)
-    m = create_model("resnet50", image_size=64, device="cuda:0", compute_dtype="bf16")
+    m = create_model("resnet50", image_size=64, device="cuda:0", compute_dtype=dtype)
     img, lab = synthetic_batch(m, 8)
-    ld = ImageNetLoader(str(tmp_path), 8, 64, 8, "cuda:0", seed=1, reader_threads=2, decode_threads=4, depth=2)
+    assert img.dtype == (torch.float32 if dtype == "fp32" else torch.bfloat16)
+    ld = ImageNetLoader(str(tmp_path), 8, 64, img.shape[3], "cuda:0", seed=1, reader_threads=2, decode_threads=4,
+                        depth=2)
     t = Trainer(m, 8, constant_lr(0.01), use_graph=True)
     losses = []
     for _ in range(5):  # eager warmup steps, capture, replays: every one reads the new batch
