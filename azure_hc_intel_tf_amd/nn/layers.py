@@ -223,6 +223,8 @@ class ConvBN(Layer):
         if self.bn and not self.training:
             z = empty_act((N, P, Q, C), dev)
             y = out if out is not None else empty_act((N, P, Q, C), dev)
+            if Fn.planes_mode() and Fn.native(x) and not Fn.is_planes(x):  # fp32 path: the GEMM operand as planes
+                x = Fn.to_planes(x)
             Fn.conv_forward(x, self.spec, self.pack.pack if Fn.native(x) else None, self.w.data, z)
             Fn.bn_inference(z, self.gamma.data, self.beta.data, self.rmean.data, self.rvar.data, self.eps, y,
                             self.relu, residual=residual)

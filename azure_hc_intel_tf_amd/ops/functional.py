@@ -925,8 +925,25 @@ class BNSaved:
 def bn_inference(z, gamma, beta, running_mean, running_var, eps, out, relu: bool, residual=None):
     """Inference BN (``--forward_only``: tf_cnn_benchmarks builds the model with
     phase_train=False): out = act(gamma*(z-moving_mean)/sqrt(moving_var+eps) + beta [+ res])."""
-    invstd = torch.rsqrt(running_var + eps)
     N, H, W, C = z.shape
+    if native(z) and z.dtype == torch.float32:
+        # fp32 path: the fp32 apply kernel of training (bn_apply_acc, z / out / residual fp32) fed
+        # moving statistics as one replica of shifted sums -- shift = moving mean, sum 0, sum of
+        # squares M * moving var -- so its mean is the moving mean exactly and its variance the moving
+        # variance to an ulp; no running-stat pointers (nothing updated), scratch saved stats
+        M = N * H * W
+        acc = torch.stack([torch.zeros_like(running_var), running_var * float(M)]).unsqueeze(0).contiguous()
+        scratch = torch.empty(2, C, dtype=torch.float32, device=z.device)
+        if residual is not None:  # the kernel reads a residual in out's format (fp32, or planes)
+            if is_planes(out) and not is_planes(residual):
+                residual = to_planes(residual)
+            elif not is_planes(out) and is_planes(residual):
+                residual = from_planes(residual)
+        _ext.ops().bn_apply_acc(z, ld(z), _pl(out), ld(out), _pl(residual), ld(residual) if residual is not None else 0,
+                                M, C, acc, 1, eps, 1.0, gamma, beta, 1 if relu else 0, scratch[0], scratch[1],
+                                None, None, running_mean)
+        return out
+    invstd = torch.rsqrt(running_var + eps)
     if native(z):
         _ext.ops().bn_apply(z, ld(z), out, ld(out), residual, ld(residual) if residual is not None else 0,
                             N * H * W, C, running_mean, invstd, gamma, beta, 1 if relu else 0)

@@ -1,0 +1,50 @@
+#!/bin/bash
+# tf_cnn_benchmarks CLI feature sweep on one MI355X at the default precision (fp32) and the 16-bit
+# modes: every flag family the reference's runners or users touch, a few steps each. A case passes
+# when the run prints "total images/sec". A Python error (rc 1) is recorded and the sweep goes on;
+# a time limit, abort or fault (rc 124/134/137/139) ends it, nothing more runs on the GPU.
+set -o pipefail
+mkdir -p gpurun_out/cli_sweep
+OUT=gpurun_out/cli_sweep
+SUM=$OUT/summary.txt
+: > $SUM
+n=0
+run() {  # run NAME FLAGS...
+  local name=$1; shift
+  n=$((n + 1))
+  timeout -k 10 240 python -u tf_cnn_benchmarks.py --display_every=2 "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  local ips
+  ips=$(grep -o "total images/sec: [0-9.]*" $OUT/$name.log | tail -1 | awk '{print $3}')
+  if [ $rc -eq 0 ] && [ -n "$ips" ]; then
+    echo "PASS $name $ips img/s :: $*" | tee -a $SUM
+  else
+    echo "FAIL(rc=$rc) $name :: $* :: $(grep -E 'Error|error' $OUT/$name.log | tail -1 | cut -c1-200)" | tee -a $SUM
+  fi
+  case $rc in 124|134|137|139) echo "stopping: rc $rc" | tee -a $SUM; exit $rc;; esac
+  return 0
+}
+R50="--model=resnet50 --batch_size=64 --num_batches=6 --num_warmup_batches=2"
+SMALL="--batch_size=16 --num_batches=4 --num_warmup_batches=1 --autotune=False"
+rm -rf /tmp/hcb_cli_ckpt
+run r50_default $R50
+run r50_forward_only $R50 --forward_only=True
+run r50_ckpt_save $R50 --train_dir=/tmp/hcb_cli_ckpt --save_model_steps=3 --optimizer=momentum
+run r50_ckpt_resume $R50 --train_dir=/tmp/hcb_cli_ckpt --save_model_steps=3 --optimizer=momentum
+run r50_trace $R50 --trace_file=$OUT/trace.json
+run r50_accuracy_smoothing $R50 --print_training_accuracy=True --label_smoothing=0.1
+run r50_eager $R50 --use_hip_graph=False
+run r50_sgd_nhwc $R50 --optimizer=sgd --data_format=NHWC
+run r50_comm_check $R50 --comm_check=True --variable_update=horovod
+run r50_compress_fp16 $R50 --gradient_compression=fp16 --variable_update=horovod
+run r50_comm_torch $R50 --comm_engine=torch --variable_update=horovod
+run r50_json $R50 --json_summary=$OUT/summary.json --benchmark_log_dir=$OUT/bench_logs
+run r50_img160 --model=resnet50 $SMALL --image_size=160
+run r50_bf16 $R50 --compute_dtype=bf16
+run r50_fp16_autoscale $R50 --use_fp16=True --fp16_enable_auto_loss_scale=True
+run r50_fp16_bf16half $R50 --use_fp16=True --half_dtype=bf16
+for m in resnet101 resnet152 resnet50_v2 resnet101_v2 resnet152_v2 inception3 trivial vgg11 vgg16 vgg19 alexnet overfeat lenet googlenet; do
+  run ${m}_fp32 --model=$m $SMALL
+  run ${m}_fp32_fwd --model=$m $SMALL --forward_only=True
+done
+echo "sweep done: $(grep -c ^PASS $SUM) pass, $(grep -c ^FAIL $SUM) fail of $n" | tee -a $SUM
