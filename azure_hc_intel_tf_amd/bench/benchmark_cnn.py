@@ -70,8 +70,8 @@ class BenchmarkCNN:
             raise ValueError(f"--variable_update={p.variable_update} is not supported; use horovod")
         if p.num_gpus != 1:
             raise ValueError("one process per MI355X: use --num_gpus=1 and launch one worker per GPU")
-        if p.label_smoothing:
-            raise ValueError("--label_smoothing is not supported")
+        if not 0.0 <= p.label_smoothing <= 1.0:
+            raise ValueError("--label_smoothing must be in [0, 1]")
         self.on_gpu = p.device == "gpu"
         if self.on_gpu and not torch.cuda.is_available():
             raise RuntimeError("--device=gpu but no GPU is visible (use --device=cpu for the CPU path)")
@@ -152,7 +152,7 @@ class BenchmarkCNN:
         self.trainer = Trainer(self.model, self.batch_size, self._lr_fn(), momentum=mom,
                                weight_decay=p.weight_decay, reducer=reducer, world_size=self.size,
                                use_graph=bool(p.use_hip_graph) and self.on_gpu and p.horovod_device != "cpu",
-                               forward_only=bool(p.forward_only),
+                               forward_only=bool(p.forward_only), label_smoothing=p.label_smoothing,
                                # --use_fp16: loss scaling as in the reference flags (static scale or
                                # automatic scaling), whichever 16-bit type computes
                                loss_scale=p.fp16_loss_scale if p.use_fp16 else None,

@@ -95,7 +95,7 @@ FLAGS: List[Flag] = [
     Flag("allow_growth", None, parse_bool, "accepted", noop_on_gpu=True),
     Flag("gradient_repacking", 0, int, "accepted", noop_on_gpu=True),
     Flag("all_reduce_spec", None, str, "accepted", noop_on_gpu=True),
-    Flag("label_smoothing", 0.0, float, "label smoothing (0 only)"),
+    Flag("label_smoothing", 0.0, float, "label smoothing of the softmax cross-entropy targets: (1-ls)*onehot + ls/num_classes"),
     Flag("image_size", 0, int, "override the model's input resolution (0 = model default)"),
     # --- MI355X engine knobs
     Flag("use_hip_graph", True, parse_bool, "capture the training step in a HIP graph"),

@@ -1216,8 +1216,11 @@ def gap_backward(dy, dx):
 
 
 # ------------------------------------------------------------------------- loss
-def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None, dl32=None):
-    """Per-row cross entropy (into row_loss) and dlogits = (softmax - onehot) * scale
+def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None, dl32=None,
+                 label_smoothing: float = 0.0):
+    """Per-row cross entropy (into row_loss) and dlogits = (softmax - target) * scale, target =
+    onehot, or (1 - ls) * onehot + ls / ncls with ``label_smoothing`` ls (tf_cnn_benchmarks
+    --label_smoothing through tf.losses.softmax_cross_entropy)
     (* scale_dev[0], a device-resident loss scale, when given); ``dl32``: with 16-bit dlogits,
     also the unrounded fp32 values (same layout), from which the classifier's bias gradient is
     summed (its batch sum cancels to ~1% of the terms: bf16 rounding of each term would cost
@@ -1225,15 +1228,19 @@ def softmax_xent(logits, labels, ncls, row_loss, dlogits, scale, scale_dev=None,
     B = labels.numel()
     if native(dlogits):
         _ext.ops().softmax_xent(logits, ld(logits), labels, ncls, row_loss, dlogits, ld(dlogits), scale, scale_dev,
-                                dl32)
+                                dl32, float(label_smoothing))
         return
     if scale_dev is not None:
         scale = scale * float(scale_dev.reshape(-1)[0])
     lg = logits[:, :ncls].float()
     lse = torch.logsumexp(lg, dim=1)
-    row_loss.copy_(lse - lg.gather(1, labels.view(-1, 1)).view(-1))
+    ls = float(label_smoothing)
+    pos, neg = 1.0 - ls, ls / ncls
+    row_loss.copy_(lse - pos * lg.gather(1, labels.view(-1, 1)).view(-1) - (neg * lg.sum(1) if ls else 0.0))
     p = torch.softmax(lg, dim=1)
-    p[torch.arange(B), labels] -= 1.0
+    if ls:
+        p -= neg
+    p[torch.arange(B), labels] -= pos
     dlogits.zero_()
     dlogits[:, :ncls].copy_(p * scale)
 

@@ -72,8 +72,10 @@ class Trainer:
                  weight_decay: float = 4e-5, reducer=None, world_size: int = 1, use_graph: bool = True,
                  nesterov: bool = False, graph_warmup: int = 2, forward_only: bool = False,
                  loss_scale: Optional[float] = None, dynamic_loss_scale: bool = False,
-                 loss_scale_interval: int = 1000, force_overlap: bool = False, comm_check: Optional[bool] = None):
+                 loss_scale_interval: int = 1000, force_overlap: bool = False, comm_check: Optional[bool] = None,
+                 label_smoothing: float = 0.0):
         self.model = model
+        self.label_smoothing = float(label_smoothing)  # --label_smoothing (the loss kernel's targets)
         self.ps = model.ps
         self.B = batch_size
         self.dev = model.device
@@ -165,7 +167,8 @@ class Trainer:
             logits = self.model.forward(images)
         self.logits = logits
         Fn.softmax_xent(logits, labels, self.model.num_classes, self.row_loss, self.dlogits, 1.0 / self.B,
-                        self.hyper[5:6] if self.loss_scaling else None, self.dlogits32)
+                        self.hyper[5:6] if self.loss_scaling else None, self.dlogits32,
+                        label_smoothing=self.label_smoothing)
 
     def _forward_backward(self, images, labels):
         self._forward(images, labels)

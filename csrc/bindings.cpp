@@ -579,8 +579,10 @@ void gap_bwd(const Tensor& dy, const Tensor& dx, int64_t N, int64_t HW, int64_t 
 
 void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_t ncls,
                   const Tensor& row_loss, const Tensor& dlogits, int64_t lddl, double scale,
-                  const c10::optional<Tensor>& scale_dev, const c10::optional<Tensor>& dl32) {
+                  const c10::optional<Tensor>& scale_dev, const c10::optional<Tensor>& dl32,
+                  double label_smoothing) {
   check_f32(logits, "logits");
+  TORCH_CHECK(label_smoothing >= 0.0 && label_smoothing <= 1.0, "hcb.softmax_xent: label_smoothing in [0, 1]");
   check_cuda(labels, "labels");
   TORCH_CHECK(labels.scalar_type() == at::kLong, "hcb.softmax_xent: labels int64");
   const bool f32 = check_act_or_f32(dlogits, "dlogits");
@@ -597,7 +599,8 @@ void softmax_xent(const Tensor& logits, int64_t ld, const Tensor& labels, int64_
   }
   hcb::launch_softmax_xent(logits.data_ptr<float>(), (int)ld, labels.data_ptr<int64_t>(), (int)B, (int)ncls,
                            row_loss.data_ptr<float>(), dlogits.data_ptr(), (int)lddl, (float)scale,
-                           scale_dev.has_value() ? scale_dev->data_ptr<float>() : nullptr, cur_stream(), f32, d32);
+                           scale_dev.has_value() ? scale_dev->data_ptr<float>() : nullptr, cur_stream(), f32, d32,
+                           (float)label_smoothing);
 }
 
 void nonfinite(const Tensor& g, const Tensor& flag) {
@@ -1250,7 +1253,7 @@ HCB_TORCH_LIBRARY(hcb, m) {
   m.def("pool_fwd_p3(Tensor x, Tensor(a!) y, Tensor(b!)? idx, int[] geom) -> ()");
   m.def("gap_fwd(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
   m.def("gap_bwd(Tensor dy, Tensor(a!) dx, int N, int HW, int C) -> ()");
-  m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale, Tensor? scale_dev=None, Tensor(c!)? dl32=None) -> ()");
+  m.def("softmax_xent(Tensor logits, int ld, Tensor labels, int ncls, Tensor(a!) row_loss, Tensor(b!) dlogits, int lddl, float scale, Tensor? scale_dev=None, Tensor(c!)? dl32=None, float label_smoothing=0.0) -> ()");
   m.def("nonfinite(Tensor g, Tensor(a!) flag) -> ()");
   m.def("loss_total(Tensor row_loss, int B, Tensor? l2, float half_wd, Tensor(a!) loss) -> ()");
   m.def("loss_scale_update(Tensor(a!) hyper, float world, bool dynamic) -> ()");

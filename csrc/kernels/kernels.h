@@ -236,7 +236,8 @@ void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t 
 // ---------------------------------------------------------------- loss / fc helpers
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
                          float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
-                         hipStream_t st, bool f32 = false, float* dl32 = nullptr);
+                         hipStream_t st, bool f32 = false, float* dl32 = nullptr,
+                         float label_smoothing = 0.f);
 constexpr int ZERO_BUFS = 6;
 void launch_zero_bufs(float* const* ptrs, const int64_t* ns, int nb, hipStream_t st);
 void launch_colsum2(const void* g, int ld, int M, int N, int is_f32, float* out, hipStream_t st);

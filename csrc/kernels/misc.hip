@@ -1,6 +1,7 @@
 // Loss, optimizer, weight-preparation, data and gradient-bucket kernels (gfx950).
 //
 //   * softmax_xent: tf.losses.sparse_softmax_cross_entropy + its gradient in one pass
+//     (label_smoothing ls: targets (1-ls)*onehot + ls/ncls, tf.losses.softmax_cross_entropy's form)
 //     (one 256-thread block per row, wave64 shuffles + LDS for the row max / sum).
 //   * sgd_momentum: TF ApplyMomentum over ALL parameters in ONE launch (flat fp32
 //     master/momentum/grad buffers; L2 weight decay folded in as wd*w for the decayed
@@ -28,8 +29,8 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
                                                            const int64_t* __restrict__ labels,
                                                            int ncls, float* row_loss,
                                                            T* dl, int lddl, float scale,
-                                                           const float* scale_dev, float* dl32) {
-  __shared__ float red[8];
+                                                           const float* scale_dev, float* dl32, float ls) {
+  __shared__ float red[12];
   if (scale_dev != nullptr) scale *= *scale_dev;  // device-resident loss scale
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float* lr = logits + (size_t)row * ld;
@@ -40,19 +41,28 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   __syncthreads();
   mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   __syncthreads();
-  float s = 0.f;
-  for (int c = tid; c < ncls; c += 256) s += __expf(lr[c] - mx);
+  float s = 0.f, sl = 0.f;
+  for (int c = tid; c < ncls; c += 256) {
+    s += __expf(lr[c] - mx);
+    sl += lr[c];  // (the smoothed targets' uniform part weighs every logit)
+  }
   s = wave_sum(s);
-  if (lane == 0) red[4 + wid] = s;
+  if (ls != 0.f) sl = wave_sum(sl);
+  if (lane == 0) {
+    red[4 + wid] = s;
+    red[8 + wid] = sl;
+  }
   __syncthreads();
   s = red[4] + red[5] + red[6] + red[7];
   const float lse = mx + __logf(s);
   const int lab = (int)labels[row];
-  if (tid == 0) row_loss[row] = lse - lr[lab];
+  const float pos = 1.f - ls, neg = ls / (float)ncls;  // target = pos * onehot + neg
+  if (tid == 0)
+    row_loss[row] = ls != 0.f ? lse - pos * lr[lab] - neg * (red[8] + red[9] + red[10] + red[11]) : lse - lr[lab];
   const float inv = 1.f / s;
   for (int c = tid; c < lddl; c += 256) {
     float g = 0.f;
-    if (c < ncls) g = (__expf(lr[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * scale;
+    if (c < ncls) g = (__expf(lr[c] - mx) * inv - ((c == lab ? pos : 0.f) + neg)) * scale;
     if constexpr (sizeof(T) == 4) {
       dl[(size_t)row * lddl + c] = g;
     } else {
@@ -541,13 +551,13 @@ static int grid_for(int64_t n) {
 
 void launch_softmax_xent(const float* logits, int ld, const int64_t* labels, int B, int ncls,
                          float* row_loss, void* dlogits, int lddl, float scale, const float* scale_dev,
-                         hipStream_t st, bool f32, float* dl32) {
+                         hipStream_t st, bool f32, float* dl32, float label_smoothing) {
   if (f32)
     hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls, row_loss,
-                       (float*)dlogits, lddl, scale, scale_dev, (float*)nullptr);
+                       (float*)dlogits, lddl, scale, scale_dev, (float*)nullptr, label_smoothing);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<uint16_t>, dim3(B), dim3(256), 0, st, logits, ld, labels, ncls, row_loss,
-                       (uint16_t*)dlogits, lddl, scale, scale_dev, dl32);
+                       (uint16_t*)dlogits, lddl, scale, scale_dev, dl32, label_smoothing);
 }
 
 // ------------------------------------------------------------------ loss scaling
