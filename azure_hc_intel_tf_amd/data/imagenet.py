@@ -112,7 +112,15 @@ class ImageNetLoader:
         self.C = channels
         self.device = torch.device(device)
         self.train = train
-        self.files = find_shards(data_dir, subset or ("train" if train else "validation"))
+        if subset is None and not train:
+            # inference (--forward_only): the validation shards when the directory has them, else the
+            # train shards (a train-only set, e.g. a benchmark copy), still with the eval preprocessing
+            try:
+                self.files = find_shards(data_dir, "validation")
+            except FileNotFoundError:
+                self.files = find_shards(data_dir, "train")
+        else:
+            self.files = find_shards(data_dir, subset or ("train" if train else "validation"))
         self.max_side = 4 * image_size
         self.pf = native().Prefetcher(self.files, rank=rank, world=world, threads=reader_threads,
                                       shuffle_buffer=shuffle_buffer if train else 1, capacity=max(8192, shuffle_buffer),

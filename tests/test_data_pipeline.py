@@ -204,6 +204,26 @@ def test_imagenet_loader_cpu(fake_dir):
     assert len(set(torch.cat(seen).tolist())) > 4
 
 
+def test_inference_loader_falls_back_to_train_shards(fake_dir, tmp_path):
+    """--forward_only reads the validation shards; a train-only directory still serves it."""
+    import make_fake_imagenet
+
+    from azure_hc_intel_tf_amd.data.imagenet import ImageNetLoader
+
+    ld = ImageNetLoader(fake_dir, 4, 32, 3, "cpu", train=False, seed=0, reader_threads=2, decode_threads=2, depth=2)
+    assert ld.files and all("validation-" in os.path.basename(f) for f in ld.files)
+    ld.close()
+    make_fake_imagenet.make(str(tmp_path), shards=2, per_shard=8, subset="train", seed=4)
+    ld = ImageNetLoader(str(tmp_path), 4, 32, 3, "cpu", train=False, seed=0, reader_threads=2, decode_threads=2,
+                        depth=2)
+    assert ld.files and all("train-" in os.path.basename(f) for f in ld.files)
+    img = torch.zeros(4, 32, 32, 3)
+    lab = torch.zeros(4, dtype=torch.int64)
+    ld.next_into(img, lab)
+    ld.close()
+    assert img.abs().max() <= 1.0 + 1e-6 and img.std() > 0.01
+
+
 def test_cli_real_data_cpu_end_to_end(fake_dir, tmp_path):
     out = tmp_path / "summary.json"
     cmd = [sys.executable, os.path.join(ROOT, "tf_cnn_benchmarks.py"), "--device=cpu", "--model=trivial",

@@ -3,10 +3,11 @@
 # modes: every flag family the reference's runners or users touch, a few steps each. A case passes
 # when the run prints "total images/sec". A Python error (rc 1) is recorded and the sweep goes on;
 # a time limit, abort or fault (rc 124/134/137/139) ends it, nothing more runs on the GPU.
+# SET=2: the second case list (real data, checkpoint timing, comm knobs, 16-bit zoo, inference).
 set -o pipefail
 mkdir -p gpurun_out/cli_sweep
 OUT=gpurun_out/cli_sweep
-SUM=$OUT/summary.txt
+SUM=$OUT/summary${SET:-}.txt
 : > $SUM
 n=0
 run() {  # run NAME FLAGS...
@@ -26,6 +27,28 @@ run() {  # run NAME FLAGS...
 }
 R50="--model=resnet50 --batch_size=64 --num_batches=6 --num_warmup_batches=2"
 SMALL="--batch_size=16 --num_batches=4 --num_warmup_batches=1 --autotune=False"
+if [ "${SET:-1}" = 2 ]; then  # second set: real data, checkpoint timing, comm knobs, 16-bit zoo, inference
+  D=/tmp/hcb_fake_imagenet
+  [ -f $D/.done ] || { timeout -k 10 300 python tools/make_fake_imagenet.py $D --shards 4 --per_shard 128 > /dev/null && touch $D/.done; } || exit 1
+  rm -rf /tmp/hcb_cli_ckpt2
+  run r50_data_fwd $R50 --data_dir=$D --data_name=imagenet --forward_only=True
+  run inception3_data --model=inception3 $SMALL --data_dir=$D --data_name=imagenet
+  run inception3_data_bf16 --model=inception3 $SMALL --data_dir=$D --data_name=imagenet --compute_dtype=bf16
+  run r50_epochs --model=resnet50 --batch_size=64 --num_epochs=0.0003 --num_warmup_batches=2
+  run r50_ckpt_secs $R50 --train_dir=/tmp/hcb_cli_ckpt2 --save_model_secs=1
+  run r50_repack_spec $R50 --gradient_repacking=4 --all_reduce_spec=nccl --variable_update=horovod
+  run r50_summary $R50 --summary_verbosity=1 --benchmark_log_dir=$OUT/bench_logs2 --tf_random_seed=7
+  run r50_hvd_cpu $R50 --horovod_device=cpu --variable_update=horovod
+  run r50_mkl_kmp $R50 --mkl=True --kmp_blocktime=1 --kmp_affinity=granularity=fine --num_intra_threads=4 --num_inter_threads=2 --xla=True
+  run r50v15_fp32 --model=resnet50_v1.5 $SMALL
+  run r50v15_fp32_fwd --model=resnet50_v1.5 $SMALL --forward_only=True
+  for m in vgg16 googlenet alexnet resnet152_v2 inception3 resnet50_v2; do
+    run ${m}_bf16_fwd --model=$m $SMALL --compute_dtype=bf16 --forward_only=True
+    run ${m}_fp16 --model=$m $SMALL --use_fp16=True
+  done
+  echo "sweep done: $(grep -c ^PASS $SUM) pass, $(grep -c ^FAIL $SUM) fail of $n" | tee -a $SUM
+  exit 0
+fi
 rm -rf /tmp/hcb_cli_ckpt
 run r50_default $R50
 run r50_forward_only $R50 --forward_only=True
