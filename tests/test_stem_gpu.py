@@ -130,5 +130,9 @@ def test_resnet_uses_s2d_stem_and_trains():
     assert isinstance(m.stem, StemS2D)
     img, lab = synthetic_batch(m, 16)
     t = Trainer(m, 16, constant_lr(0.02), use_graph=True, graph_warmup=2)
-    losses = [float(t.step(img, lab)) for _ in range(16)]
-    assert all(l == l for l in losses) and min(losses[-3:]) < 0.8 * losses[2], losses
+    # 24 steps: the bf16 loss sits on a ~3.3 plateau for a few steps before it falls again, and how
+    # long depends on the summation order of the kernels earlier tests' autotuning picked in this
+    # process (16 steps: passes alone and after the forward-only tests, 2.80 vs 0.8 * 3.36 once in
+    # the full GPU tier)
+    losses = [float(t.step(img, lab)) for _ in range(24)]
+    assert all(l == l for l in losses) and min(losses[-4:]) < 0.8 * losses[2], losses
