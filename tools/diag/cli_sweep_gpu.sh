@@ -3,7 +3,8 @@
 # modes: every flag family the reference's runners or users touch, a few steps each. A case passes
 # when the run prints "total images/sec". A Python error (rc 1) is recorded and the sweep goes on;
 # a time limit, abort or fault (rc 124/134/137/139) ends it, nothing more runs on the GPU.
-# SET=2: the second case list (real data, checkpoint timing, comm knobs, 16-bit zoo, inference).
+# SET=2: the second case list (real data, checkpoint timing, comm knobs, 16-bit zoo, inference);
+# SET=3: checkpoints across precisions and batch sizes, real data on the other model families.
 set -o pipefail
 mkdir -p gpurun_out/cli_sweep
 OUT=gpurun_out/cli_sweep
@@ -27,6 +28,22 @@ run() {  # run NAME FLAGS...
 }
 R50="--model=resnet50 --batch_size=64 --num_batches=6 --num_warmup_batches=2"
 SMALL="--batch_size=16 --num_batches=4 --num_warmup_batches=1 --autotune=False"
+if [ "${SET:-1}" = 3 ]; then  # third set: checkpoints across precisions, real data on the other families
+  D=/tmp/hcb_fake_imagenet
+  [ -f $D/.done ] || { timeout -k 10 300 python tools/make_fake_imagenet.py $D --shards 4 --per_shard 128 > /dev/null && touch $D/.done; } || exit 1
+  rm -rf /tmp/hcb_cli_ckpt3
+  run ck_fp32_save $R50 --train_dir=/tmp/hcb_cli_ckpt3 --save_model_steps=3 --optimizer=momentum
+  run ck_bf16_resume $R50 --train_dir=/tmp/hcb_cli_ckpt3 --optimizer=momentum --compute_dtype=bf16
+  run ck_fp16_resume $R50 --train_dir=/tmp/hcb_cli_ckpt3 --optimizer=momentum --use_fp16=True
+  run ck_fp32_fwd $R50 --train_dir=/tmp/hcb_cli_ckpt3 --forward_only=True
+  run ck_bs32_resume --model=resnet50 --batch_size=32 --num_batches=4 --num_warmup_batches=1 --train_dir=/tmp/hcb_cli_ckpt3 --optimizer=momentum
+  for m in resnet50_v2 googlenet vgg16 alexnet; do
+    run ${m}_data_fp32 --model=$m $SMALL --data_dir=$D --data_name=imagenet
+    run ${m}_data_fp32_fwd --model=$m $SMALL --data_dir=$D --data_name=imagenet --forward_only=True
+  done
+  echo "sweep done: $(grep -c ^PASS $SUM) pass, $(grep -c ^FAIL $SUM) fail of $n" | tee -a $SUM
+  exit 0
+fi
 if [ "${SET:-1}" = 2 ]; then  # second set: real data, checkpoint timing, comm knobs, 16-bit zoo, inference
   D=/tmp/hcb_fake_imagenet
   [ -f $D/.done ] || { timeout -k 10 300 python tools/make_fake_imagenet.py $D --shards 4 --per_shard 128 > /dev/null && touch $D/.done; } || exit 1
